@@ -1,0 +1,125 @@
+"""ctypes binding of ``libhdverify.so`` (include/hd_verify.h, include/hd_probe.h).
+
+The library is the product: there is no Python/CPU fallback.  If it is missing
+or fails to load, importing the binding raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("HD_LIB", os.path.join(HERE, "_lib", "libhdverify.so"))
+
+HD_OK = 0
+HD_EINVAL = -1
+HD_ENOMEM = -2
+HD_EDEVICE = -3
+HD_ECAP = -4
+
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+c_i8p = ctypes.POINTER(ctypes.c_int8)
+c_i64p = ctypes.POINTER(ctypes.c_int64)
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+c_i32p = ctypes.POINTER(ctypes.c_int32)
+
+
+class HdBatch(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_uint32),
+        ("type", ctypes.c_void_p),
+        ("height", ctypes.c_void_p),
+        ("round", ctypes.c_void_p),
+        ("valid_round", ctypes.c_void_p),
+        ("value32", ctypes.c_void_p),
+        ("from32", ctypes.c_void_p),
+        ("sig65", ctypes.c_void_p),
+    ]
+
+
+class HdBatchOut(ctypes.Structure):
+    _fields_ = [
+        ("type", ctypes.c_void_p),
+        ("height", ctypes.c_void_p),
+        ("round", ctypes.c_void_p),
+        ("valid_round", ctypes.c_void_p),
+        ("value32", ctypes.c_void_p),
+        ("from32", ctypes.c_void_p),
+        ("sig65", ctypes.c_void_p),
+        ("adv_class", ctypes.c_void_p),
+    ]
+
+
+class HdTallyOut(ctypes.Structure):
+    _fields_ = [
+        ("cap_counts", ctypes.c_uint32),
+        ("n_counts", ctypes.c_uint32),
+        ("count_height", ctypes.c_void_p),
+        ("count_round", ctypes.c_void_p),
+        ("count_type", ctypes.c_void_p),
+        ("count_rep", ctypes.c_void_p),
+        ("count_n", ctypes.c_void_p),
+        ("cap_hr", ctypes.c_uint32),
+        ("n_hr", ctypes.c_uint32),
+        ("hr_height", ctypes.c_void_p),
+        ("hr_round", ctypes.c_void_p),
+        ("hr_prevotes", ctypes.c_void_p),
+        ("hr_precommits", ctypes.c_void_p),
+        ("hr_any", ctypes.c_void_p),
+        ("dup", ctypes.c_void_p),
+    ]
+
+
+# every symbol include/*.h declares, with its ctypes signature
+SIGNATURES = {
+    "hd_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "hd_ctx_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "hd_ctx_set_pubkey_format": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "hd_set_signatories": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
+    "hd_verify_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p]),
+    "hd_verify_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "hd_tally": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
+                                ctypes.POINTER(HdTallyOut)]),
+    "hd_process_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(HdTallyOut)]),
+    "hd_gen_keys": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    "hd_gen_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
+                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.POINTER(HdBatchOut), ctypes.c_void_p]),
+    "hd_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "hd_ctx_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
+    "hd_abi_version": (ctypes.c_int, []),
+    "hd_probe_valu": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_double)]),
+}
+
+_LIB = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libhdverify.so (once) and attach the signatures.  Raises if absent."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"hyperdrive_amd native library not found at {path}; build it with "
+            "`python -m hyperdrive_amd.build` (there is no CPU fallback)")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+class HDError(RuntimeError):
+    def __init__(self, code: int, where: str, detail: str = ""):
+        lib = load()
+        msg = f"{where}: {lib.hd_strerror(code).decode()} ({code})"
+        if detail:
+            msg += f": {detail}"
+        super().__init__(msg)
+        self.code = code

@@ -1,0 +1,316 @@
+// hd_group.h -- secp256k1 points (a = 0), the double-scalar multiplication
+// used by recovery, and the recovery itself with libsecp256k1 semantics
+// (go-ethereum v1.9.5 crypto/secp256k1 -> secp256k1_ext_ecdsa_recover).
+//
+// SIMD design note: per-lane wNAF sparsity buys nothing on a 64-wide
+// wavefront -- some lane always has a non-zero digit, so every lane would pay
+// every addition.  The ladder therefore uses *uniform* Booth-recoded fixed
+// windows: a 4-bit window for the variable point R (table 1R..8R, Jacobian,
+// per-lane, scratch) and an 8-bit window for G (table 1G..128G, affine, staged
+// in LDS by the kernel).  Every lane runs the identical sequence of
+// doublings/additions; a zero digit is a per-lane select, and the exceptional
+// cases of the addition law (P = inf, P = +-T) are rare branches.
+//
+// Jacobian infinity is Z == 0 (all values are fully reduced, so the test is
+// exact).
+#pragma once
+#include "hd_field.h"
+
+namespace hd {
+
+struct ge { fe x, y; };          // affine
+struct gej { fe x, y, z; };      // Jacobian, Z == 0 <=> infinity
+
+HD bool gej_is_inf(const gej& a) { return fe_is_zero(a.z); }
+HD void gej_set_inf(gej& r) { fe_clear(r.x); fe_set_u32(r.y, 1); fe_clear(r.z); }
+HD void gej_set_ge(gej& r, const ge& a) { r.x = a.x; r.y = a.y; fe_set_u32(r.z, 1); }
+HD void gej_cmov(gej& r, const gej& a, bool flag) {
+    fe_cmov(r.x, a.x, flag);
+    fe_cmov(r.y, a.y, flag);
+    fe_cmov(r.z, a.z, flag);
+}
+
+// dbl-2009-l (a = 0): 2M + 5S.  inf -> inf (Z3 = 2 Y Z = 0).
+HD void gej_dbl(gej& r, const gej& a) {
+    fe A, B, C, D, E, F, t;
+    fe_sqr(A, a.x);
+    fe_sqr(B, a.y);
+    fe_sqr(C, B);
+    fe_add(t, a.x, B);
+    fe_sqr(t, t);
+    fe_sub(t, t, A);
+    fe_sub(t, t, C);
+    fe_add(D, t, t);
+    fe_add(E, A, A);
+    fe_add(E, E, A);
+    fe_sqr(F, E);
+    fe z3;
+    fe_mul(z3, a.y, a.z);
+    fe_add(r.z, z3, z3);
+    fe_add(t, D, D);
+    fe_sub(r.x, F, t);
+    fe_sub(t, D, r.x);
+    fe_mul(t, E, t);
+    fe_add(C, C, C);
+    fe_add(C, C, C);
+    fe_add(C, C, C);
+    fe_sub(r.y, t, C);
+}
+
+HD_NOINLINE void gej_dbl_slow(gej& r, const gej& a) { gej_dbl(r, a); }
+
+// r = a + b, b affine and finite (madd-2007-bl: 7M + 4S).  Handles a = inf
+// and a = +-b.
+HD void gej_add_ge(gej& r, const gej& a, const ge& b) {
+    fe z1z1, u2, s2, h, hh, i4, j, rr, v, t;
+    fe_sqr(z1z1, a.z);
+    fe_mul(u2, b.x, z1z1);
+    fe_mul(s2, b.y, a.z);
+    fe_mul(s2, s2, z1z1);
+    fe_sub(h, u2, a.x);
+    fe_sub(rr, s2, a.y);
+    bool ainf = fe_is_zero(a.z);
+    bool hzero = fe_is_zero(h);
+    if (hzero && !ainf) {
+        // a == +-b (rare): double or cancel
+        gej o;
+        if (fe_is_zero(rr)) {
+            gej bj;
+            gej_set_ge(bj, b);
+            gej_dbl_slow(o, bj);
+        } else {
+            gej_set_inf(o);
+        }
+        r = o;
+        return;
+    }
+    fe_add(rr, rr, rr);
+    fe_sqr(hh, h);
+    fe_add(i4, hh, hh);
+    fe_add(i4, i4, i4);
+    fe_mul(j, h, i4);
+    fe_mul(v, a.x, i4);
+    gej o;
+    fe_sqr(o.x, rr);
+    fe_sub(o.x, o.x, j);
+    fe_sub(o.x, o.x, v);
+    fe_sub(o.x, o.x, v);
+    fe_sub(t, v, o.x);
+    fe_mul(t, rr, t);
+    fe_mul(j, a.y, j);
+    fe_add(j, j, j);
+    fe_sub(o.y, t, j);
+    fe_add(t, a.z, h);
+    fe_sqr(t, t);
+    fe_sub(t, t, z1z1);
+    fe_sub(o.z, t, hh);
+    if (ainf) gej_set_ge(o, b);
+    r = o;
+}
+
+// r = a + b, both Jacobian, b finite (add-2007-bl: 11M + 5S).  Handles
+// a = inf and a = +-b.
+HD void gej_add(gej& r, const gej& a, const gej& b) {
+    fe z1z1, z2z2, u1, u2, s1, s2, h, rr, t;
+    fe_sqr(z1z1, a.z);
+    fe_sqr(z2z2, b.z);
+    fe_mul(u1, a.x, z2z2);
+    fe_mul(u2, b.x, z1z1);
+    fe_mul(s1, a.y, b.z);
+    fe_mul(s1, s1, z2z2);
+    fe_mul(s2, b.y, a.z);
+    fe_mul(s2, s2, z1z1);
+    fe_sub(h, u2, u1);
+    fe_sub(rr, s2, s1);
+    bool ainf = fe_is_zero(a.z);
+    bool hzero = fe_is_zero(h);
+    if (hzero && !ainf) {
+        gej o;
+        if (fe_is_zero(rr)) gej_dbl_slow(o, a);
+        else gej_set_inf(o);
+        r = o;
+        return;
+    }
+    fe i, j, v;
+    fe_add(i, h, h);
+    fe_sqr(i, i);
+    fe_mul(j, h, i);
+    fe_add(rr, rr, rr);
+    fe_mul(v, u1, i);
+    gej o;
+    fe_sqr(o.x, rr);
+    fe_sub(o.x, o.x, j);
+    fe_sub(o.x, o.x, v);
+    fe_sub(o.x, o.x, v);
+    fe_sub(t, v, o.x);
+    fe_mul(t, rr, t);
+    fe_mul(s1, s1, j);
+    fe_add(s1, s1, s1);
+    fe_sub(o.y, t, s1);
+    fe_add(t, a.z, b.z);
+    fe_sqr(t, t);
+    fe_sub(t, t, z1z1);
+    fe_sub(t, t, z2z2);
+    fe_mul(o.z, t, h);
+    if (ainf) o = b;
+    r = o;
+}
+
+// ------------------------------------------------------------ recoding
+// Booth digit of window j (width W) of a 256-bit scalar k:
+//   d = b[Wj-1] + sum_{t<W-1} 2^t b[Wj+t] - 2^(W-1) b[Wj+W-1],  |d| <= 2^(W-1)
+HD uint32_t sc_bits(const sc& k, int pos, int len) {
+    // bits [pos, pos+len) of k, bits outside [0,256) read as 0; len <= 16
+    uint32_t out = 0;
+    HD_UNROLL for (int t = 0; t < 16; t++) {
+        if (t < len) {
+            int b = pos + t;
+            uint32_t bit = (b >= 0 && b < 256) ? ((k.v[b >> 5] >> (b & 31)) & 1u) : 0u;
+            out |= bit << t;
+        }
+    }
+    return out;
+}
+template <int W>
+HD int booth_digit(const sc& k, int j) {
+    uint32_t x = sc_bits(k, W * j - 1, W + 1);
+    return (int)((x >> 1) + (x & 1)) - (int)((x >> W) << W);
+}
+
+#define HD_WR 4                       // R window
+#define HD_WG 8                       // G window
+#define HD_NWIN_R (256 / HD_WR + 1)   // 65 windows
+#define HD_NWIN_G (256 / HD_WG + 1)   // 33 windows
+#define HD_GTAB_N (1 << (HD_WG - 1))  // 128 affine multiples 1G..128G
+#define HD_RTAB_N (1 << (HD_WR - 1))  // 8 Jacobian multiples 1R..8R
+
+// Q = u1*G + u2*R.  gtab[k] = (k+1) G affine (k < 128).
+template <typename GTab>
+HD void ecmult(gej& out, const ge& R, const sc& u1, const sc& u2, GTab gtab) {
+    gej rt[HD_RTAB_N];
+    gej_set_ge(rt[0], R);
+    gej_dbl(rt[1], rt[0]);
+    HD_NOUNROLL for (int k = 2; k < HD_RTAB_N; k++) gej_add_ge(rt[k], rt[k - 1], R);
+
+    int16_t dr[HD_NWIN_R], dg[HD_NWIN_G];  // |digit| <= 128: int8 would overflow
+    HD_UNROLL for (int j = 0; j < HD_NWIN_R; j++) dr[j] = (int16_t)booth_digit<HD_WR>(u2, j);
+    HD_UNROLL for (int j = 0; j < HD_NWIN_G; j++) dg[j] = (int16_t)booth_digit<HD_WG>(u1, j);
+
+    gej acc;
+    gej_set_inf(acc);
+    HD_NOUNROLL for (int j = HD_NWIN_R - 1; j >= 0; j--) {
+        if (j != HD_NWIN_R - 1) {
+            HD_NOUNROLL for (int k = 0; k < HD_WR; k++) gej_dbl(acc, acc);
+        }
+        if ((j & 1) == 0) {
+            int d = dg[j >> 1];
+            int ad = d < 0 ? -d : d;
+            ge t = gtab[ad == 0 ? 0 : ad - 1];
+            if (d < 0) fe_neg(t.y, t.y);
+            gej s;
+            gej_add_ge(s, acc, t);
+            gej_cmov(acc, s, d != 0);
+        }
+        {
+            int d = dr[j];
+            int ad = d < 0 ? -d : d;
+            gej t = rt[ad == 0 ? 0 : ad - 1];
+            if (d < 0) fe_neg(t.y, t.y);
+            gej s;
+            gej_add(s, acc, t);
+            gej_cmov(acc, s, d != 0);
+        }
+    }
+    out = acc;
+}
+
+// G and its odd... all multiples 1G..128G in affine form (host-side build, or
+// any caller that wants the table).
+HD void build_gtab(ge* tab) {
+    ge g;
+    const uint32_t GX[8] = {0x79BE667Eu, 0xF9DCBBACu, 0x55A06295u, 0xCE870B07u,
+                            0x029BFCDBu, 0x2DCE28D9u, 0x59F2815Bu, 0x16F81798u};
+    const uint32_t GY[8] = {0x483ADA77u, 0x26A3C465u, 0x5DA4FBFCu, 0x0E1108A8u,
+                            0xFD17B448u, 0xA6855419u, 0x9C47D08Fu, 0xFB10D4B8u};
+    fe_from_be(g.x, GX);
+    fe_from_be(g.y, GY);
+    gej acc;
+    gej_set_ge(acc, g);
+    tab[0] = g;
+    for (int k = 1; k < HD_GTAB_N; k++) {
+        if (k == 1) gej_dbl(acc, acc);
+        else gej_add_ge(acc, acc, g);
+        fe zi, zi2, zi3;
+        fe_inv(zi, acc.z);
+        fe_sqr(zi2, zi);
+        fe_mul(zi3, zi2, zi);
+        fe_mul(tab[k].x, acc.x, zi2);
+        fe_mul(tab[k].y, acc.y, zi3);
+    }
+}
+
+// ------------------------------------------------------------ recovery
+// libsecp256k1 recover semantics:
+//   V >= 4 -> BAD_RECID (go-ethereum checkSignature); r or s >= n -> BAD_RS
+//   (parse_compact overflow); r or s == 0 -> BAD_RS (sig_recover);
+//   V&2 and r >= p - n -> NO_POINT; x^3+7 non-residue -> NO_POINT;
+//   Q = inf -> INFINITY.  High-S accepted.  m = digest mod n.
+// On VALID writes the affine Q (x, y).
+template <typename GTab>
+HD uint8_t recover(fe& qx, fe& qy, const uint32_t digest_be[8], const uint32_t r_be[8],
+                   const uint32_t s_be[8], uint32_t v, GTab gtab) {
+    if (v >= 4) return V_BAD_RECID;
+    sc r, s;
+    HD_UNROLL for (int i = 0; i < 8; i++) { r.v[i] = r_be[7 - i]; s.v[i] = s_be[7 - i]; }
+    if (sc_ge_n(r.v) || sc_ge_n(s.v)) return V_BAD_RS;
+    if (sc_is_zero(r) || sc_is_zero(s)) return V_BAD_RS;
+    fe x;
+    HD_UNROLL for (int i = 0; i < 8; i++) x.v[i] = r.v[i];
+    if (v & 2) {
+        // x = r + n must stay < p  <=>  r < p - n
+        // p - n = 0x14551231950B75FC4402DA1722FC9BAEE (129 bits, LE limbs below)
+        const uint32_t PMN[8] = {0x2FC9BAEEu, 0x402DA172u, 0x50B75FC4u, 0x45512319u, 1u, 0u, 0u, 0u};
+        bool lt = false, gt = false;
+        HD_UNROLL for (int i = 7; i >= 0; i--) {
+            bool g = !lt && !gt && r.v[i] > PMN[i];
+            bool l = !lt && !gt && r.v[i] < PMN[i];
+            gt = gt || g;
+            lt = lt || l;
+        }
+        if (!lt) return V_NO_POINT;
+        const uint32_t N[8] = {HD_N0, HD_N1, HD_N2, HD_N3, HD_N4, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        uint64_t c = 0;
+        HD_UNROLL for (int i = 0; i < 8; i++) { c += (uint64_t)x.v[i] + N[i]; x.v[i] = (uint32_t)c; c >>= 32; }
+    }
+    fe y2, y;
+    fe_sqr(y2, x);
+    fe_mul(y2, y2, x);
+    fe seven;
+    fe_set_u32(seven, 7);
+    fe_add(y2, y2, seven);
+    if (!fe_sqrt(y, y2)) return V_NO_POINT;
+    if ((y.v[0] & 1u) != (v & 1u)) fe_neg(y, y);
+    ge R;
+    R.x = x;
+    R.y = y;
+
+    sc m, rinv, u1, u2;
+    sc_from_be_reduce(m, digest_be);
+    sc_inv(rinv, r);
+    sc_mul(u1, m, rinv);
+    sc_neg(u1, u1);
+    sc_mul(u2, s, rinv);
+
+    gej Q;
+    ecmult(Q, R, u1, u2, gtab);
+    if (gej_is_inf(Q)) return V_INFINITY;
+    fe zi, zi2;
+    fe_inv(zi, Q.z);
+    fe_sqr(zi2, zi);
+    fe_mul(qx, Q.x, zi2);
+    fe_mul(zi2, zi2, zi);
+    fe_mul(qy, Q.y, zi2);
+    return V_VALID;
+}
+
+}  // namespace hd

@@ -1,0 +1,310 @@
+// hd_verify.hip -- gfx950 kernels and the C ABI (include/hd_verify.h) of the
+// hyperdrive batch authenticator.
+//
+// Kernels
+//   k_verify  one message per lane: digest -> secp256k1 recover -> signatory
+//             -> Equal(From) -> admitted lookup.  INT32-VALU bound (no MFMA:
+//             nothing here is a dense contraction).  The 8 KiB table of
+//             1G..128G is staged in LDS once per workgroup; the admitted set
+//             (sorted, 32 B entries) is read through L2.  A valid-bitmap word
+//             pair per wavefront comes from one __ballot.
+//   (k_gen / k_keys, the synthetic workload, live in hd_genk.hip)
+//   tally kernels: see hd_tally.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/hd_verify.h"
+#include "hd_verify_msg.h"
+#include "hd_internal.h"
+
+using namespace hd;
+
+// ---------------------------------------------------------------- kernels
+__device__ __forceinline__ void load_msg(MsgIn& m, const DevBatch& b, uint32_t i) {
+    m.type = b.type[i];
+    m.h = b.height[i];
+    m.r = b.round[i];
+    m.vr = b.valid_round ? b.valid_round[i] : -1;
+    const uint8_t* val = b.value32 + 32 * (size_t)i;
+    const uint8_t* frm = b.from32 + 32 * (size_t)i;
+    const uint8_t* sig = b.sig65 + 65 * (size_t)i;
+    HD_UNROLL for (int w = 0; w < 8; w++) {
+        m.value_be[w] = load_be32(val + 4 * w);
+        m.from_be[w] = load_be32(frm + 4 * w);
+        m.r_be[w] = load_be32(sig + 4 * w);
+        m.s_be[w] = load_be32(sig + 32 + 4 * w);
+    }
+    m.v = sig[64];
+}
+
+template <bool COMPRESSED>
+__global__ __launch_bounds__(256, 2) void k_verify(DevBatch b, const ge* __restrict__ gtab_g,
+                                                const uint32_t* __restrict__ adm, const int32_t* __restrict__ adm_perm,
+                                                uint32_t n_adm, int adm_steps, uint8_t* __restrict__ verdict,
+                                                uint8_t* __restrict__ rec32, int32_t* __restrict__ signer,
+                                                uint32_t* __restrict__ bitmap) {
+    __shared__ ge s_gtab[HD_GTAB_N];
+    {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(gtab_g);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(s_gtab);
+        for (int k = threadIdx.x; k < HD_GTAB_N * 16; k += blockDim.x) dst[k] = src[k];
+    }
+    __syncthreads();
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < b.n; base += stride) {
+        const uint32_t i = base + threadIdx.x;
+        const bool active = i < b.n;
+        uint8_t v = 0xFF;
+        if (active) {
+            MsgIn m;
+            load_msg(m, b, i);
+            uint32_t rec[8];
+            int32_t s;
+            v = verify_msg(m, (const ge*)s_gtab, adm, n_adm, adm_steps, COMPRESSED, rec, s);
+            verdict[i] = v;
+            if (rec32) {
+                uint8_t* o = rec32 + 32 * (size_t)i;
+                HD_UNROLL for (int w = 0; w < 8; w++) store_be32(o + 4 * w, rec[w]);
+            }
+            if (signer) signer[i] = s >= 0 ? adm_perm[s] : -1;
+        }
+        if (bitmap) {
+            const unsigned long long bal = __ballot(active && v == V_VALID);
+            const uint32_t wave_base = base + (threadIdx.x & ~63u);
+            if ((threadIdx.x & 63u) == 0 && wave_base < b.n) {
+                bitmap[wave_base / 32] = (uint32_t)bal;
+                if (wave_base + 32 < b.n) bitmap[wave_base / 32 + 1] = (uint32_t)(bal >> 32);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- host side
+namespace {
+const char* const kErr[] = {"ok", "invalid argument", "out of memory", "device error", "tally capacity too small"};
+}
+
+int hd_ctx_fail(hd_ctx* ctx, hipError_t e, const char* what) {
+    if (ctx) {
+        char buf[256];
+        snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+        ctx->last_error = buf;
+    }
+    return e == hipErrorOutOfMemory ? HD_ENOMEM : HD_EDEVICE;
+}
+
+int hd_dev_grow(hd_ctx* ctx, void** p, size_t* cap, size_t need) {
+    if (need <= *cap) return HD_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    size_t want = std::max(need, (size_t)4096);
+    hipError_t e = hipMalloc(p, want);
+    if (e != hipSuccess) return hd_ctx_fail(ctx, e, "hipMalloc");
+    *cap = want;
+    return HD_OK;
+}
+
+extern "C" {
+
+int hd_abi_version(void) { return 1; }
+
+const char* hd_strerror(int code) {
+    int k = -code;
+    if (k < 0 || k > 4) return "unknown error";
+    return kErr[k];
+}
+
+const char* hd_ctx_last_error(hd_ctx* ctx) { return ctx ? ctx->last_error.c_str() : ""; }
+
+int hd_ctx_create(int device, hd_ctx** out) {
+    if (!out) return HD_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return HD_EDEVICE;
+    hd_ctx* ctx = new (std::nothrow) hd_ctx();
+    if (!ctx) return HD_ENOMEM;
+    ctx->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        int rc = hd_ctx_fail(ctx, e, "hipStreamCreate");
+        delete ctx;
+        return rc;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->n_cu = prop.multiProcessorCount;
+    // G table (1G..128G affine), built once on the host with the same code
+    // the device runs, then uploaded.
+    static std::once_flag once;
+    static std::vector<ge> host_tab(HD_GTAB_N);
+    std::call_once(once, [] { build_gtab(host_tab.data()); });
+    e = hipMalloc(&ctx->d_gtab, sizeof(ge) * HD_GTAB_N);
+    if (e == hipSuccess) e = hipMemcpy(ctx->d_gtab, host_tab.data(), sizeof(ge) * HD_GTAB_N, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        int rc = hd_ctx_fail(ctx, e, "gtab upload");
+        hd_ctx_destroy(ctx);
+        return rc;
+    }
+    *out = ctx;
+    return HD_OK;
+}
+
+int hd_ctx_destroy(hd_ctx* ctx) {
+    if (!ctx) return HD_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    void* ptrs[] = {ctx->d_gtab, ctx->d_adm, ctx->d_adm_perm};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    for (auto& b : ctx->bufs)
+        if (b.p) (void)hipFree(b.p);
+    hd_tally_release(ctx);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return HD_OK;
+}
+
+int hd_ctx_set_pubkey_format(hd_ctx* ctx, int compressed) {
+    if (!ctx) return HD_EINVAL;
+    ctx->compressed = compressed != 0;
+    return HD_OK;
+}
+
+int hd_set_signatories(hd_ctx* ctx, const uint8_t* sigs32, uint32_t n) {
+    if (!ctx || (n && !sigs32)) return HD_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    // sort (stable on the original index so duplicates map to the first)
+    std::vector<uint32_t> order(n);
+    for (uint32_t i = 0; i < n; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](uint32_t a, uint32_t b) { return memcmp(sigs32 + 32 * (size_t)a, sigs32 + 32 * (size_t)b, 32) < 0; });
+    std::vector<uint32_t> words;
+    std::vector<int32_t> perm;
+    words.reserve(8 * (size_t)n);
+    for (uint32_t k = 0; k < n; k++) {
+        const uint8_t* s = sigs32 + 32 * (size_t)order[k];
+        if (!perm.empty() && memcmp(s, sigs32 + 32 * (size_t)perm.back(), 32) == 0) continue;  // dedup
+        for (int w = 0; w < 8; w++) words.push_back(load_be32(s + 4 * w));
+        perm.push_back((int32_t)order[k]);
+    }
+    uint32_t m = (uint32_t)perm.size();
+    size_t cap_a = ctx->cap_adm, cap_p = ctx->cap_adm_perm;
+    int rc = hd_dev_grow(ctx, (void**)&ctx->d_adm, &cap_a, 32 * (size_t)std::max(m, 1u));
+    if (rc) return rc;
+    ctx->cap_adm = cap_a;
+    rc = hd_dev_grow(ctx, (void**)&ctx->d_adm_perm, &cap_p, 4 * (size_t)std::max(m, 1u));
+    if (rc) return rc;
+    ctx->cap_adm_perm = cap_p;
+    hipError_t e = hipSuccess;
+    if (m) {
+        e = hipMemcpy(ctx->d_adm, words.data(), 32 * (size_t)m, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(ctx->d_adm_perm, perm.data(), 4 * (size_t)m, hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) return hd_ctx_fail(ctx, e, "set_signatories upload");
+    ctx->n_adm = m;
+    int steps = 0;
+    while ((1u << steps) < m) steps++;
+    ctx->adm_steps = steps;
+    return HD_OK;
+}
+
+int hd_verify_batch_device(hd_ctx* ctx, const hd_batch* db, uint8_t* d_verdict, uint8_t* d_recovered32,
+                           int32_t* d_signer, uint32_t* d_valid_bitmap, void* stream) {
+    if (!ctx || !db || !d_verdict) return HD_EINVAL;
+    if (db->n == 0) return HD_OK;
+    if (!db->type || !db->height || !db->round || !db->value32 || !db->from32 || !db->sig65) return HD_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    DevBatch b{db->n, db->type, db->height, db->round, db->valid_round, db->value32, db->from32, db->sig65};
+    const uint32_t threads = 256;
+    uint32_t blocks = (db->n + threads - 1) / threads;
+    uint32_t max_blocks = (uint32_t)std::max(ctx->n_cu, 1) * 8u;
+    blocks = std::min(blocks, max_blocks);
+    if (ctx->compressed)
+        k_verify<true><<<blocks, threads, 0, s>>>(b, ctx->d_gtab, ctx->d_adm, ctx->d_adm_perm, ctx->n_adm, ctx->adm_steps,
+                                                  d_verdict, d_recovered32, d_signer, d_valid_bitmap);
+    else
+        k_verify<false><<<blocks, threads, 0, s>>>(b, ctx->d_gtab, ctx->d_adm, ctx->d_adm_perm, ctx->n_adm, ctx->adm_steps,
+                                                   d_verdict, d_recovered32, d_signer, d_valid_bitmap);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hd_ctx_fail(ctx, e, "k_verify launch");
+    return HD_OK;
+}
+
+}  // extern "C"
+
+int hd_upload_batch(hd_ctx* ctx, const hd_batch* hb, hd_batch* db) {
+    const uint32_t n = hb->n;
+    struct F { const void* src; size_t sz; int slot; } f[] = {
+        {hb->type, (size_t)n, BUF_TYPE},
+        {hb->height, 8 * (size_t)n, BUF_HEIGHT},
+        {hb->round, 8 * (size_t)n, BUF_ROUND},
+        {hb->valid_round, 8 * (size_t)n, BUF_VROUND},
+        {hb->value32, 32 * (size_t)n, BUF_VALUE},
+        {hb->from32, 32 * (size_t)n, BUF_FROM},
+        {hb->sig65, 65 * (size_t)n, BUF_SIG},
+    };
+    void* dst[7];
+    for (int k = 0; k < 7; k++) {
+        if (!f[k].src) { dst[k] = nullptr; continue; }
+        int rc = hd_dev_grow(ctx, &ctx->bufs[f[k].slot].p, &ctx->bufs[f[k].slot].cap, f[k].sz);
+        if (rc) return rc;
+        dst[k] = ctx->bufs[f[k].slot].p;
+        hipError_t e = hipMemcpyAsync(dst[k], f[k].src, f[k].sz, hipMemcpyHostToDevice, ctx->stream);
+        if (e != hipSuccess) return hd_ctx_fail(ctx, e, "batch upload");
+    }
+    db->n = n;
+    db->type = (const uint8_t*)dst[0];
+    db->height = (const int64_t*)dst[1];
+    db->round = (const int64_t*)dst[2];
+    db->valid_round = (const int64_t*)dst[3];
+    db->value32 = (const uint8_t*)dst[4];
+    db->from32 = (const uint8_t*)dst[5];
+    db->sig65 = (const uint8_t*)dst[6];
+    return HD_OK;
+}
+
+int hd_verify_uploaded(hd_ctx* ctx, const hd_batch* db, uint8_t* verdict, uint8_t* recovered32, uint32_t* valid_bitmap) {
+    const uint32_t n = db->n;
+    int rc = hd_dev_grow(ctx, &ctx->bufs[BUF_VERDICT].p, &ctx->bufs[BUF_VERDICT].cap, n);
+    if (!rc) rc = hd_dev_grow(ctx, &ctx->bufs[BUF_SIGNER].p, &ctx->bufs[BUF_SIGNER].cap, 4 * (size_t)n);
+    if (!rc && recovered32) rc = hd_dev_grow(ctx, &ctx->bufs[BUF_REC].p, &ctx->bufs[BUF_REC].cap, 32 * (size_t)n);
+    size_t nwords = (n + 31) / 32;
+    if (!rc && valid_bitmap) rc = hd_dev_grow(ctx, &ctx->bufs[BUF_BITMAP].p, &ctx->bufs[BUF_BITMAP].cap, 4 * nwords);
+    if (rc) return rc;
+    uint8_t* d_v = (uint8_t*)ctx->bufs[BUF_VERDICT].p;
+    uint8_t* d_r = recovered32 ? (uint8_t*)ctx->bufs[BUF_REC].p : nullptr;
+    uint32_t* d_b = valid_bitmap ? (uint32_t*)ctx->bufs[BUF_BITMAP].p : nullptr;
+    int32_t* d_s = (int32_t*)ctx->bufs[BUF_SIGNER].p;
+    rc = hd_verify_batch_device(ctx, db, d_v, d_r, d_s, d_b, ctx->stream);
+    if (rc) return rc;
+    hipError_t e = hipMemcpyAsync(verdict, d_v, n, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && d_r) e = hipMemcpyAsync(recovered32, d_r, 32 * (size_t)n, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && d_b) e = hipMemcpyAsync(valid_bitmap, d_b, 4 * nwords, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return hd_ctx_fail(ctx, e, "verify");
+    return HD_OK;
+}
+
+extern "C" {
+
+int hd_verify_batch(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8_t* recovered32, uint32_t* valid_bitmap) {
+    if (!ctx || !batch || !verdict) return HD_EINVAL;
+    if (batch->n == 0) return HD_OK;
+    if (!batch->type || !batch->height || !batch->round || !batch->value32 || !batch->from32 || !batch->sig65)
+        return HD_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    hd_batch db;
+    int rc = hd_upload_batch(ctx, batch, &db);
+    if (rc) return rc;
+    return hd_verify_uploaded(ctx, &db, verdict, recovered32, valid_bitmap);
+}
+
+}  // extern "C"

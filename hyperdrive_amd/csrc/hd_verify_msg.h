@@ -1,0 +1,90 @@
+// hd_verify_msg.h -- the per-message hot path, one message per lane:
+//   digest (surge preimage + SHA-256)  -> recover (libsecp256k1 semantics)
+//   -> signatory = SHA-256(pubkey)     -> Equal(From)  -> From in admitted set
+//
+// Reference: process/message.go:53-78, 165-186, 263-284 (preimages);
+// process/message_test.go:147-154 (sign -> Signatory(&hash) -> Equal);
+// mq/mq.go:49-51 + replica/replica.go:69-72 (procsAllowed membership).
+#pragma once
+#include "hd_group.h"
+#include "hd_sha256.h"
+
+namespace hd {
+
+struct MsgIn {
+    uint32_t type;
+    int64_t h, r, vr;
+    uint32_t value_be[8];
+    uint32_t from_be[8];
+    uint32_t r_be[8], s_be[8];
+    uint32_t v;
+};
+
+HD void message_digest(uint32_t d[8], const MsgIn& m) {
+    if (m.type == T_PROPOSE) sha256_propose(d, m.h, m.r, m.vr, m.value_be);
+    else sha256_vote(d, m.h, m.r, m.value_be);
+}
+
+// lexicographic compare of two 32-byte strings held as 8 big-endian words
+HD int cmp_be256(const uint32_t a[8], const uint32_t b[8]) {
+    int res = 0;
+    HD_UNROLL for (int i = 7; i >= 0; i--) {
+        int c = a[i] < b[i] ? -1 : (a[i] > b[i] ? 1 : 0);
+        res = c != 0 ? c : res;
+    }
+    return res;
+}
+
+// Admitted table: n entries of 8 big-endian words, sorted ascending.  Returns
+// the index or -1.  Uniform iteration count (ceil log2) for all lanes.
+template <typename AdmTab>
+HD int32_t admitted_find(AdmTab adm, uint32_t n, int steps, const uint32_t key[8]) {
+    uint32_t lo = 0, len = n;
+    HD_NOUNROLL for (int s = 0; s < steps; s++) {
+        uint32_t half = len >> 1;
+        uint32_t mid = lo + half;
+        uint32_t e[8];
+        bool ok = mid < n && len > 1;
+        uint32_t idx = ok ? mid : 0u;
+        HD_UNROLL for (int w = 0; w < 8; w++) e[w] = adm[idx * 8 + w];
+        if (ok && cmp_be256(e, key) <= 0) lo = mid;
+        len = len - half;
+    }
+    if (n == 0) return -1;
+    uint32_t e[8];
+    HD_UNROLL for (int w = 0; w < 8; w++) e[w] = adm[lo * 8 + w];
+    return cmp_be256(e, key) == 0 ? (int32_t)lo : -1;
+}
+
+// Full verdict for one message.  rec_be receives the recovered signatory (or
+// zeros when recovery failed); signer receives the admitted-table index.
+template <typename GTab, typename AdmTab>
+HD uint8_t verify_msg(const MsgIn& m, GTab gtab, AdmTab adm, uint32_t n_adm, int adm_steps, bool compressed,
+                      uint32_t rec_be[8], int32_t& signer) {
+    signer = -1;
+    HD_UNROLL for (int i = 0; i < 8; i++) rec_be[i] = 0;
+    if (m.type < 1 || m.type > 3) return V_BAD_TYPE;
+    uint32_t d[8];
+    message_digest(d, m);
+    fe qx, qy;
+    uint8_t verdict = recover(qx, qy, d, m.r_be, m.s_be, m.v, gtab);
+    if (verdict != V_VALID) return verdict;
+    uint32_t xb[8];
+    fe_to_be(xb, qx);
+    if (compressed) {
+        sha256_pub33(rec_be, 2u | (qy.v[0] & 1u), xb);
+    } else {
+        uint32_t yb[8];
+        fe_to_be(yb, qy);
+        sha256_pub65(rec_be, xb, yb);
+    }
+    uint32_t diff = 0;
+    HD_UNROLL for (int i = 0; i < 8; i++) diff |= rec_be[i] ^ m.from_be[i];
+    if (diff) return V_SIGNATORY_MISMATCH;
+    int32_t idx = admitted_find(adm, n_adm, adm_steps, m.from_be);
+    if (idx < 0) return V_NOT_ADMITTED;
+    signer = idx;
+    return V_VALID;
+}
+
+}  // namespace hd

@@ -1,0 +1,254 @@
+"""Host-side mirror of the batch-verify boundary.
+
+In the reference the authentication of a Propose/Prevote/Precommit is a
+precondition the caller must establish before ``Replica.Propose/Prevote/
+Precommit`` (replica/replica.go:153-181; mq/mq.go:85-101 "assumes that the
+sender has already been authenticated"), and membership is the
+``procsAllowed`` filter at consume time (mq/mq.go:49-51).  This module is the
+Python face of the C ABI that takes over both for a whole batch:
+
+    v = Verifier(device=0)
+    v.set_signatories(signatories)          # replica.go:69-72 / 136-144
+    res = v.verify_batch(batch)             # per-message verdicts
+    t = v.tally(batch, res.verdict)         # first-wins logs + 2f+1 counts
+
+Per-message failures are verdicts (never exceptions); exceptions are raised
+only for invalid arguments and device failures, like the reference's
+``fmt.Errorf`` returns in process/message.go:61-77.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Dict, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import HDError, HdBatch, HdTallyOut
+
+# verdicts (include/hd_verify.h)
+VALID = 0
+BAD_RECID = 1
+BAD_RS = 2
+NO_POINT = 3
+INFINITY = 4
+SIGNATORY_MISMATCH = 5
+NOT_ADMITTED = 6
+BAD_TYPE = 7
+VERDICT_NAMES = ["VALID", "BAD_RECID", "BAD_RS", "NO_POINT", "INFINITY", "SIGNATORY_MISMATCH",
+                 "NOT_ADMITTED", "BAD_TYPE"]
+
+PROPOSE, PREVOTE, PRECOMMIT = 1, 2, 3
+
+
+def _ptr(a: Optional[np.ndarray]):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "arrays must be C-contiguous"
+    return a.ctypes.data
+
+
+@dataclass
+class Batch:
+    """Structure-of-arrays batch in host memory (hd_batch)."""
+    type: np.ndarray          # uint8[n]
+    height: np.ndarray        # int64[n]
+    round: np.ndarray         # int64[n]
+    valid_round: Optional[np.ndarray]  # int64[n] or None
+    value: np.ndarray         # uint8[n, 32]
+    frm: np.ndarray           # uint8[n, 32]
+    sig: np.ndarray           # uint8[n, 65]
+
+    def __post_init__(self):
+        n = len(self.type)
+        self.type = np.ascontiguousarray(self.type, dtype=np.uint8)
+        self.height = np.ascontiguousarray(self.height, dtype=np.int64)
+        self.round = np.ascontiguousarray(self.round, dtype=np.int64)
+        if self.valid_round is not None:
+            self.valid_round = np.ascontiguousarray(self.valid_round, dtype=np.int64)
+        self.value = np.ascontiguousarray(self.value, dtype=np.uint8).reshape(n, 32)
+        self.frm = np.ascontiguousarray(self.frm, dtype=np.uint8).reshape(n, 32)
+        self.sig = np.ascontiguousarray(self.sig, dtype=np.uint8).reshape(n, 65)
+        for name in ("height", "round"):
+            if len(getattr(self, name)) != n:
+                raise ValueError(f"{name} has {len(getattr(self, name))} entries, expected {n}")
+        if self.valid_round is not None and len(self.valid_round) != n:
+            raise ValueError("valid_round length mismatch")
+
+    def __len__(self) -> int:
+        return len(self.type)
+
+    @classmethod
+    def from_lists(cls, mtype, height, round_, valid_round, value, frm, sig) -> "Batch":
+        n = len(mtype)
+        return cls(np.array(mtype, np.uint8), np.array(height, np.int64), np.array(round_, np.int64),
+                   np.array(valid_round, np.int64) if valid_round is not None else None,
+                   np.frombuffer(b"".join(value), np.uint8).reshape(n, 32).copy() if n else np.zeros((0, 32), np.uint8),
+                   np.frombuffer(b"".join(frm), np.uint8).reshape(n, 32).copy() if n else np.zeros((0, 32), np.uint8),
+                   np.frombuffer(b"".join(sig), np.uint8).reshape(n, 65).copy() if n else np.zeros((0, 65), np.uint8))
+
+    def c_struct(self) -> HdBatch:
+        return HdBatch(len(self), _ptr(self.type), _ptr(self.height), _ptr(self.round), _ptr(self.valid_round),
+                       _ptr(self.value), _ptr(self.frm), _ptr(self.sig))
+
+
+@dataclass
+class VerifyResult:
+    verdict: np.ndarray       # uint8[n]
+    recovered: np.ndarray     # uint8[n, 32]
+    valid_bitmap: np.ndarray  # uint32[ceil(n/32)]
+
+
+@dataclass
+class TallyResult:
+    """First-wins vote logs summarised per (h, r) and per (h, r, type, value)."""
+    count: Dict[Tuple[int, int, int, bytes], int]
+    distinct: Dict[Tuple[int, int, int], int]
+    distinct_any: Dict[Tuple[int, int], int]
+    dup: np.ndarray           # uint8[n]: 0 logged, 1 identical dup, 2 double vote, 3 not a candidate
+
+
+class Verifier:
+    """One context per caller thread (the reference's Process is
+    single-goroutine, process/process.go:100-101)."""
+
+    def __init__(self, device: int = 0, compressed: bool = True):
+        self._lib = _lib.load()
+        h = ctypes.c_void_p()
+        rc = self._lib.hd_ctx_create(device, ctypes.byref(h))
+        if rc != 0:
+            raise HDError(rc, "hd_ctx_create")
+        self._ctx = h
+        self.device = device
+        self._check(self._lib.hd_ctx_set_pubkey_format(self._ctx, 1 if compressed else 0), "set_pubkey_format")
+        self.n_signatories = 0
+
+    def _check(self, rc: int, where: str):
+        if rc != 0:
+            detail = self._lib.hd_ctx_last_error(self._ctx).decode() if self._ctx else ""
+            raise HDError(rc, where, detail)
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._lib.hd_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._ctx
+
+    def set_signatories(self, signatories) -> None:
+        arr = _as_rows(signatories, 32)
+        self._check(self._lib.hd_set_signatories(self._ctx, _ptr(arr), len(arr)), "hd_set_signatories")
+        self.n_signatories = len(arr)
+
+    def verify_batch(self, batch: Batch, recovered: bool = True) -> VerifyResult:
+        n = len(batch)
+        verdict = np.zeros(n, np.uint8)
+        rec = np.zeros((n, 32), np.uint8)
+        bitmap = np.zeros((n + 31) // 32, np.uint32)
+        cb = batch.c_struct()
+        self._check(self._lib.hd_verify_batch(self._ctx, ctypes.byref(cb), _ptr(verdict),
+                                              _ptr(rec) if recovered else None, _ptr(bitmap)), "hd_verify_batch")
+        return VerifyResult(verdict, rec, bitmap)
+
+    def verify_batch_device(self, dbatch: HdBatch, d_verdict: int, d_recovered: Optional[int] = None,
+                            d_signer: Optional[int] = None, d_bitmap: Optional[int] = None,
+                            stream: Optional[int] = None) -> None:
+        """Device-resident variant: every pointer is a device address."""
+        self._check(self._lib.hd_verify_batch_device(self._ctx, ctypes.byref(dbatch), d_verdict, d_recovered,
+                                                     d_signer, d_bitmap, stream), "hd_verify_batch_device")
+
+    # ---- tally -------------------------------------------------------
+    def _tally_struct(self, n: int):
+        arrs = dict(
+            count_height=np.zeros(max(n, 1), np.int64), count_round=np.zeros(max(n, 1), np.int64),
+            count_type=np.zeros(max(n, 1), np.uint8), count_rep=np.zeros(max(n, 1), np.uint32),
+            count_n=np.zeros(max(n, 1), np.uint32), hr_height=np.zeros(max(n, 1), np.int64),
+            hr_round=np.zeros(max(n, 1), np.int64), hr_prevotes=np.zeros(max(n, 1), np.uint32),
+            hr_precommits=np.zeros(max(n, 1), np.uint32), hr_any=np.zeros(max(n, 1), np.uint32),
+            dup=np.zeros(max(n, 1), np.uint8))
+        t = HdTallyOut()
+        t.cap_counts = n
+        t.cap_hr = n
+        for k, a in arrs.items():
+            setattr(t, k, _ptr(a))
+        return t, arrs
+
+    @staticmethod
+    def _tally_result(batch: Batch, t: HdTallyOut, a) -> TallyResult:
+        count = {}
+        for k in range(t.n_counts):
+            rep = int(a["count_rep"][k])
+            count[(int(a["count_height"][k]), int(a["count_round"][k]), int(a["count_type"][k]),
+                   batch.value[rep].tobytes())] = int(a["count_n"][k])
+        distinct, distinct_any = {}, {}
+        for k in range(t.n_hr):
+            h, r = int(a["hr_height"][k]), int(a["hr_round"][k])
+            if a["hr_prevotes"][k]:
+                distinct[(h, r, PREVOTE)] = int(a["hr_prevotes"][k])
+            if a["hr_precommits"][k]:
+                distinct[(h, r, PRECOMMIT)] = int(a["hr_precommits"][k])
+            distinct_any[(h, r)] = int(a["hr_any"][k])
+        return TallyResult(count, distinct, distinct_any, a["dup"][: len(batch)].copy())
+
+    def tally(self, batch: Batch, verdict: np.ndarray) -> TallyResult:
+        n = len(batch)
+        verdict = np.ascontiguousarray(verdict, dtype=np.uint8)
+        t, a = self._tally_struct(n)
+        cb = batch.c_struct()
+        self._check(self._lib.hd_tally(self._ctx, ctypes.byref(cb), _ptr(verdict), ctypes.byref(t)), "hd_tally")
+        return self._tally_result(batch, t, a)
+
+    def process_batch(self, batch: Batch) -> Tuple[VerifyResult, TallyResult]:
+        n = len(batch)
+        verdict = np.zeros(n, np.uint8)
+        rec = np.zeros((n, 32), np.uint8)
+        bitmap = np.zeros((n + 31) // 32, np.uint32)
+        t, a = self._tally_struct(n)
+        cb = batch.c_struct()
+        self._check(self._lib.hd_process_batch(self._ctx, ctypes.byref(cb), _ptr(verdict), _ptr(rec), _ptr(bitmap),
+                                               ctypes.byref(t)), "hd_process_batch")
+        return VerifyResult(verdict, rec, bitmap), self._tally_result(batch, t, a)
+
+    # ---- synthetic workload ------------------------------------------
+    def gen_keys(self, S: int) -> Tuple[np.ndarray, np.ndarray]:
+        sigs = np.zeros((S, 32), np.uint8)
+        foreign = np.zeros((16, 32), np.uint8)
+        self._check(self._lib.hd_gen_keys(self._ctx, S, _ptr(sigs), _ptr(foreign)), "hd_gen_keys")
+        return sigs, foreign
+
+
+def _as_rows(x, width: int) -> np.ndarray:
+    if isinstance(x, np.ndarray):
+        arr = np.ascontiguousarray(x, dtype=np.uint8).reshape(-1, width)
+    else:
+        x = list(x)
+        for s in x:
+            if len(s) != width:
+                raise ValueError(f"expected {width}-byte entries")
+        arr = np.frombuffer(b"".join(x), np.uint8).reshape(-1, width).copy() if x else np.zeros((0, width), np.uint8)
+    return arr
+
+
+def probe_valu(device: int = 0, op: int = 1, iters: int = 2000) -> float:
+    """Measured lane-ops/s of one VALU instruction class (include/hd_probe.h)."""
+    lib = _lib.load()
+    out = ctypes.c_double()
+    rc = lib.hd_probe_valu(device, op, iters, ctypes.byref(out))
+    if rc != 0:
+        raise HDError(rc, "hd_probe_valu")
+    return out.value

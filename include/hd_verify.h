@@ -1,0 +1,176 @@
+/*
+ * hd_verify.h -- C ABI of the MI355X batch authenticator + tallier for
+ * hyperdrive consensus messages (libhdverify.so).
+ *
+ * Plain C: pointers and sizes only, no HIP/torch types in the signatures, so
+ * that hyperdrive's Go packages can bind it through cgo (INTEGRATION.md shows
+ * the binding).  What each entry point replaces in the reference
+ * (tuanggolt/hyperdrive @ /root/reference):
+ *
+ *   hd_verify_batch     the authentication precondition the reference leaves to
+ *                       its caller before Replica.Propose/Prevote/Precommit
+ *                       (replica/replica.go:153-181; "assumes that the sender
+ *                       has already been authenticated", mq/mq.go:85-101,
+ *                       process/process.go:95-98): per message
+ *                       NewProposeHash / NewPrevoteHash / NewPrecommitHash
+ *                       (process/message.go:53-78, 165-186, 263-284) ->
+ *                       id.Signature.Signatory(&hash) (message_test.go:152) ->
+ *                       Signatory.Equal(From) (message_test.go:154) ->
+ *                       procsAllowed[From] (mq/mq.go:49-51).
+ *   hd_set_signatories  building procsAllowed from the signatory set
+ *                       (replica/replica.go:69-72) and its rebuild on
+ *                       ResetHeight (replica/replica.go:136-144).
+ *   hd_tally            the first-wins vote logs (process/process.go:823-892)
+ *                       and the counting loops of the 2f+1 / f+1 rules
+ *                       (process.go:486-494, 534, 574-582, 626-632, 658,
+ *                       696-702, 751), for every (height, round) of a batch.
+ *
+ * Ownership: all host buffers are caller-owned; the library copies what it
+ * needs and keeps no pointer after a call returns.  Device buffers passed to
+ * the *_device variants are caller-owned device memory (HBM) on the ctx's
+ * device.  Threading: one hd_ctx per caller thread (the reference's Process is
+ * single-goroutine, process.go:100-101); distinct contexts may share a device.
+ * Errors: per-message failures are verdicts, never error returns; a negative
+ * return is an HD_E* code (invalid argument, allocation, device failure).
+ */
+#ifndef HD_VERIFY_H
+#define HD_VERIFY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes ---------------------------------------------------- */
+#define HD_OK 0
+#define HD_EINVAL (-1)   /* bad argument (NULL pointer, size mismatch)       */
+#define HD_ENOMEM (-2)   /* host or device allocation failed                 */
+#define HD_EDEVICE (-3)  /* HIP runtime / kernel failure                     */
+#define HD_ECAP (-4)     /* hd_tally_out capacity too small (n_* hold need)  */
+
+/* ---- message types (process/message.go:11-22) ------------------------ */
+#define HD_TYPE_PROPOSE 1
+#define HD_TYPE_PREVOTE 2
+#define HD_TYPE_PRECOMMIT 3
+
+/* ---- per-message verdicts -------------------------------------------- */
+#define HD_VERDICT_VALID 0              /* recovered signatory == From, From admitted */
+#define HD_VERDICT_BAD_RECID 1          /* V >= 4 (go-ethereum checkSignature)       */
+#define HD_VERDICT_BAD_RS 2             /* r or s == 0 or >= n                         */
+#define HD_VERDICT_NO_POINT 3           /* x = r (+n) not a curve x-coordinate        */
+#define HD_VERDICT_INFINITY 4           /* recovered point at infinity                */
+#define HD_VERDICT_SIGNATORY_MISMATCH 5 /* recovered signatory != From                */
+#define HD_VERDICT_NOT_ADMITTED 6       /* From not in the admitted signatory set     */
+#define HD_VERDICT_BAD_TYPE 7           /* type not Propose/Prevote/Precommit         */
+
+typedef struct hd_ctx hd_ctx;
+
+/* Structure-of-arrays batch.  Strings are raw bytes: value32 = process.Value
+ * ([32]byte), from32 = id.Signatory ([32]byte), sig65 = id.Signature
+ * (R || S || V, [65]byte).  valid_round may be NULL when the batch carries no
+ * Proposes (then -1 = InvalidRound is used). */
+typedef struct {
+    uint32_t n;
+    const uint8_t* type;
+    const int64_t* height;
+    const int64_t* round;
+    const int64_t* valid_round;
+    const uint8_t* value32;
+    const uint8_t* from32;
+    const uint8_t* sig65;
+} hd_batch;
+
+/* ---- context --------------------------------------------------------- */
+int hd_ctx_create(int device, hd_ctx** out);
+int hd_ctx_destroy(hd_ctx* ctx);
+/* 1 (default): signatory = SHA-256(33-byte compressed pubkey);
+ * 0: SHA-256(65-byte uncompressed pubkey).  [renproject/id v0.4.2] */
+int hd_ctx_set_pubkey_format(hd_ctx* ctx, int compressed);
+/* Admitted set = procsAllowed.  sigs32: n x 32 bytes, any order, duplicates
+ * allowed.  Signer indices reported by the library index this array. */
+int hd_set_signatories(hd_ctx* ctx, const uint8_t* sigs32, uint32_t n);
+
+/* ---- verification ------------------------------------------------------
+ * verdict:     n bytes (HD_VERDICT_*), required.
+ * recovered32: n x 32 bytes or NULL: recovered signatory (zeros when the
+ *              recovery itself failed).
+ * valid_bitmap: ceil(n/32) words or NULL: bit i set iff verdict[i] == VALID.
+ * Host pointers; synchronous. */
+int hd_verify_batch(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8_t* recovered32,
+                    uint32_t* valid_bitmap);
+
+/* Same, with every pointer (batch fields and outputs) in device memory of the
+ * ctx's device; signer (n x int32 or NULL) receives the index of From in the
+ * hd_set_signatories array for VALID messages, -1 otherwise.  Enqueued on
+ * `stream` (a hipStream_t, NULL = the ctx's stream); asynchronous. */
+int hd_verify_batch_device(hd_ctx* ctx, const hd_batch* dbatch, uint8_t* d_verdict, uint8_t* d_recovered32,
+                           int32_t* d_signer, uint32_t* d_valid_bitmap, void* stream);
+
+/* ---- tally --------------------------------------------------------------
+ * Input: a batch and its verdicts.  Candidates are VALID Prevotes and
+ * Precommits.  Per (height, round, type, signer) the lowest batch index wins
+ * (first-wins, process.go:834-847); later ones are duplicates: identical
+ * value -> dropped silently, different value -> what the reference hands to
+ * Catcher.CatchDoublePrevote/Precommit (process.go:838-843, 875-880).
+ * All output arrays are caller-owned with the given capacities. */
+typedef struct {
+    /* (height, round, type, value) groups, sorted by (h, r, type, value bytes) */
+    uint32_t cap_counts;
+    uint32_t n_counts;
+    int64_t* count_height;
+    int64_t* count_round;
+    uint8_t* count_type;
+    uint32_t* count_rep;   /* batch index of a message with that value */
+    uint32_t* count_n;     /* number of first-wins votes for the value  */
+    /* (height, round) groups, sorted by (h, r) */
+    uint32_t cap_hr;
+    uint32_t n_hr;
+    int64_t* hr_height;
+    int64_t* hr_round;
+    uint32_t* hr_prevotes;   /* len(PrevoteLogs[r])   */
+    uint32_t* hr_precommits; /* len(PrecommitLogs[r]) */
+    uint32_t* hr_any;        /* distinct vote signers (TraceLogs[r] without proposes) */
+    /* n bytes or NULL: 0 logged, 1 identical duplicate, 2 conflicting
+     * duplicate (double vote), 3 not a candidate */
+    uint8_t* dup;
+} hd_tally_out;
+
+int hd_tally(hd_ctx* ctx, const hd_batch* batch, const uint8_t* verdict, hd_tally_out* out);
+
+/* verify + tally with one upload of the batch */
+int hd_process_batch(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8_t* recovered32,
+                     uint32_t* valid_bitmap, hd_tally_out* tally);
+
+/* ---- synthetic workload (seeded; benchmarks/tests) --------
+ * kind 0: votes (signer = i % S, type = 2 + (i/S)%2, h = 1 + i/(2S), r = 0)
+ * kind 1: rounds (h = 1; per round 1 Propose + S Prevotes + S Precommits)
+ * adv_pct: percentage of messages corrupted by the adversarial classes. */
+int hd_gen_keys(hd_ctx* ctx, uint32_t S, uint8_t* signatories32, uint8_t* foreign32);
+typedef struct {
+    uint8_t* type;
+    int64_t* height;
+    int64_t* round;
+    int64_t* valid_round;
+    uint8_t* value32;
+    uint8_t* from32;
+    uint8_t* sig65;
+    int8_t* adv_class; /* may be NULL */
+} hd_batch_out;
+/* device pointers; messages start .. start+n-1 of the workload. */
+int hd_gen_batch_device(hd_ctx* ctx, uint32_t kind, uint64_t start, uint32_t n, uint32_t S, uint32_t adv_pct,
+                        const uint8_t* d_signatories32, const uint8_t* d_foreign32, const hd_batch_out* d_out,
+                        void* stream);
+
+/* ---- misc ------------------------------------------------------------- */
+const char* hd_strerror(int code);
+/* last HIP error text recorded by the ctx (empty if none) */
+const char* hd_ctx_last_error(hd_ctx* ctx);
+/* ABI version, bumped on any signature change */
+int hd_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HD_VERIFY_H */

@@ -1,0 +1,179 @@
+// Host (g++) build of the device math headers -- TEST HARNESS ONLY.
+// Lets the CPU-only test suite exercise, bit for bit, the arithmetic the
+// gfx950 kernels run (hyperdrive_amd/csrc/*.h), against the oracle.
+#include <string.h>
+#include <vector>
+#include "../../hyperdrive_amd/csrc/hd_gen.h"
+
+using namespace hd;
+
+static ge g_tab[HD_GTAB_N];
+static bool g_init = false;
+static const ge* gtab() {
+    if (!g_init) { build_gtab(g_tab); g_init = true; }
+    return g_tab;
+}
+static void le_in(uint32_t* o, const uint8_t* b) { for (int i = 0; i < 8; i++) o[i] = load_be32(b + 4 * (7 - i)); }
+static void le_out(uint8_t* b, const uint32_t* o) { for (int i = 0; i < 8; i++) store_be32(b + 4 * (7 - i), o[i]); }
+
+extern "C" {
+// all 32-byte operands big-endian
+void hdh_fe_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
+    fe x, y, r;
+    le_in(x.v, a);
+    le_in(y.v, b);
+    int ok = 1;
+    switch (op) {
+        case 0: fe_mul(r, x, y); break;
+        case 1: fe_sqr(r, x); break;
+        case 2: fe_add(r, x, y); break;
+        case 3: fe_sub(r, x, y); break;
+        case 4: fe_neg(r, x); break;
+        case 5: fe_inv(r, x); break;
+        case 6: ok = fe_sqrt(r, x); break;
+        default: fe_clear(r);
+    }
+    le_out(out, r.v);
+    out[32] = (uint8_t)ok;
+}
+void hdh_sc_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
+    sc x, y, r;
+    le_in(x.v, a);
+    le_in(y.v, b);
+    switch (op) {
+        case 0: sc_mul(r, x, y); break;
+        case 1: sc_sqr(r, x); break;
+        case 2: sc_neg(r, x); break;
+        case 3: sc_inv(r, x); break;
+        case 4: { uint32_t w[8]; for (int i = 0; i < 8; i++) w[i] = load_be32(a + 4 * i); sc_from_be_reduce(r, w); break; }
+        default: for (int i = 0; i < 8; i++) r.v[i] = 0;
+    }
+    le_out(out, r.v);
+}
+void hdh_gtab(uint8_t* out /* 128 x 64 */) {
+    const ge* t = gtab();
+    for (int k = 0; k < HD_GTAB_N; k++) { le_out(out + 64 * k, t[k].x.v); le_out(out + 64 * k + 32, t[k].y.v); }
+}
+int hdh_booth(const uint8_t* k32, int w, int j) {
+    sc k;
+    le_in(k.v, k32);
+    return w == 4 ? booth_digit<4>(k, j) : booth_digit<8>(k, j);
+}
+// Q = u1 G + u2 R (R affine given); returns 1 if inf; out = x||y
+int hdh_ecmult(const uint8_t* rx, const uint8_t* ry, const uint8_t* u1b, const uint8_t* u2b, uint8_t* out) {
+    ge R;
+    le_in(R.x.v, rx);
+    le_in(R.y.v, ry);
+    sc u1, u2;
+    le_in(u1.v, u1b);
+    le_in(u2.v, u2b);
+    gej Q;
+    ecmult(Q, R, u1, u2, gtab());
+    if (gej_is_inf(Q)) return 1;
+    fe x, y;
+    gej_to_ge(x, y, Q);
+    le_out(out, x.v);
+    le_out(out + 32, y.v);
+    return 0;
+}
+int hdh_recover(const uint8_t* digest, const uint8_t* sig, uint8_t* pub64) {
+    uint32_t d[8], rb[8], sb[8];
+    for (int i = 0; i < 8; i++) { d[i] = load_be32(digest + 4 * i); rb[i] = load_be32(sig + 4 * i); sb[i] = load_be32(sig + 32 + 4 * i); }
+    fe qx, qy;
+    int v = recover(qx, qy, d, rb, sb, sig[64], gtab());
+    if (v == V_VALID) { le_out(pub64, qx.v); le_out(pub64 + 32, qy.v); }
+    return v;
+}
+void hdh_sign(const uint8_t* sk32, const uint8_t* digest, uint8_t* sig65) {
+    sc sk;
+    le_in(sk.v, sk32);
+    uint32_t d[8], rb[8], sb[8], rid;
+    for (int i = 0; i < 8; i++) d[i] = load_be32(digest + 4 * i);
+    ecdsa_sign(rb, sb, rid, sk, d, gtab());
+    for (int i = 0; i < 8; i++) { store_be32(sig65 + 4 * i, rb[i]); store_be32(sig65 + 32 + 4 * i, sb[i]); }
+    sig65[64] = (uint8_t)rid;
+}
+void hdh_signer_sk(uint32_t idx, uint8_t* out) {
+    sc sk;
+    signer_sk(sk, idx);
+    le_out(out, sk.v);
+}
+void hdh_keys(uint32_t S, int compressed, uint8_t* sigs32, uint8_t* foreign32) {
+    for (uint32_t j = 0; j < S + HD_NONADMITTED_KEYS; j++) {
+        uint32_t idx = j < S ? j : HD_NONADMITTED_BASE + (j - S);
+        sc sk;
+        signer_sk(sk, idx);
+        uint32_t o[8];
+        pubkey_signatory(o, sk, compressed != 0, gtab());
+        uint8_t* dst = j < S ? sigs32 + 32 * j : foreign32 + 32 * (j - S);
+        for (int i = 0; i < 8; i++) store_be32(dst + 4 * i, o[i]);
+    }
+}
+static std::vector<uint32_t> words_of(const uint8_t* b, uint32_t n) {
+    std::vector<uint32_t> w(8 * (size_t)n);
+    for (size_t i = 0; i < 8 * (size_t)n; i++) w[i] = load_be32(b + 4 * i);
+    return w;
+}
+int hdh_gen(uint32_t kind, uint64_t start, uint32_t n, uint32_t S, uint32_t adv_pct, const uint8_t* sigs32,
+            const uint8_t* foreign32, uint8_t* type, int64_t* h, int64_t* r, int64_t* vr, uint8_t* value32,
+            uint8_t* from32, uint8_t* sig65, int8_t* cls) {
+    std::vector<uint32_t> sw = words_of(sigs32, S), fw = words_of(foreign32, HD_NONADMITTED_KEYS);
+    for (uint32_t k = 0; k < n; k++) {
+        cls[k] = (int8_t)gen_message(kind, start + k, S, adv_pct, gtab(), sw.data(), fw.data(), type[k], h[k], r[k],
+                                     vr[k], value32 + 32 * (size_t)k, from32 + 32 * (size_t)k, sig65 + 65 * (size_t)k);
+    }
+    return 0;
+}
+// host run of verify_msg over a batch (admitted must be sorted ascending)
+int hdh_verify(uint32_t n, const uint8_t* type, const int64_t* h, const int64_t* r, const int64_t* vr,
+               const uint8_t* value32, const uint8_t* from32, const uint8_t* sig65, const uint8_t* adm32,
+               uint32_t n_adm, int compressed, uint8_t* verdict, uint8_t* rec32, int32_t* signer) {
+    std::vector<uint32_t> aw = words_of(adm32, n_adm);
+    int steps = 0;
+    while ((1u << steps) < n_adm) steps++;
+    for (uint32_t i = 0; i < n; i++) {
+        MsgIn m;
+        m.type = type[i];
+        m.h = h[i];
+        m.r = r[i];
+        m.vr = vr ? vr[i] : -1;
+        for (int w = 0; w < 8; w++) {
+            m.value_be[w] = load_be32(value32 + 32 * (size_t)i + 4 * w);
+            m.from_be[w] = load_be32(from32 + 32 * (size_t)i + 4 * w);
+            m.r_be[w] = load_be32(sig65 + 65 * (size_t)i + 4 * w);
+            m.s_be[w] = load_be32(sig65 + 65 * (size_t)i + 32 + 4 * w);
+        }
+        m.v = sig65[65 * (size_t)i + 64];
+        uint32_t rec[8];
+        int32_t s;
+        verdict[i] = verify_msg(m, gtab(), aw.data(), n_adm, steps, compressed != 0, rec, s);
+        signer[i] = s;
+        for (int w = 0; w < 8; w++) store_be32(rec32 + 32 * (size_t)i + 4 * w, rec[w]);
+    }
+    return 0;
+}
+}
+extern "C" int hdh_ecmult_trace(const uint8_t* rx, const uint8_t* ry, const uint8_t* u1b, const uint8_t* u2b, uint8_t* out, uint8_t* infs) {
+    ge R; le_in(R.x.v, rx); le_in(R.y.v, ry);
+    sc u1, u2; le_in(u1.v, u1b); le_in(u2.v, u2b);
+    const ge* gt = gtab();
+    gej rt[HD_RTAB_N];
+    gej_set_ge(rt[0], R);
+    gej_dbl(rt[1], rt[0]);
+    for (int k = 2; k < HD_RTAB_N; k++) gej_add_ge(rt[k], rt[k - 1], R);
+    gej acc; gej_set_inf(acc);
+    for (int j = HD_NWIN_R - 1; j >= 0; j--) {
+        if (j != HD_NWIN_R - 1) for (int k = 0; k < HD_WR; k++) gej_dbl(acc, acc);
+        if ((j & 1) == 0) {
+            int d = booth_digit<HD_WG>(u1, j >> 1); int ad = d < 0 ? -d : d;
+            ge t = gt[ad == 0 ? 0 : ad - 1]; if (d < 0) fe_neg(t.y, t.y);
+            gej s; gej_add_ge(s, acc, t); gej_cmov(acc, s, d != 0);
+        }
+        { int d = booth_digit<HD_WR>(u2, j); int ad = d < 0 ? -d : d;
+          gej t = rt[ad == 0 ? 0 : ad - 1]; if (d < 0) fe_neg(t.y, t.y);
+          gej s; gej_add(s, acc, t); gej_cmov(acc, s, d != 0); }
+        infs[j] = gej_is_inf(acc);
+        if (!infs[j]) { fe x, y; gej_to_ge(x, y, acc); le_out(out + 64 * j, x.v); le_out(out + 64 * j + 32, y.v); }
+    }
+    return 0;
+}

@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Benchmark: verified consensus msgs/s (secp256k1) on MI355X.
+
+Workload (BASELINE.json configs[1]): batch-verify 1,048,576 synthetic
+Prevote/Precommit messages from 100 signatories per GPU (SURVEY §8(d) C2:
+signer = i % 100, type = 2 + (i/100)%2, h = 1 + i/200, r = 0; 90 % canonical
+value, 5 % nil, 5 % random), seeded, signed with RFC6979 on the GPU before the
+timed region.  One step = the hot path over one batch: k_verify (digest ->
+recover -> signatory -> Equal(From) -> admitted) over this rank's shard, the
+valid-bitmap all-gather over RCCL (N > 1), and the first-wins 2f+1 tally of
+the whole batch.  Inputs are resident in HBM when timing starts.
+
+Multi-GPU: one process per GPU (torch.distributed.run), weak scaling: rank k
+verifies messages [k*B, (k+1)*B) of the N*B-message stream (C4 generator);
+the batch metadata is replicated, only the verdict bitmaps cross xGMI.
+
+Prints ONE JSON line on rank 0.  The CPU baseline is the C restatement of the
+same path (oracle/hd_oracle.c) on the host's cores over a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+W_OPS_PER_MSG = 6.06e5          # algorithmic int32 ops per Prevote/Precommit
+BYTES_PER_MSG = 146 + 33        # HBM in + out per message
+# INT32 VALU peak of one MI355X: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (the
+# FP32-vector issue rate of MI355X_MICROARCH.md, 157.3 TFLOPS / 2 per FMA)
+VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1 << 20, help="messages per GPU")
+    ap.add_argument("--signers", type=int, default=100)
+    ap.add_argument("--adv", type=int, default=0, help="adversarial percentage (C5)")
+    ap.add_argument("--cpu-sample", type=int, default=131072)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-tally", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, S):
+    """C restatement of the reference path on the host cores (bounded sample)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    from oracle_c import COracle
+    co = COracle(os.path.join(ROOT, "oracle", "_build", "liboracle.so"))
+    return co
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist = None
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    import hyperdrive_amd as hd
+    from hyperdrive_amd import _lib
+    from hyperdrive_amd.device import DeviceBatch, generate
+    from hyperdrive_amd._lib import HdBatch
+
+    B, S = args.batch, args.signers
+    total = B * world
+    v = hd.Verifier(dev.index)
+    sigs, foreign = v.gen_keys(S)
+    v.set_signatories(sigs)
+    t0 = time.time()
+    # replicated batch metadata (whole stream), generated on this GPU
+    db, _, _ = generate(v, 0, total, S, args.adv, keys=(sigs, foreign), device=str(dev))
+    gen_s = time.time() - t0
+
+    from hyperdrive_amd.device import work_stream
+    ws = work_stream(dev)
+    torch.cuda.set_stream(ws)          # torch ops (RCCL all-gather included) share the library's stream
+    stream = ws.cuda_stream
+    lo = rank * B
+    # shard views (device pointers offset into the replicated batch)
+    shard = HdBatch(B, db.type.data_ptr() + lo, db.height.data_ptr() + 8 * lo, db.round.data_ptr() + 8 * lo,
+                    db.valid_round.data_ptr() + 8 * lo, db.value.data_ptr() + 32 * lo, db.frm.data_ptr() + 32 * lo,
+                    db.sig.data_ptr() + 65 * lo)
+    full = db.c_struct()
+    assert B % 32 == 0
+    verdict = torch.empty(B, dtype=torch.uint8, device=dev)
+    bitmap = torch.zeros(B // 32, dtype=torch.int32, device=dev)
+    bitmap_all = torch.zeros(total // 32, dtype=torch.int32, device=dev)
+    lib = _lib.load()
+    t_out, t_arr = v._tally_struct(total)
+
+    ev_k0 = torch.cuda.Event(enable_timing=True)
+    ev_k1 = torch.cuda.Event(enable_timing=True)
+    kernel_ms = []
+    tally_info = {}
+
+    def step(record=False):
+        if record:
+            ev_k0.record()
+        v.verify_batch_device(shard, verdict.data_ptr(), None, None, bitmap.data_ptr(), stream)
+        if record:
+            ev_k1.record()
+        if dist is not None:
+            dist.all_gather_into_tensor(bitmap_all, bitmap)
+            gathered = bitmap_all
+        else:
+            gathered = bitmap
+        if not args.no_tally:
+            rc = lib.hd_tally_device_bitmap(v.handle, ctypes.byref(full), gathered.data_ptr(), ctypes.byref(t_out),
+                                            stream)
+            if rc != 0:
+                raise _lib.HDError(rc, "hd_tally_device_bitmap", lib.hd_ctx_last_error(v.handle).decode())
+            tally_info["n_hr"] = t_out.n_hr
+            tally_info["n_counts"] = t_out.n_counts
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step(record=True)
+        ev_k1.synchronize()
+        kernel_ms.append(ev_k0.elapsed_time(ev_k1))
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t_start
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # sanity: verdict histogram of this shard (all VALID without --adv)
+    hist = torch.bincount(verdict.long(), minlength=8).cpu().tolist()
+
+    if rank == 0:
+        ms_step = elapsed / args.steps * 1e3
+        value = total * args.steps / elapsed
+        k_ms = sum(kernel_ms) / len(kernel_ms)
+        achieved = B * W_OPS_PER_MSG / (k_ms * 1e-3)
+        out = {
+            "metric": "verified consensus msgs/sec (secp256k1) at 1/2/4/8 MI355X; % INT32 VALU peak",
+            "value": value,
+            "unit": "msgs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 (256-bit modular integer arithmetic)",
+            "data": "synthetic (seeded RFC6979-signed votes generated on the GPU)",
+            "config": {"workload": "C2: batch-verify 1M Prevote/Precommit from 100 signatories + 2f+1 tally",
+                       "messages_per_gpu": B, "global_batch": total, "signatories": S, "adversarial_pct": args.adv,
+                       "parallelism": f"shard-by-index x{world}, RCCL all-gather of valid bitmaps"},
+            "roofline": {
+                "bound": "valu",
+                "kernel": "k_verify",
+                "achieved": achieved / 1e12,
+                "peak": VALU_PEAK_OPS / 1e12,
+                "unit": "TOP/s (int32 lane-ops)",
+                "frac": achieved / VALU_PEAK_OPS,
+                "traffic": None,
+                "kernel_ms": k_ms,
+                "algorithmic_ops_per_msg": W_OPS_PER_MSG,
+                "hbm_algorithmic_GBs": B * BYTES_PER_MSG / (k_ms * 1e-3) / 1e9,
+            },
+            "verdicts": hist,
+            "tally": tally_info,
+            "gen_s": gen_s,
+        }
+        if not args.no_cpu:
+            try:
+                out["cpu_baseline"] = run_cpu_baseline(args, db, sigs)
+            except Exception as e:  # reported, never fatal for the GPU number
+                out["cpu_baseline"] = {"error": repr(e)}
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run_cpu_baseline(args, db, sigs):
+    """Time the C restatement (oracle/hd_oracle.c, kind 'port') on host threads
+    over the first --cpu-sample messages of the same workload."""
+    import numpy as np
+    co = cpu_baseline(args, None)
+    n = min(args.cpu_sample, db.n)
+    host = db.to_host()
+    from hyperdrive_amd.verify import Batch
+    sample = Batch(host.type[:n].copy(), host.height[:n].copy(), host.round[:n].copy(), host.valid_round[:n].copy(),
+                   host.value[:n].copy(), host.frm[:n].copy(), host.sig[:n].copy())
+    threads = args.cpu_threads
+    t = time.perf_counter()
+    verdict, _ = co.verify(sample, sigs, True, threads=threads)
+    dt = time.perf_counter() - t
+    return {"value": n / dt, "unit": "msgs/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} messages of the same C2 workload, verify path (digest+recover+signatory+"
+                      f"membership) of oracle/hd_oracle.c on {threads} host threads",
+            "wall_s": dt, "valid": int((verdict == 0).sum())}
+
+
+if __name__ == "__main__":
+    main()

@@ -82,6 +82,10 @@ SIGNATURES = {
                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "hd_tally": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                 ctypes.POINTER(HdTallyOut)]),
+    "hd_tally_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.POINTER(HdTallyOut), ctypes.c_void_p]),
+    "hd_tally_device_bitmap": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
+                                              ctypes.POINTER(HdTallyOut), ctypes.c_void_p]),
     "hd_process_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(HdTallyOut)]),
     "hd_gen_keys": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),

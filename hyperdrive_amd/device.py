@@ -21,6 +21,22 @@ def _torch():
     return torch
 
 
+_STREAMS = {}
+
+
+def work_stream(device=None):
+    """A dedicated (non-default) torch stream per device for library launches.
+
+    The C ABI reads a NULL stream as "the context's own stream", and torch's
+    default stream has handle 0, so device work is always enqueued on an
+    explicit stream whose handle is non-zero."""
+    torch = _torch()
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else torch.device(device).index or 0)
+    if dev not in _STREAMS:
+        _STREAMS[dev] = torch.cuda.Stream(device=dev)
+    return _STREAMS[dev]
+
+
 @dataclass
 class DeviceBatch:
     n: int
@@ -75,11 +91,11 @@ def generate(v: Verifier, kind: int, n: int, S: int, adv_pct: int = 0, start: in
     db = DeviceBatch.empty(n, device)
     out = db.c_out()
     lib = _lib.load()
-    if stream is None:
-        stream = torch.cuda.current_stream().cuda_stream
+    ws = work_stream(device)
+    ws.wait_stream(torch.cuda.current_stream(ws.device))
     rc = lib.hd_gen_batch_device(v.handle, kind, start, n, S, adv_pct, d_sigs.data_ptr(), d_for.data_ptr(),
-                                 ctypes.byref(out), stream)
+                                 ctypes.byref(out), stream if stream else ws.cuda_stream)
     if rc != 0:
         raise _lib.HDError(rc, "hd_gen_batch_device", lib.hd_ctx_last_error(v.handle).decode())
-    torch.cuda.current_stream().synchronize()
+    ws.synchronize()
     return db, sigs, foreign

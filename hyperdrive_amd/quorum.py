@@ -1,0 +1,59 @@
+"""Host-side quorum predicates over a batch tally.
+
+The GPU tally (hd_tally) produces, per (height, round), the sizes of the
+first-wins vote logs and the per-value counts; these functions apply the exact
+comparisons of the reference's rules to them.  The automaton's step / once-flag
+gating (process.go's ``CurrentStep`` checks and ``OnceFlag``) is sequential
+control flow and stays with the caller.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional, Tuple
+
+PREVOTE, PRECOMMIT = 2, 3
+INVALID_ROUND = -1
+NIL_VALUE = bytes(32)
+
+
+def thresholds(n_signatories: int) -> Tuple[int, int, int]:
+    """f = len(signatories) / 3 (integer division, replica/replica.go:54, 138);
+    returns (f, 2f+1, f+1)."""
+    f = n_signatories // 3
+    return f, 2 * f + 1, f + 1
+
+
+def decide(tally, height: int, round_: int, f: int, propose_value: Optional[bytes] = None,
+           propose_valid: bool = False, propose_valid_round: int = INVALID_ROUND,
+           propose_signer_new: bool = False) -> Dict[str, bool]:
+    """Predicates for one (height, round) given a tally with ``count``,
+    ``distinct`` and ``distinct_any`` maps.
+
+    - timeout_prevote   L34 ``len(PrevoteLogs[r]) >= 2f+1``         process.go:534
+    - precommit_nil     L44 #prevotes for NilValue >= 2f+1          process.go:626-632
+    - timeout_precommit_reached  L47 ``len(PrecommitLogs[r]) == 2f+1`` is evaluated
+      by the automaton at the crossing; the batch reports whether the log
+      reached 2f+1                                                  process.go:658
+    - skip              L55 |TraceLogs[r]| >= f+1 (votes + valid propose signer) process.go:751
+    - precommit_value   L36 #prevotes for propose.Value >= 2f+1     process.go:574-582
+    - commit            L49 #precommits for propose.Value >= 2f+1   process.go:696-702
+    - prevote_validround L28 #prevotes in validRound for propose.Value >= 2f+1  process.go:486-494
+    """
+    q = 2 * f + 1
+    count = tally.count
+    pv = lambda v: count.get((height, round_, PREVOTE, v), 0)
+    pc = lambda v: count.get((height, round_, PRECOMMIT, v), 0)
+    out = {
+        "timeout_prevote": tally.distinct.get((height, round_, PREVOTE), 0) >= q,
+        "precommit_nil": pv(NIL_VALUE) >= q,
+        "timeout_precommit_reached": tally.distinct.get((height, round_, PRECOMMIT), 0) >= q,
+        "skip": tally.distinct_any.get((height, round_), 0) + (1 if propose_signer_new else 0) >= f + 1,
+        "precommit_value": False,
+        "commit": False,
+        "prevote_validround": False,
+    }
+    if propose_value is not None and propose_valid:
+        out["precommit_value"] = pv(propose_value) >= q
+        out["commit"] = pc(propose_value) >= q
+    if propose_value is not None and propose_valid_round > INVALID_ROUND:
+        out["prevote_validround"] = count.get((height, propose_valid_round, PREVOTE, propose_value), 0) >= q
+    return out

@@ -139,6 +139,19 @@ typedef struct {
 
 int hd_tally(hd_ctx* ctx, const hd_batch* batch, const uint8_t* verdict, hd_tally_out* out);
 
+/* Same on device-resident inputs (pointers as in hd_verify_batch_device);
+ * d_signer: the signer indices hd_verify_batch_device produced, or NULL (then
+ * From is looked up again).  Results land in the host arrays of `out`;
+ * synchronises `stream`. */
+int hd_tally_device(hd_ctx* ctx, const hd_batch* dbatch, const uint8_t* d_verdict, const int32_t* d_signer,
+                    hd_tally_out* out, void* stream);
+
+/* Same, with validity given as the valid bitmap of hd_verify_batch_device
+ * (e.g. after an all-gather of per-GPU bitmaps over RCCL); signer indices are
+ * looked up from From. */
+int hd_tally_device_bitmap(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* d_valid_bitmap, hd_tally_out* out,
+                           void* stream);
+
 /* verify + tally with one upload of the batch */
 int hd_process_batch(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8_t* recovered32,
                      uint32_t* valid_bitmap, hd_tally_out* tally);

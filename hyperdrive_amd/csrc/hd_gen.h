@@ -85,6 +85,7 @@ HD void ecmult_gen(gej& out, const sc& k, GTab gtab) {
     out = acc;
 }
 
+// affine, canonical
 HD void gej_to_ge(fe& x, fe& y, const gej& a) {
     fe zi, zi2;
     fe_inv(zi, a.z);
@@ -92,6 +93,8 @@ HD void gej_to_ge(fe& x, fe& y, const gej& a) {
     fe_mul(x, a.x, zi2);
     fe_mul(zi2, zi2, zi);
     fe_mul(y, a.y, zi2);
+    fe_normalize(x);
+    fe_normalize(y);
 }
 
 template <typename GTab>
@@ -103,7 +106,7 @@ HD void pubkey_signatory(uint32_t out_be[8], const sc& sk, bool compressed, GTab
     uint32_t xb[8];
     fe_to_be(xb, x);
     if (compressed) {
-        sha256_pub33(out_be, 2u | (y.v[0] & 1u), xb);
+        sha256_pub33(out_be, 2u | (y.n[0] & 1u), xb);
     } else {
         uint32_t yb[8];
         fe_to_be(yb, y);
@@ -149,9 +152,9 @@ HD void ecdsa_sign(uint32_t r_be[8], uint32_t s_be[8], uint32_t& recid, const sc
         ecmult_gen(Rj, k, gtab);
         fe rx, ry;
         gej_to_ge(rx, ry, Rj);
-        uint32_t rid = ry.v[0] & 1u;
+        uint32_t rid = ry.n[0] & 1u;
         uint32_t xm[8];
-        for (int i = 0; i < 8; i++) xm[i] = rx.v[i];
+        fe_to_le(xm, rx);
         if (sc_ge_n(xm)) { sc_sub_n(xm); rid |= 2u; }
         sc r;
         for (int i = 0; i < 8; i++) r.v[i] = xm[i];
@@ -331,23 +334,23 @@ HD int gen_message(uint32_t kind, uint64_t i, uint32_t S, uint32_t adv_pct, GTab
         for (int j = 2; j < 8; j++) { c += o[j]; o[j] = (uint32_t)c; c >>= 32; }
         for (int j = 0; j < 8; j++) store_be32(sig + 4 * j, o[7 - j]);
     } else if (cls == 5) {
-        fe x;
-        fe_clear(x);
-        x.v[0] = (uint32_t)w;
-        x.v[1] = (uint32_t)(w >> 32);
+        // smallest x >= w (as a 65-bit integer) with x^3 + 7 a non-residue
+        uint32_t xw[8] = {(uint32_t)w, (uint32_t)(w >> 32), 0u, 0u, 0u, 0u, 0u, 0u};
         for (;;) {
-            fe y2, y, seven;
+            fe x, y2, y, seven;
+            fe_from_le(x, xw);
             fe_sqr(y2, x);
             fe_mul(y2, y2, x);
             fe_set_u32(seven, 7);
             fe_add(y2, y2, seven);
             if (!fe_sqrt(y, y2)) break;
-            // x += 1 (x stays < 2^65)
-            uint64_t c = (uint64_t)x.v[0] + 1;
-            x.v[0] = (uint32_t)c;
-            x.v[1] += (uint32_t)(c >> 32);
+            uint64_t c = (uint64_t)xw[0] + 1;
+            xw[0] = (uint32_t)c;
+            c = (uint64_t)xw[1] + (c >> 32);
+            xw[1] = (uint32_t)c;
+            xw[2] += (uint32_t)(c >> 32);
         }
-        for (int j = 0; j < 8; j++) store_be32(sig + 4 * j, x.v[7 - j]);
+        for (int j = 0; j < 8; j++) store_be32(sig + 4 * j, xw[7 - j]);
         sig[64] &= 1;
     } else if (cls == 8) {
         if (m.type == T_PREVOTE || m.type == T_PRECOMMIT) m.type = (m.type == T_PREVOTE) ? T_PRECOMMIT : T_PREVOTE;
@@ -374,9 +377,11 @@ HD int gen_message(uint32_t kind, uint64_t i, uint32_t S, uint32_t adv_pct, GTab
         sc_from_be_reduce(mm, d);
         sc_inv(kinv, k);
         sc_mul(s, mm, kinv);
-        if (!sc_ge_n(rx.v) && !sc_is_zero(s)) {
-            for (int j = 0; j < 8; j++) { store_be32(sig + 4 * j, rx.v[7 - j]); store_be32(sig + 32 + 4 * j, s.v[7 - j]); }
-            sig[64] = (uint8_t)(ry.v[0] & 1u);
+        uint32_t rxw[8];
+        fe_to_le(rxw, rx);
+        if (!sc_ge_n(rxw) && !sc_is_zero(s)) {
+            for (int j = 0; j < 8; j++) { store_be32(sig + 4 * j, rxw[7 - j]); store_be32(sig + 32 + 4 * j, s.v[7 - j]); }
+            sig[64] = (uint8_t)(ry.n[0] & 1u);
         }
     }
     type_out = (uint8_t)m.type;

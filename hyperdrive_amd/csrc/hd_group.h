@@ -11,8 +11,7 @@
 // doublings/additions; a zero digit is a per-lane select, and the exceptional
 // cases of the addition law (P = inf, P = +-T) are rare branches.
 //
-// Jacobian infinity is Z == 0 (all values are fully reduced, so the test is
-// exact).
+// Jacobian infinity is Z == 0 (mod p), tested on the normalised value.
 #pragma once
 #include "hd_field.h"
 
@@ -30,53 +29,54 @@ HD void gej_cmov(gej& r, const gej& a, bool flag) {
     fe_cmov(r.z, a.z, flag);
 }
 
-// dbl-2009-l (a = 0): 2M + 5S.  inf -> inf (Z3 = 2 Y Z = 0).
+// Bounds (hd_field.h): point inputs have x, y tight (T) and z <= 2T; y of a
+// table entry may be a fresh negation 4p - y (<= 2^28, fine as a multiplier
+// but normalised before it is ever a subtrahend).  Outputs: x, y T, z 2T.
+
+// Doubling (a = 0), 3M + 4S: D = 4 X Y^2 computed as a product.
+// inf -> inf (Z3 = 2 Y Z = 0).  r may alias a.
 HD void gej_dbl(gej& r, const gej& a) {
-    fe A, B, C, D, E, F, t;
-    fe_sqr(A, a.x);
-    fe_sqr(B, a.y);
-    fe_sqr(C, B);
-    fe_add(t, a.x, B);
-    fe_sqr(t, t);
-    fe_sub(t, t, A);
-    fe_sub(t, t, C);
-    fe_add(D, t, t);
-    fe_add(E, A, A);
-    fe_add(E, E, A);
-    fe_sqr(F, E);
-    fe z3;
-    fe_mul(z3, a.y, a.z);
-    fe_add(r.z, z3, z3);
-    fe_add(t, D, D);
-    fe_sub(r.x, F, t);
-    fe_sub(t, D, r.x);
-    fe_mul(t, E, t);
-    fe_add(C, C, C);
-    fe_add(C, C, C);
-    fe_add(C, C, C);
-    fe_sub(r.y, t, C);
+    fe A, B, C, XB, E, F, t, u;
+    fe_sqr(A, a.x);            // T
+    fe_sqr(B, a.y);            // T
+    fe_sqr(C, B);              // T
+    fe_mul(XB, a.x, B);        // T
+    fe_mul(u, a.y, a.z);       // T
+    fe_mul_int(E, A, 3);       // 3T
+    fe_sqr(F, E);              // T
+    fe_mul_int(t, XB, 8);      // 8T <= 32p
+    fe_sub_k<32>(r.x, F, t);   // < 2^32
+    fe_norm_weak(r.x);         // X3 = E^2 - 8 X Y^2          (T)
+    fe_mul_int(t, XB, 4);      // 4T
+    fe_sub_k<4>(t, t, r.x);    // < 2^29.2
+    fe_mul(t, E, t);           // T
+    fe_mul_int(C, C, 8);       // 8T
+    fe_sub_k<32>(r.y, t, C);
+    fe_norm_weak(r.y);         // Y3 = E (4 X Y^2 - X3) - 8 Y^4 (T)
+    fe_add(r.z, u, u);         // Z3 = 2 Y Z                 (2T)
 }
 
 HD_NOINLINE void gej_dbl_slow(gej& r, const gej& a) { gej_dbl(r, a); }
 
-// r = a + b, b affine and finite (madd-2007-bl: 7M + 4S).  Handles a = inf
-// and a = +-b.
+// r = a + b, b affine and finite (madd-2007-bl shape, 8M + 3S with
+// Z3 = 2 Z1 H).  Handles a = inf and a = +-b.
 HD void gej_add_ge(gej& r, const gej& a, const ge& b) {
-    fe z1z1, u2, s2, h, hh, i4, j, rr, v, t;
-    fe_sqr(z1z1, a.z);
-    fe_mul(u2, b.x, z1z1);
-    fe_mul(s2, b.y, a.z);
-    fe_mul(s2, s2, z1z1);
-    fe_sub(h, u2, a.x);
-    fe_sub(rr, s2, a.y);
-    bool ainf = fe_is_zero(a.z);
-    bool hzero = fe_is_zero(h);
+    fe z1z1, u2, s2, h, R, t, hh, i4, j, v;
+    fe_sqr(z1z1, a.z);         // T
+    fe_mul(u2, b.x, z1z1);     // T
+    fe_mul(s2, b.y, a.z);      // T
+    fe_mul(s2, s2, z1z1);      // T
+    fe_sub(h, u2, a.x);        // H = U2 - X1   (< 2^28.4)
+    fe_sub(R, s2, a.y);        // r = S2 - Y1
+    const bool ainf = fe_is_zero(a.z);
+    const bool hzero = fe_is_zero(h);
     if (hzero && !ainf) {
         // a == +-b (rare): double or cancel
         gej o;
-        if (fe_is_zero(rr)) {
+        if (fe_is_zero(R)) {
             gej bj;
             gej_set_ge(bj, b);
+            fe_norm_weak(bj.y);
             gej_dbl_slow(o, bj);
         } else {
             gej_set_inf(o);
@@ -84,34 +84,36 @@ HD void gej_add_ge(gej& r, const gej& a, const ge& b) {
         r = o;
         return;
     }
-    fe_add(rr, rr, rr);
-    fe_sqr(hh, h);
-    fe_add(i4, hh, hh);
-    fe_add(i4, i4, i4);
-    fe_mul(j, h, i4);
-    fe_mul(v, a.x, i4);
+    fe_add(R, R, R);           // 2r            (< 2^29.4)
+    fe_sqr(hh, h);             // T
+    fe_mul_int(i4, hh, 4);     // I = 4 H^2     (4T)
+    fe_mul(j, h, i4);          // J = H I       (T)
+    fe_mul(v, a.x, i4);        // V = X1 I      (T)
     gej o;
-    fe_sqr(o.x, rr);
-    fe_sub(o.x, o.x, j);
-    fe_sub(o.x, o.x, v);
-    fe_sub(o.x, o.x, v);
+    fe_sqr(o.x, R);            // T
+    fe_add(t, v, v);
+    fe_add(t, t, j);           // 2V + J        (3T <= 8p)
+    fe_sub_k<8>(o.x, o.x, t);
+    fe_norm_weak(o.x);         // X3            (T)
     fe_sub(t, v, o.x);
-    fe_mul(t, rr, t);
+    fe_mul(t, R, t);           // r (V - X3)    (T)
     fe_mul(j, a.y, j);
-    fe_add(j, j, j);
+    fe_add(j, j, j);           // 2 Y1 J        (2T <= 4p)
     fe_sub(o.y, t, j);
-    fe_add(t, a.z, h);
-    fe_sqr(t, t);
-    fe_sub(t, t, z1z1);
-    fe_sub(o.z, t, hh);
-    if (ainf) gej_set_ge(o, b);
+    fe_norm_weak(o.y);         // Y3            (T)
+    fe_mul(o.z, a.z, h);
+    fe_add(o.z, o.z, o.z);     // Z3 = 2 Z1 H   (2T)
+    if (ainf) {
+        gej_set_ge(o, b);
+        fe_norm_weak(o.y);
+    }
     r = o;
 }
 
-// r = a + b, both Jacobian, b finite (add-2007-bl: 11M + 5S).  Handles
-// a = inf and a = +-b.
+// r = a + b, both Jacobian, b finite (add-2007-bl shape, 12M + 4S with
+// Z3 = 2 Z1 Z2 H).  Handles a = inf and a = +-b.
 HD void gej_add(gej& r, const gej& a, const gej& b) {
-    fe z1z1, z2z2, u1, u2, s1, s2, h, rr, t;
+    fe z1z1, z2z2, u1, u2, s1, s2, h, R, t;
     fe_sqr(z1z1, a.z);
     fe_sqr(z2z2, b.z);
     fe_mul(u1, a.x, z2z2);
@@ -120,39 +122,42 @@ HD void gej_add(gej& r, const gej& a, const gej& b) {
     fe_mul(s1, s1, z2z2);
     fe_mul(s2, b.y, a.z);
     fe_mul(s2, s2, z1z1);
-    fe_sub(h, u2, u1);
-    fe_sub(rr, s2, s1);
-    bool ainf = fe_is_zero(a.z);
-    bool hzero = fe_is_zero(h);
+    fe_sub(h, u2, u1);         // H
+    fe_sub(R, s2, s1);         // r
+    const bool ainf = fe_is_zero(a.z);
+    const bool hzero = fe_is_zero(h);
     if (hzero && !ainf) {
         gej o;
-        if (fe_is_zero(rr)) gej_dbl_slow(o, a);
+        if (fe_is_zero(R)) gej_dbl_slow(o, a);
         else gej_set_inf(o);
         r = o;
         return;
     }
     fe i, j, v;
     fe_add(i, h, h);
-    fe_sqr(i, i);
-    fe_mul(j, h, i);
-    fe_add(rr, rr, rr);
-    fe_mul(v, u1, i);
+    fe_sqr(i, i);              // I = (2H)^2    (T)
+    fe_mul(j, h, i);           // J = H I       (T)
+    fe_add(R, R, R);           // 2r
+    fe_mul(v, u1, i);          // V = U1 I      (T)
     gej o;
-    fe_sqr(o.x, rr);
-    fe_sub(o.x, o.x, j);
-    fe_sub(o.x, o.x, v);
-    fe_sub(o.x, o.x, v);
+    fe_sqr(o.x, R);
+    fe_add(t, v, v);
+    fe_add(t, t, j);
+    fe_sub_k<8>(o.x, o.x, t);
+    fe_norm_weak(o.x);         // X3 = r^2 - J - 2V
     fe_sub(t, v, o.x);
-    fe_mul(t, rr, t);
+    fe_mul(t, R, t);
     fe_mul(s1, s1, j);
     fe_add(s1, s1, s1);
     fe_sub(o.y, t, s1);
-    fe_add(t, a.z, b.z);
-    fe_sqr(t, t);
-    fe_sub(t, t, z1z1);
-    fe_sub(t, t, z2z2);
-    fe_mul(o.z, t, h);
-    if (ainf) o = b;
+    fe_norm_weak(o.y);         // Y3 = r (V - X3) - 2 S1 J
+    fe_mul(t, a.z, b.z);
+    fe_mul(t, t, h);
+    fe_add(o.z, t, t);         // Z3 = 2 Z1 Z2 H
+    if (ainf) {
+        o = b;
+        fe_norm_weak(o.y);
+    }
     r = o;
 }
 
@@ -246,6 +251,8 @@ HD void build_gtab(ge* tab) {
         fe_mul(zi3, zi2, zi);
         fe_mul(tab[k].x, acc.x, zi2);
         fe_mul(tab[k].y, acc.y, zi3);
+        fe_normalize(tab[k].x);
+        fe_normalize(tab[k].y);
     }
 }
 
@@ -255,7 +262,7 @@ HD void build_gtab(ge* tab) {
 //   (parse_compact overflow); r or s == 0 -> BAD_RS (sig_recover);
 //   V&2 and r >= p - n -> NO_POINT; x^3+7 non-residue -> NO_POINT;
 //   Q = inf -> INFINITY.  High-S accepted.  m = digest mod n.
-// On VALID writes the affine Q (x, y).
+// On VALID writes the affine Q (x, y), canonical.
 template <typename GTab>
 HD uint8_t recover(fe& qx, fe& qy, const uint32_t digest_be[8], const uint32_t r_be[8],
                    const uint32_t s_be[8], uint32_t v, GTab gtab) {
@@ -264,8 +271,8 @@ HD uint8_t recover(fe& qx, fe& qy, const uint32_t digest_be[8], const uint32_t r
     HD_UNROLL for (int i = 0; i < 8; i++) { r.v[i] = r_be[7 - i]; s.v[i] = s_be[7 - i]; }
     if (sc_ge_n(r.v) || sc_ge_n(s.v)) return V_BAD_RS;
     if (sc_is_zero(r) || sc_is_zero(s)) return V_BAD_RS;
-    fe x;
-    HD_UNROLL for (int i = 0; i < 8; i++) x.v[i] = r.v[i];
+    uint32_t xw[8];
+    HD_UNROLL for (int i = 0; i < 8; i++) xw[i] = r.v[i];
     if (v & 2) {
         // x = r + n must stay < p  <=>  r < p - n
         // p - n = 0x14551231950B75FC4402DA1722FC9BAEE (129 bits, LE limbs below)
@@ -280,8 +287,10 @@ HD uint8_t recover(fe& qx, fe& qy, const uint32_t digest_be[8], const uint32_t r
         if (!lt) return V_NO_POINT;
         const uint32_t N[8] = {HD_N0, HD_N1, HD_N2, HD_N3, HD_N4, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
         uint64_t c = 0;
-        HD_UNROLL for (int i = 0; i < 8; i++) { c += (uint64_t)x.v[i] + N[i]; x.v[i] = (uint32_t)c; c >>= 32; }
+        HD_UNROLL for (int i = 0; i < 8; i++) { c += (uint64_t)xw[i] + N[i]; xw[i] = (uint32_t)c; c >>= 32; }
     }
+    fe x;
+    fe_from_le(x, xw);                // x < p: canonical
     fe y2, y;
     fe_sqr(y2, x);
     fe_mul(y2, y2, x);
@@ -289,7 +298,11 @@ HD uint8_t recover(fe& qx, fe& qy, const uint32_t digest_be[8], const uint32_t r
     fe_set_u32(seven, 7);
     fe_add(y2, y2, seven);
     if (!fe_sqrt(y, y2)) return V_NO_POINT;
-    if ((y.v[0] & 1u) != (v & 1u)) fe_neg(y, y);
+    fe_normalize(y);
+    if ((uint32_t)(y.n[0] & 1u) != (v & 1u)) {
+        fe_neg(y, y);
+        fe_normalize(y);
+    }
     ge R;
     R.x = x;
     R.y = y;
@@ -310,6 +323,8 @@ HD uint8_t recover(fe& qx, fe& qy, const uint32_t digest_be[8], const uint32_t r
     fe_mul(qx, Q.x, zi2);
     fe_mul(zi2, zi2, zi);
     fe_mul(qy, Q.y, zi2);
+    fe_normalize(qx);
+    fe_normalize(qy);
     return V_VALID;
 }
 

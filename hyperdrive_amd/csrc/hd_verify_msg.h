@@ -72,7 +72,7 @@ HD uint8_t verify_msg(const MsgIn& m, GTab gtab, AdmTab adm, uint32_t n_adm, int
     uint32_t xb[8];
     fe_to_be(xb, qx);
     if (compressed) {
-        sha256_pub33(rec_be, 2u | (qy.v[0] & 1u), xb);
+        sha256_pub33(rec_be, 2u | (qy.n[0] & 1u), xb);
     } else {
         uint32_t yb[8];
         fe_to_be(yb, qy);

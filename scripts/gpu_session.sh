@@ -19,6 +19,10 @@ for step in "$@"; do
     gputest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     gputest_all) run pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 600 python bench.py ;;
-    prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu ;;
+    smoke) run smoke 300 python __graft_entry__.py smoke ;;
+    prof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu ;;
+    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu ;;
+    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu ;;
+    pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_sq -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu ;;
   esac
 done

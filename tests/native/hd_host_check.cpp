@@ -15,13 +15,15 @@ static const ge* gtab() {
 }
 static void le_in(uint32_t* o, const uint8_t* b) { for (int i = 0; i < 8; i++) o[i] = load_be32(b + 4 * (7 - i)); }
 static void le_out(uint8_t* b, const uint32_t* o) { for (int i = 0; i < 8; i++) store_be32(b + 4 * (7 - i), o[i]); }
+static void fe_in(fe& r, const uint8_t* b) { uint32_t w[8]; le_in(w, b); fe_from_le(r, w); }
+static void fe_out(uint8_t* b, const fe& a) { fe t = a; fe_normalize(t); uint32_t w[8]; fe_to_le(w, t); le_out(b, w); }
 
 extern "C" {
 // all 32-byte operands big-endian
 void hdh_fe_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
     fe x, y, r;
-    le_in(x.v, a);
-    le_in(y.v, b);
+    fe_in(x, a);
+    fe_in(y, b);
     int ok = 1;
     switch (op) {
         case 0: fe_mul(r, x, y); break;
@@ -33,7 +35,7 @@ void hdh_fe_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
         case 6: ok = fe_sqrt(r, x); break;
         default: fe_clear(r);
     }
-    le_out(out, r.v);
+    fe_out(out, r);
     out[32] = (uint8_t)ok;
 }
 void hdh_sc_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
@@ -52,7 +54,7 @@ void hdh_sc_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
 }
 void hdh_gtab(uint8_t* out /* 128 x 64 */) {
     const ge* t = gtab();
-    for (int k = 0; k < HD_GTAB_N; k++) { le_out(out + 64 * k, t[k].x.v); le_out(out + 64 * k + 32, t[k].y.v); }
+    for (int k = 0; k < HD_GTAB_N; k++) { fe_out(out + 64 * k, t[k].x); fe_out(out + 64 * k + 32, t[k].y); }
 }
 int hdh_booth(const uint8_t* k32, int w, int j) {
     sc k;
@@ -62,8 +64,8 @@ int hdh_booth(const uint8_t* k32, int w, int j) {
 // Q = u1 G + u2 R (R affine given); returns 1 if inf; out = x||y
 int hdh_ecmult(const uint8_t* rx, const uint8_t* ry, const uint8_t* u1b, const uint8_t* u2b, uint8_t* out) {
     ge R;
-    le_in(R.x.v, rx);
-    le_in(R.y.v, ry);
+    fe_in(R.x, rx);
+    fe_in(R.y, ry);
     sc u1, u2;
     le_in(u1.v, u1b);
     le_in(u2.v, u2b);
@@ -72,8 +74,8 @@ int hdh_ecmult(const uint8_t* rx, const uint8_t* ry, const uint8_t* u1b, const u
     if (gej_is_inf(Q)) return 1;
     fe x, y;
     gej_to_ge(x, y, Q);
-    le_out(out, x.v);
-    le_out(out + 32, y.v);
+    fe_out(out, x);
+    fe_out(out + 32, y);
     return 0;
 }
 int hdh_recover(const uint8_t* digest, const uint8_t* sig, uint8_t* pub64) {
@@ -81,7 +83,7 @@ int hdh_recover(const uint8_t* digest, const uint8_t* sig, uint8_t* pub64) {
     for (int i = 0; i < 8; i++) { d[i] = load_be32(digest + 4 * i); rb[i] = load_be32(sig + 4 * i); sb[i] = load_be32(sig + 32 + 4 * i); }
     fe qx, qy;
     int v = recover(qx, qy, d, rb, sb, sig[64], gtab());
-    if (v == V_VALID) { le_out(pub64, qx.v); le_out(pub64 + 32, qy.v); }
+    if (v == V_VALID) { fe_out(pub64, qx); fe_out(pub64 + 32, qy); }
     return v;
 }
 void hdh_sign(const uint8_t* sk32, const uint8_t* digest, uint8_t* sig65) {
@@ -154,7 +156,7 @@ int hdh_verify(uint32_t n, const uint8_t* type, const int64_t* h, const int64_t*
 }
 }
 extern "C" int hdh_ecmult_trace(const uint8_t* rx, const uint8_t* ry, const uint8_t* u1b, const uint8_t* u2b, uint8_t* out, uint8_t* infs) {
-    ge R; le_in(R.x.v, rx); le_in(R.y.v, ry);
+    ge R; fe_in(R.x, rx); fe_in(R.y, ry);
     sc u1, u2; le_in(u1.v, u1b); le_in(u2.v, u2b);
     const ge* gt = gtab();
     gej rt[HD_RTAB_N];
@@ -173,7 +175,20 @@ extern "C" int hdh_ecmult_trace(const uint8_t* rx, const uint8_t* ry, const uint
           gej t = rt[ad == 0 ? 0 : ad - 1]; if (d < 0) fe_neg(t.y, t.y);
           gej s; gej_add(s, acc, t); gej_cmov(acc, s, d != 0); }
         infs[j] = gej_is_inf(acc);
-        if (!infs[j]) { fe x, y; gej_to_ge(x, y, acc); le_out(out + 64 * j, x.v); le_out(out + 64 * j + 32, y.v); }
+        if (!infs[j]) { fe x, y; gej_to_ge(x, y, acc); fe_out(out + 64 * j, x); fe_out(out + 64 * j + 32, y); }
     }
     return 0;
+}
+// raw-limb access for the lazy-reduction bound tests
+extern "C" void hdh_fe_raw(int op, const uint32_t* a10, const uint32_t* b10, uint32_t* out10) {
+    fe a, b, r;
+    for (int i = 0; i < 10; i++) { a.n[i] = a10[i]; b.n[i] = b10[i]; }
+    switch (op) {
+        case 0: fe_mul(r, a, b); break;
+        case 1: fe_sqr(r, a); break;
+        case 2: r = a; fe_norm_weak(r); break;
+        case 3: r = a; fe_normalize(r); break;
+        default: fe_clear(r);
+    }
+    for (int i = 0; i < 10; i++) out10[i] = r.n[i];
 }

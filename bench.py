@@ -157,8 +157,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # sanity: verdict histogram of this shard (all VALID without --adv)
+    # correctness gate: without --adv every message of the workload is an honest
+    # vote by construction, so every verdict must be VALID and the valid bitmap
+    # full; a wrong kernel must not produce a throughput number.
     hist = torch.bincount(verdict.long(), minlength=8).cpu().tolist()
+    if args.adv == 0:
+        full_bits = int(bitmap.view(torch.uint8).cpu().numpy().astype("uint8").sum())
+        if hist[0] != B or full_bits != 255 * (B // 8):
+            print(json.dumps({"error": "verification produced wrong verdicts", "verdicts": hist}), flush=True)
+            sys.exit(1)
 
     if rank == 0:
         ms_step = elapsed / args.steps * 1e3

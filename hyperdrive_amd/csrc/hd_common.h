@@ -10,9 +10,11 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define HD __host__ __device__ __forceinline__
+#define HD_MEMBER __host__ __device__ __forceinline__
 #define HD_NOINLINE static __host__ __device__ __noinline__
 #else
 #define HD static inline
+#define HD_MEMBER inline
 #define HD_NOINLINE static
 #endif
 

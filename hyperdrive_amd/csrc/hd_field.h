@@ -104,7 +104,7 @@ HD void sqr_256(uint32_t t[16], const uint32_t a[8]) {
 // Bounds (checked in tests/test_devmath.py and asserted by construction):
 //   T  "tight" (output of mul / sqr / norm_weak): n[0..8] < 2^26 + 2^24,
 //      n[9] < 2^22 + 1 -- value < 2^256 + 2^230, NOT necessarily < p.
-//   L  "loose" (valid mul / sqr input):            n[0..8] < 2^30, n[9] < 2^26.
+//   L  "loose" (valid mul / sqr input):            n[0..8] < 2^30, n[9] < 2^25.5.
 // With L inputs every 64-bit product column sum stays < 2^63.3, so a column is
 // a chain of v_mad_u64_u32 into one 64-bit accumulator (no carry flags, no
 // moves).  fe_sub(a, b) = a + K p - b limb-wise needs b <= K p limb-wise; the
@@ -230,55 +230,57 @@ HD bool fe_eq(const fe& a, const fe& b) {  // b must be T
     return fe_is_zero(d);
 }
 
-// 19 product columns (64-bit) -> T
-HD void fe_reduce_cols(fe& r, uint64_t c[19]) {
-    // 1. carry-normalise the high columns (weight 2^(26 (10+j))) into h[0..9]
-    uint32_t h[10];
-    uint64_t t = c[10];
-    HD_UNROLL for (int j = 0; j < 8; j++) {
-        h[j] = (uint32_t)t & HD_M26;
-        t = (t >> 26) + c[11 + j];
+// Product scanning with the high column folded in as it is produced: column
+// k (weight 2^(26k)) and column k+10 (weight 2^(26k) * 2^260, 2^260 ==
+// 0x400 * 2^26 + 0x3D10 mod p) are accumulated together, so only three
+// 64-bit accumulators are live (low register pressure -> more waves/SIMD).
+// Inputs L (limbs < 2^30, top limb < 2^25.5); output T.
+template <bool SQR>
+HD void fe_mul_impl(fe& out, const fe& a, const fe& b) {
+    fe r;               // out may alias a or b
+    uint64_t chi = 0;   // carry of the high columns
+    uint64_t clo = 0;   // carry of the low columns
+    uint64_t pend = 0;  // h_{k-1} * 0x400 (< 2^36), owed to column k
+    HD_UNROLL for (int k = 0; k < 10; k++) {
+        uint64_t d = chi;
+        HD_UNROLL for (int i = k + 1; i < 10; i++) {
+            const int j = k + 10 - i;
+            if (SQR) {
+                if (i < j) d += (uint64_t)(a.n[i] << 1) * a.n[j];
+                else if (i == j) d += (uint64_t)a.n[i] * a.n[i];
+            } else {
+                d += (uint64_t)a.n[i] * b.n[j];
+            }
+        }
+        const uint32_t hk = (uint32_t)d & HD_M26;
+        chi = d >> 26;
+        uint64_t c = clo + pend + (uint64_t)hk * 0x3D10u;
+        HD_UNROLL for (int i = 0; i <= k; i++) {
+            const int j = k - i;
+            if (SQR) {
+                if (i < j) c += (uint64_t)(a.n[i] << 1) * a.n[j];
+                else if (i == j) c += (uint64_t)a.n[i] * a.n[i];
+            } else {
+                c += (uint64_t)a.n[i] * b.n[j];
+            }
+        }
+        pend = (uint64_t)hk << 10;
+        r.n[k] = (uint32_t)c & HD_M26;
+        clo = c >> 26;
     }
-    h[8] = (uint32_t)t & HD_M26;
-    h[9] = (uint32_t)(t >> 26);
-    // 2. fold: 2^260 == 0x1000003D10 = 0x400 * 2^26 + 0x3D10 (mod p)
-    HD_UNROLL for (int j = 0; j < 10; j++) c[j] += (uint64_t)h[j] * 0x3D10u;
-    HD_UNROLL for (int j = 0; j < 9; j++) c[j + 1] += (uint64_t)h[j] << 10;
-    // 3. carry-normalise the low columns
-    t = c[0];
-    HD_UNROLL for (int j = 0; j < 9; j++) {
-        r.n[j] = (uint32_t)t & HD_M26;
-        t = (t >> 26) + c[j + 1];
-    }
-    r.n[9] = (uint32_t)t & HD_M22;
-    // 4. bits >= 256: (t >> 22) plus h[9] * 0x400 at 2^260 -> weight 2^256
-    uint64_t u = (t >> 22) + ((uint64_t)h[9] << 14);
+    // bits >= 2^256: r9's top 4 bits, the low carry and the last fold at 2^260
+    // (chi is 0: top limbs < 2^25.5 keep the highest column < 2^52)
+    uint64_t u = ((clo + pend) << 4) + (r.n[9] >> 22);
+    r.n[9] &= HD_M22;
     uint64_t x = u * 0x3D1u + r.n[0];
     r.n[0] = (uint32_t)x & HD_M26;
     uint64_t y = (x >> 26) + (u << 6) + r.n[1];
     r.n[1] = (uint32_t)y & HD_M26;
     r.n[2] += (uint32_t)(y >> 26);
+    out = r;
 }
-
-HD void fe_mul(fe& r, const fe& a, const fe& b) {
-    uint64_t c[19];
-    HD_UNROLL for (int k = 0; k < 19; k++) c[k] = 0;
-    HD_UNROLL for (int i = 0; i < 10; i++) {
-        HD_UNROLL for (int j = 0; j < 10; j++) c[i + j] += (uint64_t)a.n[i] * b.n[j];
-    }
-    fe_reduce_cols(r, c);
-}
-HD void fe_sqr(fe& r, const fe& a) {
-    uint64_t c[19];
-    uint32_t d[10];
-    HD_UNROLL for (int i = 0; i < 10; i++) d[i] = a.n[i] << 1;  // a.n < 2^30 -> 2a < 2^31
-    HD_UNROLL for (int k = 0; k < 19; k++) c[k] = 0;
-    HD_UNROLL for (int i = 0; i < 10; i++) {
-        c[2 * i] += (uint64_t)a.n[i] * a.n[i];
-        HD_UNROLL for (int j = i + 1; j < 10; j++) c[i + j] += (uint64_t)d[i] * a.n[j];
-    }
-    fe_reduce_cols(r, c);
-}
+HD void fe_mul(fe& r, const fe& a, const fe& b) { fe_mul_impl<false>(r, a, b); }
+HD void fe_sqr(fe& r, const fe& a) { fe_mul_impl<true>(r, a, a); }
 HD void fe_sqr_n(fe& r, const fe& a, int n) {
     r = a;
     HD_NOUNROLL for (int i = 0; i < n; i++) fe_sqr(r, r);

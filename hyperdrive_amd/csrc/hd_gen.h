@@ -88,7 +88,7 @@ HD void ecmult_gen(gej& out, const sc& k, GTab gtab) {
 // affine, canonical
 HD void gej_to_ge(fe& x, fe& y, const gej& a) {
     fe zi, zi2;
-    fe_inv(zi, a.z);
+    fe_inv_divsteps(zi, a.z);
     fe_sqr(zi2, zi);
     fe_mul(x, a.x, zi2);
     fe_mul(zi2, zi2, zi);
@@ -168,7 +168,7 @@ HD void ecdsa_sign(uint32_t r_be[8], uint32_t s_be[8], uint32_t& recid, const sc
             if (c || sc_ge_n(o)) sc_sub_n(o);
             for (int i = 0; i < 8; i++) t.v[i] = o[i];
         }
-        sc_inv(kinv, k);
+        sc_inv_divsteps(kinv, k);
         sc_mul(s, kinv, t);
         if (sc_is_zero(r) || sc_is_zero(s)) continue;
         // high-S: s > n/2
@@ -375,7 +375,7 @@ HD int gen_message(uint32_t kind, uint64_t i, uint32_t S, uint32_t adv_pct, GTab
         gej_to_ge(rx, ry, Rj);
         sc mm, kinv, s;
         sc_from_be_reduce(mm, d);
-        sc_inv(kinv, k);
+        sc_inv_divsteps(kinv, k);
         sc_mul(s, mm, kinv);
         uint32_t rxw[8];
         fe_to_le(rxw, rx);

@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256) void k_gen(uint32_t kind, uint64_t start, uint
     {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(gtab_g);
         uint32_t* dst = reinterpret_cast<uint32_t*>(s_gtab);
-        for (int k = threadIdx.x; k < HD_GTAB_N * 16; k += blockDim.x) dst[k] = src[k];
+        for (int k = threadIdx.x; k < (int)(HD_GTAB_N * sizeof(ge) / 4); k += blockDim.x) dst[k] = src[k];
     }
     __syncthreads();
     const uint32_t stride = gridDim.x * blockDim.x;

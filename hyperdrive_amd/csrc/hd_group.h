@@ -14,6 +14,7 @@
 // Jacobian infinity is Z == 0 (mod p), tested on the normalised value.
 #pragma once
 #include "hd_field.h"
+#include "hd_modinv.h"
 
 namespace hd {
 
@@ -59,18 +60,24 @@ HD void gej_dbl(gej& r, const gej& a) {
 HD_NOINLINE void gej_dbl_slow(gej& r, const gej& a) { gej_dbl(r, a); }
 
 // r = a + b, b affine and finite (madd-2007-bl shape, 8M + 3S with
-// Z3 = 2 Z1 H).  Handles a = inf and a = +-b.
+// Z3 = 2 Z1 H).  Handles a = inf (up front, so b is dead after the first
+// products) and a = +-b.
 HD void gej_add_ge(gej& r, const gej& a, const ge& b) {
-    fe z1z1, u2, s2, h, R, t, hh, i4, j, v;
+    if (fe_is_zero(a.z)) {
+        gej o;
+        gej_set_ge(o, b);
+        fe_norm_weak(o.y);
+        r = o;
+        return;
+    }
+    fe z1z1, u2, s2, h, R, t;
     fe_sqr(z1z1, a.z);         // T
     fe_mul(u2, b.x, z1z1);     // T
     fe_mul(s2, b.y, a.z);      // T
     fe_mul(s2, s2, z1z1);      // T
     fe_sub(h, u2, a.x);        // H = U2 - X1   (< 2^28.4)
     fe_sub(R, s2, a.y);        // r = S2 - Y1
-    const bool ainf = fe_is_zero(a.z);
-    const bool hzero = fe_is_zero(h);
-    if (hzero && !ainf) {
+    if (fe_is_zero(h)) {
         // a == +-b (rare): double or cancel
         gej o;
         if (fe_is_zero(R)) {
@@ -84,12 +91,15 @@ HD void gej_add_ge(gej& r, const gej& a, const ge& b) {
         r = o;
         return;
     }
+    gej o;
+    fe_mul(o.z, a.z, h);
+    fe_add(o.z, o.z, o.z);     // Z3 = 2 Z1 H   (2T)
+    fe hh, i4, j, v;
     fe_add(R, R, R);           // 2r            (< 2^29.4)
     fe_sqr(hh, h);             // T
     fe_mul_int(i4, hh, 4);     // I = 4 H^2     (4T)
     fe_mul(j, h, i4);          // J = H I       (T)
     fe_mul(v, a.x, i4);        // V = X1 I      (T)
-    gej o;
     fe_sqr(o.x, R);            // T
     fe_add(t, v, v);
     fe_add(t, t, j);           // 2V + J        (3T <= 8p)
@@ -101,19 +111,20 @@ HD void gej_add_ge(gej& r, const gej& a, const ge& b) {
     fe_add(j, j, j);           // 2 Y1 J        (2T <= 4p)
     fe_sub(o.y, t, j);
     fe_norm_weak(o.y);         // Y3            (T)
-    fe_mul(o.z, a.z, h);
-    fe_add(o.z, o.z, o.z);     // Z3 = 2 Z1 H   (2T)
-    if (ainf) {
-        gej_set_ge(o, b);
-        fe_norm_weak(o.y);
-    }
     r = o;
 }
 
 // r = a + b, both Jacobian, b finite (add-2007-bl shape, 12M + 4S with
-// Z3 = 2 Z1 Z2 H).  Handles a = inf and a = +-b.
+// Z3 = 2 Z1 Z2 H).  Handles a = inf (up front) and a = +-b; after the
+// H == 0 test only U1, H, r, S1 and Z1 Z2 stay live.
 HD void gej_add(gej& r, const gej& a, const gej& b) {
-    fe z1z1, z2z2, u1, u2, s1, s2, h, R, t;
+    if (fe_is_zero(a.z)) {
+        gej o = b;
+        fe_norm_weak(o.y);
+        r = o;
+        return;
+    }
+    fe z1z1, z2z2, u1, u2, s1, s2, h, R, t, z12;
     fe_sqr(z1z1, a.z);
     fe_sqr(z2z2, b.z);
     fe_mul(u1, a.x, z2z2);
@@ -122,24 +133,25 @@ HD void gej_add(gej& r, const gej& a, const gej& b) {
     fe_mul(s1, s1, z2z2);
     fe_mul(s2, b.y, a.z);
     fe_mul(s2, s2, z1z1);
+    fe_mul(z12, a.z, b.z);
     fe_sub(h, u2, u1);         // H
     fe_sub(R, s2, s1);         // r
-    const bool ainf = fe_is_zero(a.z);
-    const bool hzero = fe_is_zero(h);
-    if (hzero && !ainf) {
+    if (fe_is_zero(h)) {
         gej o;
         if (fe_is_zero(R)) gej_dbl_slow(o, a);
         else gej_set_inf(o);
         r = o;
         return;
     }
+    gej o;
+    fe_mul(t, z12, h);
+    fe_add(o.z, t, t);         // Z3 = 2 Z1 Z2 H (2T)
     fe i, j, v;
     fe_add(i, h, h);
     fe_sqr(i, i);              // I = (2H)^2    (T)
     fe_mul(j, h, i);           // J = H I       (T)
     fe_add(R, R, R);           // 2r
     fe_mul(v, u1, i);          // V = U1 I      (T)
-    gej o;
     fe_sqr(o.x, R);
     fe_add(t, v, v);
     fe_add(t, t, j);
@@ -151,13 +163,6 @@ HD void gej_add(gej& r, const gej& a, const gej& b) {
     fe_add(s1, s1, s1);
     fe_sub(o.y, t, s1);
     fe_norm_weak(o.y);         // Y3 = r (V - X3) - 2 S1 J
-    fe_mul(t, a.z, b.z);
-    fe_mul(t, t, h);
-    fe_add(o.z, t, t);         // Z3 = 2 Z1 Z2 H
-    if (ainf) {
-        o = b;
-        fe_norm_weak(o.y);
-    }
     r = o;
 }
 
@@ -229,8 +234,149 @@ HD void ecmult(gej& out, const ge& R, const sc& u1, const sc& u2, GTab gtab) {
     out = acc;
 }
 
-// G and its odd... all multiples 1G..128G in affine form (host-side build, or
-// any caller that wants the table).
+// ------------------------------------------------------------ GLV
+// secp256k1 endomorphism: lambda * (x, y) = (beta * x, y), lambda^3 = 1 mod n,
+// beta^3 = 1 mod p.  A scalar k splits as k = k1 + k2 lambda (mod n) with
+// |k1|, |k2| < 2^128 (lattice basis from the extended Euclid on (n, lambda);
+// constants derived and checked in tests/test_glv.py), so u1 G + u2 R becomes
+// a 4-scalar ladder of 132 doublings instead of 256.
+HD void sc_add(sc& r, const sc& a, const sc& b) {
+    uint32_t o[8];
+    uint64_t c = 0;
+    HD_UNROLL for (int i = 0; i < 8; i++) { c += (uint64_t)a.v[i] + b.v[i]; o[i] = (uint32_t)c; c >>= 32; }
+    if (c || sc_ge_n(o)) sc_sub_n(o);
+    HD_UNROLL for (int i = 0; i < 8; i++) r.v[i] = o[i];
+}
+// round(k * g / 2^384) for a 256-bit constant g
+HD void sc_mul_shift384(sc& r, const sc& k, const uint32_t g[8]) {
+    uint32_t t[16];
+    mul_256(t, k.v, g);
+    uint64_t c = (t[11] >> 31);
+    HD_UNROLL for (int i = 0; i < 4; i++) { c += t[12 + i]; r.v[i] = (uint32_t)c; c >>= 32; }
+    r.v[4] = (uint32_t)c;
+    HD_UNROLL for (int i = 5; i < 8; i++) r.v[i] = 0;
+}
+HD void sc_split_lambda(sc& k1, sc& k2, const sc& k) {
+    const uint32_t G1[8] = {0x45DBB031u, 0xE893209Au, 0x71E8CA7Fu, 0x3DAA8A14u,
+                            0x9284EB15u, 0xE86C90E4u, 0xA7D46BCDu, 0x3086D221u};
+    const uint32_t G2[8] = {0x8AC47F71u, 0x1571B4AEu, 0x9DF506C6u, 0x221208ACu,
+                            0x0ABFE4C4u, 0x6F547FA9u, 0x010E8828u, 0xE4437ED6u};
+    sc mb1, mb2, mlam, c1, c2, t;
+    const uint32_t MB1[8] = {0x0ABFE4C3u, 0x6F547FA9u, 0x010E8828u, 0xE4437ED6u, 0u, 0u, 0u, 0u};
+    const uint32_t MB2[8] = {0x3DB1562Cu, 0xD765CDA8u, 0x0774346Du, 0x8A280AC5u,
+                             0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    const uint32_t MLAM[8] = {0xB51283CFu, 0xE0CFC810u, 0x8EC739C2u, 0xA880B9FCu,
+                              0x77ED9BA4u, 0x5AD9E3FDu, 0x3FA3CF1Fu, 0xAC9C52B3u};
+    HD_UNROLL for (int i = 0; i < 8; i++) { mb1.v[i] = MB1[i]; mb2.v[i] = MB2[i]; mlam.v[i] = MLAM[i]; }
+    sc_mul_shift384(c1, k, G1);
+    sc_mul_shift384(c2, k, G2);
+    sc_mul(c1, c1, mb1);
+    sc_mul(c2, c2, mb2);
+    sc_add(k2, c1, c2);          // k2 = -c1 b1 - c2 b2
+    sc_mul(t, k2, mlam);
+    sc_add(k1, k, t);            // k1 = k - k2 lambda
+}
+// |k| as a 5-word (160-bit) magnitude and its sign (k > n/2 means negative)
+HD bool sc_signed_abs(uint32_t a[5], const sc& k) {
+    const uint32_t NH[8] = {0x681B20A0u, 0xDFE92F46u, 0x57A4501Du, 0x5D576E73u,
+                            0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0x7FFFFFFFu};
+    bool lt = false, gt = false;
+    HD_UNROLL for (int i = 7; i >= 0; i--) {
+        bool g = !lt && !gt && k.v[i] > NH[i];
+        bool l = !lt && !gt && k.v[i] < NH[i];
+        gt = gt || g;
+        lt = lt || l;
+    }
+    sc m = k;
+    if (gt) sc_neg(m, k);
+    HD_UNROLL for (int i = 0; i < 5; i++) a[i] = m.v[i];
+    return gt;
+}
+// Booth digit of window j (width W) of a 160-bit magnitude, sign applied
+template <int W>
+HD int booth_digit160(const uint32_t a[5], int j, bool neg) {
+    uint32_t x = 0;
+    HD_UNROLL for (int t = 0; t <= W; t++) {
+        const int b = W * j - 1 + t;
+        const uint32_t bit = (b >= 0 && b < 160) ? ((a[b >> 5] >> (b & 31)) & 1u) : 0u;
+        x |= bit << t;
+    }
+    const int d = (int)((x >> 1) + (x & 1)) - (int)((x >> W) << W);
+    return neg ? -d : d;
+}
+
+#define HD_GLV_NWIN_R 33   // 4-bit windows over 132 bits
+#define HD_GLV_NWIN_G 17   // 8-bit windows over 136 bits
+
+HD void fe_beta(fe& b) {
+    const uint32_t BETA[8] = {0x719501EEu, 0xC1396C28u, 0x12F58995u, 0x9CF04975u,
+                              0xAC3434E9u, 0x6E64479Eu, 0x657C0710u, 0x7AE96A2Bu};
+    fe_from_le(b, BETA);
+}
+
+// Q = u1 G + u2 R with the endomorphism.  gtab[0..127] = (k+1) G,
+// gtab[128..255] = (k+1) lambda G (affine).  Per-lane tables of (k+1) R and
+// (k+1) lambda R (Jacobian) live in scratch.
+template <typename GTab>
+HD void ecmult_glv(gej& out, const ge& R, const sc& u1, const sc& u2, GTab gtab) {
+    gej rt[HD_RTAB_N], lt[HD_RTAB_N];
+    gej_set_ge(rt[0], R);
+    gej_dbl(rt[1], rt[0]);
+    HD_NOUNROLL for (int k = 2; k < HD_RTAB_N; k++) gej_add_ge(rt[k], rt[k - 1], R);
+    fe beta;
+    fe_beta(beta);
+    HD_NOUNROLL for (int k = 0; k < HD_RTAB_N; k++) {
+        lt[k] = rt[k];
+        fe_mul(lt[k].x, rt[k].x, beta);
+    }
+    int16_t dra[HD_GLV_NWIN_R], drb[HD_GLV_NWIN_R], dga[HD_GLV_NWIN_G], dgb[HD_GLV_NWIN_G];
+    {
+        sc k1, k2;
+        uint32_t a[5];
+        bool neg;
+        sc_split_lambda(k1, k2, u2);
+        neg = sc_signed_abs(a, k1);
+        HD_UNROLL for (int j = 0; j < HD_GLV_NWIN_R; j++) dra[j] = (int16_t)booth_digit160<HD_WR>(a, j, neg);
+        neg = sc_signed_abs(a, k2);
+        HD_UNROLL for (int j = 0; j < HD_GLV_NWIN_R; j++) drb[j] = (int16_t)booth_digit160<HD_WR>(a, j, neg);
+        sc_split_lambda(k1, k2, u1);
+        neg = sc_signed_abs(a, k1);
+        HD_UNROLL for (int j = 0; j < HD_GLV_NWIN_G; j++) dga[j] = (int16_t)booth_digit160<HD_WG>(a, j, neg);
+        neg = sc_signed_abs(a, k2);
+        HD_UNROLL for (int j = 0; j < HD_GLV_NWIN_G; j++) dgb[j] = (int16_t)booth_digit160<HD_WG>(a, j, neg);
+    }
+    gej acc;
+    gej_set_inf(acc);
+    HD_NOUNROLL for (int j = HD_GLV_NWIN_R - 1; j >= 0; j--) {
+        if (j != HD_GLV_NWIN_R - 1) {
+            HD_NOUNROLL for (int k = 0; k < HD_WR; k++) gej_dbl(acc, acc);
+        }
+        if ((j & 1) == 0) {
+            HD_NOUNROLL for (int half = 0; half < 2; half++) {
+                const int d = half ? dgb[j >> 1] : dga[j >> 1];
+                const int ad = d < 0 ? -d : d;
+                ge t = gtab[half * HD_GTAB_N + (ad == 0 ? 0 : ad - 1)];
+                if (d < 0) fe_neg(t.y, t.y);
+                gej s;
+                gej_add_ge(s, acc, t);
+                gej_cmov(acc, s, d != 0);
+            }
+        }
+        HD_NOUNROLL for (int half = 0; half < 2; half++) {
+            const int d = half ? drb[j] : dra[j];
+            const int ad = d < 0 ? -d : d;
+            gej t = half ? lt[ad == 0 ? 0 : ad - 1] : rt[ad == 0 ? 0 : ad - 1];
+            if (d < 0) fe_neg(t.y, t.y);
+            gej s;
+            gej_add(s, acc, t);
+            gej_cmov(acc, s, d != 0);
+        }
+    }
+    out = acc;
+}
+
+// All multiples 1G..128G in affine form, followed (when tab has room for
+// 2 * HD_GTAB_N entries and with_lambda) by lambda * those = (beta x, y).
 HD void build_gtab(ge* tab) {
     ge g;
     const uint32_t GX[8] = {0x79BE667Eu, 0xF9DCBBACu, 0x55A06295u, 0xCE870B07u,
@@ -246,13 +392,23 @@ HD void build_gtab(ge* tab) {
         if (k == 1) gej_dbl(acc, acc);
         else gej_add_ge(acc, acc, g);
         fe zi, zi2, zi3;
-        fe_inv(zi, acc.z);
+        fe_inv_divsteps(zi, acc.z);
         fe_sqr(zi2, zi);
         fe_mul(zi3, zi2, zi);
         fe_mul(tab[k].x, acc.x, zi2);
         fe_mul(tab[k].y, acc.y, zi3);
         fe_normalize(tab[k].x);
         fe_normalize(tab[k].y);
+    }
+}
+HD void build_gtab_glv(ge* tab) {
+    build_gtab(tab);
+    fe beta;
+    fe_beta(beta);
+    for (int k = 0; k < HD_GTAB_N; k++) {
+        fe_mul(tab[HD_GTAB_N + k].x, tab[k].x, beta);
+        fe_normalize(tab[HD_GTAB_N + k].x);
+        tab[HD_GTAB_N + k].y = tab[k].y;
     }
 }
 
@@ -263,6 +419,7 @@ HD void build_gtab(ge* tab) {
 //   V&2 and r >= p - n -> NO_POINT; x^3+7 non-residue -> NO_POINT;
 //   Q = inf -> INFINITY.  High-S accepted.  m = digest mod n.
 // On VALID writes the affine Q (x, y), canonical.
+// gtab: 2 * HD_GTAB_N entries (build_gtab_glv).
 template <typename GTab>
 HD uint8_t recover(fe& qx, fe& qy, const uint32_t digest_be[8], const uint32_t r_be[8],
                    const uint32_t s_be[8], uint32_t v, GTab gtab) {
@@ -309,16 +466,16 @@ HD uint8_t recover(fe& qx, fe& qy, const uint32_t digest_be[8], const uint32_t r
 
     sc m, rinv, u1, u2;
     sc_from_be_reduce(m, digest_be);
-    sc_inv(rinv, r);
+    sc_inv_divsteps(rinv, r);
     sc_mul(u1, m, rinv);
     sc_neg(u1, u1);
     sc_mul(u2, s, rinv);
 
     gej Q;
-    ecmult(Q, R, u1, u2, gtab);
+    ecmult_glv(Q, R, u1, u2, gtab);
     if (gej_is_inf(Q)) return V_INFINITY;
     fe zi, zi2;
-    fe_inv(zi, Q.z);
+    fe_inv_divsteps(zi, Q.z);
     fe_sqr(zi2, zi);
     fe_mul(qx, Q.x, zi2);
     fe_mul(zi2, zi2, zi);

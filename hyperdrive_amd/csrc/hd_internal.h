@@ -33,6 +33,7 @@ struct TallyWork;  // hd_tally.hip
 struct hd_ctx {
     int device = 0;
     int n_cu = 256;
+    int verify_waves = 3;   // register budget of k_verify (waves per SIMD)
     hipStream_t stream = nullptr;
     bool compressed = true;
     hd::ge* d_gtab = nullptr;

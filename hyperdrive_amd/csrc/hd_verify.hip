@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -26,34 +27,33 @@
 using namespace hd;
 
 // ---------------------------------------------------------------- kernels
-__device__ __forceinline__ void load_msg(MsgIn& m, const DevBatch& b, uint32_t i) {
-    m.type = b.type[i];
-    m.h = b.height[i];
-    m.r = b.round[i];
-    m.vr = b.valid_round ? b.valid_round[i] : -1;
-    const uint8_t* val = b.value32 + 32 * (size_t)i;
-    const uint8_t* frm = b.from32 + 32 * (size_t)i;
-    const uint8_t* sig = b.sig65 + 65 * (size_t)i;
-    HD_UNROLL for (int w = 0; w < 8; w++) {
-        m.value_be[w] = load_be32(val + 4 * w);
-        m.from_be[w] = load_be32(frm + 4 * w);
-        m.r_be[w] = load_be32(sig + 4 * w);
-        m.s_be[w] = load_be32(sig + 32 + 4 * w);
-    }
-    m.v = sig[64];
-}
+// Message i of a device batch, loaded field by field when the hot path needs
+// it (see verify_msg_src).
+struct DevSrc {
+    const DevBatch& b;
+    uint32_t i;
+    __device__ __forceinline__ uint32_t type() const { return b.type[i]; }
+    __device__ __forceinline__ int64_t h() const { return b.height[i]; }
+    __device__ __forceinline__ int64_t r() const { return b.round[i]; }
+    __device__ __forceinline__ int64_t vr() const { return b.valid_round ? b.valid_round[i] : -1; }
+    __device__ __forceinline__ uint32_t value(int w) const { return load_be32(b.value32 + 32 * (size_t)i + 4 * w); }
+    __device__ __forceinline__ uint32_t from(int w) const { return load_be32(b.from32 + 32 * (size_t)i + 4 * w); }
+    __device__ __forceinline__ uint32_t sig_r(int w) const { return load_be32(b.sig65 + 65 * (size_t)i + 4 * w); }
+    __device__ __forceinline__ uint32_t sig_s(int w) const { return load_be32(b.sig65 + 65 * (size_t)i + 32 + 4 * w); }
+    __device__ __forceinline__ uint32_t sig_v() const { return b.sig65[65 * (size_t)i + 64]; }
+};
 
-template <bool COMPRESSED>
-__global__ __launch_bounds__(256, 2) void k_verify(DevBatch b, const ge* __restrict__ gtab_g,
+template <bool COMPRESSED, int WAVES>
+__global__ __launch_bounds__(256, WAVES) void k_verify(DevBatch b, const ge* __restrict__ gtab_g,
                                                 const uint32_t* __restrict__ adm, const int32_t* __restrict__ adm_perm,
                                                 uint32_t n_adm, int adm_steps, uint8_t* __restrict__ verdict,
                                                 uint8_t* __restrict__ rec32, int32_t* __restrict__ signer,
                                                 uint32_t* __restrict__ bitmap) {
-    __shared__ ge s_gtab[HD_GTAB_N];
+    __shared__ ge s_gtab[2 * HD_GTAB_N];  // 1G..128G, lambda*(1G..128G): 20 KiB
     {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(gtab_g);
         uint32_t* dst = reinterpret_cast<uint32_t*>(s_gtab);
-        for (int k = threadIdx.x; k < HD_GTAB_N * 16; k += blockDim.x) dst[k] = src[k];
+        for (int k = threadIdx.x; k < (int)(2 * HD_GTAB_N * sizeof(ge) / 4); k += blockDim.x) dst[k] = src[k];
     }
     __syncthreads();
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -62,11 +62,10 @@ __global__ __launch_bounds__(256, 2) void k_verify(DevBatch b, const ge* __restr
         const bool active = i < b.n;
         uint8_t v = 0xFF;
         if (active) {
-            MsgIn m;
-            load_msg(m, b, i);
+            DevSrc src{b, i};
             uint32_t rec[8];
             int32_t s;
-            v = verify_msg(m, (const ge*)s_gtab, adm, n_adm, adm_steps, COMPRESSED, rec, s);
+            v = verify_msg_src(src, (const ge*)s_gtab, adm, n_adm, adm_steps, COMPRESSED, rec, s);
             verdict[i] = v;
             if (rec32) {
                 uint8_t* o = rec32 + 32 * (size_t)i;
@@ -140,13 +139,18 @@ int hd_ctx_create(int device, hd_ctx** out) {
     }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->n_cu = prop.multiProcessorCount;
-    // G table (1G..128G affine), built once on the host with the same code
-    // the device runs, then uploaded.
+    if (const char* w = getenv("HD_VERIFY_WAVES")) {
+        int v = atoi(w);
+        if (v >= 2 && v <= 4) ctx->verify_waves = v;
+    }
+    // G tables (1G..128G and lambda*(1G..128G), affine), built once on the
+    // host with the same code the device runs, then uploaded.
     static std::once_flag once;
-    static std::vector<ge> host_tab(HD_GTAB_N);
-    std::call_once(once, [] { build_gtab(host_tab.data()); });
-    e = hipMalloc(&ctx->d_gtab, sizeof(ge) * HD_GTAB_N);
-    if (e == hipSuccess) e = hipMemcpy(ctx->d_gtab, host_tab.data(), sizeof(ge) * HD_GTAB_N, hipMemcpyHostToDevice);
+    static std::vector<ge> host_tab(2 * HD_GTAB_N);
+    std::call_once(once, [] { build_gtab_glv(host_tab.data()); });
+    e = hipMalloc(&ctx->d_gtab, sizeof(ge) * 2 * HD_GTAB_N);
+    if (e == hipSuccess)
+        e = hipMemcpy(ctx->d_gtab, host_tab.data(), sizeof(ge) * 2 * HD_GTAB_N, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         int rc = hd_ctx_fail(ctx, e, "gtab upload");
         hd_ctx_destroy(ctx);
@@ -225,14 +229,24 @@ int hd_verify_batch_device(hd_ctx* ctx, const hd_batch* db, uint8_t* d_verdict, 
     DevBatch b{db->n, db->type, db->height, db->round, db->valid_round, db->value32, db->from32, db->sig65};
     const uint32_t threads = 256;
     uint32_t blocks = (db->n + threads - 1) / threads;
-    uint32_t max_blocks = (uint32_t)std::max(ctx->n_cu, 1) * 8u;
+    // resident blocks: 4 SIMDs x waves/SIMD wave slots per CU, 4 waves per block
+    uint32_t max_blocks = (uint32_t)std::max(ctx->n_cu, 1) * (uint32_t)ctx->verify_waves * 2u;
     blocks = std::min(blocks, max_blocks);
-    if (ctx->compressed)
-        k_verify<true><<<blocks, threads, 0, s>>>(b, ctx->d_gtab, ctx->d_adm, ctx->d_adm_perm, ctx->n_adm, ctx->adm_steps,
-                                                  d_verdict, d_recovered32, d_signer, d_valid_bitmap);
-    else
-        k_verify<false><<<blocks, threads, 0, s>>>(b, ctx->d_gtab, ctx->d_adm, ctx->d_adm_perm, ctx->n_adm, ctx->adm_steps,
-                                                   d_verdict, d_recovered32, d_signer, d_valid_bitmap);
+#define HD_LAUNCH_VERIFY(C, W)                                                                             \
+    k_verify<C, W><<<blocks, threads, 0, s>>>(b, ctx->d_gtab, ctx->d_adm, ctx->d_adm_perm, ctx->n_adm, ctx->adm_steps, \
+                                              d_verdict, d_recovered32, d_signer, d_valid_bitmap)
+    // waves/SIMD the kernel is register-allocated for (HD_VERIFY_WAVES = 2/3/4, default 3)
+    const int w = ctx->verify_waves;
+    if (ctx->compressed) {
+        if (w == 2) HD_LAUNCH_VERIFY(true, 2);
+        else if (w == 4) HD_LAUNCH_VERIFY(true, 4);
+        else HD_LAUNCH_VERIFY(true, 3);
+    } else {
+        if (w == 2) HD_LAUNCH_VERIFY(false, 2);
+        else if (w == 4) HD_LAUNCH_VERIFY(false, 4);
+        else HD_LAUNCH_VERIFY(false, 3);
+    }
+#undef HD_LAUNCH_VERIFY
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hd_ctx_fail(ctx, e, "k_verify launch");
     return HD_OK;

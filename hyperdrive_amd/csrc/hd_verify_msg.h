@@ -56,18 +56,33 @@ HD int32_t admitted_find(AdmTab adm, uint32_t n, int steps, const uint32_t key[8
     return cmp_be256(e, key) == 0 ? (int32_t)lo : -1;
 }
 
-// Full verdict for one message.  rec_be receives the recovered signatory (or
-// zeros when recovery failed); signer receives the admitted-table index.
-template <typename GTab, typename AdmTab>
-HD uint8_t verify_msg(const MsgIn& m, GTab gtab, AdmTab adm, uint32_t n_adm, int adm_steps, bool compressed,
-                      uint32_t rec_be[8], int32_t& signer) {
+// Full verdict for one message.  Src supplies the message fields on demand
+// (type(), h(), r(), vr(), value(w), from(w), sig_r(w), sig_s(w), sig_v()),
+// so the kernel loads each field from HBM in the phase that uses it and
+// nothing but the accumulator stays live across the ladder.  rec_be receives
+// the recovered signatory (zeros when recovery failed); signer the
+// admitted-table index.
+template <typename Src, typename GTab, typename AdmTab>
+HD uint8_t verify_msg_src(const Src& src, GTab gtab, AdmTab adm, uint32_t n_adm, int adm_steps, bool compressed,
+                          uint32_t rec_be[8], int32_t& signer) {
     signer = -1;
     HD_UNROLL for (int i = 0; i < 8; i++) rec_be[i] = 0;
-    if (m.type < 1 || m.type > 3) return V_BAD_TYPE;
+    const uint32_t type = src.type();
+    if (type < 1 || type > 3) return V_BAD_TYPE;
     uint32_t d[8];
-    message_digest(d, m);
+    {
+        uint32_t value_be[8];
+        HD_UNROLL for (int w = 0; w < 8; w++) value_be[w] = src.value(w);
+        if (type == T_PROPOSE) sha256_propose(d, src.h(), src.r(), src.vr(), value_be);
+        else sha256_vote(d, src.h(), src.r(), value_be);
+    }
     fe qx, qy;
-    uint8_t verdict = recover(qx, qy, d, m.r_be, m.s_be, m.v, gtab);
+    uint8_t verdict;
+    {
+        uint32_t r_be[8], s_be[8];
+        HD_UNROLL for (int w = 0; w < 8; w++) { r_be[w] = src.sig_r(w); s_be[w] = src.sig_s(w); }
+        verdict = recover(qx, qy, d, r_be, s_be, src.sig_v(), gtab);
+    }
     if (verdict != V_VALID) return verdict;
     uint32_t xb[8];
     fe_to_be(xb, qx);
@@ -78,13 +93,38 @@ HD uint8_t verify_msg(const MsgIn& m, GTab gtab, AdmTab adm, uint32_t n_adm, int
         fe_to_be(yb, qy);
         sha256_pub65(rec_be, xb, yb);
     }
+    uint32_t from_be[8];
     uint32_t diff = 0;
-    HD_UNROLL for (int i = 0; i < 8; i++) diff |= rec_be[i] ^ m.from_be[i];
+    HD_UNROLL for (int i = 0; i < 8; i++) {
+        from_be[i] = src.from(i);
+        diff |= rec_be[i] ^ from_be[i];
+    }
     if (diff) return V_SIGNATORY_MISMATCH;
-    int32_t idx = admitted_find(adm, n_adm, adm_steps, m.from_be);
+    int32_t idx = admitted_find(adm, n_adm, adm_steps, from_be);
     if (idx < 0) return V_NOT_ADMITTED;
     signer = idx;
     return V_VALID;
+}
+
+// MsgIn-backed source (host harness, generator)
+struct MsgSrc {
+    const MsgIn& m;
+    HD_MEMBER uint32_t type() const { return m.type; }
+    HD_MEMBER int64_t h() const { return m.h; }
+    HD_MEMBER int64_t r() const { return m.r; }
+    HD_MEMBER int64_t vr() const { return m.vr; }
+    HD_MEMBER uint32_t value(int w) const { return m.value_be[w]; }
+    HD_MEMBER uint32_t from(int w) const { return m.from_be[w]; }
+    HD_MEMBER uint32_t sig_r(int w) const { return m.r_be[w]; }
+    HD_MEMBER uint32_t sig_s(int w) const { return m.s_be[w]; }
+    HD_MEMBER uint32_t sig_v() const { return m.v; }
+};
+
+template <typename GTab, typename AdmTab>
+HD uint8_t verify_msg(const MsgIn& m, GTab gtab, AdmTab adm, uint32_t n_adm, int adm_steps, bool compressed,
+                      uint32_t rec_be[8], int32_t& signer) {
+    MsgSrc src{m};
+    return verify_msg_src(src, gtab, adm, n_adm, adm_steps, compressed, rec_be, signer);
 }
 
 }  // namespace hd

@@ -16,8 +16,8 @@ def b32(x: int) -> bytes:
 
 
 class HostMath:
-    FE_OPS = {"mul": 0, "sqr": 1, "add": 2, "sub": 3, "neg": 4, "inv": 5, "sqrt": 6}
-    SC_OPS = {"mul": 0, "sqr": 1, "neg": 2, "inv": 3, "reduce": 4}
+    FE_OPS = {"mul": 0, "sqr": 1, "add": 2, "sub": 3, "neg": 4, "inv": 5, "sqrt": 6, "inv_divsteps": 7}
+    SC_OPS = {"mul": 0, "sqr": 1, "neg": 2, "inv": 3, "reduce": 4, "inv_divsteps": 5}
 
     def __init__(self, path: str):
         L = ctypes.CDLL(path)
@@ -40,11 +40,25 @@ class HostMath:
         return int.from_bytes(out.raw, "big")
 
     def gtab(self):
-        out = ctypes.create_string_buffer(128 * 64)
+        """256 entries: (k+1) G for k < 128, then lambda (k+1) G."""
+        out = ctypes.create_string_buffer(256 * 64)
         self.L.hdh_gtab(out)
         r = out.raw
         return [(int.from_bytes(r[64 * k:64 * k + 32], "big"), int.from_bytes(r[64 * k + 32:64 * k + 64], "big"))
-                for k in range(128)]
+                for k in range(256)]
+
+    def ecmult_glv(self, R, u1: int, u2: int):
+        out = ctypes.create_string_buffer(64)
+        inf = self.L.hdh_ecmult_glv(b32(R[0]), b32(R[1]), b32(u1), b32(u2), out)
+        if inf:
+            return None
+        return int.from_bytes(out.raw[:32], "big"), int.from_bytes(out.raw[32:], "big")
+
+    def split(self, k: int):
+        a = ctypes.create_string_buffer(32)
+        b = ctypes.create_string_buffer(32)
+        self.L.hdh_split(b32(k), a, b)
+        return int.from_bytes(a.raw, "big"), int.from_bytes(b.raw, "big")
 
     def booth(self, k: int, w: int, j: int) -> int:
         return self.L.hdh_booth(b32(k), w, j)

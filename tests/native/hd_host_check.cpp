@@ -4,13 +4,14 @@
 #include <string.h>
 #include <vector>
 #include "../../hyperdrive_amd/csrc/hd_gen.h"
+#include "../../hyperdrive_amd/csrc/hd_modinv.h"
 
 using namespace hd;
 
-static ge g_tab[HD_GTAB_N];
+static ge g_tab[2 * HD_GTAB_N];
 static bool g_init = false;
 static const ge* gtab() {
-    if (!g_init) { build_gtab(g_tab); g_init = true; }
+    if (!g_init) { build_gtab_glv(g_tab); g_init = true; }
     return g_tab;
 }
 static void le_in(uint32_t* o, const uint8_t* b) { for (int i = 0; i < 8; i++) o[i] = load_be32(b + 4 * (7 - i)); }
@@ -33,6 +34,7 @@ void hdh_fe_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
         case 4: fe_neg(r, x); break;
         case 5: fe_inv(r, x); break;
         case 6: ok = fe_sqrt(r, x); break;
+        case 7: fe_inv_divsteps(r, x); break;
         default: fe_clear(r);
     }
     fe_out(out, r);
@@ -48,13 +50,14 @@ void hdh_sc_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
         case 2: sc_neg(r, x); break;
         case 3: sc_inv(r, x); break;
         case 4: { uint32_t w[8]; for (int i = 0; i < 8; i++) w[i] = load_be32(a + 4 * i); sc_from_be_reduce(r, w); break; }
+        case 5: sc_inv_divsteps(r, x); break;
         default: for (int i = 0; i < 8; i++) r.v[i] = 0;
     }
     le_out(out, r.v);
 }
 void hdh_gtab(uint8_t* out /* 128 x 64 */) {
     const ge* t = gtab();
-    for (int k = 0; k < HD_GTAB_N; k++) { fe_out(out + 64 * k, t[k].x); fe_out(out + 64 * k + 32, t[k].y); }
+    for (int k = 0; k < 2 * HD_GTAB_N; k++) { fe_out(out + 64 * k, t[k].x); fe_out(out + 64 * k + 32, t[k].y); }
 }
 int hdh_booth(const uint8_t* k32, int w, int j) {
     sc k;
@@ -191,4 +194,28 @@ extern "C" void hdh_fe_raw(int op, const uint32_t* a10, const uint32_t* b10, uin
         default: fe_clear(r);
     }
     for (int i = 0; i < 10; i++) out10[i] = r.n[i];
+}
+
+extern "C" int hdh_ecmult_glv(const uint8_t* rx, const uint8_t* ry, const uint8_t* u1b, const uint8_t* u2b, uint8_t* out) {
+    ge R;
+    fe_in(R.x, rx);
+    fe_in(R.y, ry);
+    sc u1, u2;
+    le_in(u1.v, u1b);
+    le_in(u2.v, u2b);
+    gej Q;
+    ecmult_glv(Q, R, u1, u2, gtab());
+    if (gej_is_inf(Q)) return 1;
+    fe x, y;
+    gej_to_ge(x, y, Q);
+    fe_out(out, x);
+    fe_out(out + 32, y);
+    return 0;
+}
+extern "C" void hdh_split(const uint8_t* kb, uint8_t* k1b, uint8_t* k2b) {
+    sc k, k1, k2;
+    le_in(k.v, kb);
+    sc_split_lambda(k1, k2, k);
+    le_out(k1b, k1.v);
+    le_out(k2b, k2.v);
 }

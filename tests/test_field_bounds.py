@@ -1,6 +1,6 @@
 """Worst-case limb bounds of the lazily reduced radix-2^26 field
 (hyperdrive_amd/csrc/hd_field.h): multiplier inputs up to L (limbs < 2^30, top
-< 2^26), weak normalisation of anything < 2^32, and the T output bound."""
+< 2^25.5), weak normalisation of anything < 2^32, and the T output bound."""
 import ctypes
 import random
 
@@ -35,10 +35,13 @@ def is_tight(l):
     return all(x < T_LIMB for x in l[:9]) and l[9] < T_TOP
 
 
+L_TOP = int(2 ** 25.5)   # top-limb bound of a multiplier input (largest producer: 2r < 2^25.33)
+
+
 def test_mul_sqr_worst_case_inputs(hostmath):
     rng = random.Random(21)
-    cases = [(_limbs(rng, 1 << 30, 1 << 26, True), _limbs(rng, 1 << 30, 1 << 26, True))]
-    cases += [(_limbs(rng, 1 << 30, 1 << 26), _limbs(rng, 1 << 30, 1 << 26)) for _ in range(300)]
+    cases = [(_limbs(rng, 1 << 30, L_TOP, True), _limbs(rng, 1 << 30, L_TOP, True))]
+    cases += [(_limbs(rng, 1 << 30, L_TOP), _limbs(rng, 1 << 30, L_TOP)) for _ in range(300)]
     cases += [([M26] * 9 + [(1 << 22) - 1], [M26] * 9 + [(1 << 22) - 1])]
     for a, b in cases:
         r = raw(hostmath, 0, a, b)

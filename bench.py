@@ -99,7 +99,9 @@ def main():
     ws = work_stream(dev)
     torch.cuda.set_stream(ws)          # torch ops (RCCL all-gather included) share the library's stream
     stream = ws.cuda_stream
-    lo = rank * B
+    from hyperdrive_amd.shard import gather_bitmaps, shard_range
+    lo, hi = shard_range(total, rank, world)
+    assert hi - lo == B
     # shard views (device pointers offset into the replicated batch)
     shard = HdBatch(B, db.type.data_ptr() + lo, db.height.data_ptr() + 8 * lo, db.round.data_ptr() + 8 * lo,
                     db.valid_round.data_ptr() + 8 * lo, db.value.data_ptr() + 32 * lo, db.frm.data_ptr() + 32 * lo,
@@ -108,7 +110,6 @@ def main():
     assert B % 32 == 0
     verdict = torch.empty(B, dtype=torch.uint8, device=dev)
     bitmap = torch.zeros(B // 32, dtype=torch.int32, device=dev)
-    bitmap_all = torch.zeros(total // 32, dtype=torch.int32, device=dev)
     lib = _lib.load()
     t_out, t_arr = v._tally_struct(total)
 
@@ -124,8 +125,7 @@ def main():
         if record:
             ev_k1.record()
         if dist is not None:
-            dist.all_gather_into_tensor(bitmap_all, bitmap)
-            gathered = bitmap_all
+            gathered = gather_bitmaps(bitmap, total, world)   # RCCL all-gather over xGMI
         else:
             gathered = bitmap
         if not args.no_tally:

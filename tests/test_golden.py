@@ -1,0 +1,120 @@
+"""Parity against the committed golden fixtures (tests/golden/, made by
+tests/golden/make_golden.py).
+
+CPU (-m "not gpu"): the oracle restatements (Python and C), the host build of
+the device math headers, and OpenSSL reproduce every fixture.
+GPU (-m gpu): the HIP path, called through the C ABI, reproduces every
+fixture bit for bit -- verdicts, recovered signatories, valid bitmaps, the
+first-wins tally and the quorum predicates -- with no oracle at run time.
+"""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+
+from util import OpenSSL, from_np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CASES = sorted(os.path.basename(p)[len("verify_"):-len(".npz")] for p in glob.glob(os.path.join(GOLDEN, "verify_*.npz")))
+
+
+def load_case(name):
+    from hyperdrive_amd.verify import Batch
+    z = np.load(os.path.join(GOLDEN, f"verify_{name}.npz"))  # allow_pickle=False (default)
+    b = Batch(z["type"], z["height"], z["round"], z["valid_round"], z["value"], z["frm"], z["sig"])
+    with open(os.path.join(GOLDEN, f"tally_{name}.json")) as fh:
+        tj = json.load(fh)
+    return b, z, tj
+
+
+def tally_from_json(tj):
+    count = {(h, r, t, bytes.fromhex(v)): c for h, r, t, v, c in tj["count"]}
+    distinct = {(h, r, t): c for h, r, t, c in tj["distinct"]}
+    distinct_any = {(h, r): c for h, r, c in tj["distinct_any"]}
+    return count, distinct, distinct_any, tj["dup"]
+
+
+def test_golden_cases_present():
+    assert len(CASES) >= 6, CASES
+
+
+def test_kats(oracle, coracle):
+    with open(os.path.join(GOLDEN, "kats.json")) as fh:
+        k = json.load(fh)
+    for m, d in k["sha256"]:
+        assert oracle.sha256(bytes.fromhex(m)).hex() == d
+        assert coracle.sha256(bytes.fromhex(m)).hex() == d
+    for e in k["ecrecover"]:
+        v, pub = coracle.recover(bytes.fromhex(e["digest"]), bytes.fromhex(e["sig"]))
+        assert v == 0 and pub.hex() == e["pub65"]
+    for e in k["digests"]:
+        value = bytes.fromhex(e["value"])
+        assert oracle.message_digest(oracle.PREVOTE, e["h"], e["r"], e["vr"], value).hex() == e["vote"]
+        assert coracle.digest(3, e["h"], e["r"], e["vr"], value).hex() == e["vote"]
+        assert coracle.digest(1, e["h"], e["r"], e["vr"], value).hex() == e["propose"]
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_c_oracle_and_host_headers_reproduce_fixture(coracle, hostmath, name):
+    b, z, _ = load_case(name)
+    compressed = bool(z["compressed"])
+    cv, crec = coracle.verify(b, z["admitted"], compressed, threads=4)
+    assert cv.tolist() == z["verdict"].tolist()
+    assert crec.tobytes() == z["recovered"].tobytes()
+    adm_sorted = np.array(sorted(z["admitted"].tolist()), np.uint8)
+    hv, hrec, _ = hostmath.verify(b, adm_sorted, compressed)
+    assert hv.tolist() == z["verdict"].tolist()
+    assert hrec.tobytes() == z["recovered"].tobytes()
+
+
+@pytest.mark.parametrize("name", ["edges", "votes_100signers_tail"])
+def test_python_oracle_reproduces_fixture(oracle, name):
+    b, z, tj = load_case(name)
+    ob = from_np(b)
+    adm = [bytes(r) for r in z["admitted"]]
+    vs, recs = oracle.verify_batch(ob, adm, bool(z["compressed"]))
+    assert vs == z["verdict"].tolist()
+    assert b"".join(recs) == z["recovered"].tobytes()
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_fixture_tally_and_openssl(oracle, name):
+    b, z, tj = load_case(name)
+    ob = from_np(b)
+    t = oracle.tally(ob, z["verdict"].tolist())
+    count, distinct, distinct_any, dup = tally_from_json(tj)
+    assert t.count == count and t.distinct == distinct and t.distinct_any == distinct_any and t.dup == dup
+    ossl = OpenSSL()
+    for i in np.flatnonzero(z["verdict"] == 0)[:40]:
+        d = oracle.message_digest(ob.mtype[i], ob.height[i], ob.round[i], ob.valid_round[i], ob.value[i])
+        v, Q = oracle.recover(d, ob.sig[i])
+        r, s = int.from_bytes(ob.sig[i][:32], "big"), int.from_bytes(ob.sig[i][32:64], "big")
+        assert v == 0 and ossl.verify(d, r, s, oracle.pubkey_bytes(Q, False))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", CASES)
+def test_gpu_matches_golden(gpu, name):
+    from hyperdrive_amd import quorum
+    b, z, tj = load_case(name)
+    v = gpu.Verifier(0, compressed=bool(z["compressed"]))
+    try:
+        v.set_signatories(z["admitted"])
+        res, tal = v.process_batch(b)
+        assert res.verdict.tolist() == z["verdict"].tolist()
+        assert res.recovered.tobytes() == z["recovered"].tobytes()
+        bits = np.unpackbits(res.valid_bitmap.view(np.uint8), bitorder="little")[: len(b)]
+        assert bits.tolist() == (z["verdict"] == 0).astype(int).tolist()
+        count, distinct, distinct_any, dup = tally_from_json(tj)
+        assert tal.count == count
+        assert tal.distinct == distinct
+        assert tal.distinct_any == distinct_any
+        assert tal.dup.tolist() == dup
+        for d in tj["decisions"]:
+            pv = bytes.fromhex(d["propose_value"]) if d["propose_value"] else None
+            got = quorum.decide(tal, d["h"], d["r"], tj["f"], pv, pv is not None)
+            assert got == d["decision"], d
+    finally:
+        v.close()

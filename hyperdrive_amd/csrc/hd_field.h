@@ -1,10 +1,10 @@
 // hd_field.h -- secp256k1 base-field (mod p) and scalar-field (mod n)
 // arithmetic for one message per 64-wide-wavefront lane.
 //
-// Base field: radix 2^26 x 10 limbs, lazily reduced (see the field section):
+// Base field: radix 2^29 x 9 limbs, lazily reduced (see the field section):
 // a product column is a chain of v_mad_u64_u32 into one 64-bit accumulator, so
-// the multiply needs no carry flags (a VCC carry chain costs s_nop hazards on
-// gfx950) and no operand moves; additions are 10 plain v_add_u32.
+// the multiply needs no carry flags and no operand moves; additions are 9
+// plain v_add_u32.
 // Scalar field: 8 x 32-bit limbs, fully reduced, operand-scanning schoolbook;
 // the reduction mod n folds with c = 2^256 - n (129 bits) three times.  Rare
 // carries / final subtractions are branches (taken with probability ~2^-220
@@ -19,7 +19,6 @@
 
 namespace hd {
 
-struct fe { uint32_t n[10]; };  // mod p, radix 2^26 (see below)
 struct sc { uint32_t v[8]; };  // mod n
 
 // p = 2^256 - 2^32 - 977
@@ -100,33 +99,116 @@ HD void sqr_256(uint32_t t[16], const uint32_t a[8]) {
 }
 
 // ------------------------------------------------------------- field mod p
-// Radix 2^26, 10 limbs, lazily reduced.  Value = sum n[i] 2^(26 i).
-// Bounds (checked in tests/test_devmath.py and asserted by construction):
-//   T  "tight" (output of mul / sqr / norm_weak): n[0..8] < 2^26 + 2^24,
-//      n[9] < 2^22 + 1 -- value < 2^256 + 2^230, NOT necessarily < p.
-//   L  "loose" (valid mul / sqr input):            n[0..8] < 2^30, n[9] < 2^25.5.
-// With L inputs every 64-bit product column sum stays < 2^63.3, so a column is
-// a chain of v_mad_u64_u32 into one 64-bit accumulator (no carry flags, no
-// moves).  fe_sub(a, b) = a + K p - b limb-wise needs b <= K p limb-wise; the
-// caller picks K (4 for a T subtrahend).  Exact tests (zero, equality, parity,
-// serialisation) go through fe_normalize (canonical, < p).
-#define HD_M26 0x3FFFFFFu
-#define HD_M22 0x3FFFFFu
-// p limbs: 0x3FFFC2F, 0x3FFFFBF, 7 x 0x3FFFFFF, 0x3FFFFF
-#define HD_FP0 0x3FFFC2Fu
-#define HD_FP1 0x3FFFFBFu
+// Radix 2^29, 9 limbs, lazily reduced.  Value = sum n[i] 2^(29 i) (261 bits
+// of room for a 256-bit field).
+//
+// Why 2^29 x 9 on gfx950: a 26x26..29x29-bit partial product plus a 64-bit
+// accumulate is ONE v_mad_u64_u32 (measured 4.3 cycles per wave-instruction,
+// scripts/valu_probe.hip), the most expensive instruction of the kernel, and
+// 9 limbs need 81 of them per product where 10 x 26-bit limbs need 100.  A
+// column of at most 8 full products of < 2^61 each still fits the 64-bit
+// accumulator, so no carry flags are ever needed (VCC carry chains cost
+// VOP3 issue + s_nop hazards on gfx950).
+//
+// Limb classes (inclusive per-limb maxima; M = 2^29 - 1, M24 = 2^24 - 1):
+//   T  "tight": n[0..7] <= M except n[2] <= M + 2^17, n[8] <= M24.  Every
+//      fe_mul / fe_sqr / fe_norm_weak output is T; value < 2^256 + 2^75.
+//   kT: the limb-wise sum of k tight values (fe_add, fe_mul_int, fe_sub_k).
+// fe_mul(a, b) is exact for max(a) * max(b) <= 7.9 T^2 limb-wise (e.g. T x 7T,
+// 2T x 3T); fe_sub_k<K>(a, b) = a + K p - b needs b <= K p limb-wise (K = 2
+// for a T subtrahend).  Exact tests (zero, equality, parity, serialisation)
+// go through fe_normalize (canonical, < p).
+//
+// Host test builds define HD_BOUNDS: every fe then carries per-limb upper
+// bounds (b[]) that each operation propagates by interval arithmetic and
+// checks against its precondition, so one run of a formula on the host
+// certifies its limb bounds for ALL inputs of the declared classes
+// (tests/test_field_bounds.py).  Device builds carry no bounds.
+#define HD_M29 0x1FFFFFFFu
+#define HD_M24 0xFFFFFFu
+// p limbs: 0x1FFFFC2F, 0x1FFFFFF7, 6 x 0x1FFFFFFF, 0xFFFFFF
+#define HD_FP0 0x1FFFFC2Fu
+#define HD_FP1 0x1FFFFFF7u
+#define HD_FE_T2 (HD_M29 + (1u << 17))   // T bound of limb 2
 
-HD void fe_clear(fe& r) { HD_UNROLL for (int i = 0; i < 10; i++) r.n[i] = 0; }
-HD void fe_set_u32(fe& r, uint32_t x) { fe_clear(r); r.n[0] = x & HD_M26; r.n[1] = x >> 26; }
+#if defined(HD_BOUNDS) && !defined(__HIP_DEVICE_COMPILE__)
+#define HD_BOUND_CHECKS 1
+#define HD_B(...) __VA_ARGS__
+extern "C" void hd_bound_fail(const char* what, int line);
+#define HD_BREQ(cond, what)                              \
+    do {                                                 \
+        if (!(cond)) hd_bound_fail(what, __LINE__);      \
+    } while (0)
+#else
+#define HD_B(...)
+#define HD_BREQ(cond, what) \
+    do {                    \
+    } while (0)
+#endif
 
-// 8 little-endian 32-bit words (value < 2^256) -> limbs (T, not reduced)
+struct fe {
+    uint32_t n[9];
+    HD_B(uint64_t b[9];)
+};
+
+HD uint32_t fe_p_limb(int i) { return i == 0 ? HD_FP0 : i == 1 ? HD_FP1 : i == 8 ? HD_M24 : HD_M29; }
+HD uint32_t fe_t_limb(int i) { return i == 2 ? HD_FE_T2 : i == 8 ? HD_M24 : HD_M29; }
+
+#ifdef HD_BOUND_CHECKS
+HD void fe_bound_exact(fe& r) { for (int i = 0; i < 9; i++) r.b[i] = r.n[i]; }
+HD void fe_bound_T(fe& r) { for (int i = 0; i < 9; i++) r.b[i] = fe_t_limb(i); }
+HD void fe_bound_check_values(const fe& a) {
+    for (int i = 0; i < 9; i++) HD_BREQ(a.n[i] <= a.b[i], "limb exceeds its tracked bound");
+}
+HD void fe_require_T(const fe& a, const char* what) {
+    for (int i = 0; i < 9; i++) HD_BREQ(a.b[i] <= fe_t_limb(i), what);
+}
+#define HD_REQUIRE_T(a, what) fe_require_T(a, what)
+#else
+#define HD_REQUIRE_T(a, what) \
+    do {                      \
+    } while (0)
+#endif
+
+// One v_mad_u64_u32: a * b + c.  The empty asm makes the result opaque, so
+// the compiler keeps the accumulation chain exactly as written (left alone,
+// it re-associates product scanning into operand scanning plus a 64-bit add
+// per column -- 30 % more cycles, measured).
+HD uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
+    uint64_t r = (uint64_t)a * b + c;
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(HD_NO_LAUNDER)
+    asm("" : "+v"(r));
+#endif
+    return r;
+}
+// a register copy the compiler cannot see through (keeps a constant multiplier
+// in a VGPR instead of strength-reducing a * 256 into a 64-bit shift + add)
+HD uint32_t opaque_u32(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(HD_NO_LAUNDER)
+    asm("" : "+v"(x));
+#endif
+    return x;
+}
+
+HD void fe_clear(fe& r) {
+    HD_UNROLL for (int i = 0; i < 9; i++) r.n[i] = 0;
+    HD_B(fe_bound_exact(r);)
+}
+HD void fe_set_u32(fe& r, uint32_t x) {  // x < 2^29
+    fe_clear(r);
+    r.n[0] = x;
+    HD_B(fe_bound_exact(r);)
+}
+
+// 8 little-endian 32-bit words (value < 2^256) -> limbs (canonical layout, T)
 HD void fe_from_le(fe& r, const uint32_t w[8]) {
-    HD_UNROLL for (int i = 0; i < 10; i++) {
-        const int bit = 26 * i, word = bit >> 5, off = bit & 31;
+    HD_UNROLL for (int i = 0; i < 9; i++) {
+        const int bit = 29 * i, word = bit >> 5, off = bit & 31;
         uint32_t v = w[word] >> off;
-        if (off > 6 && word + 1 < 8) v |= w[word + 1] << (32 - off);
-        r.n[i] = v & (i == 9 ? HD_M22 : HD_M26);
+        if (off > 3 && word + 1 < 8) v |= w[word + 1] << (32 - off);
+        r.n[i] = v & (i == 8 ? HD_M24 : HD_M29);
     }
+    HD_B(for (int i = 0; i < 9; i++) r.b[i] = i == 8 ? HD_M24 : HD_M29;)
 }
 HD void fe_from_be(fe& r, const uint32_t be[8]) {
     uint32_t w[8];
@@ -137,74 +219,116 @@ HD void fe_from_be(fe& r, const uint32_t be[8]) {
 // a + K p - b, limb-wise (no carries).  Requires b[i] <= K p[i].
 template <int K>
 HD void fe_sub_k(fe& r, const fe& a, const fe& b) {
-    r.n[0] = a.n[0] + (uint32_t)K * HD_FP0 - b.n[0];
-    r.n[1] = a.n[1] + (uint32_t)K * HD_FP1 - b.n[1];
-    HD_UNROLL for (int i = 2; i < 9; i++) r.n[i] = a.n[i] + (uint32_t)K * HD_M26 - b.n[i];
-    r.n[9] = a.n[9] + (uint32_t)K * HD_M22 - b.n[9];
-}
-HD void fe_sub(fe& r, const fe& a, const fe& b) { fe_sub_k<4>(r, a, b); }
-HD void fe_neg(fe& r, const fe& a) { fe z; fe_clear(z); fe_sub_k<4>(r, z, a); }
-HD void fe_add(fe& r, const fe& a, const fe& b) { HD_UNROLL for (int i = 0; i < 10; i++) r.n[i] = a.n[i] + b.n[i]; }
-HD void fe_mul_int(fe& r, const fe& a, uint32_t k) { HD_UNROLL for (int i = 0; i < 10; i++) r.n[i] = a.n[i] * k; }
-HD void fe_cmov(fe& r, const fe& a, bool flag) {
-    HD_UNROLL for (int i = 0; i < 10; i++) r.n[i] = flag ? a.n[i] : r.n[i];
-}
-
-// Weak normalisation: any limbs < 2^32 (top < 2^31) -> T.
-HD void fe_norm_weak(fe& r) {
-    uint32_t c = 0;
-    HD_UNROLL for (int i = 0; i < 9; i++) {
-        uint32_t t = r.n[i] + c;  // < 2^32: limbs < 2^32 - 2^6 in every caller
-        r.n[i] = t & HD_M26;
-        c = t >> 26;
+#ifdef HD_BOUND_CHECKS
+    fe_bound_check_values(a);
+    fe_bound_check_values(b);
+    uint64_t nb[9];
+    for (int i = 0; i < 9; i++) {
+        HD_BREQ(b.b[i] <= (uint64_t)K * fe_p_limb(i), "fe_sub_k: subtrahend exceeds K p");
+        nb[i] = a.b[i] + (uint64_t)K * fe_p_limb(i);
+        HD_BREQ(nb[i] < (1ull << 32), "fe_sub_k: limb overflow");
     }
-    uint32_t t9 = r.n[9] + c;
-    r.n[9] = t9 & HD_M22;
-    uint32_t u = t9 >> 22;  // weight 2^256 == 0x1000003D1 (mod p)
-    uint64_t x = (uint64_t)u * 0x3D1u + r.n[0];
-    r.n[0] = (uint32_t)x & HD_M26;
-    uint64_t y = (x >> 26) + ((uint64_t)u << 6) + r.n[1];
-    r.n[1] = (uint32_t)y & HD_M26;
-    r.n[2] += (uint32_t)(y >> 26);
+#endif
+    HD_UNROLL for (int i = 0; i < 9; i++) r.n[i] = a.n[i] + (uint32_t)K * fe_p_limb(i) - b.n[i];
+    HD_B(for (int i = 0; i < 9; i++) r.b[i] = nb[i];)
+}
+HD void fe_sub(fe& r, const fe& a, const fe& b) { fe_sub_k<2>(r, a, b); }
+// 2p - a (a tight): the result is 2T
+HD void fe_neg(fe& r, const fe& a) {
+    fe z;
+    fe_clear(z);
+    fe_sub_k<2>(r, z, a);
+}
+HD void fe_add(fe& r, const fe& a, const fe& b) {
+#ifdef HD_BOUND_CHECKS
+    fe_bound_check_values(a);
+    fe_bound_check_values(b);
+    uint64_t nb[9];
+    for (int i = 0; i < 9; i++) {
+        nb[i] = a.b[i] + b.b[i];
+        HD_BREQ(nb[i] < (1ull << 32), "fe_add: limb overflow");
+    }
+#endif
+    HD_UNROLL for (int i = 0; i < 9; i++) r.n[i] = a.n[i] + b.n[i];
+    HD_B(for (int i = 0; i < 9; i++) r.b[i] = nb[i];)
+}
+HD void fe_mul_int(fe& r, const fe& a, uint32_t k) {
+#ifdef HD_BOUND_CHECKS
+    fe_bound_check_values(a);
+    uint64_t nb[9];
+    for (int i = 0; i < 9; i++) {
+        nb[i] = a.b[i] * k;
+        HD_BREQ(nb[i] < (1ull << 32), "fe_mul_int: limb overflow");
+    }
+#endif
+    HD_UNROLL for (int i = 0; i < 9; i++) r.n[i] = a.n[i] * k;
+    HD_B(for (int i = 0; i < 9; i++) r.b[i] = nb[i];)
+}
+HD void fe_cmov(fe& r, const fe& a, bool flag) {
+    HD_UNROLL for (int i = 0; i < 9; i++) r.n[i] = flag ? a.n[i] : r.n[i];
+    HD_B(for (int i = 0; i < 9; i++) r.b[i] = r.b[i] > a.b[i] ? r.b[i] : a.b[i];)
 }
 
-// Canonical form: every limb < 2^26, value < p.  Input: L (or anything
-// norm_weak accepts).
+// Weak normalisation: limbs <= 2^32 - 9 -> T.  All 32-bit arithmetic.
+HD void fe_norm_weak(fe& r) {
+#ifdef HD_BOUND_CHECKS
+    fe_bound_check_values(r);
+    for (int i = 0; i < 9; i++) HD_BREQ(r.b[i] <= 0xFFFFFFF7ull, "fe_norm_weak: input limb too large");
+#endif
+    uint32_t c = 0;
+    HD_UNROLL for (int i = 0; i < 8; i++) {
+        const uint32_t t = r.n[i] + c;
+        r.n[i] = t & HD_M29;
+        c = t >> 29;
+    }
+    const uint32_t t8 = r.n[8] + c;
+    r.n[8] = t8 & HD_M24;
+    const uint32_t u = t8 >> 24;  // weight 2^256 == 0x1000003D1 (mod p); u < 2^8 + 1
+    const uint32_t x = u * 977u + r.n[0];
+    r.n[0] = x & HD_M29;
+    const uint32_t y = (x >> 29) + (u << 3) + r.n[1];  // 2^32 = 8 * 2^29
+    r.n[1] = y & HD_M29;
+    r.n[2] += y >> 29;  // <= 1
+    HD_B(fe_bound_T(r); r.b[2] = HD_M29 + 1;)
+}
+
+// Canonical form: every limb <= M29 (top <= M24), value < p.
 HD void fe_normalize(fe& r) {
     fe_norm_weak(r);
     uint32_t c = 0;
-    HD_UNROLL for (int i = 0; i < 9; i++) {
-        uint32_t t = r.n[i] + c;
-        r.n[i] = t & HD_M26;
-        c = t >> 26;
+    HD_UNROLL for (int i = 2; i < 8; i++) {
+        const uint32_t t = r.n[i] + c;
+        r.n[i] = t & HD_M29;
+        c = t >> 29;
     }
-    r.n[9] += c;
-    // value >= 2^256 (top > 22 bits) or p <= value < 2^256: subtract p once
-    uint32_t mid = r.n[2] & r.n[3] & r.n[4] & r.n[5] & r.n[6] & r.n[7] & r.n[8];
-    bool ge = (r.n[9] >> 22) != 0 ||
-              (r.n[9] == HD_M22 && mid == HD_M26 &&
+    r.n[8] += c;  // <= 2^24: value < 2^256 + 2^233
+    // value >= p  <=>  (top > M24) or (limbs 2..8 at their maxima and (n1, n0) >= (p1, p0))
+    uint32_t mid = r.n[2] & r.n[3] & r.n[4] & r.n[5] & r.n[6] & r.n[7];
+    bool ge = (r.n[8] >> 24) != 0 ||
+              (r.n[8] == HD_M24 && mid == HD_M29 &&
                (r.n[1] > HD_FP1 || (r.n[1] == HD_FP1 && r.n[0] >= HD_FP0)));
     if (ge) {
         // r - p == r + 0x1000003D1 - 2^256
-        uint32_t t = r.n[0] + 0x3D1u;
-        r.n[0] = t & HD_M26;
-        t = r.n[1] + 0x40u + (t >> 26);  // 2^32 = 2^6 * 2^26
-        r.n[1] = t & HD_M26;
-        c = t >> 26;
-        HD_UNROLL for (int i = 2; i < 9; i++) {
+        uint32_t t = r.n[0] + 977u;
+        r.n[0] = t & HD_M29;
+        t = r.n[1] + 8u + (t >> 29);
+        r.n[1] = t & HD_M29;
+        c = t >> 29;
+        HD_UNROLL for (int i = 2; i < 8; i++) {
             t = r.n[i] + c;
-            r.n[i] = t & HD_M26;
-            c = t >> 26;
+            r.n[i] = t & HD_M29;
+            c = t >> 29;
         }
-        r.n[9] = (r.n[9] + c) & HD_M22;
+        r.n[8] = (r.n[8] + c) & HD_M24;
     }
+    HD_B(for (int i = 0; i < 9; i++) r.b[i] = i == 8 ? HD_M24 : HD_M29;)
 }
 HD void fe_to_le(uint32_t w[8], const fe& a) {  // a canonical
     HD_UNROLL for (int k = 0; k < 8; k++) w[k] = 0;
-    HD_UNROLL for (int i = 0; i < 10; i++) {
-        const int bit = 26 * i, word = bit >> 5, off = bit & 31;
+    HD_UNROLL for (int i = 0; i < 9; i++) {
+        const int bit = 29 * i, word = bit >> 5, off = bit & 31;
         w[word] |= a.n[i] << off;
-        if (off > 6 && word + 1 < 8) w[word + 1] |= a.n[i] >> (32 - off);
+        if (off > 3 && word + 1 < 8) w[word + 1] |= a.n[i] >> (32 - off);
     }
 }
 HD void fe_to_be(uint32_t be[8], const fe& a) {  // a canonical
@@ -216,7 +340,7 @@ HD bool fe_is_zero(const fe& a) {
     fe t = a;
     fe_normalize(t);
     uint32_t o = 0;
-    HD_UNROLL for (int i = 0; i < 10; i++) o |= t.n[i];
+    HD_UNROLL for (int i = 0; i < 9; i++) o |= t.n[i];
     return o == 0;
 }
 HD bool fe_is_odd(const fe& a) {
@@ -224,59 +348,124 @@ HD bool fe_is_odd(const fe& a) {
     fe_normalize(t);
     return t.n[0] & 1u;
 }
-HD bool fe_eq(const fe& a, const fe& b) {  // b must be T
+HD bool fe_eq(const fe& a, const fe& b) {  // b <= 2p limb-wise (T)
     fe d;
-    fe_sub_k<4>(d, a, b);
+    fe_sub_k<2>(d, a, b);
     return fe_is_zero(d);
 }
 
-// Product scanning with the high column folded in as it is produced: column
-// k (weight 2^(26k)) and column k+10 (weight 2^(26k) * 2^260, 2^260 ==
-// 0x400 * 2^26 + 0x3D10 mod p) are accumulated together, so only three
-// 64-bit accumulators are live (low register pressure -> more waves/SIMD).
-// Inputs L (limbs < 2^30, top limb < 2^25.5); output T.
+#ifdef HD_BOUND_CHECKS
+// Interval image of fe_mul_impl: per-limb maxima of the output, and a check
+// that no 64-bit column accumulator can overflow for ANY inputs within the
+// input bounds.  Mirrors the device algorithm step by step.
+static void fe_mul_bounds(uint64_t* ob, const uint64_t* A, const uint64_t* B) {
+    typedef unsigned __int128 u128;
+    const u128 LIM = (u128)1 << 64;
+    u128 chi = 0, clo = 0;
+    uint64_t hprev = 0, r[9];
+    for (int k = 0; k < 9; k++) {
+        u128 d = chi;
+        for (int i = k + 1; i < 9; i++) d += (u128)A[i] * B[k + 9 - i];
+        HD_BREQ(d < LIM, "fe_mul: high column overflow");
+        const uint64_t hk = d > HD_M29 ? HD_M29 : (uint64_t)d;
+        chi = d >> 29;
+        u128 c = clo + (u128)hk * 0x7A20u + (k > 0 ? (u128)hprev * 256u : 0);
+        for (int i = 0; i <= k; i++) c += (u128)A[i] * B[k - i];
+        HD_BREQ(c < LIM, "fe_mul: low column overflow");
+        r[k] = c > HD_M29 ? HD_M29 : (uint64_t)c;
+        clo = c >> 29;
+        hprev = hk;
+    }
+    HD_BREQ(chi == 0, "fe_mul: carry out of the top column");
+    const u128 W = clo + (u128)hprev * 256u;
+    const u128 u = (W << 5) + (r[8] >> 24);
+    HD_BREQ(u < ((u128)1 << 42), "fe_mul: final fold too large");
+    const u128 x = u * 977u + r[0];
+    const u128 y = (x >> 29) + (u << 3) + r[1];
+    for (int i = 0; i < 9; i++) ob[i] = r[i];
+    ob[0] = HD_M29;
+    ob[1] = HD_M29;
+    ob[2] = r[2] + (uint64_t)(y >> 29);
+    ob[8] = HD_M24;
+    for (int i = 0; i < 9; i++) HD_BREQ(ob[i] <= fe_t_limb(i), "fe_mul: output not tight");
+}
+#endif
+
+// Product scanning with the high half folded in as it is produced: column k
+// (weight 2^(29k)) and column k+9 (weight 2^(29k) 2^261, 2^261 == 2^8 2^29 +
+// 0x7A20 mod p) are accumulated side by side, so only two 64-bit accumulator
+// chains are live.  hk (29 bits of column k+9) adds hk * 0x7A20 to column k
+// and hk * 2^8 to column k+1.  Output T.
+#ifdef HD_FE_NOINLINE
+#define HD_FEMUL __host__ __device__ __noinline__
+#else
+#define HD_FEMUL HD
+#endif
 template <bool SQR>
-HD void fe_mul_impl(fe& out, const fe& a, const fe& b) {
-    fe r;               // out may alias a or b
-    uint64_t chi = 0;   // carry of the high columns
-    uint64_t clo = 0;   // carry of the low columns
-    uint64_t pend = 0;  // h_{k-1} * 0x400 (< 2^36), owed to column k
-    HD_UNROLL for (int k = 0; k < 10; k++) {
+HD_FEMUL void fe_mul_impl(fe& out, const fe& a, const fe& b) {
+#ifdef HD_BOUND_CHECKS
+    fe_bound_check_values(a);
+    fe_bound_check_values(b);
+    uint64_t ob[9];
+    fe_mul_bounds(ob, a.b, SQR ? a.b : b.b);
+#endif
+    fe r;  // out may alias a or b
+    // Inputs pass through opaque copies: the AMDGPU backend otherwise carries
+    // known-bits facts (e.g. the 24-bit top limb masked by the producing
+    // multiply) into this one and mis-selects the 64-bit column products when
+    // two multiplies are inlined back to back (wrong results at -O1..-O3,
+    // correct at -O0 and with fe_mul_impl out of line; scripts/fecheck.hip).
+    uint32_t x[9], y[9];
+    HD_UNROLL for (int i = 0; i < 9; i++) x[i] = i == 8 ? opaque_u32(a.n[i]) : a.n[i];
+    if (!SQR) {
+        HD_UNROLL for (int i = 0; i < 9; i++) y[i] = i == 8 ? opaque_u32(b.n[i]) : b.n[i];
+    }
+    uint32_t a2[8];
+    if (SQR) {
+        HD_UNROLL for (int i = 0; i < 8; i++) a2[i] = x[i] << 1;
+    }
+    const uint32_t K1 = opaque_u32(0x7A20u), K2 = opaque_u32(256u);
+    uint64_t chi = 0, clo = 0;
+    uint32_t hprev = 0;
+    HD_UNROLL for (int k = 0; k < 9; k++) {
         uint64_t d = chi;
-        HD_UNROLL for (int i = k + 1; i < 10; i++) {
-            const int j = k + 10 - i;
+        HD_UNROLL for (int i = k + 1; i < 9; i++) {
+            const int j = k + 9 - i;
             if (SQR) {
-                if (i < j) d += (uint64_t)(a.n[i] << 1) * a.n[j];
-                else if (i == j) d += (uint64_t)a.n[i] * a.n[i];
+                if (i < j) d = mad64(a2[i], x[j], d);
+                else if (i == j) d = mad64(x[i], x[i], d);
             } else {
-                d += (uint64_t)a.n[i] * b.n[j];
+                d = mad64(x[i], y[j], d);
             }
         }
-        const uint32_t hk = (uint32_t)d & HD_M26;
-        chi = d >> 26;
-        uint64_t c = clo + pend + (uint64_t)hk * 0x3D10u;
+        const uint32_t hk = opaque_u32((uint32_t)d & HD_M29);
+        chi = d >> 29;
+        uint64_t c = mad64(hk, K1, clo);
+        if (k > 0) c = mad64(hprev, K2, c);
         HD_UNROLL for (int i = 0; i <= k; i++) {
             const int j = k - i;
             if (SQR) {
-                if (i < j) c += (uint64_t)(a.n[i] << 1) * a.n[j];
-                else if (i == j) c += (uint64_t)a.n[i] * a.n[i];
+                if (i < j) c = mad64(a2[i], x[j], c);
+                else if (i == j) c = mad64(x[i], x[i], c);
             } else {
-                c += (uint64_t)a.n[i] * b.n[j];
+                c = mad64(x[i], y[j], c);
             }
         }
-        pend = (uint64_t)hk << 10;
-        r.n[k] = (uint32_t)c & HD_M26;
-        clo = c >> 26;
+        r.n[k] = (uint32_t)c & HD_M29;
+        clo = c >> 29;
+        hprev = hk;
     }
-    // bits >= 2^256: r9's top 4 bits, the low carry and the last fold at 2^260
-    // (chi is 0: top limbs < 2^25.5 keep the highest column < 2^52)
-    uint64_t u = ((clo + pend) << 4) + (r.n[9] >> 22);
-    r.n[9] &= HD_M22;
-    uint64_t x = u * 0x3D1u + r.n[0];
-    r.n[0] = (uint32_t)x & HD_M26;
-    uint64_t y = (x >> 26) + (u << 6) + r.n[1];
-    r.n[1] = (uint32_t)y & HD_M26;
-    r.n[2] += (uint32_t)(y >> 26);
+    // weight 2^261: W = clo + h8 2^8; weight 2^256: u = 32 W + (r8 >> 24) (< 2^42)
+    const uint64_t u = ((clo + ((uint64_t)hprev << 8)) << 5) + (r.n[8] >> 24);
+    r.n[8] &= HD_M24;
+    // fold u (2^32 + 977): u 977 + r0, then u 2^32 = 8 u 2^29 into limb 1
+    uint64_t f0 = mad64((uint32_t)u, 977u, r.n[0]);
+    f0 += (uint64_t)((uint32_t)(u >> 32) * 977u) << 32;
+    r.n[0] = (uint32_t)f0 & HD_M29;
+    const uint64_t f1 = (f0 >> 29) + (u << 3) + r.n[1];
+    r.n[1] = (uint32_t)f1 & HD_M29;
+    r.n[2] += (uint32_t)(f1 >> 29);
+    HD_B(for (int i = 0; i < 9; i++) r.b[i] = ob[i];)
     out = r;
 }
 HD void fe_mul(fe& r, const fe& a, const fe& b) { fe_mul_impl<false>(r, a, b); }

@@ -30,39 +30,50 @@ HD void gej_cmov(gej& r, const gej& a, bool flag) {
     fe_cmov(r.z, a.z, flag);
 }
 
-// Bounds (hd_field.h): point inputs have x, y tight (T) and z <= 2T; y of a
-// table entry may be a fresh negation 4p - y (<= 2^28, fine as a multiplier
-// but normalised before it is ever a subtrahend).  Outputs: x, y T, z 2T.
+// Bounds (hd_field.h): every point coordinate is T, except that the y of a
+// table entry may be a fresh negation 2p - y (2T).  Outputs are T.  The
+// formulas are certified by the host bound tracker (HD_BOUNDS) for all inputs
+// of those classes (tests/test_field_bounds.py).
 
-// Doubling (a = 0), 3M + 4S: D = 4 X Y^2 computed as a product.
+// Doubling (a = 0), 4S + 3M (dbl-2009-l shape with D = (2X)(2Y^2) and
+// 8Y^4 = 2 (2Y^2)^2 so that no limb-wise multiple exceeds 32 bits).
 // inf -> inf (Z3 = 2 Y Z = 0).  r may alias a.
 HD void gej_dbl(gej& r, const gej& a) {
-    fe A, B, C, XB, E, F, t, u;
-    fe_sqr(A, a.x);            // T
-    fe_sqr(B, a.y);            // T
-    fe_sqr(C, B);              // T
-    fe_mul(XB, a.x, B);        // T
-    fe_mul(u, a.y, a.z);       // T
-    fe_mul_int(E, A, 3);       // 3T
-    fe_sqr(F, E);              // T
-    fe_mul_int(t, XB, 8);      // 8T <= 32p
-    fe_sub_k<32>(r.x, F, t);   // < 2^32
-    fe_norm_weak(r.x);         // X3 = E^2 - 8 X Y^2          (T)
-    fe_mul_int(t, XB, 4);      // 4T
-    fe_sub_k<4>(t, t, r.x);    // < 2^29.2
-    fe_mul(t, E, t);           // T
-    fe_mul_int(C, C, 8);       // 8T
-    fe_sub_k<32>(r.y, t, C);
-    fe_norm_weak(r.y);         // Y3 = E (4 X Y^2 - X3) - 8 Y^4 (T)
-    fe_add(r.z, u, u);         // Z3 = 2 Y Z                 (2T)
+    HD_REQUIRE_T(a.x, "gej_dbl: x");
+    HD_REQUIRE_T(a.y, "gej_dbl: y");
+    HD_REQUIRE_T(a.z, "gej_dbl: z");
+    fe A, D, C4, E, t, u;
+    fe_sqr(A, a.x);            // X^2               T
+    fe_sqr(u, a.y);            // B = Y^2           T
+    fe_add(u, u, u);           // 2B                2T
+    fe_add(t, a.x, a.x);       // 2X                2T
+    fe_mul(D, t, u);           // D = 4 X Y^2       T
+    fe_sqr(C4, u);             // 4 Y^4             T
+    fe_add(u, a.y, a.y);       // 2Y                2T
+    fe_mul(r.z, u, a.z);       // Z3 = 2 Y Z        T   (a.z, a.y dead from here)
+    fe_mul_int(E, A, 3);
+    fe_norm_weak(E);           // E = 3 X^2         T
+    fe_sqr(t, E);              // E^2               T
+    fe_add(u, D, D);           // 2D                2T
+    fe_sub_k<3>(r.x, t, u);
+    fe_norm_weak(r.x);         // X3 = E^2 - 2D     T
+    fe_sub_k<2>(t, D, r.x);    // D - X3            3T
+    fe_mul(t, E, t);           // E (D - X3)        T
+    fe_add(u, C4, C4);         // 8 Y^4             2T
+    fe_sub_k<3>(r.y, t, u);
+    fe_norm_weak(r.y);         // Y3                T
 }
 
 HD_NOINLINE void gej_dbl_slow(gej& r, const gej& a) { gej_dbl(r, a); }
 
 // r = a + b, b affine and finite (madd-2007-bl shape, 8M + 3S with
 // Z3 = 2 Z1 H).  Handles a = inf (up front, so b is dead after the first
-// products) and a = +-b.
+// products) and a = +-b.  b.y may be 2T.
 HD void gej_add_ge(gej& r, const gej& a, const ge& b) {
+    HD_REQUIRE_T(a.x, "gej_add_ge: x");
+    HD_REQUIRE_T(a.y, "gej_add_ge: y");
+    HD_REQUIRE_T(a.z, "gej_add_ge: z");
+    HD_REQUIRE_T(b.x, "gej_add_ge: b.x");
     if (fe_is_zero(a.z)) {
         gej o;
         gej_set_ge(o, b);
@@ -73,10 +84,11 @@ HD void gej_add_ge(gej& r, const gej& a, const ge& b) {
     fe z1z1, u2, s2, h, R, t;
     fe_sqr(z1z1, a.z);         // T
     fe_mul(u2, b.x, z1z1);     // T
-    fe_mul(s2, b.y, a.z);      // T
+    fe_mul(s2, b.y, a.z);      // T (2T x T)
     fe_mul(s2, s2, z1z1);      // T
-    fe_sub(h, u2, a.x);        // H = U2 - X1   (< 2^28.4)
-    fe_sub(R, s2, a.y);        // r = S2 - Y1
+    fe_sub_k<2>(h, u2, a.x);
+    fe_norm_weak(h);           // H = U2 - X1       T
+    fe_sub_k<2>(R, s2, a.y);   // r = S2 - Y1       3T
     if (fe_is_zero(h)) {
         // a == +-b (rare): double or cancel
         gej o;
@@ -92,32 +104,37 @@ HD void gej_add_ge(gej& r, const gej& a, const ge& b) {
         return;
     }
     gej o;
-    fe_mul(o.z, a.z, h);
-    fe_add(o.z, o.z, o.z);     // Z3 = 2 Z1 H   (2T)
+    fe_add(t, a.z, a.z);
+    fe_mul(o.z, t, h);         // Z3 = 2 Z1 H       T
     fe hh, i4, j, v;
-    fe_add(R, R, R);           // 2r            (< 2^29.4)
+    fe_norm_weak(R);
+    fe_add(R, R, R);           // 2r                2T
     fe_sqr(hh, h);             // T
-    fe_mul_int(i4, hh, 4);     // I = 4 H^2     (4T)
-    fe_mul(j, h, i4);          // J = H I       (T)
-    fe_mul(v, a.x, i4);        // V = X1 I      (T)
+    fe_mul_int(i4, hh, 4);     // I = 4 H^2         4T
+    fe_mul(j, h, i4);          // J = H I           T
+    fe_mul(v, a.x, i4);        // V = X1 I          T
     fe_sqr(o.x, R);            // T
     fe_add(t, v, v);
-    fe_add(t, t, j);           // 2V + J        (3T <= 8p)
-    fe_sub_k<8>(o.x, o.x, t);
-    fe_norm_weak(o.x);         // X3            (T)
-    fe_sub(t, v, o.x);
-    fe_mul(t, R, t);           // r (V - X3)    (T)
+    fe_add(t, t, j);           // 2V + J            3T
+    fe_sub_k<4>(o.x, o.x, t);
+    fe_norm_weak(o.x);         // X3                T
+    fe_sub_k<2>(t, v, o.x);    // V - X3            3T
+    fe_mul(t, R, t);           // r (V - X3)        T (2T x 3T)
     fe_mul(j, a.y, j);
-    fe_add(j, j, j);           // 2 Y1 J        (2T <= 4p)
-    fe_sub(o.y, t, j);
-    fe_norm_weak(o.y);         // Y3            (T)
+    fe_add(j, j, j);           // 2 Y1 J            2T
+    fe_sub_k<3>(o.y, t, j);
+    fe_norm_weak(o.y);         // Y3                T
     r = o;
 }
 
 // r = a + b, both Jacobian, b finite (add-2007-bl shape, 12M + 4S with
-// Z3 = 2 Z1 Z2 H).  Handles a = inf (up front) and a = +-b; after the
-// H == 0 test only U1, H, r, S1 and Z1 Z2 stay live.
+// Z3 = 2 Z1 Z2 H).  Handles a = inf (up front) and a = +-b.  b.y may be 2T.
 HD void gej_add(gej& r, const gej& a, const gej& b) {
+    HD_REQUIRE_T(a.x, "gej_add: x");
+    HD_REQUIRE_T(a.y, "gej_add: y");
+    HD_REQUIRE_T(a.z, "gej_add: z");
+    HD_REQUIRE_T(b.x, "gej_add: b.x");
+    HD_REQUIRE_T(b.z, "gej_add: b.z");
     if (fe_is_zero(a.z)) {
         gej o = b;
         fe_norm_weak(o.y);
@@ -131,11 +148,12 @@ HD void gej_add(gej& r, const gej& a, const gej& b) {
     fe_mul(u2, b.x, z1z1);
     fe_mul(s1, a.y, b.z);
     fe_mul(s1, s1, z2z2);
-    fe_mul(s2, b.y, a.z);
+    fe_mul(s2, b.y, a.z);      // 2T x T
     fe_mul(s2, s2, z1z1);
     fe_mul(z12, a.z, b.z);
-    fe_sub(h, u2, u1);         // H
-    fe_sub(R, s2, s1);         // r
+    fe_sub_k<2>(h, u2, u1);
+    fe_norm_weak(h);           // H                 T
+    fe_sub_k<2>(R, s2, s1);    // r                 3T
     if (fe_is_zero(h)) {
         gej o;
         if (fe_is_zero(R)) gej_dbl_slow(o, a);
@@ -144,24 +162,24 @@ HD void gej_add(gej& r, const gej& a, const gej& b) {
         return;
     }
     gej o;
-    fe_mul(t, z12, h);
-    fe_add(o.z, t, t);         // Z3 = 2 Z1 Z2 H (2T)
+    fe_norm_weak(R);
+    fe_add(R, R, R);           // 2r                2T
+    fe_add(t, h, h);           // 2H                2T
+    fe_mul(o.z, z12, t);       // Z3 = 2 Z1 Z2 H    T
     fe i, j, v;
-    fe_add(i, h, h);
-    fe_sqr(i, i);              // I = (2H)^2    (T)
-    fe_mul(j, h, i);           // J = H I       (T)
-    fe_add(R, R, R);           // 2r
-    fe_mul(v, u1, i);          // V = U1 I      (T)
+    fe_sqr(i, t);              // I = (2H)^2        T
+    fe_mul(j, h, i);           // J = H I           T
+    fe_mul(v, u1, i);          // V = U1 I          T
     fe_sqr(o.x, R);
     fe_add(t, v, v);
-    fe_add(t, t, j);
-    fe_sub_k<8>(o.x, o.x, t);
-    fe_norm_weak(o.x);         // X3 = r^2 - J - 2V
-    fe_sub(t, v, o.x);
-    fe_mul(t, R, t);
-    fe_mul(s1, s1, j);
+    fe_add(t, t, j);           // 2V + J            3T
+    fe_sub_k<4>(o.x, o.x, t);
+    fe_norm_weak(o.x);         // X3 = r^2 - J - 2V T
+    fe_sub_k<2>(t, v, o.x);    // V - X3            3T
+    fe_mul(t, R, t);           // T
     fe_add(s1, s1, s1);
-    fe_sub(o.y, t, s1);
+    fe_mul(s1, s1, j);         // 2 S1 J            T
+    fe_sub_k<2>(o.y, t, s1);
     fe_norm_weak(o.y);         // Y3 = r (V - X3) - 2 S1 J
     r = o;
 }

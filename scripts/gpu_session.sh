@@ -16,6 +16,8 @@ run() {  # name seconds cmd...
 for step in "$@"; do
   case $step in
     light) run first_light 600 python scripts/first_light.py ;;
+    fieldbench) run fieldbench 120 scripts/fieldbench 3 ;;
+    gtest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     gputest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     gputest_all) run pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 600 python bench.py ;;

@@ -42,15 +42,18 @@ def build_coracle() -> str:
     return out
 
 
-def build_hostmath() -> str:
-    out = os.path.join(NATIVE_DIR, "_build", "libhdhost.so")
+def build_hostmath(bounds: bool = False) -> str:
+    """bounds=True builds with -DHD_BOUNDS: every field element then carries
+    interval bounds that each operation checks (hd_field.h)."""
+    out = os.path.join(NATIVE_DIR, "_build", "libhdhost_bounds.so" if bounds else "libhdhost.so")
     csrc = os.path.join(ROOT, "hyperdrive_amd", "csrc")
     srcs = [os.path.join(NATIVE_DIR, "hd_host_check.cpp")] + [os.path.join(csrc, f) for f in os.listdir(csrc)
                                                               if f.endswith(".h")]
     if _newer(out, srcs):
         os.makedirs(os.path.dirname(out), exist_ok=True)
-        subprocess.run(["g++", "-O2", "-fPIC", "-shared", "-std=c++17", "-Wall", "-Wno-unused-function", "-o", out,
-                        srcs[0]], check=True)
+        flags = ["-DHD_BOUNDS"] if bounds else []
+        subprocess.run(["g++", "-O2", "-fPIC", "-shared", "-std=c++17", "-Wall", "-Wno-unused-function", *flags, "-o",
+                        out, srcs[0]], check=True)
     return out
 
 
@@ -70,6 +73,12 @@ def coracle():
 def hostmath():
     from hostmath import HostMath
     return HostMath(build_hostmath())
+
+
+@pytest.fixture(scope="session")
+def hostmath_bounds():
+    from hostmath import HostMath
+    return HostMath(build_hostmath(bounds=True))
 
 
 @pytest.fixture(scope="session")

@@ -1,6 +1,7 @@
 // Host (g++) build of the device math headers -- TEST HARNESS ONLY.
 // Lets the CPU-only test suite exercise, bit for bit, the arithmetic the
 // gfx950 kernels run (hyperdrive_amd/csrc/*.h), against the oracle.
+#include <stdio.h>
 #include <string.h>
 #include <vector>
 #include "../../hyperdrive_amd/csrc/hd_gen.h"
@@ -182,10 +183,14 @@ extern "C" int hdh_ecmult_trace(const uint8_t* rx, const uint8_t* ry, const uint
     }
     return 0;
 }
-// raw-limb access for the lazy-reduction bound tests
-extern "C" void hdh_fe_raw(int op, const uint32_t* a10, const uint32_t* b10, uint32_t* out10) {
+// raw-limb access for the lazy-reduction bound tests (9 limbs of 29 bits)
+extern "C" void hdh_fe_raw(int op, const uint32_t* a9, const uint32_t* b9, uint32_t* out9) {
     fe a, b, r;
-    for (int i = 0; i < 10; i++) { a.n[i] = a10[i]; b.n[i] = b10[i]; }
+    for (int i = 0; i < 9; i++) { a.n[i] = a9[i]; b.n[i] = b9[i]; }
+#ifdef HD_BOUND_CHECKS
+    fe_bound_exact(a);
+    fe_bound_exact(b);
+#endif
     switch (op) {
         case 0: fe_mul(r, a, b); break;
         case 1: fe_sqr(r, a); break;
@@ -193,8 +198,73 @@ extern "C" void hdh_fe_raw(int op, const uint32_t* a10, const uint32_t* b10, uin
         case 3: r = a; fe_normalize(r); break;
         default: fe_clear(r);
     }
-    for (int i = 0; i < 10; i++) out10[i] = r.n[i];
+    for (int i = 0; i < 9; i++) out9[i] = r.n[i];
 }
+
+#ifdef HD_BOUND_CHECKS
+// ---- bound certification (built with -DHD_BOUNDS) -------------------------
+static int g_bound_fails = 0;
+static char g_bound_first[256] = "";
+extern "C" void hd_bound_fail(const char* what, int line) {
+    if (g_bound_fails++ == 0) snprintf(g_bound_first, sizeof g_bound_first, "%s (hd_field.h/hd_group.h line %d)", what, line);
+}
+extern "C" int hdh_bound_failures(char* first, int cap) {
+    snprintf(first, cap, "%s", g_bound_first);
+    int n = g_bound_fails;
+    g_bound_fails = 0;
+    g_bound_first[0] = 0;
+    return n;
+}
+static void set_class(fe& a, int k) {  // bound = k * T (k = 1 tight, 2 = fresh negation)
+    for (int i = 0; i < 9; i++) a.b[i] = (uint64_t)k * fe_t_limb(i);
+}
+static void point_T(gej& p, int yk = 1) { set_class(p.x, 1); set_class(p.y, yk); set_class(p.z, 1); }
+// Runs every point formula (main and exceptional paths) with operand bounds
+// at their class maxima; returns the number of violated preconditions.
+extern "C" int hdh_bound_certify(const uint8_t* px, const uint8_t* py, const uint8_t* qx, const uint8_t* qy) {
+    ge P, Q;
+    fe_in(P.x, px); fe_in(P.y, py); fe_in(Q.x, qx); fe_in(Q.y, qy);
+    gej a, b, r;
+    gej_set_ge(a, P);
+    gej_dbl(a, a);                      // a: Jacobian with z != 1
+    gej_set_ge(b, Q);
+    gej_dbl(b, b);
+    point_T(a);
+    point_T(b);
+    // doubling
+    gej_dbl(r, a);
+    // mixed addition, b.y tight and negated (2T)
+    ge qn = Q;
+    set_class(qn.x, 1); set_class(qn.y, 1);
+    gej_add_ge(r, a, qn);
+    fe_neg(qn.y, Q.y); set_class(qn.y, 2);
+    gej_add_ge(r, a, qn);
+    // full addition, b.y tight and negated
+    gej bn = b;
+    gej_add(r, a, bn);
+    fe_neg(bn.y, b.y); set_class(bn.y, 2);
+    gej_add(r, a, bn);
+    // exceptional paths: a = inf; a = b (doubling); a = -b (cancel)
+    gej inf; gej_set_inf(inf);
+    gej_add_ge(r, inf, qn);
+    gej_add(r, inf, bn);
+    gej aq; gej_set_ge(aq, Q); point_T(aq);
+    ge qq = Q; set_class(qq.x, 1); set_class(qq.y, 1);
+    gej_add_ge(r, aq, qq);              // a == b
+    fe_neg(qq.y, Q.y); set_class(qq.y, 2);
+    gej_add_ge(r, aq, qq);              // a == -b
+    gej_add(r, b, b);
+    gej bneg = b; fe_neg(bneg.y, b.y); set_class(bneg.y, 2);
+    gej_add(r, b, bneg);
+    // field chains on a T input
+    fe t = P.x, o;
+    set_class(t, 1);
+    fe_inv(o, t);
+    fe_sqrt(o, t);
+    char buf[256];
+    return hdh_bound_failures(buf, sizeof buf);
+}
+#endif
 
 extern "C" int hdh_ecmult_glv(const uint8_t* rx, const uint8_t* ry, const uint8_t* u1b, const uint8_t* u2b, uint8_t* out) {
     ge R;

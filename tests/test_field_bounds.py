@@ -1,78 +1,118 @@
-"""Worst-case limb bounds of the lazily reduced radix-2^26 field
-(hyperdrive_amd/csrc/hd_field.h): multiplier inputs up to L (limbs < 2^30, top
-< 2^25.5), weak normalisation of anything < 2^32, and the T output bound."""
+"""Limb bounds of the lazily reduced radix-2^29 field (hyperdrive_amd/csrc/hd_field.h).
+
+Two layers:
+* certification: the host build with -DHD_BOUNDS carries per-limb interval
+  bounds through every operation and checks every precondition (64-bit
+  column accumulators of fe_mul, 32-bit limbs of additions, K p >= subtrahend
+  of fe_sub_k, tight outputs of the point formulas).  Running each formula
+  once with operands at their class maxima certifies it for ALL inputs of
+  those classes; the full recovery path is run on real messages as well.
+* extremes: concrete worst-case limb values through mul / sqr / weak and full
+  normalisation, checked against Python integers.
+"""
 import ctypes
 import random
 
 import numpy as np
 
 P = 2 ** 256 - 2 ** 32 - 977
-M26 = (1 << 26) - 1
-T_LIMB = (1 << 26) + (1 << 24)
-T_TOP = (1 << 22) + 1
+M29 = (1 << 29) - 1
+M24 = (1 << 24) - 1
+T = [M29, M29, M29 + (1 << 17)] + [M29] * 5 + [M24]
 
 
 def val(limbs):
-    return sum(int(x) << (26 * i) for i, x in enumerate(limbs))
+    return sum(int(x) << (29 * i) for i, x in enumerate(limbs))
 
 
-def raw(hostmath, op, a, b=None):
-    f = hostmath.L.hdh_fe_raw
-    A = (ctypes.c_uint32 * 10)(*a)
-    B = (ctypes.c_uint32 * 10)(*(b or [0] * 10))
-    O = (ctypes.c_uint32 * 10)()
-    f(op, A, B, O)
+def raw(hm, op, a, b=None):
+    A = (ctypes.c_uint32 * 9)(*a)
+    B = (ctypes.c_uint32 * 9)(*(b or [0] * 9))
+    O = (ctypes.c_uint32 * 9)()
+    hm.L.hdh_fe_raw(op, A, B, O)
     return list(O)
 
 
-def _limbs(rng, lo_max, top_max, extreme=False):
-    if extreme:
-        return [lo_max - 1] * 9 + [top_max - 1]
-    return [rng.randrange(lo_max) for _ in range(9)] + [rng.randrange(top_max)]
+def failures(hm):
+    buf = ctypes.create_string_buffer(256)
+    n = hm.L.hdh_bound_failures(buf, 256)
+    return n, buf.value.decode()
 
 
 def is_tight(l):
-    return all(x < T_LIMB for x in l[:9]) and l[9] < T_TOP
+    return all(x <= t for x, t in zip(l, T))
 
 
-L_TOP = int(2 ** 25.5)   # top-limb bound of a multiplier input (largest producer: 2r < 2^25.33)
+def b32(x):
+    return x.to_bytes(32, "big")
+
+
+def test_point_formulas_certified(oracle, hostmath_bounds):
+    hm = hostmath_bounds
+    hm.L.hdh_bound_certify.restype = ctypes.c_int
+    rng = random.Random(5)
+    for _ in range(4):
+        Pp = oracle.point_mul(rng.randrange(1, oracle.N), oracle.G)
+        Qq = oracle.point_mul(rng.randrange(1, oracle.N), oracle.G)
+        n = hm.L.hdh_bound_certify(b32(Pp[0]), b32(Pp[1]), b32(Qq[0]), b32(Qq[1]))
+        assert n == 0, failures(hm)
+
+
+def test_recovery_path_within_bounds(oracle, hostmath_bounds):
+    """every operation of recover() (sqrt, inversions, GLV ladder, affine
+    conversion) on real signatures, with tracked bounds"""
+    hm = hostmath_bounds
+    for i in range(3):
+        sk = oracle.signer_sk(i)
+        d = oracle.sha256(bytes([i]))
+        sig = oracle.sign(sk, d)
+        v, pub = hm.recover(d, sig)
+        assert v == 0
+        assert failures(hm)[0] == 0, failures(hm)
+
+
+def test_mul_bound_checker_rejects_overflow(hostmath_bounds):
+    """the certifier is live: 3T x 3T may overflow a column and must be flagged"""
+    hm = hostmath_bounds
+    a = [3 * t for t in T]
+    raw(hm, 0, a, a)
+    n, what = failures(hm)
+    assert n > 0 and "column" in what
 
 
 def test_mul_sqr_worst_case_inputs(hostmath):
     rng = random.Random(21)
-    cases = [(_limbs(rng, 1 << 30, L_TOP, True), _limbs(rng, 1 << 30, L_TOP, True))]
-    cases += [(_limbs(rng, 1 << 30, L_TOP), _limbs(rng, 1 << 30, L_TOP)) for _ in range(300)]
-    cases += [([M26] * 9 + [(1 << 22) - 1], [M26] * 9 + [(1 << 22) - 1])]
+    cases = [(T, [7 * t for t in T]), ([2 * t for t in T], [3 * t for t in T]), (T, T)]
+    cases += [([rng.randrange(2 * t + 1) for t in T], [rng.randrange(3 * t + 1) for t in T]) for _ in range(300)]
     for a, b in cases:
         r = raw(hostmath, 0, a, b)
         assert val(r) % P == val(a) * val(b) % P
         assert is_tight(r), r
-        s = raw(hostmath, 1, a)
-        assert val(s) % P == val(a) ** 2 % P
-        assert is_tight(s), s
+        if all(x <= 2 * t for x, t in zip(a, T)):
+            s = raw(hostmath, 1, a)
+            assert val(s) % P == val(a) ** 2 % P
+            assert is_tight(s), s
 
 
 def test_weak_and_full_normalisation(hostmath):
     rng = random.Random(22)
-    cases = [[(1 << 32) - (1 << 6) - 1] * 9 + [(1 << 31) - 1], [0] * 10, [M26] * 9 + [(1 << 22) - 1]]
-    # values in [p, 2^256) and just above 2^256
-    for v in [P, P + 1, 2 ** 256 - 1, 2 ** 256 + 5, 2 ** 256 + 0x1000003D0]:
-        cases.append([(v >> (26 * i)) & M26 for i in range(9)] + [v >> 234])
-    cases += [[rng.randrange((1 << 32) - (1 << 6)) for _ in range(9)] + [rng.randrange(1 << 31)] for _ in range(300)]
+    cases = [[0xFFFFFFF7] * 9, [0] * 9, T, [M29] * 8 + [M24]]
+    for v in [P, P + 1, 2 ** 256 - 1, 2 ** 256 + 5, 2 ** 256 + 0x1000003D0, 2 * P - 1]:
+        cases.append([(v >> (29 * i)) & M29 for i in range(8)] + [v >> 232])
+    cases += [[rng.randrange(0xFFFFFFF8) for _ in range(9)] for _ in range(300)]
     for a in cases:
         w = raw(hostmath, 2, a)
         assert val(w) % P == val(a) % P
         assert is_tight(w), (a, w)
         n = raw(hostmath, 3, a)
         assert val(n) == val(a) % P
-        assert all(x <= M26 for x in n[:9]) and n[9] < (1 << 22)
+        assert all(x <= M29 for x in n[:8]) and n[8] <= M24
 
 
 def test_point_ops_on_extreme_points(oracle, hostmath):
     """ecmult with points whose coordinates have long runs of 1-bits."""
     rng = random.Random(23)
     for _ in range(6):
-        # pick x with many ones, lift to a point
         while True:
             x = (P - 1 - rng.randrange(1 << 20)) if rng.random() < 0.5 else (2 ** 255 - 1 - rng.randrange(1 << 20))
             R = oracle.lift_x(x % P, 1)

@@ -127,6 +127,116 @@ HD void gej_add_ge(gej& r, const gej& a, const ge& b) {
     r = o;
 }
 
+// Mixed addition on an isomorphic curve ("effective affine", as in
+// libsecp256k1's ecmult): b is affine on E: y^2 = x^3 + 7 while a lives on
+// E': y^2 = x^3 + 7 zg^6, where a point (x, y) of E is (x zg^2, y zg^3).
+// Substituting az = a.z zg for a.z in U2 = b.x az^2, S2 = b.y az^3 adds the
+// image of b without computing it; Z3 = 2 a.z H as usual.  One multiply more
+// than gej_add_ge.  The rare paths (a = inf, a = +-b) build the image
+// explicitly.
+HD void gej_add_ge_zinv(gej& r, const gej& a, const ge& b, const fe& zg) {
+    HD_REQUIRE_T(a.x, "gej_add_ge_zinv: x");
+    HD_REQUIRE_T(a.y, "gej_add_ge_zinv: y");
+    HD_REQUIRE_T(a.z, "gej_add_ge_zinv: z");
+    HD_REQUIRE_T(b.x, "gej_add_ge_zinv: b.x");
+    HD_REQUIRE_T(zg, "gej_add_ge_zinv: zg");
+    if (fe_is_zero(a.z)) {
+        gej o;
+        fe z2;
+        fe_sqr(z2, zg);
+        fe_mul(o.x, b.x, z2);
+        fe_mul(z2, z2, zg);
+        fe_mul(o.y, b.y, z2);
+        fe_set_u32(o.z, 1);
+        r = o;
+        return;
+    }
+    fe az, z1z1, u2, s2, h, R, t;
+    fe_mul(az, a.z, zg);       // T
+    fe_sqr(z1z1, az);          // T
+    fe_mul(u2, b.x, z1z1);     // T
+    fe_mul(s2, b.y, az);       // T (2T x T)
+    fe_mul(s2, s2, z1z1);      // T
+    fe_sub_k<2>(h, u2, a.x);
+    fe_norm_weak(h);           // H = U2 - X1       T
+    fe_sub_k<2>(R, s2, a.y);   // r = S2 - Y1       3T
+    if (fe_is_zero(h)) {
+        gej o;
+        if (fe_is_zero(R)) {
+            gej bj;
+            fe z2;
+            fe_sqr(z2, zg);
+            fe_mul(bj.x, b.x, z2);
+            fe_mul(z2, z2, zg);
+            fe_mul(bj.y, b.y, z2);
+            fe_set_u32(bj.z, 1);
+            gej_dbl_slow(o, bj);
+        } else {
+            gej_set_inf(o);
+        }
+        r = o;
+        return;
+    }
+    gej o;
+    fe_add(t, a.z, a.z);
+    fe_mul(o.z, t, h);         // Z3 = 2 Z1 H       T
+    fe hh, i4, j, v;
+    fe_norm_weak(R);
+    fe_add(R, R, R);           // 2r                2T
+    fe_sqr(hh, h);
+    fe_mul_int(i4, hh, 4);     // I = 4 H^2         4T
+    fe_mul(j, h, i4);          // J = H I           T
+    fe_mul(v, a.x, i4);        // V = X1 I          T
+    fe_sqr(o.x, R);
+    fe_add(t, v, v);
+    fe_add(t, t, j);           // 2V + J            3T
+    fe_sub_k<4>(o.x, o.x, t);
+    fe_norm_weak(o.x);         // X3                T
+    fe_sub_k<2>(t, v, o.x);    // V - X3            3T
+    fe_mul(t, R, t);           // r (V - X3)        T
+    fe_mul(j, a.y, j);
+    fe_add(j, j, j);           // 2 Y1 J            2T
+    fe_sub_k<3>(o.y, t, j);
+    fe_norm_weak(o.y);         // Y3                T
+    r = o;
+}
+
+// r = a + b (b affine) for the table build, also returning the z ratio
+// zr = Z3 / Z1 = 2 H.  a != inf, a != +-b (multiples 2R..7R of a point of
+// prime order n never hit those).
+HD void gej_add_ge_zr(gej& r, const gej& a, const ge& b, fe& zr) {
+    fe z1z1, u2, s2, h, R, t;
+    fe_sqr(z1z1, a.z);
+    fe_mul(u2, b.x, z1z1);
+    fe_mul(s2, b.y, a.z);
+    fe_mul(s2, s2, z1z1);
+    fe_sub_k<2>(h, u2, a.x);
+    fe_norm_weak(h);
+    fe_sub_k<2>(R, s2, a.y);
+    gej o;
+    fe_add(zr, h, h);          // 2H                2T
+    fe_mul(o.z, a.z, zr);      // Z3 = 2 Z1 H       T
+    fe hh, i4, j, v;
+    fe_norm_weak(R);
+    fe_add(R, R, R);
+    fe_sqr(hh, h);
+    fe_mul_int(i4, hh, 4);
+    fe_mul(j, h, i4);
+    fe_mul(v, a.x, i4);
+    fe_sqr(o.x, R);
+    fe_add(t, v, v);
+    fe_add(t, t, j);
+    fe_sub_k<4>(o.x, o.x, t);
+    fe_norm_weak(o.x);
+    fe_sub_k<2>(t, v, o.x);
+    fe_mul(t, R, t);
+    fe_mul(j, a.y, j);
+    fe_add(j, j, j);
+    fe_sub_k<3>(o.y, t, j);
+    fe_norm_weak(o.y);
+    r = o;
+}
+
 // r = a + b, both Jacobian, b finite (add-2007-bl shape, 12M + 4S with
 // Z3 = 2 Z1 Z2 H).  Handles a = inf (up front) and a = +-b.  b.y may be 2T.
 HD void gej_add(gej& r, const gej& a, const gej& b) {
@@ -332,21 +442,50 @@ HD void fe_beta(fe& b) {
     fe_from_le(b, BETA);
 }
 
-// Q = u1 G + u2 R with the endomorphism.  gtab[0..127] = (k+1) G,
-// gtab[128..255] = (k+1) lambda G (affine).  Per-lane tables of (k+1) R and
-// (k+1) lambda R (Jacobian) live in scratch.
-template <typename GTab>
-HD void ecmult_glv(gej& out, const ge& R, const sc& u1, const sc& u2, GTab gtab) {
-    gej rt[HD_RTAB_N], lt[HD_RTAB_N];
-    gej_set_ge(rt[0], R);
-    gej_dbl(rt[1], rt[0]);
-    HD_NOUNROLL for (int k = 2; k < HD_RTAB_N; k++) gej_add_ge(rt[k], rt[k - 1], R);
+// Per-lane table of 1R..8R, all brought to one Jacobian Z (zg), so they are
+// affine points of the isomorphic curve E' (gej_add_ge_zinv): the R-side
+// ladder additions become mixed additions.  z ratios of the building chain
+// (dbl, then madd) give the rescale factors walking back from 8R.
+// Returns zg (T); tab[k] = (k+1) R on E', lam[k] = lambda (k+1) R on E'.
+HD void build_rtab_iso(ge tab[HD_RTAB_N], ge lam[HD_RTAB_N], fe& zg, const ge& R) {
+    gej p[HD_RTAB_N];
+    fe zr[HD_RTAB_N];          // zr[k] = Z_k / Z_{k-1}
+    gej_set_ge(p[0], R);
+    gej_dbl(p[1], p[0]);
+    fe_add(zr[1], R.y, R.y);   // Z_1 = 2 Y Z_0, Z_0 = 1
+    HD_NOUNROLL for (int k = 2; k < HD_RTAB_N; k++) gej_add_ge_zr(p[k], p[k - 1], R, zr[k]);
+    zg = p[HD_RTAB_N - 1].z;
+    tab[HD_RTAB_N - 1].x = p[HD_RTAB_N - 1].x;
+    tab[HD_RTAB_N - 1].y = p[HD_RTAB_N - 1].y;
+    fe f = zr[HD_RTAB_N - 1];  // Z_7 / Z_6
+    fe_norm_weak(f);
+    HD_NOUNROLL for (int k = HD_RTAB_N - 2; k >= 0; k--) {
+        // f = Z_7 / Z_k
+        fe f2, f3;
+        fe_sqr(f2, f);
+        fe_mul(f3, f2, f);
+        fe_mul(tab[k].x, p[k].x, f2);
+        fe_mul(tab[k].y, p[k].y, f3);
+        if (k > 0) fe_mul(f, f, zr[k]);
+    }
     fe beta;
     fe_beta(beta);
     HD_NOUNROLL for (int k = 0; k < HD_RTAB_N; k++) {
-        lt[k] = rt[k];
-        fe_mul(lt[k].x, rt[k].x, beta);
+        fe_mul(lam[k].x, tab[k].x, beta);
+        lam[k].y = tab[k].y;
     }
+}
+
+// Q = u1 G + u2 R with the endomorphism.  gtab[0..127] = (k+1) G,
+// gtab[128..255] = (k+1) lambda G (affine on E).  The accumulator runs on the
+// isomorphic curve E' of the R table (build_rtab_iso); the G additions map
+// their point on the fly (gej_add_ge_zinv) and Q is mapped back at the end
+// (Z *= zg).
+template <typename GTab>
+HD void ecmult_glv(gej& out, const ge& R, const sc& u1, const sc& u2, GTab gtab) {
+    ge rt[HD_RTAB_N], lt[HD_RTAB_N];
+    fe zg;
+    build_rtab_iso(rt, lt, zg, R);
     int16_t dra[HD_GLV_NWIN_R], drb[HD_GLV_NWIN_R], dga[HD_GLV_NWIN_G], dgb[HD_GLV_NWIN_G];
     {
         sc k1, k2;
@@ -376,20 +515,21 @@ HD void ecmult_glv(gej& out, const ge& R, const sc& u1, const sc& u2, GTab gtab)
                 ge t = gtab[half * HD_GTAB_N + (ad == 0 ? 0 : ad - 1)];
                 if (d < 0) fe_neg(t.y, t.y);
                 gej s;
-                gej_add_ge(s, acc, t);
+                gej_add_ge_zinv(s, acc, t, zg);
                 gej_cmov(acc, s, d != 0);
             }
         }
         HD_NOUNROLL for (int half = 0; half < 2; half++) {
             const int d = half ? drb[j] : dra[j];
             const int ad = d < 0 ? -d : d;
-            gej t = half ? lt[ad == 0 ? 0 : ad - 1] : rt[ad == 0 ? 0 : ad - 1];
+            ge t = half ? lt[ad == 0 ? 0 : ad - 1] : rt[ad == 0 ? 0 : ad - 1];
             if (d < 0) fe_neg(t.y, t.y);
             gej s;
-            gej_add(s, acc, t);
+            gej_add_ge(s, acc, t);
             gej_cmov(acc, s, d != 0);
         }
     }
+    fe_mul(acc.z, acc.z, zg);  // back from E' to E
     out = acc;
 }
 

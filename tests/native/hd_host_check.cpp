@@ -206,7 +206,10 @@ extern "C" void hdh_fe_raw(int op, const uint32_t* a9, const uint32_t* b9, uint3
 static int g_bound_fails = 0;
 static char g_bound_first[256] = "";
 extern "C" void hd_bound_fail(const char* what, int line) {
-    if (g_bound_fails++ == 0) snprintf(g_bound_first, sizeof g_bound_first, "%s (hd_field.h/hd_group.h line %d)", what, line);
+    if (g_bound_fails++ == 0) {
+        snprintf(g_bound_first, sizeof g_bound_first, "%s (hd_field.h/hd_group.h line %d)", what, line);
+        fprintf(stderr, "bound violation: %s\n", g_bound_first);
+    }
 }
 extern "C" int hdh_bound_failures(char* first, int cap) {
     snprintf(first, cap, "%s", g_bound_first);
@@ -256,6 +259,15 @@ extern "C" int hdh_bound_certify(const uint8_t* px, const uint8_t* py, const uin
     gej_add(r, b, b);
     gej bneg = b; fe_neg(bneg.y, b.y); set_class(bneg.y, 2);
     gej_add(r, b, bneg);
+    // isomorphic-curve additions (G side of the ladder) and the R table build
+    fe zg = b.z; set_class(zg, 1);
+    gej_add_ge_zinv(r, a, qn, zg);
+    qn.y = Q.y; set_class(qn.y, 1);
+    gej_add_ge_zinv(r, a, qn, zg);
+    gej_add_ge_zinv(r, inf, qn, zg);
+    ge rt[HD_RTAB_N], lt[HD_RTAB_N];
+    build_rtab_iso(rt, lt, zg, P);
+    for (int k = 0; k < HD_RTAB_N; k++) { fe_require_T(rt[k].x, "rtab x"); fe_require_T(rt[k].y, "rtab y"); }
     // field chains on a T input
     fe t = P.x, o;
     set_class(t, 1);

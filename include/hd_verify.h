@@ -116,7 +116,8 @@ int hd_verify_batch_device(hd_ctx* ctx, const hd_batch* dbatch, uint8_t* d_verdi
  * Catcher.CatchDoublePrevote/Precommit (process.go:838-843, 875-880).
  * All output arrays are caller-owned with the given capacities. */
 typedef struct {
-    /* (height, round, type, value) groups, sorted by (h, r, type, value bytes) */
+    /* (height, round, type, value) groups, in the batch order of each group's
+     * first message (deterministic) */
     uint32_t cap_counts;
     uint32_t n_counts;
     int64_t* count_height;
@@ -124,7 +125,8 @@ typedef struct {
     uint8_t* count_type;
     uint32_t* count_rep;   /* batch index of a message with that value */
     uint32_t* count_n;     /* number of first-wins votes for the value  */
-    /* (height, round) groups, sorted by (h, r) */
+    /* (height, round) groups, in the batch order of each round's first
+     * candidate */
     uint32_t cap_hr;
     uint32_t n_hr;
     int64_t* hr_height;
@@ -140,15 +142,14 @@ typedef struct {
 int hd_tally(hd_ctx* ctx, const hd_batch* batch, const uint8_t* verdict, hd_tally_out* out);
 
 /* Same on device-resident inputs (pointers as in hd_verify_batch_device);
- * d_signer: the signer indices hd_verify_batch_device produced, or NULL (then
- * From is looked up again).  Results land in the host arrays of `out`;
- * synchronises `stream`. */
+ * d_signer is accepted for ABI stability and ignored: the logs are keyed by
+ * From itself, which equals the recovered signatory of every VALID message.
+ * Results land in the host arrays of `out`; synchronises `stream`. */
 int hd_tally_device(hd_ctx* ctx, const hd_batch* dbatch, const uint8_t* d_verdict, const int32_t* d_signer,
                     hd_tally_out* out, void* stream);
 
 /* Same, with validity given as the valid bitmap of hd_verify_batch_device
- * (e.g. after an all-gather of per-GPU bitmaps over RCCL); signer indices are
- * looked up from From. */
+ * (e.g. after an all-gather of per-GPU bitmaps over RCCL). */
 int hd_tally_device_bitmap(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* d_valid_bitmap, hd_tally_out* out,
                            void* stream);
 

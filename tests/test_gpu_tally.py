@@ -1,0 +1,118 @@
+"""GPU tally (hd_tally / hd_tally_device_bitmap, through the C ABI) against the
+oracle's restatement of process.go's first-wins logs and count loops
+(process.go:823-892; 486-494, 534, 574-582, 626-632, 658, 696-702, 751).
+
+Cases: the process_test-style threshold scenarios (tests/tally_cases.py), a
+C5-style 64k adversarial batch with duplicates and double votes, the C3
+shape (1000 signatories, 64 rounds, proposes interleaved), a heavy-collision
+batch (few rounds, many duplicates) and the empty / no-candidate edges."""
+import numpy as np
+import pytest
+
+from hyperdrive_amd import quorum
+from tally_cases import scenarios
+from util import from_np, to_np
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def verifier(gpu):
+    v = gpu.Verifier(0)
+    yield v
+    v.close()
+
+
+def _same(tal, ot):
+    assert tal.count == ot.count
+    assert tal.distinct == ot.distinct
+    assert tal.distinct_any == ot.distinct_any
+    assert tal.dup.tolist() == ot.dup
+
+
+@pytest.mark.parametrize("sc", scenarios(), ids=lambda s: s.name)
+def test_scenarios_match_oracle(verifier, oracle, sc):
+    b = to_np(sc.b)
+    verdicts = np.array(sc.verdicts(), np.uint8)
+    tal = verifier.tally(b, verdicts)
+    ot = oracle.tally(sc.b, sc.verdicts())
+    _same(tal, ot)
+    for h, r, pvalue, pvalid, want in sc.expect:
+        got = quorum.decide(tal, h, r, sc.f, pvalue, pvalid)
+        assert got == oracle.decide_round(ot, h, r, sc.f, pvalue, pvalid)
+        for k, v in want.items():
+            assert got[k] == v, (sc.name, k)
+
+
+@pytest.mark.parametrize("kind,n,S,adv", [(0, 65536, 100, 30), (1, 128064, 1000, 10)])
+def test_generated_batches_match_oracle(verifier, oracle, kind, n, S, adv):
+    """GPU verify -> GPU tally == oracle tally over the same verdicts; the
+    C3 shape (kind 1) is the 1000-signatory, 64-round config."""
+    from hyperdrive_amd.device import generate
+    ks = verifier.gen_keys(S)
+    verifier.set_signatories(ks[0])
+    db, _, _ = generate(verifier, kind, n, S, adv, keys=ks)
+    hb = db.to_host()
+    res, tal = verifier.process_batch(hb)
+    ot = oracle.tally(from_np(hb), res.verdict.tolist())
+    _same(tal, ot)
+    f = quorum.thresholds(S)[0]
+    for (h, r) in list(ot.distinct_any)[:50]:
+        pv = oracle.canonical_value(h, r)
+        assert quorum.decide(tal, h, r, f, pv, True) == oracle.decide_round(ot, h, r, f, pv, True)
+
+
+def test_heavy_collisions(verifier, oracle):
+    """3 rounds, 40 signers, every signer votes ~25 times per (round, type) with
+    a few values: long probe chains in every table, most votes duplicates."""
+    rng = np.random.default_rng(7)
+    n = 6000
+    sigs = [oracle.sha256(b"c" + bytes([k])) for k in range(40)]
+    vals = [oracle.sha256(b"v" + bytes([k])) for k in range(3)] + [bytes(32)]
+    ob = oracle.Batch()
+    for i in range(n):
+        ob.append(int(rng.integers(2, 4)), int(rng.integers(0, 2)), int(rng.integers(0, 2)), -1,
+                  vals[int(rng.integers(0, 4))], sigs[int(rng.integers(0, 40))], bytes(65))
+    verdicts = [oracle.VALID if rng.random() < 0.9 else oracle.BAD_RS for _ in range(n)]
+    tal = verifier.tally(to_np(ob), np.array(verdicts, np.uint8))
+    _same(tal, oracle.tally(ob, verdicts))
+
+
+def test_no_candidates_and_single(verifier, oracle):
+    ob = oracle.Batch()
+    for t in (1, 2, 3):
+        ob.append(t, 1, 0, -1, bytes(32), oracle.sha256(b"x"), bytes(65))
+    verdicts = [oracle.VALID, oracle.BAD_RS, oracle.NOT_ADMITTED]     # a propose is never a candidate
+    tal = verifier.tally(to_np(ob), np.array(verdicts, np.uint8))
+    _same(tal, oracle.tally(ob, verdicts))
+    assert tal.count == {} and tal.distinct_any == {}
+    verdicts = [oracle.VALID] * 3
+    tal = verifier.tally(to_np(ob), np.array(verdicts, np.uint8))
+    _same(tal, oracle.tally(ob, verdicts))
+
+
+def test_bitmap_entry_equals_verdict_entry(verifier, oracle):
+    """hd_tally_device_bitmap (the multi-GPU path after the all-gather) gives
+    the same tally as hd_tally on the verdicts."""
+    import ctypes
+    import torch
+    from hyperdrive_amd import _lib
+    from hyperdrive_amd.device import generate, work_stream
+    n, S = 8192, 50
+    ks = verifier.gen_keys(S)
+    verifier.set_signatories(ks[0])
+    db, _, _ = generate(verifier, 0, n, S, 40, keys=ks)
+    hb = db.to_host()
+    res = verifier.verify_batch(hb)
+    ref = verifier.tally(hb, res.verdict)
+    bm = torch.from_numpy(res.valid_bitmap.view(np.int32)).cuda()
+    t, a = verifier._tally_struct(n)
+    lib = _lib.load()
+    cs = db.c_struct()
+    torch.cuda.synchronize()
+    rc = lib.hd_tally_device_bitmap(verifier.handle, ctypes.byref(cs), bm.data_ptr(), ctypes.byref(t),
+                                    work_stream().cuda_stream)
+    assert rc == 0
+    got = verifier._tally_result(hb, t, a)
+    assert got.count == ref.count and got.distinct == ref.distinct and got.distinct_any == ref.distinct_any
+    assert got.dup.tolist() == ref.dup.tolist()

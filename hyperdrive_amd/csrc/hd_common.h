@@ -12,10 +12,12 @@
 #define HD __host__ __device__ __forceinline__
 #define HD_MEMBER __host__ __device__ __forceinline__
 #define HD_NOINLINE static __host__ __device__ __noinline__
+#define HD_HOSTONLY static inline __host__
 #else
 #define HD static inline
 #define HD_MEMBER inline
 #define HD_NOINLINE static
+#define HD_HOSTONLY static inline
 #endif
 
 #if defined(__HIP_DEVICE_COMPILE__)

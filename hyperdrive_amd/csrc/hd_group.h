@@ -434,7 +434,9 @@ HD int booth_digit160(const uint32_t a[5], int j, bool neg) {
 }
 
 #define HD_GLV_NWIN_R 33   // 4-bit windows over 132 bits
-#define HD_GLV_NWIN_G 17   // 8-bit windows over 136 bits
+#define HD_WG_GLV 12       // G window of the GLV ladder (= 3 R windows)
+#define HD_GLV_NWIN_G 11   // 12-bit windows over 132 bits
+#define HD_GLV_GTAB_N (1 << (HD_WG_GLV - 1))  // 2048 affine multiples per base
 
 HD void fe_beta(fe& b) {
     const uint32_t BETA[8] = {0x719501EEu, 0xC1396C28u, 0x12F58995u, 0x9CF04975u,
@@ -476,8 +478,9 @@ HD void build_rtab_iso(ge tab[HD_RTAB_N], ge lam[HD_RTAB_N], fe& zg, const ge& R
     }
 }
 
-// Q = u1 G + u2 R with the endomorphism.  gtab[0..127] = (k+1) G,
-// gtab[128..255] = (k+1) lambda G (affine on E).  The accumulator runs on the
+// Q = u1 G + u2 R with the endomorphism.  gtab[0..2047] = (k+1) G,
+// gtab[2048..4095] = (k+1) lambda G (affine on E, 288 KiB: read through the
+// L2, 72 bytes per G addition).  The accumulator runs on the
 // isomorphic curve E' of the R table (build_rtab_iso); the G additions map
 // their point on the fly (gej_add_ge_zinv) and Q is mapped back at the end
 // (Z *= zg).
@@ -498,9 +501,9 @@ HD void ecmult_glv(gej& out, const ge& R, const sc& u1, const sc& u2, GTab gtab)
         HD_UNROLL for (int j = 0; j < HD_GLV_NWIN_R; j++) drb[j] = (int16_t)booth_digit160<HD_WR>(a, j, neg);
         sc_split_lambda(k1, k2, u1);
         neg = sc_signed_abs(a, k1);
-        HD_UNROLL for (int j = 0; j < HD_GLV_NWIN_G; j++) dga[j] = (int16_t)booth_digit160<HD_WG>(a, j, neg);
+        HD_UNROLL for (int j = 0; j < HD_GLV_NWIN_G; j++) dga[j] = (int16_t)booth_digit160<HD_WG_GLV>(a, j, neg);
         neg = sc_signed_abs(a, k2);
-        HD_UNROLL for (int j = 0; j < HD_GLV_NWIN_G; j++) dgb[j] = (int16_t)booth_digit160<HD_WG>(a, j, neg);
+        HD_UNROLL for (int j = 0; j < HD_GLV_NWIN_G; j++) dgb[j] = (int16_t)booth_digit160<HD_WG_GLV>(a, j, neg);
     }
     gej acc;
     gej_set_inf(acc);
@@ -508,11 +511,11 @@ HD void ecmult_glv(gej& out, const ge& R, const sc& u1, const sc& u2, GTab gtab)
         if (j != HD_GLV_NWIN_R - 1) {
             HD_NOUNROLL for (int k = 0; k < HD_WR; k++) gej_dbl(acc, acc);
         }
-        if ((j & 1) == 0) {
+        if (j % 3 == 0) {
             HD_NOUNROLL for (int half = 0; half < 2; half++) {
-                const int d = half ? dgb[j >> 1] : dga[j >> 1];
+                const int d = half ? dgb[j / 3] : dga[j / 3];
                 const int ad = d < 0 ? -d : d;
-                ge t = gtab[half * HD_GTAB_N + (ad == 0 ? 0 : ad - 1)];
+                ge t = gtab[half * HD_GLV_GTAB_N + (ad == 0 ? 0 : ad - 1)];
                 if (d < 0) fe_neg(t.y, t.y);
                 gej s;
                 gej_add_ge_zinv(s, acc, t, zg);
@@ -533,9 +536,10 @@ HD void ecmult_glv(gej& out, const ge& R, const sc& u1, const sc& u2, GTab gtab)
     out = acc;
 }
 
-// All multiples 1G..128G in affine form, followed (when tab has room for
-// 2 * HD_GTAB_N entries and with_lambda) by lambda * those = (beta x, y).
-HD void build_gtab(ge* tab) {
+// Multiples 1G..nG in affine form (canonical), by one chain of additions and
+// a Montgomery batch inversion of the Z coordinates (one modular inversion
+// for the whole table).  Host-side precomputation.
+HD_HOSTONLY void build_gmultiples(ge* tab, int n) {
     ge g;
     const uint32_t GX[8] = {0x79BE667Eu, 0xF9DCBBACu, 0x55A06295u, 0xCE870B07u,
                             0x029BFCDBu, 0x2DCE28D9u, 0x59F2815Bu, 0x16F81798u};
@@ -543,30 +547,51 @@ HD void build_gtab(ge* tab) {
                             0xFD17B448u, 0xA6855419u, 0x9C47D08Fu, 0xFB10D4B8u};
     fe_from_be(g.x, GX);
     fe_from_be(g.y, GY);
+    tab[0] = g;
+    if (n < 2) return;
+    fe* z = new fe[n];
+    fe* pre = new fe[n];
     gej acc;
     gej_set_ge(acc, g);
-    tab[0] = g;
-    for (int k = 1; k < HD_GTAB_N; k++) {
+    for (int k = 1; k < n; k++) {
         if (k == 1) gej_dbl(acc, acc);
         else gej_add_ge(acc, acc, g);
+        tab[k].x = acc.x;  // Jacobian X, Y until the pass below
+        tab[k].y = acc.y;
+        z[k] = acc.z;
+        if (k == 1) pre[1] = z[1];
+        else fe_mul(pre[k], pre[k - 1], z[k]);
+    }
+    fe inv;
+    fe_inv_divsteps(inv, pre[n - 1]);  // (Z_1 ... Z_{n-1})^-1
+    for (int k = n - 1; k >= 1; k--) {
         fe zi, zi2, zi3;
-        fe_inv_divsteps(zi, acc.z);
+        if (k > 1) {
+            fe_mul(zi, inv, pre[k - 1]);
+            fe_mul(inv, inv, z[k]);    // (Z_1 ... Z_{k-1})^-1
+        } else {
+            zi = inv;
+        }
         fe_sqr(zi2, zi);
         fe_mul(zi3, zi2, zi);
-        fe_mul(tab[k].x, acc.x, zi2);
-        fe_mul(tab[k].y, acc.y, zi3);
+        fe_mul(tab[k].x, tab[k].x, zi2);
+        fe_mul(tab[k].y, tab[k].y, zi3);
         fe_normalize(tab[k].x);
         fe_normalize(tab[k].y);
     }
+    delete[] z;
+    delete[] pre;
 }
-HD void build_gtab_glv(ge* tab) {
-    build_gtab(tab);
+// [1G .. HD_GLV_GTAB_N G] followed by lambda times those = (beta x, y).  The
+// first HD_GTAB_N entries double as the 8-bit-window table of ecmult_gen.
+HD_HOSTONLY void build_gtab_glv(ge* tab) {
+    build_gmultiples(tab, HD_GLV_GTAB_N);
     fe beta;
     fe_beta(beta);
-    for (int k = 0; k < HD_GTAB_N; k++) {
-        fe_mul(tab[HD_GTAB_N + k].x, tab[k].x, beta);
-        fe_normalize(tab[HD_GTAB_N + k].x);
-        tab[HD_GTAB_N + k].y = tab[k].y;
+    for (int k = 0; k < HD_GLV_GTAB_N; k++) {
+        fe_mul(tab[HD_GLV_GTAB_N + k].x, tab[k].x, beta);
+        fe_normalize(tab[HD_GLV_GTAB_N + k].x);
+        tab[HD_GLV_GTAB_N + k].y = tab[k].y;
     }
 }
 
@@ -577,7 +602,7 @@ HD void build_gtab_glv(ge* tab) {
 //   V&2 and r >= p - n -> NO_POINT; x^3+7 non-residue -> NO_POINT;
 //   Q = inf -> INFINITY.  High-S accepted.  m = digest mod n.
 // On VALID writes the affine Q (x, y), canonical.
-// gtab: 2 * HD_GTAB_N entries (build_gtab_glv).
+// gtab: 2 * HD_GLV_GTAB_N entries (build_gtab_glv).
 template <typename GTab>
 HD uint8_t recover(fe& qx, fe& qy, const uint32_t digest_be[8], const uint32_t r_be[8],
                    const uint32_t s_be[8], uint32_t v, GTab gtab) {

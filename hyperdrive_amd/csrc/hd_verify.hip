@@ -4,8 +4,9 @@
 // Kernels
 //   k_verify  one message per lane: digest -> secp256k1 recover -> signatory
 //             -> Equal(From) -> admitted lookup.  INT32-VALU bound (no MFMA:
-//             nothing here is a dense contraction).  The 8 KiB table of
-//             1G..128G is staged in LDS once per workgroup; the admitted set
+//             nothing here is a dense contraction).  The tables of
+//             1G..2048G and lambda times those (288 KiB) are read
+//             through the L2 by the 12-bit G windows; the admitted set
 //             (sorted, 32 B entries) is read through L2.  A valid-bitmap word
 //             pair per wavefront comes from one __ballot.
 //   (k_gen / k_keys, the synthetic workload, live in hd_genk.hip)
@@ -49,13 +50,6 @@ __global__ __launch_bounds__(256, WAVES) void k_verify(DevBatch b, const ge* __r
                                                 uint32_t n_adm, int adm_steps, uint8_t* __restrict__ verdict,
                                                 uint8_t* __restrict__ rec32, int32_t* __restrict__ signer,
                                                 uint32_t* __restrict__ bitmap) {
-    __shared__ ge s_gtab[2 * HD_GTAB_N];  // 1G..128G, lambda*(1G..128G): 20 KiB
-    {
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(gtab_g);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(s_gtab);
-        for (int k = threadIdx.x; k < (int)(2 * HD_GTAB_N * sizeof(ge) / 4); k += blockDim.x) dst[k] = src[k];
-    }
-    __syncthreads();
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t base = blockIdx.x * blockDim.x; base < b.n; base += stride) {
         const uint32_t i = base + threadIdx.x;
@@ -65,7 +59,7 @@ __global__ __launch_bounds__(256, WAVES) void k_verify(DevBatch b, const ge* __r
             DevSrc src{b, i};
             uint32_t rec[8];
             int32_t s;
-            v = verify_msg_src(src, (const ge*)s_gtab, adm, n_adm, adm_steps, COMPRESSED, rec, s);
+            v = verify_msg_src(src, gtab_g, adm, n_adm, adm_steps, COMPRESSED, rec, s);
             verdict[i] = v;
             if (rec32) {
                 uint8_t* o = rec32 + 32 * (size_t)i;
@@ -143,14 +137,14 @@ int hd_ctx_create(int device, hd_ctx** out) {
         int v = atoi(w);
         if (v >= 2 && v <= 4) ctx->verify_waves = v;
     }
-    // G tables (1G..128G and lambda*(1G..128G), affine), built once on the
+    // G tables (1G..2048G and lambda*(1G..2048G), affine), built once on the
     // host with the same code the device runs, then uploaded.
     static std::once_flag once;
-    static std::vector<ge> host_tab(2 * HD_GTAB_N);
+    static std::vector<ge> host_tab(2 * HD_GLV_GTAB_N);
     std::call_once(once, [] { build_gtab_glv(host_tab.data()); });
-    e = hipMalloc(&ctx->d_gtab, sizeof(ge) * 2 * HD_GTAB_N);
+    e = hipMalloc(&ctx->d_gtab, sizeof(ge) * 2 * HD_GLV_GTAB_N);
     if (e == hipSuccess)
-        e = hipMemcpy(ctx->d_gtab, host_tab.data(), sizeof(ge) * 2 * HD_GTAB_N, hipMemcpyHostToDevice);
+        e = hipMemcpy(ctx->d_gtab, host_tab.data(), sizeof(ge) * 2 * HD_GLV_GTAB_N, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         int rc = hd_ctx_fail(ctx, e, "gtab upload");
         hd_ctx_destroy(ctx);

@@ -9,7 +9,7 @@
 
 using namespace hd;
 
-static ge g_tab[2 * HD_GTAB_N];
+static ge g_tab[2 * HD_GLV_GTAB_N];
 static bool g_init = false;
 static const ge* gtab() {
     if (!g_init) { build_gtab_glv(g_tab); g_init = true; }
@@ -58,7 +58,11 @@ void hdh_sc_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
 }
 void hdh_gtab(uint8_t* out /* 128 x 64 */) {
     const ge* t = gtab();
-    for (int k = 0; k < 2 * HD_GTAB_N; k++) { fe_out(out + 64 * k, t[k].x); fe_out(out + 64 * k + 32, t[k].y); }
+    for (int k = 0; k < 2 * HD_GTAB_N; k++) {  // 1G..128G, then lambda 1G..128G
+        const ge& e = t[k < HD_GTAB_N ? k : HD_GLV_GTAB_N + (k - HD_GTAB_N)];
+        fe_out(out + 64 * k, e.x);
+        fe_out(out + 64 * k + 32, e.y);
+    }
 }
 int hdh_booth(const uint8_t* k32, int w, int j) {
     sc k;

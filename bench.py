@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-tally", action="store_true")
+    ap.add_argument("--no-aux", action="store_true", help="skip the SURVEY §8(f) side measurements")
     return ap.parse_args()
 
 
@@ -206,6 +207,11 @@ def main():
             "tally": tally_info,
             "gen_s": gen_s,
         }
+        if not args.no_aux:
+            try:
+                out["aux"] = aux_benchmarks(v, db, ws)
+            except Exception as e:  # reported, never fatal for the headline number
+                out["aux"] = {"error": repr(e)}
         if not args.no_cpu:
             try:
                 out["cpu_baseline"] = run_cpu_baseline(args, db, sigs)
@@ -215,6 +221,63 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured float4 copy)
+
+
+def _time_ms(fn, ws, reps=5):
+    """Average device time of fn() over reps launches on stream ws (HIP events)."""
+    import torch
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(ws)
+    for _ in range(reps):
+        fn()
+    e1.record(ws)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def aux_benchmarks(v, db, ws):
+    """The SURVEY §8(f) rows around the hot path, measured on the same batch
+    (not part of the headline value): the surge wire codec (HBM-bound)."""
+    import ctypes
+    import torch
+    from hyperdrive_amd import _lib
+    from hyperdrive_amd.codec import record_size
+    from hyperdrive_amd.device import DeviceBatch
+    lib = _lib.load()
+    out = {}
+    n = db.n
+    S = record_size(2, True)
+    buf = torch.empty(n * S, dtype=torch.uint8, device=db.height.device)
+    cs = db.c_struct()
+    dec = DeviceBatch.empty(n, str(db.height.device))
+    co = dec.c_out()
+    status = torch.empty(n, dtype=torch.uint8, device=db.height.device)
+
+    def enc():
+        rc = lib.hd_marshal_batch_device(v.handle, 2, 1, ctypes.byref(cs), buf.data_ptr(), buf.numel(), ws.cuda_stream)
+        assert rc == 0, rc
+
+    def decd():
+        rc = lib.hd_unmarshal_batch_device(v.handle, 2, 1, buf.data_ptr(), buf.numel(), n, ctypes.byref(co),
+                                           status.data_ptr(), ws.cuda_stream)
+        assert rc == 0, rc
+
+    ms_e = _time_ms(enc, ws)
+    ms_d = _time_ms(decd, ws)
+    ok = bool((dec.height == db.height).all()) and bool((dec.sig == db.sig).all()) and int(status.sum()) == 0
+    # algorithmic bytes: record in + SoA out (type 1, h 8, r 8, value 32, from 32, sig 65, status 1)
+    soa = 1 + 8 + 8 + 32 + 32 + 65
+    for name, ms, byts in (("surge_unmarshal_signed_prevotes", ms_d, n * (S + soa + 1)),
+                           ("surge_marshal_signed_prevotes", ms_e, n * (S + soa - 1))):
+        gbs = byts / (ms * 1e-3) / 1e9
+        out[name] = {"messages": n, "ms": ms, "msgs_per_s": n / (ms * 1e-3), "GBs": gbs,
+                     "roofline": {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS},
+                     "round_trip_ok": ok}
+    return out
 
 
 def pmc_traffic():

@@ -96,6 +96,13 @@ SIGNATURES = {
     "hd_ctx_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
     "hd_abi_version": (ctypes.c_int, []),
     "hd_probe_valu": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_double)]),
+    # include/hd_codec.h
+    "hd_record_size": (ctypes.c_uint32, [ctypes.c_int, ctypes.c_int]),
+    "hd_unmarshal_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                                 ctypes.c_uint64, ctypes.c_uint32, ctypes.POINTER(HdBatchOut),
+                                                 ctypes.c_void_p, ctypes.c_void_p]),
+    "hd_marshal_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(HdBatch),
+                                               ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
 }
 
 _LIB = None

@@ -277,6 +277,27 @@ def aux_benchmarks(v, db, ws):
         out[name] = {"messages": n, "ms": ms, "msgs_per_s": n / (ms * 1e-3), "GBs": gbs,
                      "roofline": {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS},
                      "round_trip_ok": ok}
+    # mq bulk insert (mq.go:103-143) of the verified batch: sender = the C2
+    # signer index (i % S), per-sender capacity 1000 (opt.go:19), then a full
+    # consume; wall time of the synchronous calls
+    from hyperdrive_amd.mq import MessageQueue
+    S = 100
+    sender = (torch.arange(n, device=db.height.device, dtype=torch.int64) % S).to(torch.int32)
+    q = MessageQueue(v, 1000)
+    q.insert_device(db, sender, stream=ws)            # warm (allocations)
+    q.consume(2 ** 62)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    q.insert_device(db, sender, stream=ws)
+    t1 = time.perf_counter()
+    kept = len(q)
+    b, _ = q.consume(2 ** 62)
+    t2 = time.perf_counter()
+    q.close()
+    out["mq_bulk_insert"] = {"messages": n, "senders": S, "max_capacity": 1000, "kept": kept,
+                             "insert_ms": (t1 - t0) * 1e3, "insert_msgs_per_s": n / (t1 - t0),
+                             "consume_ms_incl_download": (t2 - t1) * 1e3, "consumed": len(b),
+                             "ok": kept == S * 1000 and len(b) == kept}
     return out
 
 

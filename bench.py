@@ -298,7 +298,44 @@ def aux_benchmarks(v, db, ws):
                              "insert_ms": (t1 - t0) * 1e3, "insert_msgs_per_s": n / (t1 - t0),
                              "consume_ms_incl_download": (t2 - t1) * 1e3, "consumed": len(b),
                              "ok": kept == S * 1000 and len(b) == kept}
+    out["vote_table"] = vote_table_bench()
     return out
+
+
+def vote_table_bench():
+    """Host-side incremental vote logs (include/hd_votes.h) on the C3 shape:
+    1000 signers x 64 rounds x (prevote + precommit) = 128,000 votes of one
+    height inserted in arrival order, then every round's T-predicates
+    (quorum.decide_votes: 6 O(1) lookups, through ctypes)."""
+    import numpy as np
+    from hyperdrive_amd.quorum import decide_votes, thresholds
+    from hyperdrive_amd.verify import Batch
+    from hyperdrive_amd.votes import INSERTED, VoteLog
+    S, R = 1000, 64
+    n = 2 * S * R
+    i = np.arange(n)
+    r = (i // (2 * S)).astype(np.int64)
+    typ = (2 + i % 2).astype(np.uint8)
+    frm = np.zeros((n, 32), np.uint8)
+    frm[:, :4] = ((i // 2) % S).astype(np.uint32).view(np.uint8).reshape(n, 4)
+    val = np.zeros((n, 32), np.uint8)
+    val[:, 0] = 1
+    val[:, 8:16] = r.view(np.uint8).reshape(n, 8)
+    val[i % 20 == 7] = 0                                     # 5% nil
+    b = Batch(typ, np.ones(n, np.int64), r, None, val, frm, np.zeros((n, 65), np.uint8))
+    v = VoteLog(1)
+    v.insert_batch(b)                                        # warm: tables grown once
+    v.reset(1)
+    t0 = time.perf_counter()
+    st, _ = v.insert_batch(b)
+    t1 = time.perf_counter()
+    f = thresholds(S)[0]
+    dec = [decide_votes(v, rr, f, val[2 * S * rr].tobytes(), True, rr - 1) for rr in range(R)]
+    t2 = time.perf_counter()
+    v.close()
+    return {"votes": n, "insert_ms": (t1 - t0) * 1e3, "ns_per_vote": (t1 - t0) * 1e9 / n,
+            "predicates_ms_64_rounds": (t2 - t1) * 1e3, "all_inserted": bool((st == INSERTED).all()),
+            "commit_rounds": sum(d["commit"] for d in dec), "cores": 1}
 
 
 def pmc_traffic():

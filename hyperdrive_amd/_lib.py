@@ -112,6 +112,23 @@ SIGNATURES = {
     "hd_mq_consume": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(HdBatchOut), ctypes.c_void_p,
                                      ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
     "hd_mq_drop_below": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    # include/hd_votes.h
+    "hd_votes_create": (ctypes.c_int, [ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]),
+    "hd_votes_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "hd_votes_reset": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    "hd_votes_height": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]),
+    "hd_votes_insert": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint8, ctypes.c_int64, ctypes.c_int64,
+                                       ctypes.c_char_p, ctypes.c_char_p, c_u8p, ctypes.c_void_p]),
+    "hd_votes_insert_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
+    "hd_votes_trace_propose": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p]),
+    "hd_votes_count": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint8, ctypes.c_int64, ctypes.c_char_p,
+                                      ctypes.POINTER(ctypes.c_uint32)]),
+    "hd_votes_len": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint8, ctypes.c_int64,
+                                    ctypes.POINTER(ctypes.c_uint32)]),
+    "hd_votes_trace_len": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_uint32)]),
+    "hd_votes_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint8, ctypes.c_int64, ctypes.c_char_p,
+                                    ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
 }
 
 _LIB = None

@@ -1,6 +1,6 @@
 """Build the in-tree native library ``hyperdrive_amd/_lib/libhdverify.so``.
 
-Each ``csrc/*.hip`` translation unit is compiled for gfx950 in parallel with
+Each ``csrc/*.hip`` / ``csrc/*.cpp`` translation unit is compiled for gfx950 in parallel with
 ``hipcc -c`` and linked with ``hipcc -shared``.  The library is built in-tree
 so that it travels with the repository snapshot to the GPU box.
 
@@ -30,7 +30,8 @@ CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno
 
 
 def _sources():
-    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    # *.hip: device + host code; *.cpp: host-only C++ (hd_votes)
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
 
 
 def _deps():

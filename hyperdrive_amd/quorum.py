@@ -57,3 +57,27 @@ def decide(tally, height: int, round_: int, f: int, propose_value: Optional[byte
     if propose_value is not None and propose_valid_round > INVALID_ROUND:
         out["prevote_validround"] = count.get((height, propose_valid_round, PREVOTE, propose_value), 0) >= q
     return out
+
+
+def decide_votes(votes, round_: int, f: int, propose_value: Optional[bytes] = None, propose_valid: bool = False,
+                 propose_valid_round: int = INVALID_ROUND) -> Dict[str, bool]:
+    """The same predicates as :func:`decide`, for the current height of an
+    incremental :class:`hyperdrive_amd.votes.VoteLog` (include/hd_votes.h):
+    every value is one O(1) lookup where process.go runs its O(n) loops.  A
+    valid propose's signer is already in the log's trace (trace_propose)."""
+    q = 2 * f + 1
+    out = {
+        "timeout_prevote": votes.len(PREVOTE, round_) >= q,                 # process.go:534
+        "precommit_nil": votes.count(PREVOTE, round_, NIL_VALUE) >= q,     # 626-632
+        "timeout_precommit_reached": votes.len(PRECOMMIT, round_) >= q,    # 658
+        "skip": votes.trace_len(round_) >= f + 1,                          # 751
+        "precommit_value": False,
+        "commit": False,
+        "prevote_validround": False,
+    }
+    if propose_value is not None and propose_valid:
+        out["precommit_value"] = votes.count(PREVOTE, round_, propose_value) >= q     # 574-582
+        out["commit"] = votes.count(PRECOMMIT, round_, propose_value) >= q            # 696-702
+    if propose_value is not None and propose_valid_round > INVALID_ROUND:
+        out["prevote_validround"] = votes.count(PREVOTE, propose_valid_round, propose_value) >= q  # 486-494
+    return out

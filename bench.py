@@ -241,7 +241,8 @@ def _time_ms(fn, ws, reps=5):
 
 def aux_benchmarks(v, db, ws):
     """The SURVEY §8(f) rows around the hot path, measured on the same batch
-    (not part of the headline value): the surge wire codec (HBM-bound)."""
+    (not part of the headline value): the surge wire codec (HBM-bound), mq
+    bulk insert, the digest lanes and the host vote table."""
     import ctypes
     import torch
     from hyperdrive_amd import _lib
@@ -298,6 +299,14 @@ def aux_benchmarks(v, db, ws):
                              "insert_ms": (t1 - t0) * 1e3, "insert_msgs_per_s": n / (t1 - t0),
                              "consume_ms_incl_download": (t2 - t1) * 1e3, "consumed": len(b),
                              "ok": kept == S * 1000 and len(b) == kept}
+    # digest lanes (include/hd_digest.h): preimage digests of the batch;
+    # ~81 B of HBM per message (type, h, r, value in; 32 B out)
+    from hyperdrive_amd.digest import KECCAK256, SHA256, digest_device
+    dgo = torch.empty((n, 32), dtype=torch.uint8, device=db.height.device)
+    for algo, name in ((SHA256, "sha256"), (KECCAK256, "keccak256")):
+        ms = _time_ms(lambda: digest_device(v, algo, db, out=dgo, stream=ws), ws)
+        out["digest_" + name] = {"messages": n, "ms": ms, "msgs_per_s": n / (ms * 1e-3),
+                                 "GBs": n * 81 / (ms * 1e-3) / 1e9}
     out["vote_table"] = vote_table_bench()
     return out
 

@@ -112,6 +112,14 @@ SIGNATURES = {
     "hd_mq_consume": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(HdBatchOut), ctypes.c_void_p,
                                      ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
     "hd_mq_drop_below": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    # include/hd_digest.h
+    "hd_digest_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(HdBatch),
+                                              ctypes.c_void_p, ctypes.c_void_p]),
+    "hd_hash_bytes_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    "hd_verify_batch_digest_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
+                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                     ctypes.c_void_p, ctypes.c_void_p]),
     # include/hd_votes.h
     "hd_votes_create": (ctypes.c_int, [ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]),
     "hd_votes_destroy": (ctypes.c_int, [ctypes.c_void_p]),

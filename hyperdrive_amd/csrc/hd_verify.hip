@@ -21,6 +21,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/hd_digest.h"
 #include "../../include/hd_verify.h"
 #include "hd_verify_msg.h"
 #include "hd_internal.h"
@@ -33,6 +34,7 @@ using namespace hd;
 struct DevSrc {
     const DevBatch& b;
     uint32_t i;
+    const uint8_t* dg;  // caller-supplied digests (hd_verify_batch_digest_device) or NULL
     __device__ __forceinline__ uint32_t type() const { return b.type[i]; }
     __device__ __forceinline__ int64_t h() const { return b.height[i]; }
     __device__ __forceinline__ int64_t r() const { return b.round[i]; }
@@ -42,6 +44,8 @@ struct DevSrc {
     __device__ __forceinline__ uint32_t sig_r(int w) const { return load_be32(b.sig65 + 65 * (size_t)i + 4 * w); }
     __device__ __forceinline__ uint32_t sig_s(int w) const { return load_be32(b.sig65 + 65 * (size_t)i + 32 + 4 * w); }
     __device__ __forceinline__ uint32_t sig_v() const { return b.sig65[65 * (size_t)i + 64]; }
+    __device__ __forceinline__ bool has_digest() const { return dg != nullptr; }
+    __device__ __forceinline__ uint32_t digest(int w) const { return load_be32(dg + 32 * (size_t)i + 4 * w); }
 };
 
 template <bool COMPRESSED, int WAVES>
@@ -49,14 +53,14 @@ __global__ __launch_bounds__(256, WAVES) void k_verify(DevBatch b, const ge* __r
                                                 const uint32_t* __restrict__ adm, const int32_t* __restrict__ adm_perm,
                                                 uint32_t n_adm, int adm_steps, uint8_t* __restrict__ verdict,
                                                 uint8_t* __restrict__ rec32, int32_t* __restrict__ signer,
-                                                uint32_t* __restrict__ bitmap) {
+                                                uint32_t* __restrict__ bitmap, const uint8_t* __restrict__ digest_in) {
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t base = blockIdx.x * blockDim.x; base < b.n; base += stride) {
         const uint32_t i = base + threadIdx.x;
         const bool active = i < b.n;
         uint8_t v = 0xFF;
         if (active) {
-            DevSrc src{b, i};
+            DevSrc src{b, i, digest_in};
             uint32_t rec[8];
             int32_t s;
             v = verify_msg_src(src, gtab_g, adm, n_adm, adm_steps, COMPRESSED, rec, s);
@@ -213,11 +217,11 @@ int hd_set_signatories(hd_ctx* ctx, const uint8_t* sigs32, uint32_t n) {
     return HD_OK;
 }
 
-int hd_verify_batch_device(hd_ctx* ctx, const hd_batch* db, uint8_t* d_verdict, uint8_t* d_recovered32,
-                           int32_t* d_signer, uint32_t* d_valid_bitmap, void* stream) {
-    if (!ctx || !db || !d_verdict) return HD_EINVAL;
-    if (db->n == 0) return HD_OK;
-    if (!db->type || !db->height || !db->round || !db->value32 || !db->from32 || !db->sig65) return HD_EINVAL;
+}  // extern "C"
+
+namespace {
+int launch_verify(hd_ctx* ctx, const hd_batch* db, const uint8_t* d_digest, uint8_t* d_verdict, uint8_t* d_recovered32,
+                  int32_t* d_signer, uint32_t* d_valid_bitmap, void* stream) {
     (void)hipSetDevice(ctx->device);
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
     DevBatch b{db->n, db->type, db->height, db->round, db->valid_round, db->value32, db->from32, db->sig65};
@@ -228,7 +232,7 @@ int hd_verify_batch_device(hd_ctx* ctx, const hd_batch* db, uint8_t* d_verdict, 
     blocks = std::min(blocks, max_blocks);
 #define HD_LAUNCH_VERIFY(C, W)                                                                             \
     k_verify<C, W><<<blocks, threads, 0, s>>>(b, ctx->d_gtab, ctx->d_adm, ctx->d_adm_perm, ctx->n_adm, ctx->adm_steps, \
-                                              d_verdict, d_recovered32, d_signer, d_valid_bitmap)
+                                              d_verdict, d_recovered32, d_signer, d_valid_bitmap, d_digest)
     // waves/SIMD the kernel is register-allocated for (HD_VERIFY_WAVES = 2/3/4, default 3)
     const int w = ctx->verify_waves;
     if (ctx->compressed) {
@@ -244,6 +248,25 @@ int hd_verify_batch_device(hd_ctx* ctx, const hd_batch* db, uint8_t* d_verdict, 
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hd_ctx_fail(ctx, e, "k_verify launch");
     return HD_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int hd_verify_batch_device(hd_ctx* ctx, const hd_batch* db, uint8_t* d_verdict, uint8_t* d_recovered32,
+                           int32_t* d_signer, uint32_t* d_valid_bitmap, void* stream) {
+    if (!ctx || !db || !d_verdict) return HD_EINVAL;
+    if (db->n == 0) return HD_OK;
+    if (!db->type || !db->height || !db->round || !db->value32 || !db->from32 || !db->sig65) return HD_EINVAL;
+    return launch_verify(ctx, db, nullptr, d_verdict, d_recovered32, d_signer, d_valid_bitmap, stream);
+}
+
+int hd_verify_batch_digest_device(hd_ctx* ctx, const hd_batch* db, const uint8_t* d_digest32, uint8_t* d_verdict,
+                                  uint8_t* d_recovered32, int32_t* d_signer, uint32_t* d_valid_bitmap, void* stream) {
+    if (!ctx || !db || !d_verdict || !d_digest32) return HD_EINVAL;
+    if (db->n == 0) return HD_OK;
+    if (!db->type || !db->from32 || !db->sig65) return HD_EINVAL;
+    return launch_verify(ctx, db, d_digest32, d_verdict, d_recovered32, d_signer, d_valid_bitmap, stream);
 }
 
 }  // extern "C"

@@ -57,7 +57,8 @@ HD int32_t admitted_find(AdmTab adm, uint32_t n, int steps, const uint32_t key[8
 }
 
 // Full verdict for one message.  Src supplies the message fields on demand
-// (type(), h(), r(), vr(), value(w), from(w), sig_r(w), sig_s(w), sig_v()),
+// (type(), h(), r(), vr(), value(w), from(w), sig_r(w), sig_s(w), sig_v(),
+// and has_digest() / digest(w) when the digest is given rather than computed),
 // so the kernel loads each field from HBM in the phase that uses it and
 // nothing but the accumulator stays live across the ladder.  rec_be receives
 // the recovered signatory (zeros when recovery failed); signer the
@@ -70,7 +71,10 @@ HD uint8_t verify_msg_src(const Src& src, GTab gtab, AdmTab adm, uint32_t n_adm,
     const uint32_t type = src.type();
     if (type < 1 || type > 3) return V_BAD_TYPE;
     uint32_t d[8];
-    {
+    if (src.has_digest()) {
+        // caller-supplied digest (include/hd_digest.h), e.g. a Keccak-256 lane
+        HD_UNROLL for (int w = 0; w < 8; w++) d[w] = src.digest(w);
+    } else {
         uint32_t value_be[8];
         HD_UNROLL for (int w = 0; w < 8; w++) value_be[w] = src.value(w);
         if (type == T_PROPOSE) sha256_propose(d, src.h(), src.r(), src.vr(), value_be);
@@ -118,6 +122,8 @@ struct MsgSrc {
     HD_MEMBER uint32_t sig_r(int w) const { return m.r_be[w]; }
     HD_MEMBER uint32_t sig_s(int w) const { return m.s_be[w]; }
     HD_MEMBER uint32_t sig_v() const { return m.v; }
+    HD_MEMBER bool has_digest() const { return false; }
+    HD_MEMBER uint32_t digest(int) const { return 0; }
 };
 
 template <typename GTab, typename AdmTab>

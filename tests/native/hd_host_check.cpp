@@ -5,6 +5,7 @@
 #include <string.h>
 #include <vector>
 #include "../../hyperdrive_amd/csrc/hd_gen.h"
+#include "../../hyperdrive_amd/csrc/hd_keccak.h"
 #include "../../hyperdrive_amd/csrc/hd_modinv.h"
 
 using namespace hd;
@@ -304,4 +305,26 @@ extern "C" void hdh_split(const uint8_t* kb, uint8_t* k1b, uint8_t* k2b) {
     sc_split_lambda(k1, k2, k);
     le_out(k1b, k1.v);
     le_out(k2b, k2.v);
+}
+
+// Keccak sponge of hd_keccak.h over a host byte string (pad 0x01 Keccak-256,
+// 0x06 SHA3-256)
+extern "C" void hdh_keccak_bytes(int pad, const uint8_t* data, uint64_t len, uint8_t* out32) {
+    uint32_t d[8];
+    keccak256_bytes(d, len, (uint8_t)pad, [&](uint64_t off) {
+        uint64_t lane = 0;
+        for (int k = 0; k < 8; k++)
+            if (off + k < len) lane |= (uint64_t)data[off + k] << (8 * k);
+        return lane;
+    });
+    for (int w = 0; w < 8; w++) store_be32(out32 + 4 * w, d[w]);
+}
+// preimage digest of one message with the fixed-size Keccak paths
+extern "C" void hdh_keccak_msg(int pad, int type, int64_t h, int64_t r, int64_t vr, const uint8_t* value32,
+                               uint8_t* out32) {
+    uint32_t v[8], d[8];
+    for (int w = 0; w < 8; w++) v[w] = load_be32(value32 + 4 * w);
+    if (type == T_PROPOSE) keccak256_propose(d, h, r, vr, v, (uint8_t)pad);
+    else keccak256_vote(d, h, r, v, (uint8_t)pad);
+    for (int w = 0; w < 8; w++) store_be32(out32 + 4 * w, d[w]);
 }

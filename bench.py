@@ -207,12 +207,14 @@ def main():
             "tally": tally_info,
             "gen_s": gen_s,
         }
-        if not args.no_aux:
+        # aux rows and the CPU baseline: single-GPU runs only (the N>1 runs
+        # report the sharded headline path; other ranks wait at the barrier)
+        if not args.no_aux and world == 1:
             try:
                 out["aux"] = aux_benchmarks(v, db, ws)
             except Exception as e:  # reported, never fatal for the headline number
                 out["aux"] = {"error": repr(e)}
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:
             try:
                 out["cpu_baseline"] = run_cpu_baseline(args, db, sigs)
             except Exception as e:  # reported, never fatal for the GPU number
@@ -307,6 +309,25 @@ def aux_benchmarks(v, db, ws):
         ms = _time_ms(lambda: digest_device(v, algo, db, out=dgo, stream=ws), ws)
         out["digest_" + name] = {"messages": n, "ms": ms, "msgs_per_s": n / (ms * 1e-3),
                                  "GBs": n * 81 / (ms * 1e-3) / 1e9}
+    # end-to-end replica ingress from wire bytes (hyperdrive_amd/ingress.py):
+    # unmarshal -> verify -> filterHeight -> mq insert, then flush the
+    # current height into the vote logs; wall time of the synchronous chain
+    from hyperdrive_amd.codec import marshal_device
+    from hyperdrive_amd.ingress import Ingress
+    wire = marshal_device(v, 2, db, with_sig=True, stream=ws)
+    ing = Ingress(v, height=1, max_capacity=1000)
+    ing.push_wire(2, wire, n, stream=ws)                  # warm (allocations)
+    ing.reset_height(1)
+    ing.mq.drop_below(2 ** 62)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    vg = ing.push_wire(2, wire, n, stream=ws)
+    res = ing.flush()
+    t1 = time.perf_counter()
+    out["ingress_wire_to_votes"] = {"messages": n, "ms": (t1 - t0) * 1e3, "msgs_per_s": n / (t1 - t0),
+                                    "valid": int((vg == 0).sum()), "consumed_height_1": len(res.consumed),
+                                    "buffered": len(ing.mq)}
+    ing.close()
     out["vote_table"] = vote_table_bench()
     return out
 

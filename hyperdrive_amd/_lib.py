@@ -108,6 +108,8 @@ SIGNATURES = {
     "hd_mq_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "hd_mq_insert_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                            ctypes.c_void_p]),
+    "hd_mq_insert_verified_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
+                                                    ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     "hd_mq_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "hd_mq_consume": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(HdBatchOut), ctypes.c_void_p,
                                      ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),

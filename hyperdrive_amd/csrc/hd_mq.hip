@@ -89,6 +89,14 @@ __global__ void k_mq_flag_new(uint32_t n, const int32_t* __restrict__ sender, ui
     if (i < n) flag[i] = sender[i] >= 0;
 }
 
+// Replica.Run ingress (replica.go:117-131): a verified message enters the
+// queue iff VALID and filterHeight passes (height >= current, replica.go:247-249)
+__global__ void k_mq_ingress(uint32_t n, const uint8_t* __restrict__ verdict, const int32_t* __restrict__ signer,
+                             const int64_t* __restrict__ height, int64_t min_height, int32_t* __restrict__ snd) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) snd[i] = (verdict[i] == HD_VERDICT_VALID && height[i] >= min_height) ? signer[i] : -1;
+}
+
 __global__ void k_mq_keys(MqSrc s, uint32_t T, int64_t* __restrict__ hk, int64_t* __restrict__ rk,
                           uint32_t* __restrict__ sk, uint32_t* __restrict__ iota) {
     const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -185,7 +193,7 @@ int bits_of(uint64_t range) {
 }  // namespace
 
 enum MqSlot { MQ_FLAG, MQ_NEWIDX, MQ_NSEL, MQ_HK, MQ_RK, MQ_SK, MQ_PERM0, MQ_PERM1, MQ_K64A, MQ_K64B, MQ_K32A, MQ_K32B,
-              MQ_HEAD, MQ_KEEP, MQ_SEL, MQ_RED, MQ_TMP, MQ__N };
+              MQ_HEAD, MQ_KEEP, MQ_SEL, MQ_RED, MQ_TMP, MQ_SND, MQ__N };
 
 struct hd_mq {
     hd_ctx* ctx = nullptr;
@@ -398,6 +406,22 @@ int hd_mq_insert_device(hd_mq* q, const hd_batch* d_batch, const int32_t* d_send
     q->pool.n = kept;
     QCHK(hipStreamSynchronize(s), "mq insert sync");
     return HD_OK;
+}
+
+int hd_mq_insert_verified_device(hd_mq* q, const hd_batch* d_batch, const uint8_t* d_verdict, const int32_t* d_signer,
+                                 int64_t min_height, void* stream) {
+    if (!q || !d_batch || !d_verdict || !d_signer) return HD_EINVAL;
+    const uint32_t nb = d_batch->n;
+    if (nb == 0) return HD_OK;
+    if (!d_batch->height) return HD_EINVAL;
+    (void)hipSetDevice(q->ctx->device);
+    hipStream_t s = stream ? (hipStream_t)stream : q->ctx->stream;
+    int rc = 0;
+    int32_t* snd = (int32_t*)qbuf(q, MQ_SND, 4 * (size_t)nb, &rc);
+    if (rc) return rc;
+    k_mq_ingress<<<nblk(nb), 256, 0, s>>>(nb, d_verdict, d_signer, d_batch->height, min_height, snd);
+    QCHK(hipGetLastError(), "k_mq_ingress");
+    return hd_mq_insert_device(q, d_batch, snd, stream);
 }
 
 int hd_mq_consume(hd_mq* q, int64_t h, const hd_batch_out* out, int32_t* out_sender, uint32_t cap, uint32_t* n_out) {

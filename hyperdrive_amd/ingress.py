@@ -1,0 +1,95 @@
+"""Batch ingress of one replica on the GPU: wire bytes -> SoA -> verify ->
+message queue -> the current height's vote logs.
+
+The reference handles one message per channel receive (replica/replica.go:
+88-151): authentication is the caller's job, ``filterHeight`` drops heights
+below the Process's (:247-249), ``mq.Insert*`` buffers per sender
+(mq/mq.go:85-143), and ``flush`` consumes the current height into
+``process.Propose/Prevote/Precommit`` (:253-265), whose vote logs the count
+rules read (process/process.go:823-892).  ``Ingress`` runs the same chain
+for a whole batch:
+
+    ing = Ingress(verifier, height=h)
+    ing.push_wire(PREVOTE, buf, n)          # unmarshal + verify + filterHeight + mq insert (GPU)
+    res = ing.flush()                       # mq.Consume(h) + vote-log inserts (host table)
+    res.proposes                            # handed to the CPU's insertPropose (scheduler/validator)
+    ing.reset_height(h + 1)                 # ResetHeight: logs emptied, mq.DropMessagesBelowHeight
+
+Batch semantics: a flush consumes everything buffered at the current height
+in one go; the reference may advance the height in the middle of a flush
+(a commit inside process.Precommit), which the caller reproduces by calling
+``reset_height`` and flushing again.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from .codec import record_size, unmarshal_device
+from .device import DeviceBatch, _torch, work_stream
+from .mq import MessageQueue
+from .verify import PROPOSE, Batch, Verifier
+from .votes import VoteLog
+
+
+@dataclass
+class FlushResult:
+    consumed: Batch            # every message consumed, in consumption order
+    senders: np.ndarray        # int32 admitted index per consumed message
+    vote_status: np.ndarray    # HD_VOTE_* per consumed message (NOT_VOTE for proposes)
+    double_of: np.ndarray      # batch index of the logged vote for DOUBLE, else votes.NO_INDEX
+    proposes: np.ndarray       # indices (into consumed) of the proposes, for the CPU
+
+
+class Ingress:
+    def __init__(self, v: Verifier, height: int = 1, max_capacity: int = 1000):
+        self.v = v
+        self.height = int(height)
+        self.mq = MessageQueue(v, max_capacity)
+        self.votes = VoteLog(self.height)
+
+    def close(self):
+        self.mq.close()
+        self.votes.close()
+
+    def push_device(self, batch: DeviceBatch, stream=None):
+        """Verify a device batch and buffer its VALID messages with height >=
+        the current height.  Returns the device verdict tensor."""
+        torch = _torch()
+        dev = batch.height.device
+        n = batch.n
+        verdict = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+        signer = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        if n == 0:
+            return verdict[:0]
+        ws = stream or work_stream(dev)
+        ws.wait_stream(torch.cuda.current_stream(ws.device))
+        self.v.verify_batch_device(batch.c_struct(), verdict.data_ptr(), None, signer.data_ptr(), None, ws.cuda_stream)
+        self.mq.insert_verified_device(batch, verdict, signer, self.height, stream=ws)
+        return verdict[:n]
+
+    def push_wire(self, mtype: int, buf, n: int, with_sig: bool = True, stream=None):
+        """Unmarshal n `mtype` records from a device byte buffer and push them.
+        Records the buffer ends inside are dropped (Unmarshal's error,
+        process/message.go:126-149).  Returns the verdicts of the complete records."""
+        size = record_size(mtype, with_sig)
+        complete = min(n, buf.numel() // size) if size else 0
+        if complete == 0:
+            return _torch().empty(0, dtype=_torch().uint8, device=buf.device)
+        db, _ = unmarshal_device(self.v, mtype, buf, complete, with_sig, stream=stream)
+        return self.push_device(db, stream=stream)
+
+    def flush(self) -> FlushResult:
+        b, senders = self.mq.consume(self.height)
+        status, double_of = self.votes.insert_batch(b)
+        return FlushResult(b, senders, status, double_of, np.flatnonzero(b.type == PROPOSE))
+
+    def reset_height(self, height: int) -> None:
+        self.height = int(height)
+        self.votes.reset(self.height)
+        self.mq.drop_below(self.height)
+
+
+__all__ = ["Ingress", "FlushResult"]

@@ -54,6 +54,17 @@ class MessageQueue:
         self._check(self._lib.hd_mq_insert_device(self._q, ctypes.byref(cs), sender.data_ptr(), ws.cuda_stream),
                     "hd_mq_insert_device")
 
+    def insert_verified_device(self, batch: DeviceBatch, verdict, signer, min_height: int, stream=None) -> None:
+        """Replica ingress: insert the VALID messages with height >= min_height
+        (filterHeight), sender = signer[i] (device tensors from verify)."""
+        torch = _torch()
+        ws = stream or work_stream(batch.height.device)
+        ws.wait_stream(torch.cuda.current_stream(ws.device))
+        cs = batch.c_struct()
+        self._check(self._lib.hd_mq_insert_verified_device(self._q, ctypes.byref(cs), verdict.data_ptr(),
+                                                           signer.data_ptr(), int(min_height), ws.cuda_stream),
+                    "hd_mq_insert_verified_device")
+
     def __len__(self) -> int:
         n = ctypes.c_uint64()
         self._check(self._lib.hd_mq_size(self._q, ctypes.byref(n)), "hd_mq_size")

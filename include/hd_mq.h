@@ -36,6 +36,14 @@ int hd_mq_destroy(hd_mq* q);
  * Synchronises `stream` (a hipStream_t, NULL = the ctx's stream). */
 int hd_mq_insert_device(hd_mq* q, const hd_batch* d_batch, const int32_t* d_sender, void* stream);
 
+/* Replica.Run ingress of a verified batch (replica/replica.go:117-131):
+ * message i is inserted iff d_verdict[i] == HD_VERDICT_VALID and its height
+ * >= min_height (filterHeight, replica.go:247-249; min_height = the Process's
+ * CurrentHeight), with sender d_signer[i] (the admitted index written by
+ * hd_verify_batch_device).  Synchronises `stream`. */
+int hd_mq_insert_verified_device(hd_mq* q, const hd_batch* d_batch, const uint8_t* d_verdict, const int32_t* d_signer,
+                                 int64_t min_height, void* stream);
+
 /* number of buffered messages */
 int hd_mq_size(hd_mq* q, uint64_t* n);
 

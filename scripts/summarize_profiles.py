@@ -46,3 +46,29 @@ if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
     out["hbm_bytes_corrected"] = (2 * out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024
 json.dump(out, open(os.path.join(dst, "pmc_k_verify.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
+
+# every kernel's per-launch HBM traffic (the aux rows: codec, mq, digest, tally)
+allk = collections.defaultdict(lambda: collections.defaultdict(list))
+for name in ("pmc_fetch", "pmc_write"):
+    path = os.path.join(src, name, "run_counter_collection.csv")
+    if not os.path.exists(path):
+        continue
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        allk[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+durs = {}
+for r in csv.DictReader(open(os.path.join(dst, "kernel_stats.csv"))):
+    durs[r["Name"].split("(")[0].replace("void ", "")] = float(r["AverageNs"])
+kern = {}
+for k, cs in allk.items():
+    e = {c: sum(v) / len(v) for c, v in cs.items()}
+    e["launches"] = max(len(v) for v in cs.values())
+    if "FETCH_SIZE" in e and "WRITE_SIZE" in e:
+        e["bytes_raw"] = (e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024
+        e["bytes_corrected"] = (2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024
+        if k in durs:
+            e["avg_ns"] = durs[k]
+            e["GBs_corrected"] = e["bytes_corrected"] / durs[k]
+    kern[k] = e
+if kern:
+    json.dump(kern, open(os.path.join(dst, "pmc_kernels.json"), "w"), indent=1)

@@ -138,3 +138,66 @@ def test_adversarial_full_mix_vs_c_oracle(verifier, oracle, coracle):
     assert res.recovered.tobytes() == crec.tobytes()
     hist = np.bincount(res.verdict, minlength=8)
     assert hist[0] > 0.7 * N and all(hist[k] > 0 for k in range(1, 7))
+
+
+def test_c4_16m_sharded_emulation(verifier, coracle):
+    """BASELINE configs[3] (16M messages, sharded over 8 GPUs) on one GPU: the
+    8 rank shards (shard_range) verified one after another into their bitmap
+    slices give exactly the single-launch bitmap; all 16M honest votes are
+    VALID with signer = i mod S; a seeded sample matches the C oracle; the
+    tally from the concatenated shard bitmaps equals the tally from the
+    single-launch verdicts."""
+    import torch
+    from hyperdrive_amd.device import generate, work_stream
+    from hyperdrive_amd.shard import shard_range
+    from hyperdrive_amd._lib import HdBatch
+    N, S, W = 1 << 24, 100, 8
+    ks = verifier.gen_keys(S)
+    verifier.set_signatories(ks[0])
+    db, _, _ = generate(verifier, 0, N, S, 0, keys=ks)
+    ws = work_stream()
+    verdict = torch.empty(N, dtype=torch.uint8, device="cuda")
+    signer = torch.empty(N, dtype=torch.int32, device="cuda")
+    bm_full = torch.zeros(N // 32, dtype=torch.int32, device="cuda")
+    verifier.verify_batch_device(db.c_struct(), verdict.data_ptr(), None, signer.data_ptr(), bm_full.data_ptr(),
+                                 ws.cuda_stream)
+    bm_sh = torch.zeros(N // 32, dtype=torch.int32, device="cuda")
+    v_sh = torch.empty(N, dtype=torch.uint8, device="cuda")
+    for k in range(W):
+        lo, hi = shard_range(N, k, W)
+        sh = HdBatch(hi - lo, db.type.data_ptr() + lo, db.height.data_ptr() + 8 * lo, db.round.data_ptr() + 8 * lo,
+                     db.valid_round.data_ptr() + 8 * lo, db.value.data_ptr() + 32 * lo,
+                     db.frm.data_ptr() + 32 * lo, db.sig.data_ptr() + 65 * lo)
+        verifier.verify_batch_device(sh, v_sh.data_ptr() + lo, None, None, bm_sh.data_ptr() + 4 * (lo // 32),
+                                     ws.cuda_stream)
+    ws.synchronize()
+    assert torch.equal(bm_full, bm_sh) and torch.equal(verdict, v_sh)
+    assert int((verdict != 0).sum()) == 0
+    idx = torch.arange(N, device="cuda", dtype=torch.int64)
+    assert bool((signer.long() == idx % S).all())
+    rng = np.random.default_rng(16)
+    pick = np.sort(rng.choice(N, 256, replace=False))
+    p = torch.from_numpy(pick).cuda()
+    from hyperdrive_amd.verify import Batch
+    sb = Batch(db.type[p].cpu().numpy(), db.height[p].cpu().numpy(), db.round[p].cpu().numpy(),
+               db.valid_round[p].cpu().numpy(), db.value[p].cpu().numpy(), db.frm[p].cpu().numpy(),
+               db.sig[p].cpu().numpy())
+    cv, _ = coracle.verify(sb, ks[0], True, threads=8)
+    assert cv.tolist() == [0] * len(pick)
+    # tally: bitmap path (what every rank runs after the all-gather) == verdict path
+    import ctypes
+    from hyperdrive_amd import _lib
+    lib = _lib.load()
+    t1, a1 = verifier._tally_struct(N)
+    t2, a2 = verifier._tally_struct(N)
+    full = db.c_struct()
+    assert lib.hd_tally_device_bitmap(verifier.handle, ctypes.byref(full), bm_sh.data_ptr(), ctypes.byref(t1),
+                                      ws.cuda_stream) == 0
+    assert lib.hd_tally_device(verifier.handle, ctypes.byref(full), verdict.data_ptr(), None, ctypes.byref(t2),
+                               ws.cuda_stream) == 0
+    assert (t1.n_hr, t1.n_counts) == (t2.n_hr, t2.n_counts)
+    for k in ("count_height", "count_round", "count_type", "count_n", "hr_height", "hr_prevotes", "hr_precommits",
+              "hr_any"):
+        m = t1.n_counts if k.startswith("count") else t1.n_hr
+        assert np.array_equal(a1[k][:m], a2[k][:m]), k
+    assert t1.n_hr == N // (2 * S) + (1 if N % (2 * S) else 0)

@@ -46,7 +46,10 @@ def test_wire_to_vote_logs_matches_restatements(verifier, coracle, cap):
     # again by mq, then logged as identical duplicates
     rng = np.random.default_rng(cap)
     extra = rng.choice(n, 200, replace=False)
-    order = np.concatenate([np.arange(n), extra])
+    # arrival with heights shuffled by up to +-50: out-of-order
+    # heights reach mq, which must restore (height, round, arrival) order
+    jitter = np.arange(n) + rng.integers(-50, 51, n) * 2 * S
+    order = np.concatenate([np.argsort(jitter, kind="stable"), extra])
     # arrival = per-type wire buffers pushed in this order: prevotes, precommits
     adm = {sigs[k].tobytes(): k for k in range(S)}
     ing = Ingress(verifier, height=H0, max_capacity=cap)

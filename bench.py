@@ -110,54 +110,71 @@ def main():
                     db.sig.data_ptr() + 65 * lo)
     full = db.c_struct()
     assert B % 32 == 0
-    verdict = torch.empty(B, dtype=torch.uint8, device=dev)
-    bitmap = torch.zeros(B // 32, dtype=torch.int32, device=dev)
+    # double-buffered outputs: the tally of step k (its own stream) overlaps
+    # the verification of step k+1; every step's verify and tally complete
+    # inside the timed region
+    verdicts = [torch.empty(B, dtype=torch.uint8, device=dev) for _ in range(2)]
+    bitmaps = [torch.zeros(B // 32, dtype=torch.int32, device=dev) for _ in range(2)]
     lib = _lib.load()
     t_out, t_arr = v._tally_struct(total)
+    ts = torch.cuda.Stream(device=dev)
 
-    ev_k0 = torch.cuda.Event(enable_timing=True)
-    ev_k1 = torch.cuda.Event(enable_timing=True)
-    kernel_ms = []
+    ev_k = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     tally_info = {}
 
-    def step(record=False):
+    def verify(k, record=False):
+        buf = k % 2
         if record:
-            ev_k0.record()
-        v.verify_batch_device(shard, verdict.data_ptr(), None, None, bitmap.data_ptr(), stream)
+            ev_k[k][0].record(ws)
+        v.verify_batch_device(shard, verdicts[buf].data_ptr(), None, None, bitmaps[buf].data_ptr(), stream)
         if record:
-            ev_k1.record()
+            ev_k[k][1].record(ws)
         if dist is not None:
-            gathered = gather_bitmaps(bitmap, total, world)   # RCCL all-gather over xGMI
+            gathered = gather_bitmaps(bitmaps[buf], total, world)   # RCCL all-gather over xGMI
         else:
-            gathered = bitmap
-        if not args.no_tally:
-            rc = lib.hd_tally_device_bitmap(v.handle, ctypes.byref(full), gathered.data_ptr(), ctypes.byref(t_out),
-                                            stream)
-            if rc != 0:
-                raise _lib.HDError(rc, "hd_tally_device_bitmap", lib.hd_ctx_last_error(v.handle).decode())
-            tally_info["n_hr"] = t_out.n_hr
-            tally_info["n_counts"] = t_out.n_counts
+            gathered = bitmaps[buf]
+        done = torch.cuda.Event()
+        done.record(ws)
+        return gathered, done
 
-    for _ in range(args.warmup):
-        step()
+    def tally(pending):
+        if pending is None or args.no_tally:
+            return
+        gathered, done = pending
+        ts.wait_event(done)
+        rc = lib.hd_tally_device_bitmap(v.handle, ctypes.byref(full), gathered.data_ptr(), ctypes.byref(t_out),
+                                        ts.cuda_stream)
+        if rc != 0:
+            raise _lib.HDError(rc, "hd_tally_device_bitmap", lib.hd_ctx_last_error(v.handle).decode())
+        tally_info["n_hr"] = t_out.n_hr
+        tally_info["n_counts"] = t_out.n_counts
+
+    def run(steps, record):
+        pending = None
+        for k in range(steps):
+            nxt = verify(k, record)
+            tally(pending)
+            pending = nxt
+        tally(pending)
+
+    run(args.warmup, False)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
-    for _ in range(args.steps):
-        step(record=True)
-        ev_k1.synchronize()
-        kernel_ms.append(ev_k0.elapsed_time(ev_k1))
+    run(args.steps, True)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
+    kernel_ms = [a.elapsed_time(b) for a, b in ev_k]
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    verdict, bitmap = verdicts[(args.steps - 1) % 2], bitmaps[(args.steps - 1) % 2]
 
     # correctness gate: without --adv every message of the workload is an honest
     # vote by construction, so every verdict must be VALID and the valid bitmap

@@ -5,8 +5,10 @@ or fails to load, importing the binding raises immediately.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
+import weakref
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HD_LIB", os.path.join(HERE, "_lib", "libhdverify.so"))
@@ -170,3 +172,22 @@ class HDError(RuntimeError):
             msg += f": {detail}"
         super().__init__(msg)
         self.code = code
+
+
+# Native handles still open at interpreter exit are closed by an atexit hook
+# (queues and vote tables before their contexts), while the HIP runtime and
+# torch are still alive, instead of by finalizers during teardown.
+_LIVE = weakref.WeakSet()
+
+
+def track(obj) -> None:
+    _LIVE.add(obj)
+
+
+@atexit.register
+def _close_all() -> None:
+    for o in sorted(list(_LIVE), key=lambda o: getattr(o, "_close_rank", 0)):
+        try:
+            o.close()
+        except Exception:
+            pass

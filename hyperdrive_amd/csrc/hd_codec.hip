@@ -182,8 +182,9 @@ uint32_t hd_record_size(int type, int with_sig) {
 
 int hd_unmarshal_batch_device(hd_ctx* ctx, int type, int with_sig, const uint8_t* d_buf, uint64_t len, uint32_t n,
                               const hd_batch_out* d_out, uint8_t* d_status, void* stream) {
-    if (!ctx || !d_out || hd_record_size(type, with_sig) == 0) return HD_EINVAL;
+    if (!ctx || hd_record_size(type, with_sig) == 0) return HD_EINVAL;
     if (n == 0) return HD_OK;
+    if (!d_out) return HD_EINVAL;
     if (!d_buf || !d_status || !d_out->type || !d_out->height || !d_out->round || !d_out->value32 || !d_out->from32)
         return HD_EINVAL;
     if (type == T_PROPOSE && !d_out->valid_round) return HD_EINVAL;

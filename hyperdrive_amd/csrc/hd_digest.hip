@@ -139,8 +139,9 @@ uint32_t grid_for(const hd_ctx* ctx, uint32_t n) {
 extern "C" {
 
 int hd_digest_batch_device(hd_ctx* ctx, int algo, const hd_batch* db, uint8_t* d_digest32, void* stream) {
-    if (!ctx || !db || !d_digest32 || algo < HD_DIGEST_SHA256 || algo > HD_DIGEST_SHA3_256) return HD_EINVAL;
+    if (!ctx || !db || algo < HD_DIGEST_SHA256 || algo > HD_DIGEST_SHA3_256) return HD_EINVAL;
     if (db->n == 0) return HD_OK;
+    if (!d_digest32) return HD_EINVAL;
     if (!db->type || !db->height || !db->round || !db->value32) return HD_EINVAL;
     if ((uintptr_t)d_digest32 & 15) return HD_EINVAL;   // 16-byte stores
     (void)hipSetDevice(ctx->device);
@@ -156,8 +157,9 @@ int hd_digest_batch_device(hd_ctx* ctx, int algo, const hd_batch* db, uint8_t* d
 
 int hd_hash_bytes_device(hd_ctx* ctx, int algo, const uint8_t* d_data, const uint64_t* d_offsets, uint32_t n,
                          uint8_t* d_out32, void* stream) {
-    if (!ctx || !d_offsets || !d_out32 || algo < HD_DIGEST_SHA256 || algo > HD_DIGEST_SHA3_256) return HD_EINVAL;
+    if (!ctx || algo < HD_DIGEST_SHA256 || algo > HD_DIGEST_SHA3_256) return HD_EINVAL;
     if (n == 0) return HD_OK;
+    if (!d_offsets || !d_out32) return HD_EINVAL;
     if ((uintptr_t)d_out32 & 15) return HD_EINVAL;
     (void)hipSetDevice(ctx->device);
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;

@@ -344,9 +344,10 @@ int hd_mq_size(hd_mq* q, uint64_t* n) {
 }
 
 int hd_mq_insert_device(hd_mq* q, const hd_batch* d_batch, const int32_t* d_sender, void* stream) {
-    if (!q || !d_batch || !d_sender) return HD_EINVAL;
+    if (!q || !d_batch) return HD_EINVAL;
     const uint32_t nb = d_batch->n;
-    if (nb == 0) return HD_OK;
+    if (nb == 0) return HD_OK;  // empty device tensors may have NULL data pointers
+    if (!d_sender) return HD_EINVAL;
     if (!d_batch->type || !d_batch->height || !d_batch->round || !d_batch->value32 || !d_batch->from32)
         return HD_EINVAL;
     (void)hipSetDevice(q->ctx->device);
@@ -410,9 +411,10 @@ int hd_mq_insert_device(hd_mq* q, const hd_batch* d_batch, const int32_t* d_send
 
 int hd_mq_insert_verified_device(hd_mq* q, const hd_batch* d_batch, const uint8_t* d_verdict, const int32_t* d_signer,
                                  int64_t min_height, void* stream) {
-    if (!q || !d_batch || !d_verdict || !d_signer) return HD_EINVAL;
+    if (!q || !d_batch) return HD_EINVAL;
     const uint32_t nb = d_batch->n;
     if (nb == 0) return HD_OK;
+    if (!d_verdict || !d_signer) return HD_EINVAL;
     if (!d_batch->height) return HD_EINVAL;
     (void)hipSetDevice(q->ctx->device);
     hipStream_t s = stream ? (hipStream_t)stream : q->ctx->stream;

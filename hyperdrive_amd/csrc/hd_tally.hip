@@ -440,7 +440,8 @@ int hd_tally(hd_ctx* ctx, const hd_batch* batch, const uint8_t* verdict, hd_tall
 int hd_tally_device(hd_ctx* ctx, const hd_batch* dbatch, const uint8_t* d_verdict, const int32_t* d_signer,
                     hd_tally_out* out, void* stream) {
     (void)d_signer;  // logs are keyed by From itself (equal to the signer for VALID messages)
-    if (!ctx || !dbatch || !d_verdict || !tally_out_ok(out)) return HD_EINVAL;
+    if (!ctx || !dbatch || !tally_out_ok(out)) return HD_EINVAL;
+    if (dbatch->n && !d_verdict) return HD_EINVAL;
     out->n_counts = out->n_hr = 0;
     if (dbatch->n == 0) return HD_OK;
     (void)hipSetDevice(ctx->device);
@@ -449,7 +450,8 @@ int hd_tally_device(hd_ctx* ctx, const hd_batch* dbatch, const uint8_t* d_verdic
 
 int hd_tally_device_bitmap(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* d_valid_bitmap, hd_tally_out* out,
                            void* stream) {
-    if (!ctx || !dbatch || !d_valid_bitmap || !tally_out_ok(out)) return HD_EINVAL;
+    if (!ctx || !dbatch || !tally_out_ok(out)) return HD_EINVAL;
+    if (dbatch->n && !d_valid_bitmap) return HD_EINVAL;
     out->n_counts = out->n_hr = 0;
     if (dbatch->n == 0) return HD_OK;
     (void)hipSetDevice(ctx->device);

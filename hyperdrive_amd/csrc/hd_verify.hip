@@ -256,16 +256,18 @@ extern "C" {
 
 int hd_verify_batch_device(hd_ctx* ctx, const hd_batch* db, uint8_t* d_verdict, uint8_t* d_recovered32,
                            int32_t* d_signer, uint32_t* d_valid_bitmap, void* stream) {
-    if (!ctx || !db || !d_verdict) return HD_EINVAL;
-    if (db->n == 0) return HD_OK;
+    if (!ctx || !db) return HD_EINVAL;
+    if (db->n == 0) return HD_OK;  // empty device tensors may have NULL data pointers
+    if (!d_verdict) return HD_EINVAL;
     if (!db->type || !db->height || !db->round || !db->value32 || !db->from32 || !db->sig65) return HD_EINVAL;
     return launch_verify(ctx, db, nullptr, d_verdict, d_recovered32, d_signer, d_valid_bitmap, stream);
 }
 
 int hd_verify_batch_digest_device(hd_ctx* ctx, const hd_batch* db, const uint8_t* d_digest32, uint8_t* d_verdict,
                                   uint8_t* d_recovered32, int32_t* d_signer, uint32_t* d_valid_bitmap, void* stream) {
-    if (!ctx || !db || !d_verdict || !d_digest32) return HD_EINVAL;
+    if (!ctx || !db) return HD_EINVAL;
     if (db->n == 0) return HD_OK;
+    if (!d_verdict || !d_digest32) return HD_EINVAL;
     if (!db->type || !db->from32 || !db->sig65) return HD_EINVAL;
     return launch_verify(ctx, db, d_digest32, d_verdict, d_recovered32, d_signer, d_valid_bitmap, stream);
 }

@@ -28,6 +28,7 @@ class MessageQueue:
             raise _lib.HDError(rc, "hd_mq_create")
         self._q = h
         self.max_capacity = max_capacity
+        _lib.track(self)
 
     def close(self):
         if getattr(self, "_q", None):

@@ -120,6 +120,8 @@ class Verifier:
         if rc != 0:
             raise HDError(rc, "hd_ctx_create")
         self._ctx = h
+        self._close_rank = 1          # closed after the queues / tables that use it
+        _lib.track(self)
         self.device = device
         self._check(self._lib.hd_ctx_set_pubkey_format(self._ctx, 1 if compressed else 0), "set_pubkey_format")
         self.n_signatories = 0

@@ -39,6 +39,7 @@ class VoteLog:
         h = ctypes.c_void_p()
         self._check(self._lib.hd_votes_create(int(height), ctypes.byref(h)), "hd_votes_create")
         self._v = h
+        _lib.track(self)
 
     def _check(self, rc: int, where: str):
         if rc != 0:

@@ -194,3 +194,52 @@ def test_million_message_insert(verifier):
     keep = np.concatenate([order[snd[order] == k][:1000] for k in range(S)])
     assert idx.tolist() == keep.tolist()
     q.close()
+
+
+@pytest.mark.gpu
+def test_extreme_keys_and_empty_inputs(verifier):
+    """int64-extreme heights / rounds (InvalidRound = -1, negative and maximal
+    values) order exactly like the restatement; empty batches, batches with no
+    insertable message, and consume/drop on an empty queue are no-ops."""
+    import torch
+    from hyperdrive_amd.device import DeviceBatch
+    from hyperdrive_amd.mq import MessageQueue
+    rng = np.random.default_rng(77)
+    ext = np.array([-(1 << 63), -(1 << 62), -2, -1, 0, 1, 2, (1 << 62), (1 << 63) - 1], dtype=np.int64)
+    q = MessageQueue(verifier, 5)
+    o = OracleMQ(5)
+    b, s = q.consume(0)
+    assert len(b) == 0 and len(s) == 0 and len(q) == 0
+    q.drop_below(1 << 40)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    empty = DeviceBatch(0, t(np.zeros(0, np.uint8)), t(np.zeros(0, np.int64)), t(np.zeros(0, np.int64)),
+                        t(np.zeros(0, np.int64)), t(np.zeros((0, 32), np.uint8)), t(np.zeros((0, 32), np.uint8)),
+                        t(np.zeros((0, 65), np.uint8)))
+    q.insert_device(empty, t(np.zeros(0, np.int32)))
+    for step in range(6):
+        n = 400
+        h = rng.choice(ext, n)
+        r = rng.choice(ext, n)
+        typ = rng.integers(1, 4, n).astype(np.uint8)
+        val = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+        snd = rng.integers(-1, 4, n).astype(np.int32)
+        if step == 3:
+            snd[:] = -1                                    # nothing insertable
+        db = DeviceBatch(n, t(typ), t(h), t(r), t(np.full(n, -1, np.int64)), t(val), t(np.zeros((n, 32), np.uint8)),
+                         t(np.zeros((n, 65), np.uint8)))
+        q.insert_device(db, t(snd))
+        for i in range(n):
+            if snd[i] >= 0:
+                o.insert(int(snd[i]), (int(h[i]), int(r[i]), int(typ[i]), -1, val[i].tobytes(), bytes(32),
+                                       bytes(65)))
+        assert len(q) == len(o)
+    hh = int(ext[4])
+    b, s = q.consume(hh)
+    n_o, want = o.consume(hh)
+    assert _as_tuples(b, s) == want
+    q.drop_below(int(ext[7]))
+    o.drop_below(int(ext[7]))
+    b, s = q.consume((1 << 63) - 1)
+    n_o, want = o.consume((1 << 63) - 1)
+    assert _as_tuples(b, s) == want and len(q) == 0
+    q.close()

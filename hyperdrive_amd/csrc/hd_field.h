@@ -440,9 +440,6 @@ HD_FEMUL void fe_mul_impl(fe& out, const fe& a, const fe& b) {
         }
         const uint32_t hk = opaque_u32((uint32_t)d & HD_M29);
         chi = d >> 29;
-#ifdef HD_FE_SEQ
-        asm volatile("" : "+v"(clo) : "v"(d));
-#endif
         uint64_t c = mad64(hk, K1, clo);
         if (k > 0) c = mad64(hprev, K2, c);
         HD_UNROLL for (int i = 0; i <= k; i++) {
@@ -457,9 +454,6 @@ HD_FEMUL void fe_mul_impl(fe& out, const fe& a, const fe& b) {
         r.n[k] = (uint32_t)c & HD_M29;
         clo = c >> 29;
         hprev = hk;
-#ifdef HD_FE_SEQ
-        asm volatile("" : "+v"(chi) : "v"(c));
-#endif
     }
     // weight 2^261: W = clo + h8 2^8; weight 2^256: u = 32 W + (r8 >> 24) (< 2^42)
     const uint64_t u = ((clo + ((uint64_t)hprev << 8)) << 5) + (r.n[8] >> 24);

@@ -59,6 +59,11 @@ __global__ __launch_bounds__(256) void k_probe(uint32_t iters, uint32_t seed, ui
                 if (OP == 21) asm volatile("v_lshlrev_b64 %0, 7, %0" : "+v"(acc[k]));
                 if (OP == 22) asm volatile("v_mov_b32 %0, %1" : "=v"(x[k]) : "v"(y[k]));
                 if (OP == 23) asm volatile("v_bfe_u32 %0, %0, 3, 26" : "+v"(x[k]));
+                if (OP == 24) asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0\n\ts_nop 0"
+                                           : "+v"(acc[k]), "=s"(cy[k]) : "v"(x[k]), "v"(b));
+                if (OP == 25) asm volatile("s_nop 0\n\tv_add_u32 %0, %0, %1" : "+v"(x[k]) : "v"(b));
+                if (OP == 26) asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0\n\tv_mad_u64_u32 %0, %1, %2, %3, %0"
+                                           : "+v"(acc[k]), "=s"(cy[k]) : "v"(x[k]), "v"(b));
             }
         }
     }
@@ -76,9 +81,10 @@ static const char* NAMES[] = {"v_add_u32", "v_mad_u64_u32", "v_mul_lo_u32", "v_m
                               "v_dot4_u32_u8", "v_add_co+v_addc_co (2 instr)", "v_add3_u32", "v_and_b32",
                               "v_lshl_add_u32", "v_mul_u32_u24", "mad_u64 + add_u32 (2 instr)", "v_dot2_u32_u16",
                               "v_cndmask_b32", "v_lshrrev_b32", "mad_u64 + add + and (3 instr)", "v_add_co_u32",
-                              "v_lshlrev_b64", "v_mov_b32", "v_bfe_u32"};
-static const int NINSTR[] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1, 1, 2, 1, 1, 1, 3, 1, 1, 1, 1};
-#define NOPS 24
+                              "v_lshlrev_b64", "v_mov_b32", "v_bfe_u32", "mad + s_nop 0 (1 VALU)",
+                              "s_nop 0 + v_add_u32 (1 VALU)", "mad -> dependent mad (2 instr)"};
+static const int NINSTR[] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1, 1, 2, 1, 1, 1, 3, 1, 1, 1, 1, 1, 1, 2};
+#define NOPS 27
 
 template <int OP>
 static void run(int blocks, uint32_t iters, uint32_t* d, uint64_t* clk, int ncu) {

@@ -1,0 +1,384 @@
+// hd_fastverify.hip -- the known-key fast path of hd_verify_batch_device and
+// the tables it runs on (hd_fixedbase.h).
+//
+// Per batch, stream-ordered, no host synchronisation:
+//   k_verify_fast   one message per lane: a message whose claimed From is an
+//                   admitted signatory with a known key is checked with two
+//                   fixed-base multiplications (44 mixed additions, no
+//                   doublings, no square root); VALID / early exact verdicts
+//                   are final, everything else is appended to a list
+//   k_verify        (hd_verify.hip) the full libsecp256k1-semantics recovery
+//                   over that list only; VALID messages of signatories without
+//                   a known key publish the recovered key to their slot
+//   k_fb_bitmap     the valid bitmap from the final verdicts
+//   k_fb_list / k_fb_bases / k_fb_entries / k_fb_ready
+//                   build the tables of newly learned keys (22 window bases,
+//                   then 22 x 2048 affine multiples, one per lane); with
+//                   nothing learned each exits at once
+// Slot 0 holds the tables of G, built when the context is created.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/hd_verify.h"
+#include "hd_fixedbase.h"
+#include "hd_internal.h"
+#include "hd_verify_msg.h"
+
+using namespace hd;
+
+struct FbWork {
+    uint32_t nslots = 0;        // allocated slots; slot 0 = G
+    uint32_t max_slots = 2049;  // HD_FB_MAX_SLOTS
+    ge* tab = nullptr;          // nslots x HD_FB_TAB
+    ge* base = nullptr;         // nslots x HD_FB_NWIN window bases
+    ge* pub = nullptr;          // nslots keys
+    uint32_t* state = nullptr;  // nslots HD_FB_* states
+    int32_t* adm_slot = nullptr;  // admitted sorted index -> slot
+    size_t cap_adm_slot = 0;
+    uint32_t* list = nullptr;     // slot work list (nslots)
+    uint32_t* counts = nullptr;   // [0] slots to build, [1] messages for the slow path
+    uint32_t* slow = nullptr;     // message index list
+    size_t cap_slow = 0;
+    std::unordered_map<std::string, uint32_t> slot_of;  // signatory -> slot
+    std::vector<uint32_t> free_slots;
+    uint32_t used = 1;            // slots handed out so far (slot 0 = G)
+};
+
+namespace {
+
+#define FBCHK(expr, what)                                \
+    do {                                                 \
+        hipError_t e_ = (expr);                          \
+        if (e_ != hipSuccess) return hd_ctx_fail(ctx, e_, what); \
+    } while (0)
+
+// message i of a device batch, fields on demand (as DevSrc in hd_verify.hip)
+struct FastSrc {
+    const DevBatch& b;
+    uint32_t i;
+    const uint8_t* dg;
+    __device__ __forceinline__ uint32_t type() const { return b.type[i]; }
+    __device__ __forceinline__ uint32_t value(int w) const { return load_be32(b.value32 + 32 * (size_t)i + 4 * w); }
+    __device__ __forceinline__ uint32_t from(int w) const { return load_be32(b.from32 + 32 * (size_t)i + 4 * w); }
+    __device__ __forceinline__ uint32_t sig_r(int w) const { return load_be32(b.sig65 + 65 * (size_t)i + 4 * w); }
+    __device__ __forceinline__ uint32_t sig_s(int w) const { return load_be32(b.sig65 + 65 * (size_t)i + 32 + 4 * w); }
+    __device__ __forceinline__ uint32_t sig_v() const { return b.sig65[65 * (size_t)i + 64]; }
+};
+
+__global__ __launch_bounds__(256) void k_verify_fast(DevBatch b, const uint8_t* __restrict__ digest_in,
+                                                     const ge* __restrict__ tab, const uint32_t* __restrict__ state,
+                                                     const int32_t* __restrict__ adm_slot,
+                                                     const uint32_t* __restrict__ adm, const int32_t* __restrict__ adm_perm,
+                                                     uint32_t n_adm, int adm_steps, uint8_t* __restrict__ verdict,
+                                                     uint8_t* __restrict__ rec32, int32_t* __restrict__ signer,
+                                                     uint32_t* __restrict__ slow, uint32_t* __restrict__ n_slow) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool to_slow = false;
+    if (i < b.n) {
+        FastSrc src{b, i, digest_in};
+        const uint32_t type = src.type();
+        uint8_t v = HD_NEEDS_SLOW;
+        int32_t idx = -1;
+        uint32_t from_be[8];
+        HD_UNROLL for (int w = 0; w < 8; w++) from_be[w] = src.from(w);
+        if (type >= 1 && type <= 3) {
+            idx = admitted_find(adm, n_adm, adm_steps, from_be);
+            const int32_t slot = idx >= 0 ? adm_slot[idx] : -1;
+            if (slot >= 0 && state[slot] == HD_FB_READY) {
+                uint32_t d[8];
+                if (digest_in) {
+                    HD_UNROLL for (int w = 0; w < 8; w++) d[w] = load_be32(digest_in + 32 * (size_t)i + 4 * w);
+                } else {
+                    uint32_t value_be[8];
+                    HD_UNROLL for (int w = 0; w < 8; w++) value_be[w] = src.value(w);
+                    if (type == T_PROPOSE)
+                        sha256_propose(d, b.height[i], b.round[i], b.valid_round ? b.valid_round[i] : -1, value_be);
+                    else
+                        sha256_vote(d, b.height[i], b.round[i], value_be);
+                }
+                uint32_t r_be[8], s_be[8];
+                HD_UNROLL for (int w = 0; w < 8; w++) { r_be[w] = src.sig_r(w); s_be[w] = src.sig_s(w); }
+                v = verify_fast(d, r_be, s_be, src.sig_v(), tab, tab + (size_t)slot * HD_FB_TAB);
+            }
+        } else {
+            v = V_BAD_TYPE;
+        }
+        if (v == HD_NEEDS_SLOW) {
+            to_slow = true;
+        } else {
+            // VALID: the recovered key is the signatory's, so the recovered
+            // signatory is From; early verdicts recover nothing
+            const bool ok = v == V_VALID;
+            verdict[i] = v;
+            if (rec32) {
+                uint8_t* o = rec32 + 32 * (size_t)i;
+                HD_UNROLL for (int k = 0; k < 8; k++) store_be32(o + 4 * k, ok ? from_be[k] : 0u);
+            }
+            if (signer) signer[i] = ok ? adm_perm[idx] : -1;
+        }
+    }
+    // wave-aggregated append of the slow-path indices (order is irrelevant:
+    // every message is verified on its own)
+    const unsigned long long bal = __ballot(to_slow);
+    if (bal) {
+        const uint32_t lane = threadIdx.x & 63u;
+        const uint32_t leader = (uint32_t)__ffsll((long long)bal) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(n_slow, (uint32_t)__popcll(bal));
+        base = __shfl(base, (int)leader);
+        if (to_slow) slow[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1))] = i;
+    }
+}
+
+__global__ void k_fb_bitmap(uint32_t n, const uint8_t* __restrict__ verdict, uint32_t* __restrict__ bitmap) {
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (32 * w >= n) return;
+    uint32_t bits = 0;
+    const uint32_t lim = min(32u, n - 32 * w);
+    for (uint32_t k = 0; k < lim; k++) bits |= (uint32_t)(verdict[32 * w + k] == V_VALID) << k;
+    bitmap[w] = bits;
+}
+
+__global__ void k_fb_list(uint32_t nslots, const uint32_t* __restrict__ state, uint32_t* __restrict__ list,
+                          uint32_t* __restrict__ count) {
+    __shared__ uint32_t c;
+    if (threadIdx.x == 0) c = 0;
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < nslots; k += blockDim.x)
+        if (state[k] == HD_FB_LEARNED) list[atomicAdd(&c, 1u)] = k;
+    __syncthreads();
+    if (threadIdx.x == 0) *count = c;
+}
+
+__global__ __launch_bounds__(256) void k_fb_bases(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
+                                                  const ge* __restrict__ pub, ge* __restrict__ base) {
+    const uint32_t total = *count * HD_FB_NWIN;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+        const uint32_t slot = list[t / HD_FB_NWIN], j = t % HD_FB_NWIN;
+        ge o;
+        fb_window_base(o, pub[slot], (int)j);
+        base[(size_t)slot * HD_FB_NWIN + j] = o;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fb_entries(const uint32_t* __restrict__ list,
+                                                    const uint32_t* __restrict__ count, const ge* __restrict__ base,
+                                                    ge* __restrict__ tab) {
+    const uint32_t total = *count * HD_FB_TAB;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+        const uint32_t slot = list[t / HD_FB_TAB], e = t % HD_FB_TAB;
+        const uint32_t j = e / HD_FB_N, d = e % HD_FB_N + 1;
+        ge o;
+        fb_entry(o, base[(size_t)slot * HD_FB_NWIN + j], d);
+        tab[(size_t)slot * HD_FB_TAB + e] = o;
+    }
+}
+
+__global__ void k_fb_ready(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
+                           uint32_t* __restrict__ state) {
+    for (uint32_t k = threadIdx.x; k < *count; k += blockDim.x) state[list[k]] = HD_FB_READY;
+}
+
+int fb_grow_slots(hd_ctx* ctx, uint32_t want) {
+    FbWork* f = ctx->fb;
+    if (want <= f->nslots) return HD_OK;
+    const uint32_t n = std::min(f->max_slots, std::max(want, 2 * f->nslots));
+    ge *tab = nullptr, *base = nullptr, *pub = nullptr;
+    uint32_t *state = nullptr, *list = nullptr;
+    FBCHK(hipMalloc(&tab, sizeof(ge) * HD_FB_TAB * (size_t)n), "fb tables");
+    FBCHK(hipMalloc(&base, sizeof(ge) * HD_FB_NWIN * (size_t)n), "fb bases");
+    FBCHK(hipMalloc(&pub, sizeof(ge) * (size_t)n), "fb keys");
+    FBCHK(hipMalloc(&state, 4 * (size_t)n), "fb state");
+    FBCHK(hipMalloc(&list, 4 * (size_t)n), "fb list");
+    FBCHK(hipMemset(state, 0, 4 * (size_t)n), "fb state clear");
+    if (f->nslots) {
+        const size_t k = f->nslots;
+        FBCHK(hipMemcpy(tab, f->tab, sizeof(ge) * HD_FB_TAB * k, hipMemcpyDeviceToDevice), "fb copy");
+        FBCHK(hipMemcpy(base, f->base, sizeof(ge) * HD_FB_NWIN * k, hipMemcpyDeviceToDevice), "fb copy");
+        FBCHK(hipMemcpy(pub, f->pub, sizeof(ge) * k, hipMemcpyDeviceToDevice), "fb copy");
+        FBCHK(hipMemcpy(state, f->state, 4 * k, hipMemcpyDeviceToDevice), "fb copy");
+        (void)hipFree(f->tab);
+        (void)hipFree(f->base);
+        (void)hipFree(f->pub);
+        (void)hipFree(f->state);
+        (void)hipFree(f->list);
+    }
+    f->tab = tab;
+    f->base = base;
+    f->pub = pub;
+    f->state = state;
+    f->list = list;
+    f->nslots = n;
+    return HD_OK;
+}
+
+// build the tables of every LEARNED slot, stream-ordered
+int fb_learn(hd_ctx* ctx, hipStream_t s) {
+    FbWork* f = ctx->fb;
+    const uint32_t g = (uint32_t)std::max(ctx->n_cu, 1) * 4u;
+    k_fb_list<<<1, 256, 0, s>>>(f->nslots, f->state, f->list, f->counts);
+    k_fb_bases<<<g, 256, 0, s>>>(f->list, f->counts, f->pub, f->base);
+    k_fb_entries<<<g * 2, 256, 0, s>>>(f->list, f->counts, f->base, f->tab);
+    k_fb_ready<<<1, 256, 0, s>>>(f->list, f->counts, f->state);
+    FBCHK(hipGetLastError(), "fb table kernels");
+    return HD_OK;
+}
+
+}  // namespace
+
+int hd_fb_init(hd_ctx* ctx) {
+    if (ctx->fb) return HD_OK;
+    ctx->fb = new (std::nothrow) FbWork();
+    if (!ctx->fb) return HD_ENOMEM;
+    FbWork* f = ctx->fb;
+    if (const char* m = getenv("HD_FB_MAX_SLOTS")) f->max_slots = std::max(1, atoi(m)) + 1u;
+    FBCHK(hipMalloc(&f->counts, 8), "fb counts");
+    int rc = fb_grow_slots(ctx, 1);
+    if (rc) return rc;
+    // slot 0: G
+    ge g;
+    const uint32_t GX[8] = {0x79BE667Eu, 0xF9DCBBACu, 0x55A06295u, 0xCE870B07u,
+                            0x029BFCDBu, 0x2DCE28D9u, 0x59F2815Bu, 0x16F81798u};
+    const uint32_t GY[8] = {0x483ADA77u, 0x26A3C465u, 0x5DA4FBFCu, 0x0E1108A8u,
+                            0xFD17B448u, 0xA6855419u, 0x9C47D08Fu, 0xFB10D4B8u};
+    fe_from_be(g.x, GX);
+    fe_from_be(g.y, GY);
+    const uint32_t learned = HD_FB_LEARNED;
+    FBCHK(hipMemcpy(f->pub, &g, sizeof(ge), hipMemcpyHostToDevice), "fb G");
+    FBCHK(hipMemcpy(f->state, &learned, 4, hipMemcpyHostToDevice), "fb G state");
+    rc = fb_learn(ctx, ctx->stream);
+    if (rc) return rc;
+    FBCHK(hipStreamSynchronize(ctx->stream), "fb G tables");
+    return HD_OK;
+}
+
+void hd_fb_release(hd_ctx* ctx) {
+    if (!ctx || !ctx->fb) return;
+    FbWork* f = ctx->fb;
+    void* ptrs[] = {f->tab, f->base, f->pub, f->state, f->list, f->counts, f->slow, f->adm_slot};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    delete f;
+    ctx->fb = nullptr;
+}
+
+int hd_fb_map_signatories(hd_ctx* ctx, const uint8_t* sorted, uint32_t m) {
+    FbWork* f = ctx->fb;
+    std::unordered_map<std::string, uint32_t> keep;
+    std::vector<int32_t> adm_slot(std::max(m, 1u), -1);
+    std::vector<uint32_t> fresh;
+    for (uint32_t k = 0; k < m; k++) {
+        std::string key(reinterpret_cast<const char*>(sorted + 32 * (size_t)k), 32);
+        auto it = f->slot_of.find(key);
+        if (it != f->slot_of.end()) {
+            adm_slot[k] = (int32_t)it->second;
+            keep.emplace(key, it->second);
+            f->slot_of.erase(it);
+        }
+    }
+    // signatories no longer admitted give their slots back
+    for (auto& kv : f->slot_of) {
+        f->free_slots.push_back(kv.second);
+        fresh.push_back(kv.second);
+    }
+    f->slot_of.swap(keep);
+    for (uint32_t k = 0; k < m; k++) {
+        if (adm_slot[k] >= 0) continue;
+        uint32_t slot;
+        if (!f->free_slots.empty()) {
+            slot = f->free_slots.back();
+            f->free_slots.pop_back();
+        } else if (f->used < f->max_slots) {
+            slot = f->used++;
+        } else {
+            continue;  // over the slot cap: this signatory always takes the full recovery
+        }
+        adm_slot[k] = (int32_t)slot;
+        f->slot_of.emplace(std::string(reinterpret_cast<const char*>(sorted + 32 * (size_t)k), 32), slot);
+        fresh.push_back(slot);
+    }
+    int rc = fb_grow_slots(ctx, f->used);
+    if (rc) return rc;
+    for (uint32_t slot : fresh) FBCHK(hipMemset(f->state + slot, 0, 4), "fb slot reset");
+    rc = hd_dev_grow(ctx, (void**)&f->adm_slot, &f->cap_adm_slot, 4 * adm_slot.size());
+    if (rc) return rc;
+    FBCHK(hipMemcpy(f->adm_slot, adm_slot.data(), 4 * adm_slot.size(), hipMemcpyHostToDevice), "fb adm_slot");
+    return HD_OK;
+}
+
+int hd_fb_clear_keys(hd_ctx* ctx) {
+    FbWork* f = ctx->fb;
+    FBCHK(hipDeviceSynchronize(), "fb clear sync");
+    if (f->nslots > 1) FBCHK(hipMemset(f->state + 1, 0, 4 * (size_t)(f->nslots - 1)), "fb clear");
+    return HD_OK;
+}
+
+int hd_fb_verify(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict, uint8_t* d_rec32,
+                 int32_t* d_signer, uint32_t* d_bitmap, hipStream_t s) {
+    FbWork* f = ctx->fb;
+    int rc = hd_dev_grow(ctx, (void**)&f->slow, &f->cap_slow, 4 * (size_t)b.n);
+    if (rc) return rc;
+    const uint32_t blocks = (b.n + 255) / 256;
+    FBCHK(hipMemsetAsync(f->counts + 1, 0, 4, s), "fb count reset");
+    if (ctx->n_adm > 0 && f->adm_slot) {
+        k_verify_fast<<<blocks, 256, 0, s>>>(b, d_digest, f->tab, f->state, f->adm_slot, ctx->d_adm, ctx->d_adm_perm,
+                                             ctx->n_adm, ctx->adm_steps, d_verdict, d_rec32, d_signer, f->slow,
+                                             f->counts + 1);
+        FBCHK(hipGetLastError(), "k_verify_fast launch");
+        const SlowCtl ctl{f->slow, f->counts + 1, f->adm_slot, f->state, f->pub};
+        rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl, blocks, s);
+        if (rc) return rc;
+        if (d_bitmap) {
+            k_fb_bitmap<<<((b.n + 31) / 32 + 255) / 256, 256, 0, s>>>(b.n, d_verdict, d_bitmap);
+            FBCHK(hipGetLastError(), "k_fb_bitmap launch");
+        }
+        return fb_learn(ctx, s);
+    }
+    // no admitted set: every message takes the full recovery (it ends in
+    // NOT_ADMITTED at best), nothing to learn
+    const SlowCtl none{nullptr, nullptr, nullptr, nullptr, nullptr};
+    return hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, none, blocks, s);
+}
+
+extern "C" {
+
+int hd_ctx_set_fastpath(hd_ctx* ctx, int enable) {
+    if (!ctx) return HD_EINVAL;
+    if (enable && !ctx->fb) {
+        (void)hipSetDevice(ctx->device);
+        int rc = hd_fb_init(ctx);
+        if (rc) return rc;
+        // map the current admitted set (sorted words -> bytes)
+        if (ctx->n_adm) {
+            std::vector<uint32_t> words(8 * (size_t)ctx->n_adm);
+            FBCHK(hipMemcpy(words.data(), ctx->d_adm, 32 * (size_t)ctx->n_adm, hipMemcpyDeviceToHost), "adm read");
+            std::vector<uint8_t> sorted(32 * (size_t)ctx->n_adm);
+            for (size_t k = 0; k < words.size(); k++) store_be32(&sorted[4 * k], words[k]);
+            rc = hd_fb_map_signatories(ctx, sorted.data(), ctx->n_adm);
+            if (rc) return rc;
+        }
+    }
+    ctx->fastpath = enable != 0;
+    return HD_OK;
+}
+
+int hd_ctx_known_keys(hd_ctx* ctx, uint32_t* n) {
+    if (!ctx || !n) return HD_EINVAL;
+    *n = 0;
+    if (!ctx->fb || ctx->fb->nslots <= 1) return HD_OK;
+    (void)hipSetDevice(ctx->device);
+    FbWork* f = ctx->fb;
+    FBCHK(hipDeviceSynchronize(), "known keys sync");
+    std::vector<uint32_t> st(f->nslots);
+    FBCHK(hipMemcpy(st.data(), f->state, 4 * (size_t)f->nslots, hipMemcpyDeviceToHost), "state read");
+    for (uint32_t k = 1; k < f->nslots; k++) *n += st[k] == HD_FB_READY;
+    return HD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,137 @@
+// hd_fixedbase.h -- verification against a known public key with fixed-base
+// tables (the fast path of k_verify; DESIGN.md §4 "Known-key fast path").
+//
+// The reference authenticates a message by recovering the public key Q from
+// (digest, r, s, v) and comparing SHA-256(Q) with the claimed From
+// (libsecp256k1 recover; process/message_test.go:147-154).
+// Once a signatory's public key P is known -- learned from a message of that
+// signatory that verified VALID through the full recovery, so SHA-256(P) is
+// its signatory -- a message claiming that From is VALID iff its recovered key
+// is P, i.e. iff
+//
+//     R == s^-1 (m G + r P)        R = lift(r [+ n], v & 1), m = digest mod n
+//
+// (then Q = r^-1 (s R - m G) = P).  Both scalar multiplications have fixed
+// bases, so they run without doublings over per-base tables of
+// 22 windows x 2048 affine multiples: entry (j, d) = d 2^(12j) B, and each
+// signed 12-bit Booth digit costs one mixed addition.  No square root is
+// needed: the affine result is compared with x and the parity of y.
+//
+// verify_fast returns V_VALID only when that identity holds, an exact early
+// verdict (BAD_RECID, BAD_RS, NO_POINT for r + n >= p) where the reference's
+// first checks decide, and HD_NEEDS_SLOW otherwise; the caller then runs the
+// full recovery, which yields the reference verdict and recovered signatory.
+#pragma once
+#include "hd_group.h"
+
+namespace hd {
+
+#define HD_FB_W 12
+#define HD_FB_NWIN 22                      // Booth windows over a 256-bit scalar (264 bits)
+#define HD_FB_N 2048                       // |digit| <= 2^(W-1)
+#define HD_FB_TAB (HD_FB_NWIN * HD_FB_N)   // affine entries per base (3.2 MB of ge)
+#define HD_NEEDS_SLOW 0xFEu
+
+// slot states of the per-signatory tables (device memory, hd_fastverify.hip)
+#define HD_FB_EMPTY 0u     // no key known
+#define HD_FB_CLAIMED 1u   // a recovering lane is writing the key
+#define HD_FB_LEARNED 2u   // key known, tables not built yet
+#define HD_FB_READY 3u     // tables built
+
+// acc += u B, tab = the base's HD_FB_TAB entries
+template <typename Tab>
+HD void fb_accumulate(gej& acc, const sc& u, Tab tab) {
+    HD_NOUNROLL for (int j = 0; j < HD_FB_NWIN; j++) {
+        const int d = booth_digit<HD_FB_W>(u, j);
+        const int ad = d < 0 ? -d : d;
+        ge t = tab[j * HD_FB_N + (ad == 0 ? 0 : ad - 1)];
+        if (d < 0) fe_neg(t.y, t.y);
+        gej s;
+        gej_add_ge(s, acc, t);
+        gej_cmov(acc, s, d != 0);
+    }
+}
+
+// The reference's first checks (recover, SURVEY Appendix A items 2-4 up to
+// the lift): V >= 4, r / s range, r + n >= p.  On success x = r (+ n) as a
+// canonical field element and r, s as scalars; returns V_VALID to continue.
+HD uint8_t sig_prefix(sc& r, sc& s, fe& x, const uint32_t r_be[8], const uint32_t s_be[8], uint32_t v) {
+    if (v >= 4) return V_BAD_RECID;
+    HD_UNROLL for (int i = 0; i < 8; i++) { r.v[i] = r_be[7 - i]; s.v[i] = s_be[7 - i]; }
+    if (sc_ge_n(r.v) || sc_ge_n(s.v)) return V_BAD_RS;
+    if (sc_is_zero(r) || sc_is_zero(s)) return V_BAD_RS;
+    uint32_t xw[8];
+    HD_UNROLL for (int i = 0; i < 8; i++) xw[i] = r.v[i];
+    if (v & 2) {
+        // r + n < p  <=>  r < p - n = 0x14551231950B75FC4402DA1722FC9BAEE
+        const uint32_t PMN[8] = {0x2FC9BAEEu, 0x402DA172u, 0x50B75FC4u, 0x45512319u, 1u, 0u, 0u, 0u};
+        bool lt = false, gt = false;
+        HD_UNROLL for (int i = 7; i >= 0; i--) {
+            const bool g = !lt && !gt && r.v[i] > PMN[i];
+            const bool l = !lt && !gt && r.v[i] < PMN[i];
+            gt = gt || g;
+            lt = lt || l;
+        }
+        if (!lt) return V_NO_POINT;
+        const uint32_t N[8] = {HD_N0, HD_N1, HD_N2, HD_N3, HD_N4, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        uint64_t c = 0;
+        HD_UNROLL for (int i = 0; i < 8; i++) { c += (uint64_t)xw[i] + N[i]; xw[i] = (uint32_t)c; c >>= 32; }
+    }
+    fe_from_le(x, xw);
+    return V_VALID;
+}
+
+// VALID iff lift(r [+n], v & 1) == s^-1 (m G + r P); see the header comment.
+template <typename GT, typename PT>
+HD uint8_t verify_fast(const uint32_t digest_be[8], const uint32_t r_be[8], const uint32_t s_be[8], uint32_t v,
+                       GT gtab, PT ptab) {
+    sc r, s;
+    fe x;
+    const uint8_t pre = sig_prefix(r, s, x, r_be, s_be, v);
+    if (pre != V_VALID) return pre;
+    sc m, sinv, u1, u2;
+    sc_from_be_reduce(m, digest_be);
+    sc_inv_divsteps(sinv, s);
+    sc_mul(u1, m, sinv);
+    sc_mul(u2, r, sinv);
+    gej acc;
+    gej_set_inf(acc);
+    fb_accumulate(acc, u1, gtab);
+    fb_accumulate(acc, u2, ptab);
+    if (gej_is_inf(acc)) return HD_NEEDS_SLOW;
+    fe zi, zi2, ax, ay;
+    fe_inv_divsteps(zi, acc.z);
+    fe_sqr(zi2, zi);
+    fe_mul(ax, acc.x, zi2);
+    fe_mul(zi2, zi2, zi);
+    fe_mul(ay, acc.y, zi2);
+    fe_normalize(ax);
+    fe_normalize(ay);
+    uint32_t diff = (ay.n[0] & 1u) ^ (v & 1u);
+    HD_UNROLL for (int i = 0; i < 9; i++) diff |= ax.n[i] ^ x.n[i];
+    return diff ? HD_NEEDS_SLOW : V_VALID;
+}
+
+// ---- table construction (one entry per lane) --------------------------
+// 2^(12 j) B, affine canonical
+HD void fb_window_base(ge& out, const ge& B, int j) {
+    gej a;
+    gej_set_ge(a, B);
+    HD_NOUNROLL for (int k = 0; k < HD_FB_W * j; k++) gej_dbl(a, a);
+    gej_to_ge(out.x, out.y, a);
+}
+
+// d Bj for 1 <= d <= 2048, affine canonical (double-and-add from the top bit)
+HD void fb_entry(ge& out, const ge& Bj, uint32_t d) {
+    int top = 31;
+    while (top > 0 && !((d >> top) & 1u)) top--;
+    gej a;
+    gej_set_ge(a, Bj);
+    HD_NOUNROLL for (int b = top - 1; b >= 0; b--) {
+        gej_dbl(a, a);
+        if ((d >> b) & 1u) gej_add_ge(a, a, Bj);
+    }
+    gej_to_ge(out.x, out.y, a);
+}
+
+}  // namespace hd

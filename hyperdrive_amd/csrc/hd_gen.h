@@ -85,18 +85,6 @@ HD void ecmult_gen(gej& out, const sc& k, GTab gtab) {
     out = acc;
 }
 
-// affine, canonical
-HD void gej_to_ge(fe& x, fe& y, const gej& a) {
-    fe zi, zi2;
-    fe_inv_divsteps(zi, a.z);
-    fe_sqr(zi2, zi);
-    fe_mul(x, a.x, zi2);
-    fe_mul(zi2, zi2, zi);
-    fe_mul(y, a.y, zi2);
-    fe_normalize(x);
-    fe_normalize(y);
-}
-
 template <typename GTab>
 HD void pubkey_signatory(uint32_t out_be[8], const sc& sk, bool compressed, GTab gtab) {
     gej P;

@@ -595,6 +595,18 @@ HD_HOSTONLY void build_gtab_glv(ge* tab) {
     }
 }
 
+// affine, canonical (a finite)
+HD void gej_to_ge(fe& x, fe& y, const gej& a) {
+    fe zi, zi2;
+    fe_inv_divsteps(zi, a.z);
+    fe_sqr(zi2, zi);
+    fe_mul(x, a.x, zi2);
+    fe_mul(zi2, zi2, zi);
+    fe_mul(y, a.y, zi2);
+    fe_normalize(x);
+    fe_normalize(y);
+}
+
 // ------------------------------------------------------------ recovery
 // libsecp256k1 recover semantics:
 //   V >= 4 -> BAD_RECID (go-ethereum checkSignature); r or s >= n -> BAD_RS

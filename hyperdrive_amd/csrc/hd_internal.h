@@ -29,6 +29,7 @@ struct DevBuf {
 };
 
 struct TallyWork;  // hd_tally.hip
+struct FbWork;     // hd_fastverify.hip: known-key tables and fast-path scratch
 
 struct hd_ctx {
     int device = 0;
@@ -44,6 +45,8 @@ struct hd_ctx {
     int adm_steps = 0;
     DevBuf bufs[BUF__COUNT];
     TallyWork* tally = nullptr;
+    FbWork* fb = nullptr;
+    bool fastpath = true;   // known-key fast path (HD_VERIFY_FASTPATH=0 disables)
     std::string last_error;
 };
 
@@ -52,3 +55,23 @@ int hd_dev_grow(hd_ctx* ctx, void** p, size_t* cap, size_t need);
 int hd_upload_batch(hd_ctx* ctx, const hd_batch* hb, hd_batch* db);
 int hd_verify_uploaded(hd_ctx* ctx, const hd_batch* db, uint8_t* verdict, uint8_t* recovered32, uint32_t* valid_bitmap);
 void hd_tally_release(hd_ctx* ctx);
+
+// known-key fast path (hd_fastverify.hip)
+int hd_fb_init(hd_ctx* ctx);                    // tables of G (slot 0); at context creation
+void hd_fb_release(hd_ctx* ctx);
+int hd_fb_map_signatories(hd_ctx* ctx, const uint8_t* sorted_sigs32, uint32_t m);  // after hd_set_signatories
+int hd_fb_clear_keys(hd_ctx* ctx);               // pubkey format changed: learned keys no longer apply
+// fast kernel + slow recovery of the rest + learning; the whole verify of a device batch
+int hd_fb_verify(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict, uint8_t* d_rec32,
+                 int32_t* d_signer, uint32_t* d_bitmap, hipStream_t s);
+
+// slow-path control for k_verify (hd_verify.hip): an index list and key learning
+struct SlowCtl {
+    const uint32_t* list;   // message indices to verify, or NULL for all
+    const uint32_t* count;  // device count of list
+    const int32_t* adm_slot;  // admitted sorted index -> table slot (-1 none), NULL: no learning
+    uint32_t* fb_state;
+    hd::ge* fb_pub;
+};
+int hd_launch_slow(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict, uint8_t* d_rec32,
+                   int32_t* d_signer, uint32_t* d_bitmap, const SlowCtl& ctl, uint32_t blocks, hipStream_t s);

@@ -23,6 +23,7 @@
 
 #include "../../include/hd_digest.h"
 #include "../../include/hd_verify.h"
+#include "hd_fixedbase.h"
 #include "hd_verify_msg.h"
 #include "hd_internal.h"
 
@@ -48,28 +49,45 @@ struct DevSrc {
     __device__ __forceinline__ uint32_t digest(int w) const { return load_be32(dg + 32 * (size_t)i + 4 * w); }
 };
 
+// With ctl.list, lane p verifies message ctl.list[p] for p < *ctl.count (the
+// known-key fast path's leftovers); with ctl.adm_slot, a VALID message whose
+// signatory has no known key yet publishes its recovered key to the
+// signatory's table slot (first writer wins, hd_fixedbase.h states).
 template <bool COMPRESSED, int WAVES>
 __global__ __launch_bounds__(256, WAVES) void k_verify(DevBatch b, const ge* __restrict__ gtab_g,
                                                 const uint32_t* __restrict__ adm, const int32_t* __restrict__ adm_perm,
                                                 uint32_t n_adm, int adm_steps, uint8_t* __restrict__ verdict,
                                                 uint8_t* __restrict__ rec32, int32_t* __restrict__ signer,
-                                                uint32_t* __restrict__ bitmap, const uint8_t* __restrict__ digest_in) {
+                                                uint32_t* __restrict__ bitmap, const uint8_t* __restrict__ digest_in,
+                                                SlowCtl ctl) {
     const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t base = blockIdx.x * blockDim.x; base < b.n; base += stride) {
-        const uint32_t i = base + threadIdx.x;
-        const bool active = i < b.n;
+    const uint32_t total = ctl.list ? *ctl.count : b.n;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += stride) {
+        const uint32_t p = base + threadIdx.x;
+        const bool active = p < total;
         uint8_t v = 0xFF;
         if (active) {
+            const uint32_t i = ctl.list ? ctl.list[p] : p;
             DevSrc src{b, i, digest_in};
             uint32_t rec[8];
             int32_t s;
-            v = verify_msg_src(src, gtab_g, adm, n_adm, adm_steps, COMPRESSED, rec, s);
+            ge q;
+            v = verify_msg_src(src, gtab_g, adm, n_adm, adm_steps, COMPRESSED, rec, s, ctl.adm_slot ? &q : nullptr);
             verdict[i] = v;
             if (rec32) {
                 uint8_t* o = rec32 + 32 * (size_t)i;
                 HD_UNROLL for (int w = 0; w < 8; w++) store_be32(o + 4 * w, rec[w]);
             }
             if (signer) signer[i] = s >= 0 ? adm_perm[s] : -1;
+            if (ctl.adm_slot && v == V_VALID) {
+                const int32_t slot = ctl.adm_slot[s];
+                if (slot >= 0 && ctl.fb_state[slot] == HD_FB_EMPTY &&
+                    atomicCAS(&ctl.fb_state[slot], HD_FB_EMPTY, HD_FB_CLAIMED) == HD_FB_EMPTY) {
+                    ctl.fb_pub[slot] = q;
+                    __threadfence();
+                    atomicExch(&ctl.fb_state[slot], HD_FB_LEARNED);
+                }
+            }
         }
         if (bitmap) {
             const unsigned long long bal = __ballot(active && v == V_VALID);
@@ -141,6 +159,7 @@ int hd_ctx_create(int device, hd_ctx** out) {
         int v = atoi(w);
         if (v >= 2 && v <= 4) ctx->verify_waves = v;
     }
+    if (const char* f = getenv("HD_VERIFY_FASTPATH")) ctx->fastpath = atoi(f) != 0;
     // G tables (1G..2048G and lambda*(1G..2048G), affine), built once on the
     // host with the same code the device runs, then uploaded.
     static std::once_flag once;
@@ -153,6 +172,13 @@ int hd_ctx_create(int device, hd_ctx** out) {
         int rc = hd_ctx_fail(ctx, e, "gtab upload");
         hd_ctx_destroy(ctx);
         return rc;
+    }
+    if (ctx->fastpath) {
+        const int rc = hd_fb_init(ctx);
+        if (rc) {
+            hd_ctx_destroy(ctx);
+            return rc;
+        }
     }
     *out = ctx;
     return HD_OK;
@@ -168,6 +194,7 @@ int hd_ctx_destroy(hd_ctx* ctx) {
     for (auto& b : ctx->bufs)
         if (b.p) (void)hipFree(b.p);
     hd_tally_release(ctx);
+    hd_fb_release(ctx);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return HD_OK;
@@ -175,13 +202,20 @@ int hd_ctx_destroy(hd_ctx* ctx) {
 
 int hd_ctx_set_pubkey_format(hd_ctx* ctx, int compressed) {
     if (!ctx) return HD_EINVAL;
-    ctx->compressed = compressed != 0;
+    const bool c = compressed != 0;
+    if (c != ctx->compressed) {
+        ctx->compressed = c;
+        // keys were learned under the other signatory derivation
+        if (ctx->fb) return hd_fb_clear_keys(ctx);
+    }
     return HD_OK;
 }
 
 int hd_set_signatories(hd_ctx* ctx, const uint8_t* sigs32, uint32_t n) {
     if (!ctx || (n && !sigs32)) return HD_EINVAL;
     (void)hipSetDevice(ctx->device);
+    // kernels of earlier calls (any stream) may still read the admitted tables
+    if (hipDeviceSynchronize() != hipSuccess) return hd_ctx_fail(ctx, hipGetLastError(), "set_signatories sync");
     // sort (stable on the original index so duplicates map to the first)
     std::vector<uint32_t> order(n);
     for (uint32_t i = 0; i < n; i++) order[i] = i;
@@ -214,26 +248,21 @@ int hd_set_signatories(hd_ctx* ctx, const uint8_t* sigs32, uint32_t n) {
     int steps = 0;
     while ((1u << steps) < m) steps++;
     ctx->adm_steps = steps;
+    if (ctx->fb) {
+        std::vector<uint8_t> sorted(32 * (size_t)m);
+        for (uint32_t k = 0; k < m; k++) memcpy(&sorted[32 * (size_t)k], sigs32 + 32 * (size_t)perm[k], 32);
+        return hd_fb_map_signatories(ctx, sorted.data(), m);
+    }
     return HD_OK;
 }
 
 }  // extern "C"
 
-namespace {
-int launch_verify(hd_ctx* ctx, const hd_batch* db, const uint8_t* d_digest, uint8_t* d_verdict, uint8_t* d_recovered32,
-                  int32_t* d_signer, uint32_t* d_valid_bitmap, void* stream) {
-    (void)hipSetDevice(ctx->device);
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-    DevBatch b{db->n, db->type, db->height, db->round, db->valid_round, db->value32, db->from32, db->sig65};
-    const uint32_t threads = 256;
-    // one block per 256 messages, no grid-stride: the dispatcher hands a CU a
-    // new block whenever one retires, which balances the last round better
-    // than a resident-sized grid looping over the batch (measured on 1M:
-    // 13.2 ms vs 13.5 ms at 2x resident blocks, 14.3 ms at 1x)
-    const uint32_t blocks = (db->n + threads - 1) / threads;
-#define HD_LAUNCH_VERIFY(C, W)                                                                             \
-    k_verify<C, W><<<blocks, threads, 0, s>>>(b, ctx->d_gtab, ctx->d_adm, ctx->d_adm_perm, ctx->n_adm, ctx->adm_steps, \
-                                              d_verdict, d_recovered32, d_signer, d_valid_bitmap, d_digest)
+int hd_launch_slow(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict, uint8_t* d_rec32,
+                   int32_t* d_signer, uint32_t* d_bitmap, const SlowCtl& ctl, uint32_t blocks, hipStream_t s) {
+#define HD_LAUNCH_VERIFY(C, W)                                                                                    \
+    k_verify<C, W><<<blocks, 256, 0, s>>>(b, ctx->d_gtab, ctx->d_adm, ctx->d_adm_perm, ctx->n_adm, ctx->adm_steps, \
+                                          d_verdict, d_rec32, d_signer, d_bitmap, d_digest, ctl)
     // waves/SIMD the kernel is register-allocated for (HD_VERIFY_WAVES = 2/3/4, default 3)
     const int w = ctx->verify_waves;
     if (ctx->compressed) {
@@ -249,6 +278,23 @@ int launch_verify(hd_ctx* ctx, const hd_batch* db, const uint8_t* d_digest, uint
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hd_ctx_fail(ctx, e, "k_verify launch");
     return HD_OK;
+}
+
+namespace {
+int launch_verify(hd_ctx* ctx, const hd_batch* db, const uint8_t* d_digest, uint8_t* d_verdict, uint8_t* d_recovered32,
+                  int32_t* d_signer, uint32_t* d_valid_bitmap, void* stream) {
+    (void)hipSetDevice(ctx->device);
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    DevBatch b{db->n, db->type, db->height, db->round, db->valid_round, db->value32, db->from32, db->sig65};
+    if (ctx->fastpath && ctx->fb)
+        return hd_fb_verify(ctx, b, d_digest, d_verdict, d_recovered32, d_signer, d_valid_bitmap, s);
+    // one block per 256 messages, no grid-stride: the dispatcher hands a CU a
+    // new block whenever one retires, which balances the last round better
+    // than a resident-sized grid looping over the batch (measured on 1M:
+    // 13.2 ms vs 13.5 ms at 2x resident blocks, 14.3 ms at 1x)
+    const uint32_t blocks = (db->n + 255) / 256;
+    const SlowCtl none{nullptr, nullptr, nullptr, nullptr, nullptr};
+    return hd_launch_slow(ctx, b, d_digest, d_verdict, d_recovered32, d_signer, d_valid_bitmap, none, blocks, s);
 }
 }  // namespace
 

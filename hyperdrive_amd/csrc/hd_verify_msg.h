@@ -62,10 +62,10 @@ HD int32_t admitted_find(AdmTab adm, uint32_t n, int steps, const uint32_t key[8
 // so the kernel loads each field from HBM in the phase that uses it and
 // nothing but the accumulator stays live across the ladder.  rec_be receives
 // the recovered signatory (zeros when recovery failed); signer the
-// admitted-table index.
+// admitted-table index; qout (optional) the recovered key of a VALID message.
 template <typename Src, typename GTab, typename AdmTab>
 HD uint8_t verify_msg_src(const Src& src, GTab gtab, AdmTab adm, uint32_t n_adm, int adm_steps, bool compressed,
-                          uint32_t rec_be[8], int32_t& signer) {
+                          uint32_t rec_be[8], int32_t& signer, ge* qout = nullptr) {
     signer = -1;
     HD_UNROLL for (int i = 0; i < 8; i++) rec_be[i] = 0;
     const uint32_t type = src.type();
@@ -107,6 +107,10 @@ HD uint8_t verify_msg_src(const Src& src, GTab gtab, AdmTab adm, uint32_t n_adm,
     int32_t idx = admitted_find(adm, n_adm, adm_steps, from_be);
     if (idx < 0) return V_NOT_ADMITTED;
     signer = idx;
+    if (qout) {  // the recovered key, for the known-key tables (hd_fixedbase.h)
+        qout->x = qx;
+        qout->y = qy;
+    }
     return V_VALID;
 }
 

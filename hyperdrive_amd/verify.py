@@ -157,6 +157,15 @@ class Verifier:
         self._check(self._lib.hd_set_signatories(self._ctx, _ptr(arr), len(arr)), "hd_set_signatories")
         self.n_signatories = len(arr)
 
+    def set_fastpath(self, enable: bool) -> None:
+        """Known-key fast path on/off (include/hd_verify.h hd_ctx_set_fastpath)."""
+        self._check(self._lib.hd_ctx_set_fastpath(self._ctx, 1 if enable else 0), "hd_ctx_set_fastpath")
+
+    def known_keys(self) -> int:
+        n = ctypes.c_uint32()
+        self._check(self._lib.hd_ctx_known_keys(self._ctx, ctypes.byref(n)), "hd_ctx_known_keys")
+        return int(n.value)
+
     def verify_batch(self, batch: Batch, recovered: bool = True) -> VerifyResult:
         n = len(batch)
         verdict = np.zeros(n, np.uint8)

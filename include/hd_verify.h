@@ -91,6 +91,18 @@ int hd_ctx_set_pubkey_format(hd_ctx* ctx, int compressed);
 /* Admitted set = procsAllowed.  sigs32: n x 32 bytes, any order, duplicates
  * allowed.  Signer indices reported by the library index this array. */
 int hd_set_signatories(hd_ctx* ctx, const uint8_t* sigs32, uint32_t n);
+/* Known-key fast path (on by default; HD_VERIFY_FASTPATH=0 in the
+ * environment turns it off for new contexts).  The first message of an
+ * admitted signatory that verifies VALID through the full recovery teaches
+ * the context that signatory's public key; later messages claiming that
+ * signatory are checked against the key with fixed-base tables
+ * (R == s^-1 (m G + r P)) and only fall back to the full recovery when the
+ * check fails.  Verdicts, recovered signatories, signer indices and bitmaps
+ * are identical either way.  Keys are kept across hd_set_signatories for
+ * signatories that stay admitted and dropped when the pubkey format changes. */
+int hd_ctx_set_fastpath(hd_ctx* ctx, int enable);
+/* number of admitted signatories whose key tables are built (synchronises) */
+int hd_ctx_known_keys(hd_ctx* ctx, uint32_t* n);
 
 /* ---- verification ------------------------------------------------------
  * verdict:     n bytes (HD_VERDICT_*), required.

@@ -5,6 +5,7 @@
 #include <string.h>
 #include <vector>
 #include "../../hyperdrive_amd/csrc/hd_gen.h"
+#include "../../hyperdrive_amd/csrc/hd_fixedbase.h"
 #include "../../hyperdrive_amd/csrc/hd_keccak.h"
 #include "../../hyperdrive_amd/csrc/hd_modinv.h"
 
@@ -327,4 +328,53 @@ extern "C" void hdh_keccak_msg(int pad, int type, int64_t h, int64_t r, int64_t 
     if (type == T_PROPOSE) keccak256_propose(d, h, r, vr, v, (uint8_t)pad);
     else keccak256_vote(d, h, r, v, (uint8_t)pad);
     for (int w = 0; w < 8; w++) store_be32(out32 + 4 * w, d[w]);
+}
+
+// Known-key fast path of hd_fixedbase.h on the host: tables of G and of the
+// key (x, y big-endian) are built with fb_window_base / fb_entry exactly as
+// the device builds them (cached for the last key), then verify_fast.
+static std::vector<ge> fb_tables(const ge& B) {
+    std::vector<ge> t(HD_FB_TAB);
+    for (int j = 0; j < HD_FB_NWIN; j++) {
+        ge bj;
+        fb_window_base(bj, B, j);
+        for (uint32_t d = 1; d <= HD_FB_N; d++) fb_entry(t[j * HD_FB_N + d - 1], bj, d);
+    }
+    return t;
+}
+extern "C" int hdh_fb_verify(const uint8_t* pub64, const uint8_t* digest, const uint8_t* sig65) {
+    static std::vector<ge> gt, pt;
+    static uint8_t last[64];
+    static bool have = false;
+    if (gt.empty()) {
+        ge g;
+        g.x = gtab()[0].x;
+        g.y = gtab()[0].y;
+        gt = fb_tables(g);
+    }
+    if (!have || memcmp(last, pub64, 64) != 0) {
+        ge P;
+        fe_in(P.x, pub64);
+        fe_in(P.y, pub64 + 32);
+        pt = fb_tables(P);
+        memcpy(last, pub64, 64);
+        have = true;
+    }
+    uint32_t d[8], r[8], sw[8];
+    for (int w = 0; w < 8; w++) {
+        d[w] = load_be32(digest + 4 * w);
+        r[w] = load_be32(sig65 + 4 * w);
+        sw[w] = load_be32(sig65 + 32 + 4 * w);
+    }
+    return verify_fast(d, r, sw, sig65[64], gt.data(), pt.data());
+}
+// one table entry d 2^(12 j) B (x || y big-endian), for the table-layout test
+extern "C" void hdh_fb_entry(const uint8_t* b64, int j, uint32_t d, uint8_t* out64) {
+    ge B, bj, e;
+    fe_in(B.x, b64);
+    fe_in(B.y, b64 + 32);
+    fb_window_base(bj, B, j);
+    fb_entry(e, bj, d);
+    fe_out(out64, e.x);
+    fe_out(out64 + 32, e.y);
 }

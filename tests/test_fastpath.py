@@ -1,0 +1,164 @@
+"""Known-key fast path (hd_fixedbase.h, hd_fastverify.hip).
+
+The fast path may only answer VALID when the full recovery would return
+exactly the known key, and otherwise must either give the reference's early
+verdict (BAD_RECID, BAD_RS, NO_POINT for r + n >= p) or hand the message to
+the full recovery.  CPU: the device header built for the host, against the
+oracle's recovery (oracle/hd_pyoracle.py), on honest, malleated, wrong-key,
+wrong-digest, wrong-parity, malformed and r + n signatures, and the table
+layout against oracle point multiplication.  GPU: verifying a batch with the
+fast path (keys learned on the first pass) gives bit-identical verdicts,
+recovered signatories, signer indices and bitmaps to the full recovery
+alone (HD_VERIFY_FASTPATH=0) on the adversarial mix, and the second pass
+really takes the fast path."""
+import ctypes
+import os
+import random
+
+import numpy as np
+import pytest
+
+NEEDS_SLOW = 0xFE
+
+
+@pytest.fixture(scope="module")
+def fb(hostmath):
+    L = hostmath.L
+    L.hdh_fb_verify.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
+    L.hdh_fb_verify.restype = ctypes.c_int
+    L.hdh_fb_entry.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_char_p]
+    return L
+
+
+def _pub64(q):
+    return q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big")
+
+
+def _verify(fb, q, digest, sig):
+    return fb.hdh_fb_verify(_pub64(q), digest, sig)
+
+
+def test_table_entries_are_window_multiples(fb, oracle):
+    O = oracle
+    for j, d in [(0, 1), (0, 2048), (1, 1), (7, 1234), (21, 1), (21, 2048)]:
+        out = ctypes.create_string_buffer(64)
+        fb.hdh_fb_entry(_pub64((O.GX, O.GY)), j, d, out)
+        want = O.point_mul(d << (12 * j), (O.GX, O.GY))
+        assert out.raw == _pub64(want), (j, d)
+
+
+def test_fast_path_agrees_with_recovery(fb, oracle):
+    O = oracle
+    rng = random.Random(12)
+    sk = O.signer_sk(3)
+    P = O.pubkey_of(sk)
+    other = O.pubkey_of(O.signer_sk(4))
+    n_valid = 0
+    for t in range(60):
+        digest = bytes(rng.randrange(256) for _ in range(32))
+        sig = O.sign(sk, digest)
+        kind = t % 6
+        if kind == 1:                       # high-S malleation: still recovers P
+            s = O.N - int.from_bytes(sig[32:64], "big")
+            sig = sig[:32] + s.to_bytes(32, "big") + bytes([sig[64] ^ 1])
+        elif kind == 2:                     # wrong parity: another key
+            sig = sig[:64] + bytes([sig[64] ^ 1])
+        elif kind == 3:                     # another digest
+            digest = bytes(rng.randrange(256) for _ in range(32))
+        elif kind == 4:                     # another signer's key
+            sig = O.sign(O.signer_sk(4), digest)
+        elif kind == 5:                     # random r, s
+            sig = rng.randrange(1, O.N).to_bytes(32, "big") + rng.randrange(1, O.N).to_bytes(32, "big") + \
+                bytes([rng.randrange(2)])
+        v, q = O.recover(digest, sig)
+        got = _verify(fb, P, digest, sig)
+        if v == O.VALID and q == P:
+            assert got == O.VALID, t
+            n_valid += 1
+        else:
+            assert got == NEEDS_SLOW, (t, v)
+        if kind == 4:
+            assert _verify(fb, other, digest, sig) == O.VALID
+    assert n_valid >= 20
+
+
+def test_early_verdicts_match_recovery(fb, oracle):
+    O = oracle
+    P = O.pubkey_of(O.signer_sk(3))
+    d = bytes(range(32))
+    good = O.sign(O.signer_sk(3), d)
+    r, s = good[:32], good[32:64]
+    cases = [
+        (r + s + bytes([4]), O.BAD_RECID),
+        (r + s + bytes([255]), O.BAD_RECID),
+        (bytes(32) + s + bytes([0]), O.BAD_RS),
+        (r + bytes(32) + bytes([1]), O.BAD_RS),
+        (O.N.to_bytes(32, "big") + s + bytes([0]), O.BAD_RS),
+        (r + O.N.to_bytes(32, "big") + bytes([0]), O.BAD_RS),
+        ((O.P - O.N).to_bytes(32, "big") + s + bytes([2]), O.NO_POINT),
+        ((O.N - 1).to_bytes(32, "big") + s + bytes([3]), O.NO_POINT),
+    ]
+    for sig, want in cases:
+        assert O.recover(d, sig)[0] == want
+        assert _verify(fb, P, d, sig) == want
+
+
+def test_r_plus_n_recovery_to_the_known_key(fb, oracle):
+    """v & 2 (x = r + n): craft R with x >= n, any s; the key it recovers to
+    is then the known key, and the fast path must accept exactly it."""
+    O = oracle
+    rng = random.Random(5)
+    for _ in range(200):
+        r = rng.randrange(1, O.P - O.N)
+        R = O.lift_x(r + O.N, 0)
+        if R is not None:
+            break
+    digest = bytes(rng.randrange(256) for _ in range(32))
+    s = rng.randrange(1, O.N)
+    sig = r.to_bytes(32, "big") + s.to_bytes(32, "big") + bytes([2])
+    v, q = O.recover(digest, sig)
+    assert v == O.VALID
+    assert _verify(fb, q, digest, sig) == O.VALID
+    assert _verify(fb, q, digest, sig[:64] + bytes([3])) == NEEDS_SLOW
+
+
+# ---------------------------------------------------------------- GPU
+def _run(v, db, n):
+    import torch
+    from hyperdrive_amd.device import work_stream
+    ws = work_stream()
+    outs = [torch.empty(n, dtype=torch.uint8, device="cuda"), torch.empty(n, dtype=torch.int32, device="cuda"),
+            torch.empty((n, 32), dtype=torch.uint8, device="cuda"),
+            torch.zeros((n + 31) // 32, dtype=torch.int32, device="cuda")]
+    v.verify_batch_device(db.c_struct(), outs[0].data_ptr(), outs[2].data_ptr(), outs[1].data_ptr(),
+                          outs[3].data_ptr(), ws.cuda_stream)
+    ws.synchronize()
+    return outs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("compressed", [True, False])
+@pytest.mark.parametrize("kind,S,n,adv", [(0, 100, 100_003, 30), (1, 1000, 40_000, 30), (0, 7, 5000, 0)])
+def test_fast_path_equals_full_recovery(gpu, kind, S, n, adv, compressed):
+    import torch
+    from hyperdrive_amd.device import generate
+    from hyperdrive_amd.verify import Verifier
+    fast = Verifier(0, compressed=compressed)
+    slow = Verifier(0, compressed=compressed)
+    slow.set_fastpath(False)
+    ks = fast.gen_keys(S)
+    db, _, _ = generate(fast, kind, n, S, adv, keys=ks, start=4242)
+    for v in (fast, slow):
+        v.set_signatories(ks[0])
+    ref = _run(slow, db, n)
+    assert fast.known_keys() == 0
+    first = _run(fast, db, n)                    # learns the keys of the signers it sees
+    learned = fast.known_keys()
+    second = _run(fast, db, n)                   # fast path for every learned signer
+    for a, b, c in zip(ref, first, second):
+        assert torch.equal(a, b) and torch.equal(a, c)
+    signers_valid = len(set(ref[1][ref[0] == 0].cpu().tolist()))
+    assert learned == signers_valid and slow.known_keys() == 0
+    assert int((ref[0] == 0).sum()) > 0
+    fast.close()
+    slow.close()

@@ -79,7 +79,8 @@ SIGNATURES = {
     "hd_ctx_set_pubkey_format": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hd_set_signatories": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
     "hd_ctx_set_fastpath": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
-    "hd_ctx_known_keys": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
+    "hd_ctx_fastpath_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
+                                             ctypes.POINTER(ctypes.c_uint32)]),
     "hd_verify_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_void_p]),
     "hd_verify_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,

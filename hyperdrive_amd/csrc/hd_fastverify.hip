@@ -71,7 +71,8 @@ struct FastSrc {
     __device__ __forceinline__ uint32_t sig_v() const { return b.sig65[65 * (size_t)i + 64]; }
 };
 
-__global__ __launch_bounds__(256) void k_verify_fast(DevBatch b, const uint8_t* __restrict__ digest_in,
+template <int WAVES>
+__global__ __launch_bounds__(256, WAVES) void k_verify_fast(DevBatch b, const uint8_t* __restrict__ digest_in,
                                                      const ge* __restrict__ tab, const uint32_t* __restrict__ state,
                                                      const int32_t* __restrict__ adm_slot,
                                                      const uint32_t* __restrict__ adm, const int32_t* __restrict__ adm_perm,
@@ -327,9 +328,16 @@ int hd_fb_verify(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_
     const uint32_t blocks = (b.n + 255) / 256;
     FBCHK(hipMemsetAsync(f->counts + 1, 0, 4, s), "fb count reset");
     if (ctx->n_adm > 0 && f->adm_slot) {
-        k_verify_fast<<<blocks, 256, 0, s>>>(b, d_digest, f->tab, f->state, f->adm_slot, ctx->d_adm, ctx->d_adm_perm,
-                                             ctx->n_adm, ctx->adm_steps, d_verdict, d_rec32, d_signer, f->slow,
-                                             f->counts + 1);
+        static const int fw = getenv("HD_FAST_WAVES") ? atoi(getenv("HD_FAST_WAVES")) : 3;
+#define HD_LAUNCH_FAST(W)                                                                                        \
+    k_verify_fast<W><<<blocks, 256, 0, s>>>(b, d_digest, f->tab, f->state, f->adm_slot, ctx->d_adm, ctx->d_adm_perm, \
+                                            ctx->n_adm, ctx->adm_steps, d_verdict, d_rec32, d_signer, f->slow,       \
+                                            f->counts + 1)
+        if (fw == 2) HD_LAUNCH_FAST(2);
+        else if (fw == 4) HD_LAUNCH_FAST(4);
+        else if (fw == 5) HD_LAUNCH_FAST(5);
+        else HD_LAUNCH_FAST(3);
+#undef HD_LAUNCH_FAST
         FBCHK(hipGetLastError(), "k_verify_fast launch");
         const SlowCtl ctl{f->slow, f->counts + 1, f->adm_slot, f->state, f->pub};
         rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl, blocks, s);
@@ -368,16 +376,20 @@ int hd_ctx_set_fastpath(hd_ctx* ctx, int enable) {
     return HD_OK;
 }
 
-int hd_ctx_known_keys(hd_ctx* ctx, uint32_t* n) {
-    if (!ctx || !n) return HD_EINVAL;
-    *n = 0;
-    if (!ctx->fb || ctx->fb->nslots <= 1) return HD_OK;
+int hd_ctx_fastpath_stats(hd_ctx* ctx, uint32_t* known_keys, uint32_t* last_fallback) {
+    if (!ctx) return HD_EINVAL;
+    if (known_keys) *known_keys = 0;
+    if (last_fallback) *last_fallback = 0;
+    if (!ctx->fb) return HD_OK;
     (void)hipSetDevice(ctx->device);
     FbWork* f = ctx->fb;
-    FBCHK(hipDeviceSynchronize(), "known keys sync");
-    std::vector<uint32_t> st(f->nslots);
-    FBCHK(hipMemcpy(st.data(), f->state, 4 * (size_t)f->nslots, hipMemcpyDeviceToHost), "state read");
-    for (uint32_t k = 1; k < f->nslots; k++) *n += st[k] == HD_FB_READY;
+    FBCHK(hipDeviceSynchronize(), "fastpath stats sync");
+    if (known_keys && f->nslots > 1) {
+        std::vector<uint32_t> st(f->nslots);
+        FBCHK(hipMemcpy(st.data(), f->state, 4 * (size_t)f->nslots, hipMemcpyDeviceToHost), "state read");
+        for (uint32_t k = 1; k < f->nslots; k++) *known_keys += st[k] == HD_FB_READY;
+    }
+    if (last_fallback) FBCHK(hipMemcpy(last_fallback, f->counts + 1, 4, hipMemcpyDeviceToHost), "fallback read");
     return HD_OK;
 }
 

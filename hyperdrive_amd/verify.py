@@ -161,10 +161,16 @@ class Verifier:
         """Known-key fast path on/off (include/hd_verify.h hd_ctx_set_fastpath)."""
         self._check(self._lib.hd_ctx_set_fastpath(self._ctx, 1 if enable else 0), "hd_ctx_set_fastpath")
 
+    def fastpath_stats(self) -> Tuple[int, int]:
+        """(signatories with built key tables, messages of the last verify
+        call that took the full recovery)."""
+        k, f = ctypes.c_uint32(), ctypes.c_uint32()
+        self._check(self._lib.hd_ctx_fastpath_stats(self._ctx, ctypes.byref(k), ctypes.byref(f)),
+                    "hd_ctx_fastpath_stats")
+        return int(k.value), int(f.value)
+
     def known_keys(self) -> int:
-        n = ctypes.c_uint32()
-        self._check(self._lib.hd_ctx_known_keys(self._ctx, ctypes.byref(n)), "hd_ctx_known_keys")
-        return int(n.value)
+        return self.fastpath_stats()[0]
 
     def verify_batch(self, batch: Batch, recovered: bool = True) -> VerifyResult:
         n = len(batch)

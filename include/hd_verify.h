@@ -101,8 +101,10 @@ int hd_set_signatories(hd_ctx* ctx, const uint8_t* sigs32, uint32_t n);
  * are identical either way.  Keys are kept across hd_set_signatories for
  * signatories that stay admitted and dropped when the pubkey format changes. */
 int hd_ctx_set_fastpath(hd_ctx* ctx, int enable);
-/* number of admitted signatories whose key tables are built (synchronises) */
-int hd_ctx_known_keys(hd_ctx* ctx, uint32_t* n);
+/* known_keys: admitted signatories whose key tables are built;
+ * last_fallback: messages of the last verify call that took the full
+ * recovery (either may be NULL; synchronises the device) */
+int hd_ctx_fastpath_stats(hd_ctx* ctx, uint32_t* known_keys, uint32_t* last_fallback);
 
 /* ---- verification ------------------------------------------------------
  * verdict:     n bytes (HD_VERDICT_*), required.

@@ -1,7 +1,9 @@
 """Condense rocprofv3 outputs under gpurun_out/ into profiles/<round>/.
 
 profiles/<round>/kernel_stats.csv   rocprofv3 --kernel-trace --stats summary
-profiles/<round>/pmc_k_verify.json  per-launch PMC averages of k_verify and the
+profiles/<round>/pmc_k_verify_fast.json, pmc_k_verify.json
+                                    per-launch PMC averages of the known-key check and of
+                                    the full recovery, and the
                                     HBM traffic derived per MI355X_MICROARCH.md
                                     (FETCH_SIZE/WRITE_SIZE are KiB; FETCH_SIZE
                                     under-reports wide streaming reads by 2x on
@@ -19,33 +21,43 @@ src = "gpurun_out"
 dst = os.path.join("profiles", rnd)
 os.makedirs(dst, exist_ok=True)
 shutil.copy(os.path.join(src, "prof", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
-out = {}
-for name in ("pmc_fetch", "pmc_write", "pmc_stall", "pmc_sq", "pmc_icache"):
-    path = os.path.join(src, name, "run_counter_collection.csv")
-    if not os.path.exists(path):
-        continue
-    per = collections.defaultdict(list)
-    meta = {}
-    for r in csv.DictReader(open(path)):
-        if "k_verify" not in r["Kernel_Name"]:
+def kernel_pmc(match, outname):
+    """per-launch PMC averages of the kernels whose name contains `match`"""
+    out = {}
+    for name in ("pmc_fetch", "pmc_write", "pmc_stall", "pmc_sq", "pmc_icache"):
+        path = os.path.join(src, name, "run_counter_collection.csv")
+        if not os.path.exists(path):
             continue
-        per[r["Counter_Name"]].append(float(r["Counter_Value"]))
-        meta = {"grid": int(r["Grid_Size"]), "workgroup": int(r["Workgroup_Size"]), "lds": int(r["LDS_Block_Size"]),
-                "scratch": int(r["Scratch_Size"]), "vgpr": int(r["VGPR_Count"]), "sgpr": int(r["SGPR_Count"])}
-    for c, v in per.items():
-        out[c] = sum(v) / len(v)
-    out.setdefault("dispatch", meta)
-stats = {}
-for r in csv.DictReader(open(os.path.join(dst, "kernel_stats.csv"))):
-    if "k_verify" in r["Name"]:
-        stats = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
-                 "max_ns": float(r["MaxNs"])}
-out["kernel_stats"] = stats
-if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
-    out["hbm_bytes_raw"] = (out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024
-    out["hbm_bytes_corrected"] = (2 * out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024
-json.dump(out, open(os.path.join(dst, "pmc_k_verify.json"), "w"), indent=1)
-print(json.dumps(out, indent=1))
+        per = collections.defaultdict(list)
+        meta = {}
+        for r in csv.DictReader(open(path)):
+            if match not in r["Kernel_Name"]:
+                continue
+            per[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            meta = {"grid": int(r["Grid_Size"]), "workgroup": int(r["Workgroup_Size"]),
+                    "lds": int(r["LDS_Block_Size"]), "scratch": int(r["Scratch_Size"]), "vgpr": int(r["VGPR_Count"]),
+                    "sgpr": int(r["SGPR_Count"])}
+        for c, v in per.items():
+            out[c] = sum(v) / len(v)
+        if meta:
+            out.setdefault("dispatch", meta)
+    if not out:
+        return
+    stats = {}
+    for r in csv.DictReader(open(os.path.join(dst, "kernel_stats.csv"))):
+        if match in r["Name"]:
+            stats = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
+                     "max_ns": float(r["MaxNs"])}
+    out["kernel_stats"] = stats
+    if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
+        out["hbm_bytes_raw"] = (out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024
+        out["hbm_bytes_corrected"] = (2 * out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024
+    json.dump(out, open(os.path.join(dst, outname), "w"), indent=1)
+    print(outname, json.dumps(out, indent=1))
+
+
+kernel_pmc("k_verify_fast", "pmc_k_verify_fast.json")   # the known-key check (dominant)
+kernel_pmc("k_verify<", "pmc_k_verify.json")            # the full recovery (fallback list)
 
 # every kernel's per-launch HBM traffic (the aux rows: codec, mq, digest, tally)
 allk = collections.defaultdict(lambda: collections.defaultdict(list))

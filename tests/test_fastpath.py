@@ -154,11 +154,16 @@ def test_fast_path_equals_full_recovery(gpu, kind, S, n, adv, compressed):
     assert fast.known_keys() == 0
     first = _run(fast, db, n)                    # learns the keys of the signers it sees
     learned = fast.known_keys()
+    fallback_first = fast.fastpath_stats()[1]
     second = _run(fast, db, n)                   # fast path for every learned signer
+    fallback_second = fast.fastpath_stats()[1]
     for a, b, c in zip(ref, first, second):
         assert torch.equal(a, b) and torch.equal(a, c)
     signers_valid = len(set(ref[1][ref[0] == 0].cpu().tolist()))
     assert learned == signers_valid and slow.known_keys() == 0
+    # second pass: only the non-VALID messages (minus early verdicts) fall back
+    n_invalid = int((ref[0] != 0).sum())
+    assert fallback_first >= n - int((ref[0] == 7).sum()) and fallback_second <= n_invalid
     assert int((ref[0] == 0).sum()) > 0
     fast.close()
     slow.close()

@@ -19,14 +19,14 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "_lib")
-OBJDIR = os.path.join(LIBDIR, "obj")
-LIB = os.path.join(LIBDIR, "libhdverify.so")
+OBJDIR = os.environ.get("HD_BUILD_OBJDIR", os.path.join(LIBDIR, "obj"))
+LIB = os.environ.get("HD_BUILD_LIB", os.path.join(LIBDIR, "libhdverify.so"))
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 ARCH = os.environ.get("HD_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 
 CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-          "-I" + INCLUDE]
+          "-I" + INCLUDE] + (["-DHD_FB_W=" + os.environ["HD_FB_W"]] if os.environ.get("HD_FB_W") else [])
 
 
 def _sources():

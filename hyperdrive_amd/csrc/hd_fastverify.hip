@@ -4,7 +4,7 @@
 // Per batch, stream-ordered, no host synchronisation:
 //   k_verify_fast   one message per lane: a message whose claimed From is an
 //                   admitted signatory with a known key is checked with two
-//                   fixed-base multiplications (44 mixed additions, no
+//                   fixed-base multiplications (34 mixed additions, no
 //                   doublings, no square root); VALID / early exact verdicts
 //                   are final, everything else is appended to a list
 //   k_verify        (hd_verify.hip) the full libsecp256k1-semantics recovery
@@ -12,9 +12,11 @@
 //                   a known key publish the recovered key to their slot
 //   k_fb_bitmap     the valid bitmap from the final verdicts
 //   k_fb_list / k_fb_bases / k_fb_entries / k_fb_ready
-//                   build the tables of newly learned keys (22 window bases,
-//                   then 22 x 2048 affine multiples, one per lane); with
-//                   nothing learned each exits at once
+//                   build the tables of newly learned keys (HD_FB_NWIN window
+//                   bases, then HD_FB_NWIN x HD_FB_N affine multiples, one per
+//                   lane); with nothing learned each exits at once
+// Table memory is capped by HD_FB_MAX_BYTES (default 64 GiB of the 288 GB):
+// signatories beyond the cap always take the full recovery.
 // Slot 0 holds the tables of G, built when the context is created.
 #include <hip/hip_runtime.h>
 
@@ -34,7 +36,7 @@ using namespace hd;
 
 struct FbWork {
     uint32_t nslots = 0;        // allocated slots; slot 0 = G
-    uint32_t max_slots = 2049;  // HD_FB_MAX_SLOTS
+    uint32_t max_slots = 0;     // from HD_FB_MAX_BYTES (slot 0 included)
     ge* tab = nullptr;          // nslots x HD_FB_TAB
     ge* base = nullptr;         // nslots x HD_FB_NWIN window bases
     ge* pub = nullptr;          // nslots keys
@@ -238,7 +240,10 @@ int hd_fb_init(hd_ctx* ctx) {
     ctx->fb = new (std::nothrow) FbWork();
     if (!ctx->fb) return HD_ENOMEM;
     FbWork* f = ctx->fb;
-    if (const char* m = getenv("HD_FB_MAX_SLOTS")) f->max_slots = std::max(1, atoi(m)) + 1u;
+    double budget = 64.0 * (1ull << 30);
+    if (const char* m = getenv("HD_FB_MAX_BYTES")) budget = atof(m);
+    const double per_slot = (double)sizeof(ge) * (HD_FB_TAB + HD_FB_NWIN + 1) + 8;
+    f->max_slots = (uint32_t)std::max(1.0, std::min(1e6, budget / per_slot));
     FBCHK(hipMalloc(&f->counts, 8), "fb counts");
     int rc = fb_grow_slots(ctx, 1);
     if (rc) return rc;

@@ -12,10 +12,11 @@
 //     R == s^-1 (m G + r P)        R = lift(r [+ n], v & 1), m = digest mod n
 //
 // (then Q = r^-1 (s R - m G) = P).  Both scalar multiplications have fixed
-// bases, so they run without doublings over per-base tables of
-// 22 windows x 2048 affine multiples: entry (j, d) = d 2^(12j) B, and each
-// signed 12-bit Booth digit costs one mixed addition.  No square root is
-// needed: the affine result is compared with x and the parity of y.
+// bases, so they run without doublings over per-base tables of W-bit Booth
+// windows: entry (j, d) = d 2^(W j) B for 1 <= d <= 2^(W-1), and each signed
+// digit costs one mixed addition (W = 16: 17 windows, 34 additions per
+// message for the two scalars, 40 MB of affine points per base).  No square
+// root is needed: the affine result is compared with x and the parity of y.
 //
 // verify_fast returns V_VALID only when that identity holds, an exact early
 // verdict (BAD_RECID, BAD_RS, NO_POINT for r + n >= p) where the reference's
@@ -26,10 +27,12 @@
 
 namespace hd {
 
-#define HD_FB_W 12
-#define HD_FB_NWIN 22                      // Booth windows over a 256-bit scalar (264 bits)
-#define HD_FB_N 2048                       // |digit| <= 2^(W-1)
-#define HD_FB_TAB (HD_FB_NWIN * HD_FB_N)   // affine entries per base (3.2 MB of ge)
+#ifndef HD_FB_W
+#define HD_FB_W 16   // 17 windows x 32768 entries (40 MB of tables per key); 12: 22 x 2048 (3.2 MB)
+#endif
+#define HD_FB_NWIN ((257 + HD_FB_W - 1) / HD_FB_W)  // Booth windows over a 256-bit scalar
+#define HD_FB_N (1 << (HD_FB_W - 1))                // |digit| <= 2^(W-1)
+#define HD_FB_TAB (HD_FB_NWIN * HD_FB_N)   // affine entries per base
 #define HD_NEEDS_SLOW 0xFEu
 
 // slot states of the per-signatory tables (device memory, hd_fastverify.hip)
@@ -113,7 +116,7 @@ HD uint8_t verify_fast(const uint32_t digest_be[8], const uint32_t r_be[8], cons
 }
 
 // ---- table construction (one entry per lane) --------------------------
-// 2^(12 j) B, affine canonical
+// 2^(W j) B, affine canonical
 HD void fb_window_base(ge& out, const ge& B, int j) {
     gej a;
     gej_set_ge(a, B);
@@ -121,7 +124,7 @@ HD void fb_window_base(ge& out, const ge& B, int j) {
     gej_to_ge(out.x, out.y, a);
 }
 
-// d Bj for 1 <= d <= 2048, affine canonical (double-and-add from the top bit)
+// d Bj for 1 <= d <= 2^(W-1), affine canonical (double-and-add from the top bit)
 HD void fb_entry(ge& out, const ge& Bj, uint32_t d) {
     int top = 31;
     while (top > 0 && !((d >> top) & 1u)) top--;

@@ -298,9 +298,9 @@ HD void gej_add(gej& r, const gej& a, const gej& b) {
 // Booth digit of window j (width W) of a 256-bit scalar k:
 //   d = b[Wj-1] + sum_{t<W-1} 2^t b[Wj+t] - 2^(W-1) b[Wj+W-1],  |d| <= 2^(W-1)
 HD uint32_t sc_bits(const sc& k, int pos, int len) {
-    // bits [pos, pos+len) of k, bits outside [0,256) read as 0; len <= 16
+    // bits [pos, pos+len) of k, bits outside [0,256) read as 0; len <= 17
     uint32_t out = 0;
-    HD_UNROLL for (int t = 0; t < 16; t++) {
+    HD_UNROLL for (int t = 0; t < 17; t++) {
         if (t < len) {
             int b = pos + t;
             uint32_t bit = (b >= 0 && b < 256) ? ((k.v[b >> 5] >> (b & 31)) & 1u) : 0u;

@@ -41,17 +41,73 @@ namespace hd {
 #define HD_FB_LEARNED 2u   // key known, tables not built yet
 #define HD_FB_READY 3u     // tables built
 
-// acc += u B, tab = the base's HD_FB_TAB entries
+// a + b for a finite Jacobian a and an affine b, with no exceptional cases:
+// the madd of gej_add_ge (8M + 3S, Z3 = 2 Z1 H) without its a = inf and
+// a = +-b branches.  If a = +-b then H = 0 and Z3 = 0, and since every later
+// Z is a multiple of this one the sum ends with Z = 0: verify_fast then
+// hands the message to the full recovery, so no answer depends on it.
+HD void gej_add_ge_nx(gej& r, const gej& a, const ge& b) {
+    HD_REQUIRE_T(a.x, "gej_add_ge_nx: x");
+    HD_REQUIRE_T(a.y, "gej_add_ge_nx: y");
+    HD_REQUIRE_T(a.z, "gej_add_ge_nx: z");
+    HD_REQUIRE_T(b.x, "gej_add_ge_nx: b.x");
+    fe z1z1, u2, s2, h, R, t;
+    fe_sqr(z1z1, a.z);         // T
+    fe_mul(u2, b.x, z1z1);     // T
+    fe_mul(s2, b.y, a.z);      // T (2T x T)
+    fe_mul(s2, s2, z1z1);      // T
+    fe_sub_k<2>(h, u2, a.x);
+    fe_norm_weak(h);           // H = U2 - X1       T
+    fe_sub_k<2>(R, s2, a.y);   // r = S2 - Y1       3T
+    gej o;
+    fe_add(t, a.z, a.z);
+    fe_mul(o.z, t, h);         // Z3 = 2 Z1 H       T
+    fe hh, i4, j, v;
+    fe_norm_weak(R);
+    fe_add(R, R, R);           // 2r                2T
+    fe_sqr(hh, h);             // T
+    fe_mul_int(i4, hh, 4);     // I = 4 H^2         4T
+    fe_mul(j, h, i4);          // J = H I           T
+    fe_mul(v, a.x, i4);        // V = X1 I          T
+    fe_sqr(o.x, R);            // T
+    fe_add(t, v, v);
+    fe_add(t, t, j);           // 2V + J            3T
+    fe_sub_k<4>(o.x, o.x, t);
+    fe_norm_weak(o.x);         // X3                T
+    fe_sub_k<2>(t, v, o.x);    // V - X3            3T
+    fe_mul(t, R, t);           // r (V - X3)        T (2T x 3T)
+    fe_mul(j, a.y, j);
+    fe_add(j, j, j);           // 2 Y1 J            2T
+    fe_sub_k<3>(o.y, t, j);
+    fe_norm_weak(o.y);         // Y3                T
+    r = o;
+}
+
+// acc += u B over the base's HD_FB_TAB entries.  `started` is false while acc
+// is still the point at infinity (no non-zero digit yet); the first non-zero
+// digit sets acc to its table point.  The next window's point is loaded
+// before the current addition, so its HBM latency hides under the math.
 template <typename Tab>
-HD void fb_accumulate(gej& acc, const sc& u, Tab tab) {
+HD void fb_accumulate(gej& acc, bool& started, const sc& u, Tab tab) {
+    int d = booth_digit<HD_FB_W>(u, 0);
+    ge t = tab[(d < 0 ? -d : d) == 0 ? 0 : (d < 0 ? -d : d) - 1];
     HD_NOUNROLL for (int j = 0; j < HD_FB_NWIN; j++) {
-        const int d = booth_digit<HD_FB_W>(u, j);
-        const int ad = d < 0 ? -d : d;
-        ge t = tab[j * HD_FB_N + (ad == 0 ? 0 : ad - 1)];
-        if (d < 0) fe_neg(t.y, t.y);
+        ge cur = t;
+        const int dc = d;
+        if (j + 1 < HD_FB_NWIN) {
+            d = booth_digit<HD_FB_W>(u, j + 1);
+            const int ad = d < 0 ? -d : d;
+            t = tab[(j + 1) * HD_FB_N + (ad == 0 ? 0 : ad - 1)];
+        }
+        if (dc < 0) fe_neg(cur.y, cur.y);
         gej s;
-        gej_add_ge(s, acc, t);
-        gej_cmov(acc, s, d != 0);
+        gej_add_ge_nx(s, acc, cur);
+        gej first;
+        gej_set_ge(first, cur);
+        fe_norm_weak(first.y);
+        gej_cmov(s, first, !started);
+        gej_cmov(acc, s, dc != 0);
+        started = started || dc != 0;
     }
 }
 
@@ -99,9 +155,11 @@ HD uint8_t verify_fast(const uint32_t digest_be[8], const uint32_t r_be[8], cons
     sc_mul(u2, r, sinv);
     gej acc;
     gej_set_inf(acc);
-    fb_accumulate(acc, u1, gtab);
-    fb_accumulate(acc, u2, ptab);
-    if (gej_is_inf(acc)) return HD_NEEDS_SLOW;
+    bool started = false;
+    fb_accumulate(acc, started, u1, gtab);
+    fb_accumulate(acc, started, u2, ptab);
+    // infinity, or a degenerate addition on the way (Z = 0): full recovery
+    if (!started || gej_is_inf(acc)) return HD_NEEDS_SLOW;
     fe zi, zi2, ax, ay;
     fe_inv_divsteps(zi, acc.z);
     fe_sqr(zi2, zi);

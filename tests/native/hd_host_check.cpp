@@ -265,6 +265,13 @@ extern "C" int hdh_bound_certify(const uint8_t* px, const uint8_t* py, const uin
     gej_add(r, b, b);
     gej bneg = b; fe_neg(bneg.y, b.y); set_class(bneg.y, 2);
     gej_add(r, b, bneg);
+    // the known-key check's addition (no exceptional branches), b.y 2T and T,
+    // and its first-digit start (an affine point, y weakly normalised)
+    fe_neg(qn.y, Q.y); set_class(qn.y, 2);
+    gej_add_ge_nx(r, a, qn);
+    qn.y = Q.y; set_class(qn.y, 1);
+    gej_add_ge_nx(r, a, qn);
+    gej_add_ge_nx(r, aq, qq);           // a == -b: Z3 = 0, still in bounds
     // isomorphic-curve additions (G side of the ladder) and the R table build
     fe zg = b.z; set_class(zg, 1);
     gej_add_ge_zinv(r, a, qn, zg);

@@ -344,8 +344,12 @@ int hd_fb_verify(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_
         else HD_LAUNCH_FAST(3);
 #undef HD_LAUNCH_FAST
         FBCHK(hipGetLastError(), "k_verify_fast launch");
+        // the fallback list is usually short (its length is only known on the
+        // device): a grid of 4 blocks per CU walks it, instead of one block
+        // per 256 messages that would mostly start and exit
         const SlowCtl ctl{f->slow, f->counts + 1, f->adm_slot, f->state, f->pub};
-        rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl, blocks, s);
+        const uint32_t slow_blocks = std::min(blocks, (uint32_t)std::max(ctx->n_cu, 1) * 4u);
+        rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl, slow_blocks, s);
         if (rc) return rc;
         if (d_bitmap) {
             k_fb_bitmap<<<((b.n + 31) / 32 + 255) / 256, 256, 0, s>>>(b.n, d_verdict, d_bitmap);

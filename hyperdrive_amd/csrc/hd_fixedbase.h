@@ -83,19 +83,37 @@ HD void gej_add_ge_nx(gej& r, const gej& a, const ge& b) {
     r = o;
 }
 
+// Booth digit j of u for the table width: bits [W j - 1, W j + W - 1] of u
+// (bits outside [0, 256) read 0).  The words are picked with selects over
+// the 8 limbs instead of a runtime array index, which would put u in scratch.
+HD uint32_t sc_word_sel(const sc& k, int w) {
+    uint32_t o = 0;
+    HD_UNROLL for (int i = 0; i < 8; i++) o = (w == i) ? k.v[i] : o;
+    return o;
+}
+HD int fb_digit(const sc& k, int j) {
+    const int lo = HD_FB_W * j - 1;                 // lowest bit of the window (may be -1)
+    const int wlo = lo < 0 ? 0 : (lo >> 5);
+    const uint32_t a = sc_word_sel(k, wlo), b = sc_word_sel(k, wlo + 1);   // b = 0 past the top
+    const uint64_t pair = ((uint64_t)b << 32) | a;
+    const uint32_t x = lo < 0 ? (uint32_t)(pair << 1) & ((1u << (HD_FB_W + 1)) - 1)
+                              : (uint32_t)(pair >> (lo & 31)) & ((1u << (HD_FB_W + 1)) - 1);
+    return (int)((x >> 1) + (x & 1)) - (int)((x >> HD_FB_W) << HD_FB_W);
+}
+
 // acc += u B over the base's HD_FB_TAB entries.  `started` is false while acc
 // is still the point at infinity (no non-zero digit yet); the first non-zero
 // digit sets acc to its table point.  The next window's point is loaded
 // before the current addition, so its HBM latency hides under the math.
 template <typename Tab>
 HD void fb_accumulate(gej& acc, bool& started, const sc& u, Tab tab) {
-    int d = booth_digit<HD_FB_W>(u, 0);
+    int d = fb_digit(u, 0);
     ge t = tab[(d < 0 ? -d : d) == 0 ? 0 : (d < 0 ? -d : d) - 1];
     HD_NOUNROLL for (int j = 0; j < HD_FB_NWIN; j++) {
         ge cur = t;
         const int dc = d;
         if (j + 1 < HD_FB_NWIN) {
-            d = booth_digit<HD_FB_W>(u, j + 1);
+            d = fb_digit(u, j + 1);
             const int ad = d < 0 ? -d : d;
             t = tab[(j + 1) * HD_FB_N + (ad == 0 ? 0 : ad - 1)];
         }

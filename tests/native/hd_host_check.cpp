@@ -385,3 +385,10 @@ extern "C" void hdh_fb_entry(const uint8_t* b64, int j, uint32_t d, uint8_t* out
     fe_out(out64, e.x);
     fe_out(out64 + 32, e.y);
 }
+// fb_digit (the known-key check's window digits) for a 256-bit scalar (BE)
+extern "C" int hdh_fb_digits(const uint8_t* k32, int* out) {
+    sc k;
+    le_in(k.v, k32);
+    for (int j = 0; j < HD_FB_NWIN; j++) out[j] = fb_digit(k, j);
+    return HD_FB_NWIN;
+}

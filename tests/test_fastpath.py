@@ -167,3 +167,20 @@ def test_fast_path_equals_full_recovery(gpu, kind, S, n, adv, compressed):
     assert int((ref[0] == 0).sum()) > 0
     fast.close()
     slow.close()
+
+
+def test_window_digits_recode_the_scalar(fb, oracle):
+    """fb_digit: signed Booth digits d_j in [-2^(W-1), 2^(W-1)] with
+    sum d_j 2^(W j) == k, for random and edge scalars (host build, W = 12)."""
+    fb.hdh_fb_digits.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
+    fb.hdh_fb_digits.restype = ctypes.c_int
+    rng = random.Random(8)
+    ks = [0, 1, oracle.N - 1, (1 << 255), (1 << 256) - 1, 0x7FF, 0x800, 0xFFF] + \
+         [rng.randrange(1 << 256) for _ in range(200)]
+    for k in ks:
+        out = np.zeros(64, np.int32)
+        nwin = fb.hdh_fb_digits(k.to_bytes(32, "big"), out.ctypes.data)
+        w = 12
+        assert nwin == (257 + w - 1) // w
+        assert all(-(1 << (w - 1)) <= int(d) <= (1 << (w - 1)) for d in out[:nwin])
+        assert sum(int(d) << (w * j) for j, d in enumerate(out[:nwin])) == k

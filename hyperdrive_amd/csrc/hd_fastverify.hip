@@ -73,6 +73,8 @@ struct FastSrc {
     __device__ __forceinline__ uint32_t sig_v() const { return b.sig65[65 * (size_t)i + 64]; }
 };
 
+// Lane t checks messages 2t and 2t + 1 (verify_fast2: one inversion of each
+// kind for the pair).
 template <int WAVES>
 __global__ __launch_bounds__(256, WAVES) void k_verify_fast(DevBatch b, const uint8_t* __restrict__ digest_in,
                                                      const ge* __restrict__ tab, const uint32_t* __restrict__ state,
@@ -81,61 +83,83 @@ __global__ __launch_bounds__(256, WAVES) void k_verify_fast(DevBatch b, const ui
                                                      uint32_t n_adm, int adm_steps, uint8_t* __restrict__ verdict,
                                                      uint8_t* __restrict__ rec32, int32_t* __restrict__ signer,
                                                      uint32_t* __restrict__ slow, uint32_t* __restrict__ n_slow) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    bool to_slow = false;
-    if (i < b.n) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    FastIn in[2];
+    int32_t idx[2], slot[2];
+    bool present[2], bad_type[2];
+    HD_UNROLL for (int k = 0; k < 2; k++) {
+        const uint32_t i = 2 * t + k;
+        present[k] = i < b.n;
+        bad_type[k] = false;
+        idx[k] = -1;
+        slot[k] = -1;
+        HD_UNROLL for (int w = 0; w < 8; w++) in[k].digest_be[w] = in[k].r_be[w] = in[k].s_be[w] = 0u;
+        in[k].v = 0;
+        in[k].ready = false;
+        if (!present[k]) continue;
         FastSrc src{b, i, digest_in};
         const uint32_t type = src.type();
-        uint8_t v = HD_NEEDS_SLOW;
-        int32_t idx = -1;
+        if (type < 1 || type > 3) {
+            bad_type[k] = true;
+            continue;
+        }
         uint32_t from_be[8];
         HD_UNROLL for (int w = 0; w < 8; w++) from_be[w] = src.from(w);
-        if (type >= 1 && type <= 3) {
-            idx = admitted_find(adm, n_adm, adm_steps, from_be);
-            const int32_t slot = idx >= 0 ? adm_slot[idx] : -1;
-            if (slot >= 0 && state[slot] == HD_FB_READY) {
-                uint32_t d[8];
-                if (digest_in) {
-                    HD_UNROLL for (int w = 0; w < 8; w++) d[w] = load_be32(digest_in + 32 * (size_t)i + 4 * w);
-                } else {
-                    uint32_t value_be[8];
-                    HD_UNROLL for (int w = 0; w < 8; w++) value_be[w] = src.value(w);
-                    if (type == T_PROPOSE)
-                        sha256_propose(d, b.height[i], b.round[i], b.valid_round ? b.valid_round[i] : -1, value_be);
-                    else
-                        sha256_vote(d, b.height[i], b.round[i], value_be);
-                }
-                uint32_t r_be[8], s_be[8];
-                HD_UNROLL for (int w = 0; w < 8; w++) { r_be[w] = src.sig_r(w); s_be[w] = src.sig_s(w); }
-                v = verify_fast(d, r_be, s_be, src.sig_v(), tab, tab + (size_t)slot * HD_FB_TAB);
-            }
+        idx[k] = admitted_find(adm, n_adm, adm_steps, from_be);
+        slot[k] = idx[k] >= 0 ? adm_slot[idx[k]] : -1;
+        in[k].ready = slot[k] >= 0 && state[slot[k]] == HD_FB_READY;
+        if (!in[k].ready) continue;
+        if (digest_in) {
+            HD_UNROLL for (int w = 0; w < 8; w++) in[k].digest_be[w] = load_be32(digest_in + 32 * (size_t)i + 4 * w);
         } else {
-            v = V_BAD_TYPE;
+            uint32_t value_be[8];
+            HD_UNROLL for (int w = 0; w < 8; w++) value_be[w] = src.value(w);
+            if (type == T_PROPOSE)
+                sha256_propose(in[k].digest_be, b.height[i], b.round[i], b.valid_round ? b.valid_round[i] : -1,
+                               value_be);
+            else
+                sha256_vote(in[k].digest_be, b.height[i], b.round[i], value_be);
         }
-        if (v == HD_NEEDS_SLOW) {
-            to_slow = true;
-        } else {
-            // VALID: the recovered key is the signatory's, so the recovered
-            // signatory is From; early verdicts recover nothing
-            const bool ok = v == V_VALID;
-            verdict[i] = v;
-            if (rec32) {
-                uint8_t* o = rec32 + 32 * (size_t)i;
-                HD_UNROLL for (int k = 0; k < 8; k++) store_be32(o + 4 * k, ok ? from_be[k] : 0u);
-            }
-            if (signer) signer[i] = ok ? adm_perm[idx] : -1;
+        HD_UNROLL for (int w = 0; w < 8; w++) { in[k].r_be[w] = src.sig_r(w); in[k].s_be[w] = src.sig_s(w); }
+        in[k].v = src.sig_v();
+    }
+    uint8_t v[2];
+    __shared__ FastPark park[256];
+    verify_fast2(v, in, tab, tab + (size_t)(slot[0] > 0 ? slot[0] : 0) * HD_FB_TAB,
+                 tab + (size_t)(slot[1] > 0 ? slot[1] : 0) * HD_FB_TAB, &park[threadIdx.x]);
+    bool to_slow[2];
+    HD_UNROLL for (int k = 0; k < 2; k++) {
+        const uint32_t i = 2 * t + k;
+        to_slow[k] = false;
+        if (!present[k]) continue;
+        if (bad_type[k]) v[k] = V_BAD_TYPE;
+        if (v[k] == HD_NEEDS_SLOW) {
+            to_slow[k] = true;
+            continue;
         }
+        // VALID: the recovered key is the signatory's, so the recovered
+        // signatory is From; early verdicts recover nothing
+        const bool ok = v[k] == V_VALID;
+        verdict[i] = v[k];
+        if (rec32) {
+            uint8_t* o = rec32 + 32 * (size_t)i;
+            const uint8_t* f = b.from32 + 32 * (size_t)i;
+            HD_UNROLL for (int w = 0; w < 8; w++) store_be32(o + 4 * w, ok ? load_be32(f + 4 * w) : 0u);
+        }
+        if (signer) signer[i] = ok ? adm_perm[idx[k]] : -1;
     }
     // wave-aggregated append of the slow-path indices (order is irrelevant:
     // every message is verified on its own)
-    const unsigned long long bal = __ballot(to_slow);
-    if (bal) {
-        const uint32_t lane = threadIdx.x & 63u;
-        const uint32_t leader = (uint32_t)__ffsll((long long)bal) - 1;
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(n_slow, (uint32_t)__popcll(bal));
-        base = __shfl(base, (int)leader);
-        if (to_slow) slow[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1))] = i;
+    HD_UNROLL for (int k = 0; k < 2; k++) {
+        const unsigned long long bal = __ballot(to_slow[k]);
+        if (bal) {
+            const uint32_t lane = threadIdx.x & 63u;
+            const uint32_t leader = (uint32_t)__ffsll((long long)bal) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(n_slow, (uint32_t)__popcll(bal));
+            base = __shfl(base, (int)leader);
+            if (to_slow[k]) slow[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1))] = 2 * t + k;
+        }
     }
 }
 
@@ -331,11 +355,12 @@ int hd_fb_verify(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_
     int rc = hd_dev_grow(ctx, (void**)&f->slow, &f->cap_slow, 4 * (size_t)b.n);
     if (rc) return rc;
     const uint32_t blocks = (b.n + 255) / 256;
+    const uint32_t fast_blocks = ((b.n + 1) / 2 + 255) / 256;   // two messages per lane
     FBCHK(hipMemsetAsync(f->counts + 1, 0, 4, s), "fb count reset");
     if (ctx->n_adm > 0 && f->adm_slot) {
-        static const int fw = getenv("HD_FAST_WAVES") ? atoi(getenv("HD_FAST_WAVES")) : 3;
+        static const int fw = getenv("HD_FAST_WAVES") ? atoi(getenv("HD_FAST_WAVES")) : 2;
 #define HD_LAUNCH_FAST(W)                                                                                        \
-    k_verify_fast<W><<<blocks, 256, 0, s>>>(b, d_digest, f->tab, f->state, f->adm_slot, ctx->d_adm, ctx->d_adm_perm, \
+    k_verify_fast<W><<<fast_blocks, 256, 0, s>>>(b, d_digest, f->tab, f->state, f->adm_slot, ctx->d_adm, ctx->d_adm_perm, \
                                             ctx->n_adm, ctx->adm_steps, d_verdict, d_rec32, d_signer, f->slow,       \
                                             f->counts + 1)
         if (fw == 2) HD_LAUNCH_FAST(2);

@@ -191,6 +191,99 @@ HD uint8_t verify_fast(const uint32_t digest_be[8], const uint32_t r_be[8], cons
     return diff ? HD_NEEDS_SLOW : V_VALID;
 }
 
+// ---- two messages per lane ------------------------------------------------
+// The two inversions (s^-1 mod n, Z^-1 mod p) are a third of the check.  A
+// lane that checks two messages inverts the products s_a s_b and Z_a Z_b once
+// and recovers each inverse with one multiply (Montgomery's trick): half an
+// inversion per message.  A message that cannot take part (early verdict,
+// unknown key, degenerate sum) contributes a factor 1 and keeps its outcome.
+struct FastIn {
+    uint32_t digest_be[8];
+    uint32_t r_be[8];
+    uint32_t s_be[8];
+    uint32_t v;
+    bool ready;                 // key tables available for this message
+};
+
+// Parking space for the first message's sum and x while the second one is
+// computed (the kernel passes a per-lane slot in LDS: keeping both sums in
+// registers spills to scratch).
+struct FastPark {
+    gej acc;
+    fe x;
+};
+
+template <typename GT, typename PT>
+HD void verify_fast2(uint8_t out[2], const FastIn in[2], GT gtab, PT ptab0, PT ptab1, FastPark* park) {
+    sc r[2], s[2], m[2];
+    fe x[2];
+    bool live[2];
+    HD_UNROLL for (int k = 0; k < 2; k++) {
+        out[k] = HD_NEEDS_SLOW;
+        live[k] = false;
+        HD_UNROLL for (int i = 0; i < 8; i++) r[k].v[i] = s[k].v[i] = m[k].v[i] = 0u;
+        fe_clear(x[k]);
+        if (!in[k].ready) continue;
+        const uint8_t pre = sig_prefix(r[k], s[k], x[k], in[k].r_be, in[k].s_be, in[k].v);
+        if (pre != V_VALID) {
+            out[k] = pre;
+            continue;
+        }
+        live[k] = true;
+        sc_from_be_reduce(m[k], in[k].digest_be);
+    }
+    // s^-1 for both from one inversion
+    sc one;
+    HD_UNROLL for (int i = 0; i < 8; i++) one.v[i] = i == 0 ? 1u : 0u;
+    sc sa = live[0] ? s[0] : one, sb = live[1] ? s[1] : one, prod, inv, ia, ib;
+    sc_mul(prod, sa, sb);
+    sc_inv_divsteps(inv, prod);
+    sc_mul(ia, inv, sb);
+    sc_mul(ib, inv, sa);
+    gej acc[2];
+    bool ok[2];
+    HD_UNROLL for (int k = 0; k < 2; k++) {
+        sc u1, u2;
+        const sc& si = k == 0 ? ia : ib;
+        sc_mul(u1, m[k], si);
+        sc_mul(u2, r[k], si);
+        gej_set_inf(acc[k]);
+        bool started = false;
+        fb_accumulate(acc[k], started, u1, gtab);
+        fb_accumulate(acc[k], started, u2, k == 0 ? ptab0 : ptab1);
+        ok[k] = live[k] && started && !gej_is_inf(acc[k]);
+        if (k == 0) {
+            park->acc = acc[0];
+            park->x = x[0];
+        }
+    }
+    acc[0] = park->acc;
+    x[0] = park->x;
+    // Z^-1 for both from one inversion
+    fe fone;
+    fe_set_u32(fone, 1);
+    fe za = acc[0].z, zb = acc[1].z, zp, zi, zia, zib;
+    fe_cmov(za, fone, !ok[0]);
+    fe_cmov(zb, fone, !ok[1]);
+    fe_mul(zp, za, zb);
+    fe_inv_divsteps(zi, zp);
+    fe_mul(zia, zi, zb);
+    fe_mul(zib, zi, za);
+    HD_UNROLL for (int k = 0; k < 2; k++) {
+        if (!ok[k]) continue;
+        fe z = k == 0 ? zia : zib, z2, ax, ay;
+        fe_sqr(z2, z);
+        fe_mul(ax, acc[k].x, z2);
+        fe_mul(z2, z2, z);
+        fe_mul(ay, acc[k].y, z2);
+        fe_normalize(ax);
+        fe_normalize(ay);
+        uint32_t diff = (ay.n[0] & 1u) ^ (in[k].v & 1u);
+        HD_UNROLL for (int i = 0; i < 9; i++) diff |= ax.n[i] ^ x[k].n[i];
+        out[k] = diff ? HD_NEEDS_SLOW : V_VALID;
+    }
+}
+
 // ---- table construction (one entry per lane) --------------------------
 // 2^(W j) B, affine canonical
 HD void fb_window_base(ge& out, const ge& B, int j) {

@@ -349,8 +349,11 @@ static std::vector<ge> fb_tables(const ge& B) {
     }
     return t;
 }
+static std::vector<ge> fb_gt, fb_pt;
+std::vector<ge>* hdh_fb_cache(int which) { return which == 0 ? &fb_gt : &fb_pt; }
 extern "C" int hdh_fb_verify(const uint8_t* pub64, const uint8_t* digest, const uint8_t* sig65) {
-    static std::vector<ge> gt, pt;
+    std::vector<ge>& gt = fb_gt;
+    std::vector<ge>& pt = fb_pt;
     static uint8_t last[64];
     static bool have = false;
     if (gt.empty()) {
@@ -391,4 +394,24 @@ extern "C" int hdh_fb_digits(const uint8_t* k32, int* out) {
     le_in(k.v, k32);
     for (int j = 0; j < HD_FB_NWIN; j++) out[j] = fb_digit(k, j);
     return HD_FB_NWIN;
+}
+
+// verify_fast2 on the host: two messages against two keys' tables (the
+// caches of hdh_fb_verify are reused: both messages use the same key)
+extern "C" void hdh_fb_verify2(const uint8_t* pub64, const uint8_t* digests, const uint8_t* sigs, const int* ready,
+                               uint8_t* out) {
+    uint8_t dummy[65] = {0};
+    hdh_fb_verify(pub64, dummy, dummy);  // builds / refreshes the table caches
+    FastIn in[2];
+    for (int k = 0; k < 2; k++) {
+        for (int w = 0; w < 8; w++) {
+            in[k].digest_be[w] = load_be32(digests + 32 * k + 4 * w);
+            in[k].r_be[w] = load_be32(sigs + 65 * k + 4 * w);
+            in[k].s_be[w] = load_be32(sigs + 65 * k + 32 + 4 * w);
+        }
+        in[k].v = sigs[65 * k + 64];
+        in[k].ready = ready[k] != 0;
+    }
+    FastPark park;
+    verify_fast2(out, in, hdh_fb_cache(0)->data(), hdh_fb_cache(1)->data(), hdh_fb_cache(1)->data(), &park);
 }

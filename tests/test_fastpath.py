@@ -184,3 +184,31 @@ def test_window_digits_recode_the_scalar(fb, oracle):
         assert nwin == (257 + w - 1) // w
         assert all(-(1 << (w - 1)) <= int(d) <= (1 << (w - 1)) for d in out[:nwin])
         assert sum(int(d) << (w * j) for j, d in enumerate(out[:nwin])) == k
+
+
+def test_pairwise_check_equals_single(fb, oracle):
+    """verify_fast2 (two messages per lane, one inversion of each kind for
+    the pair) gives each message the verdict verify_fast gives it alone,
+    whatever its partner is (ready or not, early verdict, fallback)."""
+    O = oracle
+    fb.hdh_fb_verify2.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_char_p]
+    rng = random.Random(21)
+    sk = O.signer_sk(3)
+    P = O.pubkey_of(sk)
+    msgs = []
+    for t in range(24):
+        d = bytes(rng.randrange(256) for _ in range(32))
+        sig = O.sign(sk, d)
+        if t % 4 == 1:
+            sig = sig[:64] + bytes([sig[64] ^ 1])            # fallback
+        elif t % 4 == 2:
+            sig = sig[:64] + bytes([7])                      # BAD_RECID
+        msgs.append((d, sig))
+    for a in range(0, len(msgs), 2):
+        for ready in ([1, 1], [1, 0], [0, 1]):
+            (da, sa), (db, sb) = msgs[a], msgs[(a + 3) % len(msgs)]
+            out = ctypes.create_string_buffer(2)
+            fb.hdh_fb_verify2(_pub64(P), da + db, sa + sb, np.array(ready, np.int32).ctypes.data, out)
+            for k, (d, s) in enumerate([(da, sa), (db, sb)]):
+                want = _verify(fb, P, d, s) if ready[k] else NEEDS_SLOW
+                assert out.raw[k] == want, (a, ready, k)

@@ -213,75 +213,85 @@ struct FastPark {
     fe x;
 };
 
+// stage 1 of one message: the early checks and the scalars
+HD bool fast_prefix(uint8_t& out, sc& r, sc& s, sc& m, fe& x, const FastIn& in) {
+    HD_UNROLL for (int i = 0; i < 8; i++) r.v[i] = s.v[i] = m.v[i] = 0u;
+    fe_clear(x);
+    out = HD_NEEDS_SLOW;
+    if (!in.ready) return false;
+    const uint8_t pre = sig_prefix(r, s, x, in.r_be, in.s_be, in.v);
+    if (pre != V_VALID) {
+        out = pre;
+        return false;
+    }
+    sc_from_be_reduce(m, in.digest_be);
+    return true;
+}
+
+// stage 2 of one message: u1 G + u2 P with u1 = m / s, u2 = r / s
+template <typename GT, typename PT>
+HD bool fast_sum(gej& acc, bool live, const sc& m, const sc& r, const sc& sinv, GT gtab, PT ptab) {
+    sc u1, u2;
+    sc_mul(u1, m, sinv);
+    sc_mul(u2, r, sinv);
+    gej_set_inf(acc);
+    bool started = false;
+    fb_accumulate(acc, started, u1, gtab);
+    fb_accumulate(acc, started, u2, ptab);
+    return live && started && !gej_is_inf(acc);
+}
+
+// stage 3 of one message: affine x and y parity against (x, v & 1)
+HD uint8_t fast_final(const gej& acc, const fe& zinv, const fe& x, uint32_t v) {
+    fe z2, ax, ay;
+    fe_sqr(z2, zinv);
+    fe_mul(ax, acc.x, z2);
+    fe_mul(z2, z2, zinv);
+    fe_mul(ay, acc.y, z2);
+    fe_normalize(ax);
+    fe_normalize(ay);
+    uint32_t diff = (ay.n[0] & 1u) ^ (v & 1u);
+    HD_UNROLL for (int i = 0; i < 9; i++) diff |= ax.n[i] ^ x.n[i];
+    return diff ? HD_NEEDS_SLOW : V_VALID;
+}
+
+// The stages are written out per message (no arrays indexed by the message:
+// the compiler keeps such a loop rolled and the arrays in scratch).
 template <typename GT, typename PT>
 HD void verify_fast2(uint8_t out[2], const FastIn in[2], GT gtab, PT ptab0, PT ptab1, FastPark* park) {
-    sc r[2], s[2], m[2];
-    fe x[2];
-    bool live[2];
-    HD_UNROLL for (int k = 0; k < 2; k++) {
-        out[k] = HD_NEEDS_SLOW;
-        live[k] = false;
-        HD_UNROLL for (int i = 0; i < 8; i++) r[k].v[i] = s[k].v[i] = m[k].v[i] = 0u;
-        fe_clear(x[k]);
-        if (!in[k].ready) continue;
-        const uint8_t pre = sig_prefix(r[k], s[k], x[k], in[k].r_be, in[k].s_be, in[k].v);
-        if (pre != V_VALID) {
-            out[k] = pre;
-            continue;
-        }
-        live[k] = true;
-        sc_from_be_reduce(m[k], in[k].digest_be);
-    }
+    sc r0, s0, m0, r1, s1, m1;
+    fe x0, x1;
+    uint8_t o0, o1;
+    const bool live0 = fast_prefix(o0, r0, s0, m0, x0, in[0]);
+    const bool live1 = fast_prefix(o1, r1, s1, m1, x1, in[1]);
     // s^-1 for both from one inversion
     sc one;
     HD_UNROLL for (int i = 0; i < 8; i++) one.v[i] = i == 0 ? 1u : 0u;
-    sc sa = live[0] ? s[0] : one, sb = live[1] ? s[1] : one, prod, inv, ia, ib;
+    sc sa = live0 ? s0 : one, sb = live1 ? s1 : one, prod, inv, ia, ib;
     sc_mul(prod, sa, sb);
     sc_inv_divsteps(inv, prod);
     sc_mul(ia, inv, sb);
     sc_mul(ib, inv, sa);
-    gej acc[2];
-    bool ok[2];
-    HD_UNROLL for (int k = 0; k < 2; k++) {
-        sc u1, u2;
-        const sc& si = k == 0 ? ia : ib;
-        sc_mul(u1, m[k], si);
-        sc_mul(u2, r[k], si);
-        gej_set_inf(acc[k]);
-        bool started = false;
-        fb_accumulate(acc[k], started, u1, gtab);
-        fb_accumulate(acc[k], started, u2, k == 0 ? ptab0 : ptab1);
-        ok[k] = live[k] && started && !gej_is_inf(acc[k]);
-        if (k == 0) {
-            park->acc = acc[0];
-            park->x = x[0];
-        }
-    }
-    acc[0] = park->acc;
-    x[0] = park->x;
+    gej acc;
+    const bool ok0 = fast_sum(acc, live0, m0, r0, ia, gtab, ptab0);
+    park->acc = acc;
+    park->x = x0;
+    gej acc1;
+    const bool ok1 = fast_sum(acc1, live1, m1, r1, ib, gtab, ptab1);
+    acc = park->acc;
+    x0 = park->x;
     // Z^-1 for both from one inversion
     fe fone;
     fe_set_u32(fone, 1);
-    fe za = acc[0].z, zb = acc[1].z, zp, zi, zia, zib;
-    fe_cmov(za, fone, !ok[0]);
-    fe_cmov(zb, fone, !ok[1]);
+    fe za = acc.z, zb = acc1.z, zp, zi, zia, zib;
+    fe_cmov(za, fone, !ok0);
+    fe_cmov(zb, fone, !ok1);
     fe_mul(zp, za, zb);
     fe_inv_divsteps(zi, zp);
     fe_mul(zia, zi, zb);
     fe_mul(zib, zi, za);
-    HD_UNROLL for (int k = 0; k < 2; k++) {
-        if (!ok[k]) continue;
-        fe z = k == 0 ? zia : zib, z2, ax, ay;
-        fe_sqr(z2, z);
-        fe_mul(ax, acc[k].x, z2);
-        fe_mul(z2, z2, z);
-        fe_mul(ay, acc[k].y, z2);
-        fe_normalize(ax);
-        fe_normalize(ay);
-        uint32_t diff = (ay.n[0] & 1u) ^ (in[k].v & 1u);
-        HD_UNROLL for (int i = 0; i < 9; i++) diff |= ax.n[i] ^ x[k].n[i];
-        out[k] = diff ? HD_NEEDS_SLOW : V_VALID;
-    }
+    out[0] = ok0 ? fast_final(acc, zia, x0, in[0].v) : o0;
+    out[1] = ok1 ? fast_final(acc1, zib, x1, in[1].v) : o1;
 }
 
 // ---- table construction (one entry per lane) --------------------------

@@ -133,6 +133,20 @@ __device__ __forceinline__ void wave_add(uint32_t* ctr, uint32_t slot, bool inc)
     if (!mine && inc) atomicAdd(&ctr[slot], 1u);
 }
 
+// Lanes of a wavefront usually share their round (batches arrive in height
+// order): the first active lane -- the lowest batch index among them -- probes
+// for every lane whose key equals its key and broadcasts the slot; the
+// others probe on their own.  Skipping the followers' probes keeps the
+// first-wins claim exact: their indices are higher than the leader's.  This
+// turns up to 64 same-address CAS / atomicMin per wavefront into one.
+__device__ __forceinline__ int first_active_lane() {
+    return __ffsll((long long)__ballot(true)) - 1;
+}
+__device__ __forceinline__ int64_t shfl64(int64_t v, int src) {
+    const int lo = __shfl((int)(uint32_t)v, src, 64), hi = __shfl((int)(uint32_t)((uint64_t)v >> 32), src, 64);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
 __device__ __forceinline__ uint64_t hash_hr(int64_t h, int64_t r) {
     return mix64((uint64_t)h * 0x9E3779B97F4A7C15ull ^ mix64((uint64_t)r));
 }
@@ -158,8 +172,16 @@ __global__ void k_tally_logs(DevBatch b, const uint8_t* __restrict__ verdict, co
         const uint8_t* from = b.from32 + 32 * (size_t)i;
         const uint64_t hhr = hash_hr(h, r);
         bool created;
-        const uint32_t g = probe(G.claim, mask, hhr, i,
-                                 [&](uint32_t c) { return b.height[c] == h && b.round[c] == r; }, created);
+        const int lead = first_active_lane();
+        const bool follower = shfl64(h, lead) == h && shfl64(r, lead) == r && (int)(threadIdx.x & 63) != lead;
+        uint32_t g = kEmpty;
+        if (!follower)
+            g = probe(G.claim, mask, hhr, i, [&](uint32_t c) { return b.height[c] == h && b.round[c] == r; },
+                      created);
+        {
+            const uint32_t gl = (uint32_t)__shfl((int)g, lead, 64);
+            if (follower) g = gl;
+        }
         const uint32_t d = probe(D, mask, hash_log(hhr, from, t), i,
                                  [&](uint32_t c) {
                                      return b.type[c] == t && b.height[c] == h && b.round[c] == r &&
@@ -204,11 +226,32 @@ __global__ void k_tally_values(DevBatch b, const uint32_t* __restrict__ D, GTab 
         wave_add(G.nboth, g, both);
         const uint64_t hv = *reinterpret_cast<const uint64_t*>(value) ^ *reinterpret_cast<const uint64_t*>(value + 8);
         bool created;
-        const uint32_t c = probe(C.claim, mask, mix64(hv ^ ((uint64_t)g << 1 | (t & 1u))), i,
-                                 [&](uint32_t o) {
-                                     return gslot[o] == g && b.type[o] == t && eq32(b.value32 + 32 * (size_t)o, value);
-                                 },
-                                 created);
+        // same (round, type, value) as the wave's first active winner: share its slot
+        const int lead = first_active_lane();
+        const uint4* vw = reinterpret_cast<const uint4*>(value);
+        const uint4 v0 = vw[0], v1 = vw[1];
+        uint32_t diff = (uint32_t)__shfl((int)g, lead, 64) ^ g;
+        diff |= (uint32_t)__shfl((int)t, lead, 64) ^ t;
+        diff |= (uint32_t)__shfl((int)v0.x, lead, 64) ^ v0.x;
+        diff |= (uint32_t)__shfl((int)v0.y, lead, 64) ^ v0.y;
+        diff |= (uint32_t)__shfl((int)v0.z, lead, 64) ^ v0.z;
+        diff |= (uint32_t)__shfl((int)v0.w, lead, 64) ^ v0.w;
+        diff |= (uint32_t)__shfl((int)v1.x, lead, 64) ^ v1.x;
+        diff |= (uint32_t)__shfl((int)v1.y, lead, 64) ^ v1.y;
+        diff |= (uint32_t)__shfl((int)v1.z, lead, 64) ^ v1.z;
+        diff |= (uint32_t)__shfl((int)v1.w, lead, 64) ^ v1.w;
+        const bool follower = diff == 0 && (int)(threadIdx.x & 63) != lead;
+        uint32_t c = kEmpty;
+        if (!follower)
+            c = probe(C.claim, mask, mix64(hv ^ ((uint64_t)g << 1 | (t & 1u))), i,
+                      [&](uint32_t o) {
+                          return gslot[o] == g && b.type[o] == t && eq32(b.value32 + 32 * (size_t)o, value);
+                      },
+                      created);
+        {
+            const uint32_t cl = (uint32_t)__shfl((int)c, lead, 64);
+            if (follower) c = cl;
+        }
         wave_add(C.n, c, true);
     }
 }

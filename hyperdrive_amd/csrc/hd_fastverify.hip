@@ -4,7 +4,7 @@
 // Per batch, stream-ordered, no host synchronisation:
 //   k_verify_fast   one message per lane: a message whose claimed From is an
 //                   admitted signatory with a known key is checked with two
-//                   fixed-base multiplications (34 mixed additions, no
+//                   fixed-base multiplications (32 mixed additions, no
 //                   doublings, no square root); VALID / early exact verdicts
 //                   are final, everything else is appended to a list
 //   k_verify        (hd_verify.hip) the full libsecp256k1-semantics recovery
@@ -200,7 +200,9 @@ __global__ __launch_bounds__(256) void k_fb_entries(const uint32_t* __restrict__
     const uint32_t total = *count * HD_FB_TAB;
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
         const uint32_t slot = list[t / HD_FB_TAB], e = t % HD_FB_TAB;
-        const uint32_t j = e / HD_FB_N, d = e % HD_FB_N + 1;
+        int j;
+        uint32_t d;
+        fb_entry_pos(e, j, d);
         ge o;
         fb_entry(o, base[(size_t)slot * HD_FB_NWIN + j], d);
         tab[(size_t)slot * HD_FB_TAB + e] = o;

@@ -14,7 +14,7 @@
 // (then Q = r^-1 (s R - m G) = P).  Both scalar multiplications have fixed
 // bases, so they run without doublings over per-base tables of W-bit Booth
 // windows: entry (j, d) = d 2^(W j) B for 1 <= d <= 2^(W-1), and each signed
-// digit costs one mixed addition (W = 16: 17 windows, 34 additions per
+// digit costs one mixed addition (W = 16: 16 windows, 32 additions per
 // message for the two scalars, 40 MB of affine points per base).  No square
 // root is needed: the affine result is compared with x and the parity of y.
 //
@@ -30,9 +30,15 @@ namespace hd {
 #ifndef HD_FB_W
 #define HD_FB_W 16   // 17 windows x 32768 entries (40 MB of tables per key); 12: 22 x 2048 (3.2 MB)
 #endif
-#define HD_FB_NWIN ((257 + HD_FB_W - 1) / HD_FB_W)  // Booth windows over a 256-bit scalar
-#define HD_FB_N (1 << (HD_FB_W - 1))                // |digit| <= 2^(W-1)
-#define HD_FB_TAB (HD_FB_NWIN * HD_FB_N)   // affine entries per base
+// Windows 0 .. NWIN-2 take signed Booth digits |d| <= 2^(W-1); the top window
+// takes the remaining TOPBITS bits plus the Booth carry unsigned,
+// 0 <= d <= 2^TOPBITS, so no extra window is spent on the carry (W = 16: 16
+// windows, the top one with 65536 entries; 15 x 32768 + 65536 points).
+#define HD_FB_NWIN ((256 + HD_FB_W - 1) / HD_FB_W)
+#define HD_FB_N (1 << (HD_FB_W - 1))
+#define HD_FB_TOPBITS (256 - HD_FB_W * (HD_FB_NWIN - 1))
+#define HD_FB_NTOP (1 << HD_FB_TOPBITS)
+#define HD_FB_TAB ((HD_FB_NWIN - 1) * HD_FB_N + HD_FB_NTOP)   // affine entries per base
 #define HD_NEEDS_SLOW 0xFEu
 
 // slot states of the per-signatory tables (device memory, hd_fastverify.hip)
@@ -98,7 +104,14 @@ HD int fb_digit(const sc& k, int j) {
     const uint64_t pair = ((uint64_t)b << 32) | a;
     const uint32_t x = lo < 0 ? (uint32_t)(pair << 1) & ((1u << (HD_FB_W + 1)) - 1)
                               : (uint32_t)(pair >> (lo & 31)) & ((1u << (HD_FB_W + 1)) - 1);
+    if (j == HD_FB_NWIN - 1) return (int)((x >> 1) + (x & 1));   // top window: unsigned, bits past 255 are 0
     return (int)((x >> 1) + (x & 1)) - (int)((x >> HD_FB_W) << HD_FB_W);
+}
+// table entry (window, multiple) of entry number e (builder side)
+HD void fb_entry_pos(uint32_t e, int& j, uint32_t& d) {
+    const uint32_t jj = e / HD_FB_N;
+    j = (int)(jj < HD_FB_NWIN - 1 ? jj : HD_FB_NWIN - 1);
+    d = e - (uint32_t)j * HD_FB_N + 1;
 }
 
 // acc += u B over the base's HD_FB_TAB entries.  `started` is false while acc
@@ -303,7 +316,8 @@ HD void fb_window_base(ge& out, const ge& B, int j) {
     gej_to_ge(out.x, out.y, a);
 }
 
-// d Bj for 1 <= d <= 2^(W-1), affine canonical (double-and-add from the top bit)
+// d Bj for 1 <= d <= 2^(W-1) (2^TOPBITS in the top window), affine canonical
+// (double-and-add from the top bit)
 HD void fb_entry(ge& out, const ge& Bj, uint32_t d) {
     int top = 31;
     while (top > 0 && !((d >> top) & 1u)) top--;

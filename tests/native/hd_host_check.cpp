@@ -342,10 +342,15 @@ extern "C" void hdh_keccak_msg(int pad, int type, int64_t h, int64_t r, int64_t 
 // the device builds them (cached for the last key), then verify_fast.
 static std::vector<ge> fb_tables(const ge& B) {
     std::vector<ge> t(HD_FB_TAB);
-    for (int j = 0; j < HD_FB_NWIN; j++) {
-        ge bj;
-        fb_window_base(bj, B, j);
-        for (uint32_t d = 1; d <= HD_FB_N; d++) fb_entry(t[j * HD_FB_N + d - 1], bj, d);
+    ge bj;
+    int jprev = -1;
+    for (uint32_t e = 0; e < HD_FB_TAB; e++) {
+        int j;
+        uint32_t d;
+        fb_entry_pos(e, j, d);
+        if (j != jprev) fb_window_base(bj, B, j);
+        jprev = j;
+        fb_entry(t[e], bj, d);
     }
     return t;
 }

@@ -40,7 +40,7 @@ def _verify(fb, q, digest, sig):
 
 def test_table_entries_are_window_multiples(fb, oracle):
     O = oracle
-    for j, d in [(0, 1), (0, 2048), (1, 1), (7, 1234), (21, 1), (21, 2048)]:
+    for j, d in [(0, 1), (0, 2048), (1, 1), (7, 1234), (21, 1), (21, 16)]:
         out = ctypes.create_string_buffer(64)
         fb.hdh_fb_entry(_pub64((O.GX, O.GY)), j, d, out)
         want = O.point_mul(d << (12 * j), (O.GX, O.GY))
@@ -170,8 +170,9 @@ def test_fast_path_equals_full_recovery(gpu, kind, S, n, adv, compressed):
 
 
 def test_window_digits_recode_the_scalar(fb, oracle):
-    """fb_digit: signed Booth digits d_j in [-2^(W-1), 2^(W-1)] with
-    sum d_j 2^(W j) == k, for random and edge scalars (host build, W = 12)."""
+    """fb_digit: signed Booth digits d_j in [-2^(W-1), 2^(W-1)], the top one
+    unsigned, with sum d_j 2^(W j) == k, for random and edge scalars (host
+    build, W = 12)."""
     fb.hdh_fb_digits.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
     fb.hdh_fb_digits.restype = ctypes.c_int
     rng = random.Random(8)
@@ -181,8 +182,9 @@ def test_window_digits_recode_the_scalar(fb, oracle):
         out = np.zeros(64, np.int32)
         nwin = fb.hdh_fb_digits(k.to_bytes(32, "big"), out.ctypes.data)
         w = 12
-        assert nwin == (257 + w - 1) // w
-        assert all(-(1 << (w - 1)) <= int(d) <= (1 << (w - 1)) for d in out[:nwin])
+        assert nwin == (256 + w - 1) // w
+        assert all(-(1 << (w - 1)) <= int(d) <= (1 << (w - 1)) for d in out[:nwin - 1])
+        assert 0 <= int(out[nwin - 1]) <= (1 << (256 - w * (nwin - 1)))     # top window: unsigned
         assert sum(int(d) << (w * j) for j, d in enumerate(out[:nwin])) == k
 
 

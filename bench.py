@@ -32,11 +32,11 @@ sys.path.insert(0, ROOT)
 W_OPS_PER_MSG = 6.06e5          # algorithmic int32 ops per Prevote/Precommit (full recovery)
 # The same cost model (M = one 256-bit modular multiply = 160 int32 ops) for
 # the known-key check R == s^-1 (m G + r P) that VALID messages of known
-# signatories take: 32 mixed additions (8M + 3S each) + s^-1
+# signatories take: 29 mixed additions (8M + 3S each) + s^-1
 # mod n (296 M, as SURVEY's r^-1) + u1, u2 (2 M) + affine conversion (274 M)
 # + one SHA-256 compression (2,200 ops)
 M_OPS = 160
-W_FAST_OPS_PER_MSG = (32 * 11 + 296 + 2 + 274) * M_OPS + 2200
+W_FAST_OPS_PER_MSG = (29 * 11 + 296 + 2 + 274) * M_OPS + 2200
 BYTES_PER_MSG = 146 + 33        # HBM in + out per message
 # INT32 VALU peak of one MI355X: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (the
 # FP32-vector issue rate of MI355X_MICROARCH.md, 157.3 TFLOPS / 2 per FMA)

@@ -4,7 +4,7 @@
 // Per batch, stream-ordered, no host synchronisation:
 //   k_verify_fast   one message per lane: a message whose claimed From is an
 //                   admitted signatory with a known key is checked with two
-//                   fixed-base multiplications (32 mixed additions, no
+//                   fixed-base multiplications (29 mixed additions, no
 //                   doublings, no square root); VALID / early exact verdicts
 //                   are final, everything else is appended to a list
 //   k_verify        (hd_verify.hip) the full libsecp256k1-semantics recovery
@@ -17,13 +17,16 @@
 //                   lane); with nothing learned each exits at once
 // Table memory is capped by HD_FB_MAX_BYTES (default 64 GiB of the 288 GB):
 // signatories beyond the cap always take the full recovery.
-// Slot 0 holds the tables of G, built when the context is created.
+// G has one table with wider windows (HD_FB_WG bits: 13 additions for u1
+// instead of 16), built once per device and process (fb_g_table).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <map>
+#include <mutex>
 #include <unordered_map>
 #include <vector>
 
@@ -35,7 +38,8 @@
 using namespace hd;
 
 struct FbWork {
-    uint32_t nslots = 0;        // allocated slots; slot 0 = G
+    const ge* gtab = nullptr;   // the shared G table of the device (fb_g_table)
+    uint32_t nslots = 0;        // allocated slots; slot 0 is unused
     uint32_t max_slots = 0;     // from HD_FB_MAX_BYTES (slot 0 included)
     ge* tab = nullptr;          // nslots x HD_FB_TAB
     ge* base = nullptr;         // nslots x HD_FB_NWIN window bases
@@ -77,7 +81,7 @@ struct FastSrc {
 // kind for the pair).
 template <int WAVES>
 __global__ __launch_bounds__(256, WAVES) void k_verify_fast(DevBatch b, const uint8_t* __restrict__ digest_in,
-                                                     const ge* __restrict__ tab, const uint32_t* __restrict__ state,
+                                                     const ge* __restrict__ gtab, const ge* __restrict__ tab, const uint32_t* __restrict__ state,
                                                      const int32_t* __restrict__ adm_slot,
                                                      const uint32_t* __restrict__ adm, const int32_t* __restrict__ adm_perm,
                                                      uint32_t n_adm, int adm_steps, uint8_t* __restrict__ verdict,
@@ -125,7 +129,7 @@ __global__ __launch_bounds__(256, WAVES) void k_verify_fast(DevBatch b, const ui
     }
     uint8_t v[2];
     __shared__ FastPark park[256];
-    verify_fast2(v, in, tab, tab + (size_t)(slot[0] > 0 ? slot[0] : 0) * HD_FB_TAB,
+    verify_fast2(v, in, gtab, tab + (size_t)(slot[0] > 0 ? slot[0] : 0) * HD_FB_TAB,
                  tab + (size_t)(slot[1] > 0 ? slot[1] : 0) * HD_FB_TAB, &park[threadIdx.x]);
     bool to_slow[2];
     HD_UNROLL for (int k = 0; k < 2; k++) {
@@ -183,29 +187,33 @@ __global__ void k_fb_list(uint32_t nslots, const uint32_t* __restrict__ state, u
     if (threadIdx.x == 0) *count = c;
 }
 
+template <int W>
 __global__ __launch_bounds__(256) void k_fb_bases(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
                                                   const ge* __restrict__ pub, ge* __restrict__ base) {
-    const uint32_t total = *count * HD_FB_NWIN;
+    constexpr int NW = FbL<W>::NWIN;
+    const uint32_t total = *count * NW;
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-        const uint32_t slot = list[t / HD_FB_NWIN], j = t % HD_FB_NWIN;
+        const uint32_t slot = list[t / NW], j = t % NW;
         ge o;
-        fb_window_base(o, pub[slot], (int)j);
-        base[(size_t)slot * HD_FB_NWIN + j] = o;
+        fb_window_base(o, pub[slot], W, (int)j);
+        base[(size_t)slot * NW + j] = o;
     }
 }
 
+template <int W>
 __global__ __launch_bounds__(256) void k_fb_entries(const uint32_t* __restrict__ list,
                                                     const uint32_t* __restrict__ count, const ge* __restrict__ base,
                                                     ge* __restrict__ tab) {
-    const uint32_t total = *count * HD_FB_TAB;
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-        const uint32_t slot = list[t / HD_FB_TAB], e = t % HD_FB_TAB;
+    constexpr uint32_t TAB = FbL<W>::TAB;
+    const uint64_t total = (uint64_t)*count * TAB;
+    for (uint64_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t slot = list[t / TAB], e = (uint32_t)(t % TAB);
         int j;
         uint32_t d;
-        fb_entry_pos(e, j, d);
+        fb_entry_pos<W>(e, j, d);
         ge o;
-        fb_entry(o, base[(size_t)slot * HD_FB_NWIN + j], d);
-        tab[(size_t)slot * HD_FB_TAB + e] = o;
+        fb_entry(o, base[(size_t)slot * FbL<W>::NWIN + j], d);
+        tab[(size_t)slot * TAB + e] = o;
     }
 }
 
@@ -252,14 +260,55 @@ int fb_learn(hd_ctx* ctx, hipStream_t s) {
     FbWork* f = ctx->fb;
     const uint32_t g = (uint32_t)std::max(ctx->n_cu, 1) * 4u;
     k_fb_list<<<1, 256, 0, s>>>(f->nslots, f->state, f->list, f->counts);
-    k_fb_bases<<<g, 256, 0, s>>>(f->list, f->counts, f->pub, f->base);
-    k_fb_entries<<<g * 2, 256, 0, s>>>(f->list, f->counts, f->base, f->tab);
+    k_fb_bases<HD_FB_W><<<g, 256, 0, s>>>(f->list, f->counts, f->pub, f->base);
+    k_fb_entries<HD_FB_W><<<g * 2, 256, 0, s>>>(f->list, f->counts, f->base, f->tab);
     k_fb_ready<<<1, 256, 0, s>>>(f->list, f->counts, f->state);
     FBCHK(hipGetLastError(), "fb table kernels");
     return HD_OK;
 }
 
 }  // namespace
+
+// The G table (W = HD_FB_WG) is built once per device and process and shared
+// by every context on that device.
+static std::mutex g_fb_g_mutex;
+static std::map<int, ge*> g_fb_g_tables;
+
+static int fb_g_table(hd_ctx* ctx, const ge** out) {
+    std::lock_guard<std::mutex> lock(g_fb_g_mutex);
+    auto it = g_fb_g_tables.find(ctx->device);
+    if (it != g_fb_g_tables.end()) {
+        *out = it->second;
+        return HD_OK;
+    }
+    ge g;
+    const uint32_t GX[8] = {0x79BE667Eu, 0xF9DCBBACu, 0x55A06295u, 0xCE870B07u,
+                            0x029BFCDBu, 0x2DCE28D9u, 0x59F2815Bu, 0x16F81798u};
+    const uint32_t GY[8] = {0x483ADA77u, 0x26A3C465u, 0x5DA4FBFCu, 0x0E1108A8u,
+                            0xFD17B448u, 0xA6855419u, 0x9C47D08Fu, 0xFB10D4B8u};
+    fe_from_be(g.x, GX);
+    fe_from_be(g.y, GY);
+    ge *tab = nullptr, *base = nullptr, *pub = nullptr;
+    uint32_t* cl = nullptr;  // [0] = list {0}, [1] = count 1
+    FBCHK(hipMalloc(&tab, sizeof(ge) * (size_t)FbL<HD_FB_WG>::TAB), "G table");
+    FBCHK(hipMalloc(&base, sizeof(ge) * FbL<HD_FB_WG>::NWIN), "G bases");
+    FBCHK(hipMalloc(&pub, sizeof(ge)), "G point");
+    FBCHK(hipMalloc(&cl, 8), "G list");
+    const uint32_t hl[2] = {0u, 1u};
+    FBCHK(hipMemcpy(pub, &g, sizeof(ge), hipMemcpyHostToDevice), "G point");
+    FBCHK(hipMemcpy(cl, hl, 8, hipMemcpyHostToDevice), "G list");
+    const uint32_t grid = (uint32_t)std::max(ctx->n_cu, 1) * 8u;
+    k_fb_bases<HD_FB_WG><<<1, 64, 0, ctx->stream>>>(cl, cl + 1, pub, base);
+    k_fb_entries<HD_FB_WG><<<grid, 256, 0, ctx->stream>>>(cl, cl + 1, base, tab);
+    FBCHK(hipGetLastError(), "G table kernels");
+    FBCHK(hipStreamSynchronize(ctx->stream), "G table build");
+    (void)hipFree(base);
+    (void)hipFree(pub);
+    (void)hipFree(cl);
+    g_fb_g_tables[ctx->device] = tab;
+    *out = tab;
+    return HD_OK;
+}
 
 int hd_fb_init(hd_ctx* ctx) {
     if (ctx->fb) return HD_OK;
@@ -273,21 +322,7 @@ int hd_fb_init(hd_ctx* ctx) {
     FBCHK(hipMalloc(&f->counts, 8), "fb counts");
     int rc = fb_grow_slots(ctx, 1);
     if (rc) return rc;
-    // slot 0: G
-    ge g;
-    const uint32_t GX[8] = {0x79BE667Eu, 0xF9DCBBACu, 0x55A06295u, 0xCE870B07u,
-                            0x029BFCDBu, 0x2DCE28D9u, 0x59F2815Bu, 0x16F81798u};
-    const uint32_t GY[8] = {0x483ADA77u, 0x26A3C465u, 0x5DA4FBFCu, 0x0E1108A8u,
-                            0xFD17B448u, 0xA6855419u, 0x9C47D08Fu, 0xFB10D4B8u};
-    fe_from_be(g.x, GX);
-    fe_from_be(g.y, GY);
-    const uint32_t learned = HD_FB_LEARNED;
-    FBCHK(hipMemcpy(f->pub, &g, sizeof(ge), hipMemcpyHostToDevice), "fb G");
-    FBCHK(hipMemcpy(f->state, &learned, 4, hipMemcpyHostToDevice), "fb G state");
-    rc = fb_learn(ctx, ctx->stream);
-    if (rc) return rc;
-    FBCHK(hipStreamSynchronize(ctx->stream), "fb G tables");
-    return HD_OK;
+    return fb_g_table(ctx, &f->gtab);
 }
 
 void hd_fb_release(hd_ctx* ctx) {
@@ -362,7 +397,7 @@ int hd_fb_verify(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_
     if (ctx->n_adm > 0 && f->adm_slot) {
         static const int fw = getenv("HD_FAST_WAVES") ? atoi(getenv("HD_FAST_WAVES")) : 2;
 #define HD_LAUNCH_FAST(W)                                                                                        \
-    k_verify_fast<W><<<fast_blocks, 256, 0, s>>>(b, d_digest, f->tab, f->state, f->adm_slot, ctx->d_adm, ctx->d_adm_perm, \
+    k_verify_fast<W><<<fast_blocks, 256, 0, s>>>(b, d_digest, f->gtab, f->tab, f->state, f->adm_slot, ctx->d_adm, ctx->d_adm_perm, \
                                             ctx->n_adm, ctx->adm_steps, d_verdict, d_rec32, d_signer, f->slow,       \
                                             f->counts + 1)
         if (fw == 2) HD_LAUNCH_FAST(2);

@@ -28,17 +28,27 @@
 namespace hd {
 
 #ifndef HD_FB_W
-#define HD_FB_W 16   // 17 windows x 32768 entries (40 MB of tables per key); 12: 22 x 2048 (3.2 MB)
+#define HD_FB_W 16    // per-key tables: 16 windows, 15 x 32768 + 65536 points (40 MB)
 #endif
+#ifndef HD_FB_WG
+#define HD_FB_WG 20   // the one shared G table: 13 windows, 12 x 2^19 + 2^16 points (458 MB)
+#endif
+
 // Windows 0 .. NWIN-2 take signed Booth digits |d| <= 2^(W-1); the top window
 // takes the remaining TOPBITS bits plus the Booth carry unsigned,
-// 0 <= d <= 2^TOPBITS, so no extra window is spent on the carry (W = 16: 16
-// windows, the top one with 65536 entries; 15 x 32768 + 65536 points).
-#define HD_FB_NWIN ((256 + HD_FB_W - 1) / HD_FB_W)
-#define HD_FB_N (1 << (HD_FB_W - 1))
-#define HD_FB_TOPBITS (256 - HD_FB_W * (HD_FB_NWIN - 1))
-#define HD_FB_NTOP (1 << HD_FB_TOPBITS)
-#define HD_FB_TAB ((HD_FB_NWIN - 1) * HD_FB_N + HD_FB_NTOP)   // affine entries per base
+// 0 <= d <= 2^TOPBITS, so no extra window is spent on the carry.  Entry
+// (j, d) of a base B is d 2^(W j) B at index j N + d - 1.
+template <int W>
+struct FbL {
+    static constexpr int NWIN = (256 + W - 1) / W;
+    static constexpr uint32_t N = 1u << (W - 1);
+    static constexpr int TOPBITS = 256 - W * (NWIN - 1);
+    static constexpr uint32_t NTOP = 1u << TOPBITS;
+    static constexpr uint32_t TAB = (uint32_t)(NWIN - 1) * N + NTOP;   // affine entries per base
+};
+#define HD_FB_NWIN (FbL<HD_FB_W>::NWIN)
+#define HD_FB_N (FbL<HD_FB_W>::N)
+#define HD_FB_TAB (FbL<HD_FB_W>::TAB)
 #define HD_NEEDS_SLOW 0xFEu
 
 // slot states of the per-signatory tables (device memory, hd_fastverify.hip)
@@ -97,38 +107,40 @@ HD uint32_t sc_word_sel(const sc& k, int w) {
     HD_UNROLL for (int i = 0; i < 8; i++) o = (w == i) ? k.v[i] : o;
     return o;
 }
+template <int W>
 HD int fb_digit(const sc& k, int j) {
-    const int lo = HD_FB_W * j - 1;                 // lowest bit of the window (may be -1)
+    const int lo = W * j - 1;                       // lowest bit of the window (may be -1)
     const int wlo = lo < 0 ? 0 : (lo >> 5);
     const uint32_t a = sc_word_sel(k, wlo), b = sc_word_sel(k, wlo + 1);   // b = 0 past the top
     const uint64_t pair = ((uint64_t)b << 32) | a;
-    const uint32_t x = lo < 0 ? (uint32_t)(pair << 1) & ((1u << (HD_FB_W + 1)) - 1)
-                              : (uint32_t)(pair >> (lo & 31)) & ((1u << (HD_FB_W + 1)) - 1);
-    if (j == HD_FB_NWIN - 1) return (int)((x >> 1) + (x & 1));   // top window: unsigned, bits past 255 are 0
-    return (int)((x >> 1) + (x & 1)) - (int)((x >> HD_FB_W) << HD_FB_W);
+    const uint32_t m = (1u << (W + 1)) - 1;
+    const uint32_t x = lo < 0 ? (uint32_t)(pair << 1) & m : (uint32_t)(pair >> (lo & 31)) & m;
+    if (j == FbL<W>::NWIN - 1) return (int)((x >> 1) + (x & 1));   // top window: unsigned, bits past 255 are 0
+    return (int)((x >> 1) + (x & 1)) - (int)((x >> W) << W);
 }
 // table entry (window, multiple) of entry number e (builder side)
+template <int W>
 HD void fb_entry_pos(uint32_t e, int& j, uint32_t& d) {
-    const uint32_t jj = e / HD_FB_N;
-    j = (int)(jj < HD_FB_NWIN - 1 ? jj : HD_FB_NWIN - 1);
-    d = e - (uint32_t)j * HD_FB_N + 1;
+    const uint32_t jj = e / FbL<W>::N;
+    j = (int)(jj < (uint32_t)(FbL<W>::NWIN - 1) ? jj : (uint32_t)(FbL<W>::NWIN - 1));
+    d = e - (uint32_t)j * FbL<W>::N + 1;
 }
 
 // acc += u B over the base's HD_FB_TAB entries.  `started` is false while acc
 // is still the point at infinity (no non-zero digit yet); the first non-zero
 // digit sets acc to its table point.  The next window's point is loaded
 // before the current addition, so its HBM latency hides under the math.
-template <typename Tab>
+template <int W, typename Tab>
 HD void fb_accumulate(gej& acc, bool& started, const sc& u, Tab tab) {
-    int d = fb_digit(u, 0);
+    int d = fb_digit<W>(u, 0);
     ge t = tab[(d < 0 ? -d : d) == 0 ? 0 : (d < 0 ? -d : d) - 1];
-    HD_NOUNROLL for (int j = 0; j < HD_FB_NWIN; j++) {
+    HD_NOUNROLL for (int j = 0; j < FbL<W>::NWIN; j++) {
         ge cur = t;
         const int dc = d;
-        if (j + 1 < HD_FB_NWIN) {
-            d = fb_digit(u, j + 1);
+        if (j + 1 < FbL<W>::NWIN) {
+            d = fb_digit<W>(u, j + 1);
             const int ad = d < 0 ? -d : d;
-            t = tab[(j + 1) * HD_FB_N + (ad == 0 ? 0 : ad - 1)];
+            t = tab[(j + 1) * FbL<W>::N + (ad == 0 ? 0 : ad - 1)];
         }
         if (dc < 0) fe_neg(cur.y, cur.y);
         gej s;
@@ -187,8 +199,8 @@ HD uint8_t verify_fast(const uint32_t digest_be[8], const uint32_t r_be[8], cons
     gej acc;
     gej_set_inf(acc);
     bool started = false;
-    fb_accumulate(acc, started, u1, gtab);
-    fb_accumulate(acc, started, u2, ptab);
+    fb_accumulate<HD_FB_WG>(acc, started, u1, gtab);
+    fb_accumulate<HD_FB_W>(acc, started, u2, ptab);
     // infinity, or a degenerate addition on the way (Z = 0): full recovery
     if (!started || gej_is_inf(acc)) return HD_NEEDS_SLOW;
     fe zi, zi2, ax, ay;
@@ -249,8 +261,8 @@ HD bool fast_sum(gej& acc, bool live, const sc& m, const sc& r, const sc& sinv, 
     sc_mul(u2, r, sinv);
     gej_set_inf(acc);
     bool started = false;
-    fb_accumulate(acc, started, u1, gtab);
-    fb_accumulate(acc, started, u2, ptab);
+    fb_accumulate<HD_FB_WG>(acc, started, u1, gtab);
+    fb_accumulate<HD_FB_W>(acc, started, u2, ptab);
     return live && started && !gej_is_inf(acc);
 }
 
@@ -309,10 +321,10 @@ HD void verify_fast2(uint8_t out[2], const FastIn in[2], GT gtab, PT ptab0, PT p
 
 // ---- table construction (one entry per lane) --------------------------
 // 2^(W j) B, affine canonical
-HD void fb_window_base(ge& out, const ge& B, int j) {
+HD void fb_window_base(ge& out, const ge& B, int W, int j) {
     gej a;
     gej_set_ge(a, B);
-    HD_NOUNROLL for (int k = 0; k < HD_FB_W * j; k++) gej_dbl(a, a);
+    HD_NOUNROLL for (int k = 0; k < W * j; k++) gej_dbl(a, a);
     gej_to_ge(out.x, out.y, a);
 }
 

@@ -54,7 +54,7 @@ def build_hostmath(bounds: bool = False) -> str:
         # the fixed-base tables at 12-bit windows (22 x 2048 entries): the
         # product's 16-bit tables (17 x 32768) take ~10 s per key to build on
         # one host core; the algorithm is the same for every window width
-        flags = (["-DHD_BOUNDS"] if bounds else []) + ["-DHD_FB_W=12"]
+        flags = (["-DHD_BOUNDS"] if bounds else []) + ["-DHD_FB_W=12", "-DHD_FB_WG=12"]
         subprocess.run(["g++", "-O2", "-fPIC", "-shared", "-std=c++17", "-Wall", "-Wno-unused-function", *flags, "-o",
                         out, srcs[0]], check=True)
     return out

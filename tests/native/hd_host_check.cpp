@@ -340,15 +340,16 @@ extern "C" void hdh_keccak_msg(int pad, int type, int64_t h, int64_t r, int64_t 
 // Known-key fast path of hd_fixedbase.h on the host: tables of G and of the
 // key (x, y big-endian) are built with fb_window_base / fb_entry exactly as
 // the device builds them (cached for the last key), then verify_fast.
+template <int W>
 static std::vector<ge> fb_tables(const ge& B) {
-    std::vector<ge> t(HD_FB_TAB);
+    std::vector<ge> t(FbL<W>::TAB);
     ge bj;
     int jprev = -1;
-    for (uint32_t e = 0; e < HD_FB_TAB; e++) {
+    for (uint32_t e = 0; e < FbL<W>::TAB; e++) {
         int j;
         uint32_t d;
-        fb_entry_pos(e, j, d);
-        if (j != jprev) fb_window_base(bj, B, j);
+        fb_entry_pos<W>(e, j, d);
+        if (j != jprev) fb_window_base(bj, B, W, j);
         jprev = j;
         fb_entry(t[e], bj, d);
     }
@@ -365,13 +366,13 @@ extern "C" int hdh_fb_verify(const uint8_t* pub64, const uint8_t* digest, const 
         ge g;
         g.x = gtab()[0].x;
         g.y = gtab()[0].y;
-        gt = fb_tables(g);
+        gt = fb_tables<HD_FB_WG>(g);
     }
     if (!have || memcmp(last, pub64, 64) != 0) {
         ge P;
         fe_in(P.x, pub64);
         fe_in(P.y, pub64 + 32);
-        pt = fb_tables(P);
+        pt = fb_tables<HD_FB_W>(P);
         memcpy(last, pub64, 64);
         have = true;
     }
@@ -388,7 +389,7 @@ extern "C" void hdh_fb_entry(const uint8_t* b64, int j, uint32_t d, uint8_t* out
     ge B, bj, e;
     fe_in(B.x, b64);
     fe_in(B.y, b64 + 32);
-    fb_window_base(bj, B, j);
+    fb_window_base(bj, B, HD_FB_W, j);
     fb_entry(e, bj, d);
     fe_out(out64, e.x);
     fe_out(out64 + 32, e.y);
@@ -397,7 +398,7 @@ extern "C" void hdh_fb_entry(const uint8_t* b64, int j, uint32_t d, uint8_t* out
 extern "C" int hdh_fb_digits(const uint8_t* k32, int* out) {
     sc k;
     le_in(k.v, k32);
-    for (int j = 0; j < HD_FB_NWIN; j++) out[j] = fb_digit(k, j);
+    for (int j = 0; j < HD_FB_NWIN; j++) out[j] = fb_digit<HD_FB_W>(k, j);
     return HD_FB_NWIN;
 }
 

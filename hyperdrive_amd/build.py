@@ -26,7 +26,7 @@ ARCH = os.environ.get("HD_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 
 CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-          "-I" + INCLUDE] + (["-DHD_FB_W=" + os.environ["HD_FB_W"]] if os.environ.get("HD_FB_W") else [])
+          "-I" + INCLUDE] + ["-D%s=%s" % (k, os.environ[k]) for k in ("HD_FB_W", "HD_FB_WG") if os.environ.get(k)]
 
 
 def _sources():

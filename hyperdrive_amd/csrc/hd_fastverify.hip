@@ -51,9 +51,14 @@ struct FbWork {
     uint32_t* counts = nullptr;   // [0] slots to build, [1] messages for the slow path
     uint32_t* slow = nullptr;     // message index list
     size_t cap_slow = 0;
+    uint32_t* rows = nullptr;     // the split check's per-message rows (SplitRows, 83 words per message)
+    size_t cap_rows = 0;
     std::unordered_map<std::string, uint32_t> slot_of;  // signatory -> slot
     std::vector<uint32_t> free_slots;
     uint32_t used = 1;            // slots handed out so far (slot 0 = G)
+    int wp = HD_FB_W;             // window width of the per-key tables (HD_FB_W or HD_FB_WW)
+    double budget = 0;            // table bytes allowed (HD_FB_MAX_BYTES), shared per device
+    size_t bytes = 0;             // table bytes this context holds
 };
 
 namespace {
@@ -167,6 +172,288 @@ __global__ __launch_bounds__(256, WAVES) void k_verify_fast(DevBatch b, const ui
     }
 }
 
+// ---- the split check: K messages per lane share each inversion ----------
+// k_verify_fast inverts s and Z once per two messages.  The split form runs
+// the same check in three kernels so that one inversion of each kind serves
+// K messages of a lane (Montgomery's trick over K), with the per-message
+// state in word-major HBM rows between them (lane t reads word w of message
+// i at w * n + i, coalesced):
+//   k_fast_scalars  K per lane: lookup, digest, early checks; prefix products
+//                   of s, one inversion mod n, then u1 = m/s, u2 = r/s
+//   k_fast_sums     one per lane: u1 G + u2 P (29 mixed additions)
+//   k_fast_final    K per lane: prefix products of Z, one inversion mod p,
+//                   the comparison, the outputs and the fallback list
+// Message i of lane t is i = j T + t (j < K, T = ceil(n / K)), so every step
+// j of a wave touches consecutive messages.  The verdicts are the ones
+// verify_fast2 gives: same early checks, same sums, same comparison.
+#define HD_FAST_LIVE 0xFDu   // aux code: keep going (the rest are final verdicts or HD_NEEDS_SLOW)
+
+template <int NW>
+HD void soa_load(uint32_t (&w)[NW], const uint32_t* __restrict__ p, uint32_t n, uint32_t i) {
+    HD_UNROLL for (int k = 0; k < NW; k++) w[k] = p[(size_t)k * n + i];
+}
+template <int NW>
+HD void soa_store(uint32_t* __restrict__ p, uint32_t n, uint32_t i, const uint32_t (&w)[NW]) {
+    HD_UNROLL for (int k = 0; k < NW; k++) p[(size_t)k * n + i] = w[k];
+}
+
+struct SplitRows {
+    uint32_t* aux;   // n: slot << 8 | code
+    int32_t* idx;    // n: admitted (sorted) index
+    uint32_t* u1;    // 8n: m, then m / s
+    uint32_t* u2;    // 8n: r, then r / s
+    uint32_t* pre;   // 9n: prefix products (s: 8 words, then Z: 9 words)
+    uint32_t* xyz;   // 27n: the Jacobian sum
+    uint32_t* dig;   // (NWIN(WG) + NWIN(W)) n: window digits as table references (fb_ref)
+};
+
+// a Booth digit of window w as a reference into the base's table: entry
+// index | HD_REF_NEG for a negative digit, HD_REF_ZERO for 0 (entry 0 of the
+// window is then read and discarded)
+#define HD_REF_NEG 0x80000000u
+#define HD_REF_ZERO 0x40000000u
+#define HD_REF_IDX 0x3FFFFFFFu
+template <int W>
+HD uint32_t fb_ref(int d, int w) {
+    const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+    const uint32_t base = (uint32_t)w * FbL<W>::N;
+    return d == 0 ? (base | HD_REF_ZERO) : ((base + ad - 1) | (d < 0 ? HD_REF_NEG : 0u));
+}
+
+template <int K, int WP>
+__global__ __launch_bounds__(256) void k_fast_scalars(DevBatch b, const uint8_t* __restrict__ digest_in,
+                                                      const uint32_t* __restrict__ state,
+                                                      const int32_t* __restrict__ adm_slot,
+                                                      const uint32_t* __restrict__ adm, uint32_t n_adm,
+                                                      int adm_steps, uint32_t T, SplitRows rows) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const uint32_t n = b.n;
+    sc acc;
+    HD_UNROLL for (int w = 0; w < 8; w++) acc.v[w] = w == 0 ? 1u : 0u;
+    uint32_t live = 0;   // bit j: message j of this lane goes on
+    HD_NOUNROLL for (int j = 0; j < K; j++) {
+        const uint32_t i = (uint32_t)j * T + t;
+        if (i >= n) break;
+        FastSrc src{b, i, digest_in};
+        const uint32_t type = src.type();
+        uint32_t code = HD_NEEDS_SLOW, slot = 0;
+        int32_t idx = -1;
+        if (type < 1 || type > 3) {
+            code = V_BAD_TYPE;
+        } else {
+            uint32_t from_be[8];
+            HD_UNROLL for (int w = 0; w < 8; w++) from_be[w] = src.from(w);
+            idx = admitted_find(adm, n_adm, adm_steps, from_be);
+            const int32_t sl = idx >= 0 ? adm_slot[idx] : -1;
+            if (sl >= 0 && state[sl] == HD_FB_READY) {
+                slot = (uint32_t)sl;
+                FastIn in;
+                if (digest_in) {
+                    HD_UNROLL for (int w = 0; w < 8; w++) in.digest_be[w] = load_be32(digest_in + 32 * (size_t)i + 4 * w);
+                } else {
+                    uint32_t value_be[8];
+                    HD_UNROLL for (int w = 0; w < 8; w++) value_be[w] = src.value(w);
+                    if (type == T_PROPOSE)
+                        sha256_propose(in.digest_be, b.height[i], b.round[i],
+                                       b.valid_round ? b.valid_round[i] : -1, value_be);
+                    else
+                        sha256_vote(in.digest_be, b.height[i], b.round[i], value_be);
+                }
+                HD_UNROLL for (int w = 0; w < 8; w++) { in.r_be[w] = src.sig_r(w); in.s_be[w] = src.sig_s(w); }
+                in.v = src.sig_v();
+                in.ready = true;
+                sc r, s, m;
+                fe x;
+                uint8_t o;
+                if (fast_prefix(o, r, s, m, x, in)) {
+                    code = HD_FAST_LIVE;
+                    live |= 1u << j;
+                    soa_store(rows.u1, n, i, m.v);
+                    soa_store(rows.u2, n, i, r.v);
+                    sc_mul(acc, acc, s);
+                } else {
+                    code = o;
+                }
+            }
+        }
+        rows.aux[i] = slot << 8 | code;
+        rows.idx[i] = idx;
+        soa_store(rows.pre, n, i, acc.v);
+    }
+    if (!live) return;
+    sc inv;
+    sc_inv_divsteps(inv, acc);   // a product of scalars in [1, n): never 0
+    HD_NOUNROLL for (int j = K - 1; j >= 0; j--) {
+        if (!((live >> j) & 1u)) continue;
+        const uint32_t i = (uint32_t)j * T + t;
+        sc prev, sinv, s, u;
+        if (j > 0) {
+            soa_load(prev.v, rows.pre, n, i - T);
+        } else {
+            HD_UNROLL for (int w = 0; w < 8; w++) prev.v[w] = w == 0 ? 1u : 0u;
+        }
+        sc_mul(sinv, inv, prev);
+        FastSrc src{b, i, digest_in};
+        HD_UNROLL for (int w = 0; w < 8; w++) s.v[w] = src.sig_s(7 - w);
+        sc_mul(inv, inv, s);
+        // u1 = m / s and u2 = r / s leave as their window digits: table
+        // references of the G windows, then of the P windows
+        soa_load(u.v, rows.u1, n, i);
+        sc_mul(u, u, sinv);
+        HD_UNROLL for (int w = 0; w < FbL<HD_FB_WG>::NWIN; w++)
+            rows.dig[(size_t)w * n + i] = fb_ref<HD_FB_WG>(fb_digit<HD_FB_WG>(u, w), w);
+        soa_load(u.v, rows.u2, n, i);
+        sc_mul(u, u, sinv);
+        HD_UNROLL for (int w = 0; w < FbL<WP>::NWIN; w++)
+            rows.dig[(size_t)(FbL<HD_FB_WG>::NWIN + w) * n + i] = fb_ref<WP>(fb_digit<WP>(u, w), w);
+    }
+}
+
+// u1 G + u2 P from the digit rows: the first G window's point starts the
+// sum (no addition), then one mixed addition per further window, the next
+// point loaded one addition ahead.  A zero digit contributes nothing; while
+// no digit has been non-zero the sum is the point at infinity.
+HD void sum_step(gej& acc, bool& started, ge cur, uint32_t ec) {
+    if (ec & HD_REF_NEG) fe_neg(cur.y, cur.y);
+    gej s;
+    gej_add_ge_nx(s, acc, cur);
+    gej first;
+    gej_set_ge(first, cur);
+    fe_norm_weak(first.y);
+    gej_cmov(s, first, !started);
+    const bool nz = !(ec & HD_REF_ZERO);
+    gej_cmov(acc, s, nz);
+    started = started || nz;
+}
+
+template <int WAVES, int WP>
+__global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const ge* __restrict__ gtab,
+                                                          const ge* __restrict__ tab, SplitRows rows) {
+    constexpr int NG = FbL<HD_FB_WG>::NWIN, NT = NG + FbL<WP>::NWIN;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t a = rows.aux[i];
+    if ((a & 0xFFu) != HD_FAST_LIVE) return;
+    const ge* __restrict__ ptab = tab + (size_t)(a >> 8) * FbL<WP>::TAB;
+    const uint32_t* __restrict__ dp = rows.dig + i;
+    uint32_t e = *dp;
+    gej acc;
+    {
+        ge p0 = gtab[e & HD_REF_IDX];
+        if (e & HD_REF_NEG) fe_neg(p0.y, p0.y);
+        fe_norm_weak(p0.y);
+        gej_set_ge(acc, p0);
+    }
+    bool started = !(e & HD_REF_ZERO);
+    if (!started) gej_set_inf(acc);
+    dp += n;
+    e = *dp;
+    ge t = gtab[e & HD_REF_IDX];
+    HD_NOUNROLL for (int j = 1; j < NG; j++) {
+        const ge cur = t;
+        const uint32_t ec = e;
+        dp += n;
+        e = *dp;
+        t = (j + 1 < NG ? gtab : ptab)[e & HD_REF_IDX];
+        sum_step(acc, started, cur, ec);
+    }
+    HD_NOUNROLL for (int j = NG; j < NT; j++) {
+        const ge cur = t;
+        const uint32_t ec = e;
+        if (j + 1 < NT) {
+            dp += n;
+            e = *dp;
+            t = ptab[e & HD_REF_IDX];
+        }
+        sum_step(acc, started, cur, ec);
+    }
+    // infinity, or a degenerate addition on the way (Z = 0): full recovery
+    if (!started || gej_is_inf(acc)) {
+        rows.aux[i] = (a & ~0xFFu) | HD_NEEDS_SLOW;
+        return;
+    }
+    soa_store(rows.xyz, n, i, acc.x.n);
+    soa_store(rows.xyz + 9 * (size_t)n, n, i, acc.y.n);
+    soa_store(rows.xyz + 18 * (size_t)n, n, i, acc.z.n);
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_fast_final(DevBatch b, uint32_t T, SplitRows rows,
+                                                    const int32_t* __restrict__ adm_perm,
+                                                    uint8_t* __restrict__ verdict, uint8_t* __restrict__ rec32,
+                                                    int32_t* __restrict__ signer, uint32_t* __restrict__ slow,
+                                                    uint32_t* __restrict__ n_slow) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const uint32_t n = b.n;
+    const uint32_t* zrow = rows.xyz + 18 * (size_t)n;
+    fe acc;
+    fe_set_u32(acc, 1);
+    uint32_t live = 0;
+    HD_NOUNROLL for (int j = 0; j < K; j++) {
+        const uint32_t i = (uint32_t)j * T + t;
+        if (i >= n) break;
+        if ((rows.aux[i] & 0xFFu) == HD_FAST_LIVE) {
+            fe z;
+            soa_load(z.n, zrow, n, i);
+            fe_mul(acc, acc, z);
+            live |= 1u << j;
+        }
+        soa_store(rows.pre, n, i, acc.n);
+    }
+    fe inv;
+    if (live) fe_inv_divsteps(inv, acc);   // a product of non-zero Z: never 0
+    HD_NOUNROLL for (int j = K - 1; j >= 0; j--) {
+        const uint32_t i = (uint32_t)j * T + t;
+        const bool present = i < n;
+        uint8_t v = HD_NEEDS_SLOW;
+        if (present) {
+            v = (uint8_t)(rows.aux[i] & 0xFFu);
+            if ((live >> j) & 1u) {
+                fe prev, zi, z;
+                if (j > 0) soa_load(prev.n, rows.pre, n, i - T);
+                else fe_set_u32(prev, 1);
+                fe_mul(zi, inv, prev);
+                soa_load(z.n, zrow, n, i);
+                fe_mul(inv, inv, z);
+                gej s;
+                soa_load(s.x.n, rows.xyz, n, i);
+                soa_load(s.y.n, rows.xyz + 9 * (size_t)n, n, i);
+                s.z = z;
+                FastSrc src{b, i, nullptr};
+                uint32_t r_be[8], s_be[8];
+                HD_UNROLL for (int w = 0; w < 8; w++) { r_be[w] = src.sig_r(w); s_be[w] = src.sig_s(w); }
+                const uint32_t sv = src.sig_v();
+                sc r_, s_;
+                fe x;
+                (void)sig_prefix(r_, s_, x, r_be, s_be, sv);   // VALID here: k_fast_scalars passed it
+                v = fast_final(s, zi, x, sv);
+            }
+            if (v != HD_NEEDS_SLOW) {
+                const bool ok = v == V_VALID;
+                verdict[i] = v;
+                if (rec32) {
+                    uint8_t* o = rec32 + 32 * (size_t)i;
+                    const uint8_t* f = b.from32 + 32 * (size_t)i;
+                    HD_UNROLL for (int w = 0; w < 8; w++) store_be32(o + 4 * w, ok ? load_be32(f + 4 * w) : 0u);
+                }
+                if (signer) signer[i] = ok ? adm_perm[rows.idx[i]] : -1;
+            }
+        }
+        const bool to_slow = present && v == HD_NEEDS_SLOW;
+        const unsigned long long bal = __ballot(to_slow);
+        if (bal) {
+            const uint32_t lane = threadIdx.x & 63u;
+            const uint32_t leader = (uint32_t)__ffsll((long long)bal) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(n_slow, (uint32_t)__popcll(bal));
+            base = __shfl(base, (int)leader);
+            if (to_slow) slow[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1))] = i;
+        }
+    }
+}
+
 __global__ void k_fb_bitmap(uint32_t n, const uint8_t* __restrict__ verdict, uint32_t* __restrict__ bitmap) {
     const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
     if (32 * w >= n) return;
@@ -222,36 +509,64 @@ __global__ void k_fb_ready(const uint32_t* __restrict__ list, const uint32_t* __
     for (uint32_t k = threadIdx.x; k < *count; k += blockDim.x) state[list[k]] = HD_FB_READY;
 }
 
+// per-key table geometry of width wp
+size_t fb_tab_entries(int wp) { return wp == HD_FB_WW ? FbL<HD_FB_WW>::TAB : FbL<HD_FB_W>::TAB; }
+int fb_nwin(int wp) { return wp == HD_FB_WW ? FbL<HD_FB_WW>::NWIN : FbL<HD_FB_W>::NWIN; }
+double fb_slot_bytes(int wp) { return (double)sizeof(ge) * (double)(fb_tab_entries(wp) + fb_nwin(wp) + 1) + 8; }
+
+// table bytes held by all contexts of a device (the budget is per device)
+std::mutex g_fb_bytes_mutex;
+std::map<int, size_t> g_fb_bytes;
+void fb_account(hd_ctx* ctx, size_t add, size_t sub) {
+    std::lock_guard<std::mutex> lock(g_fb_bytes_mutex);
+    size_t& d = g_fb_bytes[ctx->device];
+    d = d + add - std::min(d, sub);
+    ctx->fb->bytes = ctx->fb->bytes + add - std::min(ctx->fb->bytes, sub);
+}
+size_t fb_device_bytes(int device) {
+    std::lock_guard<std::mutex> lock(g_fb_bytes_mutex);
+    return g_fb_bytes[device];
+}
+
+void fb_free_tables(hd_ctx* ctx) {
+    FbWork* f = ctx->fb;
+    void* ptrs[] = {f->tab, f->base, f->pub, f->state, f->list};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    f->tab = f->base = f->pub = nullptr;
+    f->state = f->list = nullptr;
+    f->nslots = 0;
+    fb_account(ctx, 0, f->bytes);
+}
+
 int fb_grow_slots(hd_ctx* ctx, uint32_t want) {
     FbWork* f = ctx->fb;
     if (want <= f->nslots) return HD_OK;
     const uint32_t n = std::min(f->max_slots, std::max(want, 2 * f->nslots));
+    const size_t TAB = fb_tab_entries(f->wp), NWIN = (size_t)fb_nwin(f->wp);
     ge *tab = nullptr, *base = nullptr, *pub = nullptr;
     uint32_t *state = nullptr, *list = nullptr;
-    FBCHK(hipMalloc(&tab, sizeof(ge) * HD_FB_TAB * (size_t)n), "fb tables");
-    FBCHK(hipMalloc(&base, sizeof(ge) * HD_FB_NWIN * (size_t)n), "fb bases");
+    FBCHK(hipMalloc(&tab, sizeof(ge) * TAB * (size_t)n), "fb tables");
+    FBCHK(hipMalloc(&base, sizeof(ge) * NWIN * (size_t)n), "fb bases");
     FBCHK(hipMalloc(&pub, sizeof(ge) * (size_t)n), "fb keys");
     FBCHK(hipMalloc(&state, 4 * (size_t)n), "fb state");
     FBCHK(hipMalloc(&list, 4 * (size_t)n), "fb list");
     FBCHK(hipMemset(state, 0, 4 * (size_t)n), "fb state clear");
     if (f->nslots) {
         const size_t k = f->nslots;
-        FBCHK(hipMemcpy(tab, f->tab, sizeof(ge) * HD_FB_TAB * k, hipMemcpyDeviceToDevice), "fb copy");
-        FBCHK(hipMemcpy(base, f->base, sizeof(ge) * HD_FB_NWIN * k, hipMemcpyDeviceToDevice), "fb copy");
+        FBCHK(hipMemcpy(tab, f->tab, sizeof(ge) * TAB * k, hipMemcpyDeviceToDevice), "fb copy");
+        FBCHK(hipMemcpy(base, f->base, sizeof(ge) * NWIN * k, hipMemcpyDeviceToDevice), "fb copy");
         FBCHK(hipMemcpy(pub, f->pub, sizeof(ge) * k, hipMemcpyDeviceToDevice), "fb copy");
         FBCHK(hipMemcpy(state, f->state, 4 * k, hipMemcpyDeviceToDevice), "fb copy");
-        (void)hipFree(f->tab);
-        (void)hipFree(f->base);
-        (void)hipFree(f->pub);
-        (void)hipFree(f->state);
-        (void)hipFree(f->list);
     }
+    fb_free_tables(ctx);
     f->tab = tab;
     f->base = base;
     f->pub = pub;
     f->state = state;
     f->list = list;
     f->nslots = n;
+    fb_account(ctx, (size_t)(fb_slot_bytes(f->wp) * n), 0);
     return HD_OK;
 }
 
@@ -260,8 +575,13 @@ int fb_learn(hd_ctx* ctx, hipStream_t s) {
     FbWork* f = ctx->fb;
     const uint32_t g = (uint32_t)std::max(ctx->n_cu, 1) * 4u;
     k_fb_list<<<1, 256, 0, s>>>(f->nslots, f->state, f->list, f->counts);
-    k_fb_bases<HD_FB_W><<<g, 256, 0, s>>>(f->list, f->counts, f->pub, f->base);
-    k_fb_entries<HD_FB_W><<<g * 2, 256, 0, s>>>(f->list, f->counts, f->base, f->tab);
+    if (f->wp == HD_FB_WW) {
+        k_fb_bases<HD_FB_WW><<<g, 256, 0, s>>>(f->list, f->counts, f->pub, f->base);
+        k_fb_entries<HD_FB_WW><<<g * 2, 256, 0, s>>>(f->list, f->counts, f->base, f->tab);
+    } else {
+        k_fb_bases<HD_FB_W><<<g, 256, 0, s>>>(f->list, f->counts, f->pub, f->base);
+        k_fb_entries<HD_FB_W><<<g * 2, 256, 0, s>>>(f->list, f->counts, f->base, f->tab);
+    }
     k_fb_ready<<<1, 256, 0, s>>>(f->list, f->counts, f->state);
     FBCHK(hipGetLastError(), "fb table kernels");
     return HD_OK;
@@ -315,10 +635,9 @@ int hd_fb_init(hd_ctx* ctx) {
     ctx->fb = new (std::nothrow) FbWork();
     if (!ctx->fb) return HD_ENOMEM;
     FbWork* f = ctx->fb;
-    double budget = 64.0 * (1ull << 30);
-    if (const char* m = getenv("HD_FB_MAX_BYTES")) budget = atof(m);
-    const double per_slot = (double)sizeof(ge) * (HD_FB_TAB + HD_FB_NWIN + 1) + 8;
-    f->max_slots = (uint32_t)std::max(1.0, std::min(1e6, budget / per_slot));
+    f->budget = 64.0 * (1ull << 30);
+    if (const char* m = getenv("HD_FB_MAX_BYTES")) f->budget = atof(m);
+    f->max_slots = (uint32_t)std::max(1.0, std::min(1e6, f->budget / fb_slot_bytes(f->wp)));
     FBCHK(hipMalloc(&f->counts, 8), "fb counts");
     int rc = fb_grow_slots(ctx, 1);
     if (rc) return rc;
@@ -328,15 +647,52 @@ int hd_fb_init(hd_ctx* ctx) {
 void hd_fb_release(hd_ctx* ctx) {
     if (!ctx || !ctx->fb) return;
     FbWork* f = ctx->fb;
-    void* ptrs[] = {f->tab, f->base, f->pub, f->state, f->list, f->counts, f->slow, f->adm_slot};
+    fb_free_tables(ctx);
+    void* ptrs[] = {f->counts, f->slow, f->adm_slot, f->rows};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete f;
     ctx->fb = nullptr;
 }
 
+// messages per lane of the split check (HD_FAST_K: 8, the default, or 16; 0
+// = the paired single-kernel check k_verify_fast)
+static int fast_split_k() {
+    static const int k = [] {
+        const char* e = getenv("HD_FAST_K");
+        const int v = e ? atoi(e) : 8;
+        return v <= 0 ? 0 : v <= 8 ? 8 : 16;
+    }();
+    return k;
+}
+
+// Per-key window width for an admitted set of m: the wide tables
+// (HD_FB_WW, 13 additions for u2 instead of 16, 12x the bytes) when all m keys
+// fit the device's table budget next to what other contexts hold, else the
+// narrow ones.  HD_FB_PW=16|20 forces one; the paired check (HD_FAST_K=0)
+// only has the narrow form.
+static int fb_pick_width(hd_ctx* ctx, uint32_t m) {
+    if (fast_split_k() == 0) return HD_FB_W;
+    if (const char* e = getenv("HD_FB_PW")) return atoi(e) == HD_FB_WW ? HD_FB_WW : HD_FB_W;
+    FbWork* f = ctx->fb;
+    const double others = (double)(fb_device_bytes(ctx->device) - std::min(fb_device_bytes(ctx->device), f->bytes));
+    const double need = fb_slot_bytes(HD_FB_WW) * ((double)m + 1);
+    return need <= f->budget - others ? HD_FB_WW : HD_FB_W;
+}
+
 int hd_fb_map_signatories(hd_ctx* ctx, const uint8_t* sorted, uint32_t m) {
     FbWork* f = ctx->fb;
+    const int wp = fb_pick_width(ctx, m);
+    if (wp != f->wp) {
+        // another table width: every key is learned again (full recovery)
+        FBCHK(hipDeviceSynchronize(), "fb width change sync");
+        fb_free_tables(ctx);
+        f->slot_of.clear();
+        f->free_slots.clear();
+        f->used = 1;
+        f->wp = wp;
+        f->max_slots = (uint32_t)std::max(1.0, std::min(1e6, f->budget / fb_slot_bytes(wp)));
+    }
     std::unordered_map<std::string, uint32_t> keep;
     std::vector<int32_t> adm_slot(std::max(m, 1u), -1);
     std::vector<uint32_t> fresh;
@@ -386,6 +742,30 @@ int hd_fb_clear_keys(hd_ctx* ctx) {
     return HD_OK;
 }
 
+// k_fast_sums occupancy (HD_SUM_WAVES: 2, 3 = the default, or 4)
+template <int WP>
+static void launch_sums(uint32_t blocks, hipStream_t s, uint32_t n, const ge* gtab, const ge* tab,
+                        const SplitRows& rows) {
+    static const int w = getenv("HD_SUM_WAVES") ? atoi(getenv("HD_SUM_WAVES")) : 3;
+    if (w == 2) k_fast_sums<2, WP><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
+    else if (w == 4) k_fast_sums<4, WP><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
+    else k_fast_sums<3, WP><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
+}
+
+template <int K, int WP>
+static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict,
+                         uint8_t* d_rec32, int32_t* d_signer, const SplitRows& rows, hipStream_t s) {
+    FbWork* f = ctx->fb;
+    const uint32_t n = b.n;
+    const uint32_t T = (n + (uint32_t)K - 1) / (uint32_t)K;
+    const uint32_t tb = (T + 255) / 256;
+    k_fast_scalars<K, WP><<<tb, 256, 0, s>>>(b, d_digest, f->state, f->adm_slot, ctx->d_adm, ctx->n_adm,
+                                             ctx->adm_steps, T, rows);
+    launch_sums<WP>((n + 255) / 256, s, n, f->gtab, f->tab, rows);
+    k_fast_final<K><<<tb, 256, 0, s>>>(b, T, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer, f->slow,
+                                       f->counts + 1);
+}
+
 int hd_fb_verify(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict, uint8_t* d_rec32,
                  int32_t* d_signer, uint32_t* d_bitmap, hipStream_t s) {
     FbWork* f = ctx->fb;
@@ -394,6 +774,38 @@ int hd_fb_verify(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_
     const uint32_t blocks = (b.n + 255) / 256;
     const uint32_t fast_blocks = ((b.n + 1) / 2 + 255) / 256;   // two messages per lane
     FBCHK(hipMemsetAsync(f->counts + 1, 0, 4, s), "fb count reset");
+    if (ctx->n_adm > 0 && f->adm_slot && fast_split_k() > 0) {
+        constexpr size_t ROW_WORDS = 54 + FbL<HD_FB_WG>::NWIN + FbL<HD_FB_W>::NWIN;   // the narrow width has more windows
+        rc = hd_dev_grow(ctx, (void**)&f->rows, &f->cap_rows, 4 * ROW_WORDS * (size_t)b.n);
+        if (rc) return rc;
+        const uint32_t n = b.n;
+        SplitRows rows;
+        rows.aux = f->rows;
+        rows.idx = (int32_t*)(f->rows + (size_t)n);
+        rows.u1 = f->rows + 2 * (size_t)n;
+        rows.u2 = f->rows + 10 * (size_t)n;
+        rows.pre = f->rows + 18 * (size_t)n;
+        rows.xyz = f->rows + 27 * (size_t)n;
+        rows.dig = f->rows + 54 * (size_t)n;
+        const bool k16 = fast_split_k() == 16;
+        if (f->wp == HD_FB_WW) {
+            if (k16) launch_split<16, HD_FB_WW>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, rows, s);
+            else launch_split<8, HD_FB_WW>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, rows, s);
+        } else {
+            if (k16) launch_split<16, HD_FB_W>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, rows, s);
+            else launch_split<8, HD_FB_W>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, rows, s);
+        }
+        FBCHK(hipGetLastError(), "split check launch");
+        const SlowCtl ctl{f->slow, f->counts + 1, f->adm_slot, f->state, f->pub};
+        const uint32_t slow_blocks = std::min(blocks, (uint32_t)std::max(ctx->n_cu, 1) * 4u);
+        rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl, slow_blocks, s);
+        if (rc) return rc;
+        if (d_bitmap) {
+            k_fb_bitmap<<<((b.n + 31) / 32 + 255) / 256, 256, 0, s>>>(b.n, d_verdict, d_bitmap);
+            FBCHK(hipGetLastError(), "k_fb_bitmap launch");
+        }
+        return fb_learn(ctx, s);
+    }
     if (ctx->n_adm > 0 && f->adm_slot) {
         static const int fw = getenv("HD_FAST_WAVES") ? atoi(getenv("HD_FAST_WAVES")) : 2;
 #define HD_LAUNCH_FAST(W)                                                                                        \

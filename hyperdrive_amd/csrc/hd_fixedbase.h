@@ -30,8 +30,11 @@ namespace hd {
 #ifndef HD_FB_W
 #define HD_FB_W 16    // per-key tables: 16 windows, 15 x 32768 + 65536 points (40 MB)
 #endif
+#ifndef HD_FB_WW
+#define HD_FB_WW 20   // wide per-key tables: 13 windows, 12 x 2^19 + 2^16 points (490 MB), when the budget holds them
+#endif
 #ifndef HD_FB_WG
-#define HD_FB_WG 20   // the one shared G table: 13 windows, 12 x 2^19 + 2^16 points (458 MB)
+#define HD_FB_WG 24   // the one shared G table: 11 windows, 10 x 2^23 + 2^16 points (6.0 GB)
 #endif
 
 // Windows 0 .. NWIN-2 take signed Booth digits |d| <= 2^(W-1); the top window

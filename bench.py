@@ -32,11 +32,20 @@ sys.path.insert(0, ROOT)
 W_OPS_PER_MSG = 6.06e5          # algorithmic int32 ops per Prevote/Precommit (full recovery)
 # The same cost model (M = one 256-bit modular multiply = 160 int32 ops) for
 # the known-key check R == s^-1 (m G + r P) that VALID messages of known
-# signatories take: 29 mixed additions (8M + 3S each) + s^-1
-# mod n (296 M, as SURVEY's r^-1) + u1, u2 (2 M) + affine conversion (274 M)
-# + one SHA-256 compression (2,200 ops)
+# signatories take, for the geometry the context reports
+# (hd_ctx_fastpath_geometry): one table point per window, the first loaded and
+# the rest mixed additions (8M + 3S each); s^-1 mod n (296 M, as SURVEY's
+# r^-1) and Z^-1 mod p (274 M) once per `per_inv` messages; Montgomery's trick
+# (3 M per message and kind), u1 and u2 (2 M), the affine comparison (1S + 3M);
+# one SHA-256 compression (2,200 ops).
 M_OPS = 160
-W_FAST_OPS_PER_MSG = (29 * 11 + 296 + 2 + 274) * M_OPS + 2200
+
+
+def fast_ops_per_msg(g_windows, key_windows, per_inv):
+    adds = g_windows + key_windows - 1
+    return (adds * 11 + (296 + 274) / per_inv + 2 * 3 + 2 + 4) * M_OPS + 2200
+
+
 BYTES_PER_MSG = 146 + 33        # HBM in + out per message
 # INT32 VALU peak of one MI355X: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (the
 # FP32-vector issue rate of MI355X_MICROARCH.md, 157.3 TFLOPS / 2 per FMA)
@@ -211,7 +220,9 @@ def main():
         known, fallback = v.fastpath_stats()
         # messages of the last step by path: full recovery for `fallback`,
         # the known-key check for the rest
-        w_msg = ((B - fallback) * W_FAST_OPS_PER_MSG + fallback * W_OPS_PER_MSG) / B
+        geom = v.fastpath_geometry()
+        w_fast = fast_ops_per_msg(*geom)
+        w_msg = ((B - fallback) * w_fast + fallback * W_OPS_PER_MSG) / B
         achieved = B * w_msg / (k_ms * 1e-3)
         out = {
             "metric": "verified consensus msgs/sec (secp256k1) at 1/2/4/8 MI355X; % INT32 VALU peak",
@@ -231,7 +242,8 @@ def main():
                        "parallelism": f"shard-by-index x{world}, RCCL all-gather of valid bitmaps"},
             "roofline": {
                 "bound": "valu",
-                "kernel": "k_verify_fast (known-key check; k_verify on the fallback list)",
+                "kernel": "verify call: k_fast_scalars + k_fast_sums + k_fast_final (known-key check), "
+                          "k_verify on the fallback list",
                 "achieved": achieved / 1e12,
                 "peak": VALU_PEAK_OPS / 1e12,
                 "unit": "TOP/s (int32 lane-ops)",
@@ -240,7 +252,8 @@ def main():
                 "traffic_detail": pmc_traffic(),
                 "kernel_ms": k_ms,
                 "algorithmic_ops_per_msg": w_msg,
-                "ops_model": {"known_key_check": W_FAST_OPS_PER_MSG, "full_recovery": W_OPS_PER_MSG,
+                "ops_model": {"known_key_check": w_fast, "full_recovery": W_OPS_PER_MSG,
+                              "geometry": {"g_windows": geom[0], "key_windows": geom[1], "msgs_per_inversion": geom[2]},
                               "fallback_msgs_last_step": fallback, "known_signatories": known},
                 "hbm_algorithmic_GBs": B * BYTES_PER_MSG / (k_ms * 1e-3) / 1e9,
             },
@@ -411,17 +424,18 @@ def vote_table_bench():
 
 
 def pmc_traffic():
-    """HBM bytes per launch of the dominant kernel (k_verify_fast) from the
-    committed rocprofv3 PMC passes (profiles/round1/pmc_k_verify_fast.json:
-    FETCH_SIZE + WRITE_SIZE, separate passes, KiB -> bytes; FETCH_SIZE doubled
-    per MI355X_MICROARCH.md's gfx950 correction).  The table reads (32 x 72 B
-    per message) dominate; the batch itself is 179 B/message."""
-    path = os.path.join(ROOT, "profiles", "round1", "pmc_k_verify_fast.json")
+    """HBM bytes per verify call of the known-key check from the committed
+    rocprofv3 PMC passes (profiles/round1/pmc_known_key_check.json: FETCH_SIZE +
+    WRITE_SIZE of k_fast_scalars, k_fast_sums and k_fast_final, separate
+    passes, KiB -> bytes; FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950
+    correction).  The table reads (24 x 72 B per message) dominate; the batch
+    itself is 179 B/message and the rows between the kernels ~0.5 kB."""
+    path = os.path.join(ROOT, "profiles", "round1", "pmc_known_key_check.json")
     try:
         with open(path) as fh:
             p = json.load(fh)
         return {"bytes_per_launch_raw": p["hbm_bytes_raw"], "bytes_per_launch_corrected": p["hbm_bytes_corrected"],
-                "source": "profiles/round1/pmc_k_verify_fast.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"}
+                "source": "profiles/round1/pmc_known_key_check.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"}
     except (OSError, KeyError, ValueError):
         return None
 

@@ -859,6 +859,15 @@ int hd_ctx_set_fastpath(hd_ctx* ctx, int enable) {
     return HD_OK;
 }
 
+int hd_ctx_fastpath_geometry(hd_ctx* ctx, int* g_windows, int* key_windows, int* msgs_per_inversion) {
+    if (!ctx) return HD_EINVAL;
+    const int k = fast_split_k();
+    if (g_windows) *g_windows = FbL<HD_FB_WG>::NWIN;
+    if (key_windows) *key_windows = fb_nwin(ctx->fb ? ctx->fb->wp : HD_FB_W);
+    if (msgs_per_inversion) *msgs_per_inversion = k > 0 ? k : 2;
+    return HD_OK;
+}
+
 int hd_ctx_fastpath_stats(hd_ctx* ctx, uint32_t* known_keys, uint32_t* last_fallback) {
     if (!ctx) return HD_EINVAL;
     if (known_keys) *known_keys = 0;

@@ -169,6 +169,14 @@ class Verifier:
                     "hd_ctx_fastpath_stats")
         return int(k.value), int(f.value)
 
+    def fastpath_geometry(self) -> Tuple[int, int, int]:
+        """(G table windows, per-key table windows, messages sharing one
+        inversion) of the known-key check as this context runs it."""
+        g, k, m = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        self._check(self._lib.hd_ctx_fastpath_geometry(self._ctx, ctypes.byref(g), ctypes.byref(k), ctypes.byref(m)),
+                    "hd_ctx_fastpath_geometry")
+        return int(g.value), int(k.value), int(m.value)
+
     def known_keys(self) -> int:
         return self.fastpath_stats()[0]
 

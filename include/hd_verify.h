@@ -105,6 +105,13 @@ int hd_ctx_set_fastpath(hd_ctx* ctx, int enable);
  * last_fallback: messages of the last verify call that took the full
  * recovery (either may be NULL; synchronises the device) */
 int hd_ctx_fastpath_stats(hd_ctx* ctx, uint32_t* known_keys, uint32_t* last_fallback);
+/* Shape of the known-key check as the context runs it now (for cost models):
+ * g_windows / key_windows: fixed-base windows of the G table and of the
+ * per-key tables (one table point each; the first is loaded, the rest are
+ * mixed additions); msgs_per_inversion: messages that share one inversion of
+ * each kind (8 or 16 for the split check, 2 for the paired kernel).
+ * Host-only (no device access); any pointer may be NULL. */
+int hd_ctx_fastpath_geometry(hd_ctx* ctx, int* g_windows, int* key_windows, int* msgs_per_inversion);
 
 /* ---- verification ------------------------------------------------------
  * verdict:     n bytes (HD_VERDICT_*), required.

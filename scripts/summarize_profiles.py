@@ -1,7 +1,7 @@
 """Condense rocprofv3 outputs under gpurun_out/ into profiles/<round>/.
 
 profiles/<round>/kernel_stats.csv   rocprofv3 --kernel-trace --stats summary
-profiles/<round>/pmc_k_verify_fast.json, pmc_k_verify.json
+profiles/<round>/pmc_k_fast_{scalars,sums,final}.json, pmc_known_key_check.json, pmc_k_verify.json
                                     per-launch PMC averages of the known-key check and of
                                     the full recovery, and the
                                     HBM traffic derived per MI355X_MICROARCH.md
@@ -63,9 +63,22 @@ def kernel_pmc(match, outname, skip_first=False):
         out["hbm_bytes_corrected"] = (2 * out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024
     json.dump(out, open(os.path.join(dst, outname), "w"), indent=1)
     print(outname, json.dumps(out, indent=1))
+    return out
 
 
-kernel_pmc("k_verify_fast", "pmc_k_verify_fast.json", skip_first=True)   # the known-key check (dominant)
+# the known-key check: its three kernels, and their sum per verify call
+parts = [kernel_pmc(k, "pmc_%s.json" % k, skip_first=True) for k in ("k_fast_scalars", "k_fast_sums", "k_fast_final")]
+if all(parts) and all("hbm_bytes_raw" in p for p in parts):
+    tot = {"kernels": ["k_fast_scalars", "k_fast_sums", "k_fast_final"],
+           "hbm_bytes_raw": sum(p["hbm_bytes_raw"] for p in parts),
+           "hbm_bytes_corrected": sum(p["hbm_bytes_corrected"] for p in parts)}
+    if all("kernel_stats" in p for p in parts):
+        tot["avg_ns"] = sum(p["kernel_stats"]["avg_ns"] for p in parts)
+    for c in ("SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE"):
+        if all(c in p for p in parts):
+            tot[c] = sum(p[c] for p in parts)
+    json.dump(tot, open(os.path.join(dst, "pmc_known_key_check.json"), "w"), indent=1)
+    print("pmc_known_key_check.json", json.dumps(tot, indent=1))
 kernel_pmc("k_verify<", "pmc_k_verify.json")   # the full recovery (warmup learning pass + empty fallback lists)
 
 # every kernel's per-launch HBM traffic (the aux rows: codec, mq, digest, tally)

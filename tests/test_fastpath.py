@@ -214,3 +214,39 @@ def test_pairwise_check_equals_single(fb, oracle):
             for k, (d, s) in enumerate([(da, sa), (db, sb)]):
                 want = _verify(fb, P, d, s) if ready[k] else NEEDS_SLOW
                 assert out.raw[k] == want, (a, ready, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("width", [16, 20])
+def test_key_table_widths_equal_full_recovery(gpu, monkeypatch, width):
+    """Both per-key table widths (HD_FB_PW: 16-bit windows, 16 additions for
+    u2; 20-bit, 13 additions) give the full recovery's outputs on the
+    adversarial mix, a ragged batch (n not a multiple of the 8 messages per
+    lane of the split check), and after the admitted set is re-mapped at the
+    other width (every key is learned again)."""
+    import torch
+    from hyperdrive_amd.device import generate
+    from hyperdrive_amd.verify import Verifier
+    monkeypatch.setenv("HD_FB_PW", str(width))
+    S, n = 40, 20_011
+    fast = Verifier(0)
+    slow = Verifier(0)
+    slow.set_fastpath(False)
+    ks = fast.gen_keys(S)
+    db, _, _ = generate(fast, 0, n, S, 30, keys=ks, start=777)
+    for v in (fast, slow):
+        v.set_signatories(ks[0])
+    ref = _run(slow, db, n)
+    for _ in range(2):
+        got = _run(fast, db, n)
+        assert all(torch.equal(a, b) for a, b in zip(ref, got))
+    assert fast.known_keys() > 0 and fast.fastpath_stats()[1] <= int((ref[0] != 0).sum())
+    monkeypatch.setenv("HD_FB_PW", str(36 - width))
+    fast.set_signatories(ks[0])
+    assert fast.known_keys() == 0
+    for _ in range(2):
+        got = _run(fast, db, n)
+        assert all(torch.equal(a, b) for a, b in zip(ref, got))
+    assert fast.known_keys() > 0
+    fast.close()
+    slow.close()

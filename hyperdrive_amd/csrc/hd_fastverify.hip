@@ -38,10 +38,10 @@
 using namespace hd;
 
 struct FbWork {
-    const ge* gtab = nullptr;   // the shared G table of the device (fb_g_table)
+    const gp* gtab = nullptr;   // the shared G table of the device (fb_g_table)
     uint32_t nslots = 0;        // allocated slots; slot 0 is unused
     uint32_t max_slots = 0;     // from HD_FB_MAX_BYTES (slot 0 included)
-    ge* tab = nullptr;          // nslots x HD_FB_TAB
+    gp* tab = nullptr;          // nslots x fb_tab_entries(wp) packed points
     ge* base = nullptr;         // nslots x HD_FB_NWIN window bases
     ge* pub = nullptr;          // nslots keys
     uint32_t* state = nullptr;  // nslots HD_FB_* states
@@ -86,7 +86,7 @@ struct FastSrc {
 // kind for the pair).
 template <int WAVES>
 __global__ __launch_bounds__(256, WAVES) void k_verify_fast(DevBatch b, const uint8_t* __restrict__ digest_in,
-                                                     const ge* __restrict__ gtab, const ge* __restrict__ tab, const uint32_t* __restrict__ state,
+                                                     const gp* __restrict__ gtab, const gp* __restrict__ tab, const uint32_t* __restrict__ state,
                                                      const int32_t* __restrict__ adm_slot,
                                                      const uint32_t* __restrict__ adm, const int32_t* __restrict__ adm_perm,
                                                      uint32_t n_adm, int adm_steps, uint8_t* __restrict__ verdict,
@@ -134,8 +134,8 @@ __global__ __launch_bounds__(256, WAVES) void k_verify_fast(DevBatch b, const ui
     }
     uint8_t v[2];
     __shared__ FastPark park[256];
-    verify_fast2(v, in, gtab, tab + (size_t)(slot[0] > 0 ? slot[0] : 0) * HD_FB_TAB,
-                 tab + (size_t)(slot[1] > 0 ? slot[1] : 0) * HD_FB_TAB, &park[threadIdx.x]);
+    verify_fast2(v, in, GpTab{gtab}, GpTab{tab + (size_t)(slot[0] > 0 ? slot[0] : 0) * HD_FB_TAB},
+                 GpTab{tab + (size_t)(slot[1] > 0 ? slot[1] : 0) * HD_FB_TAB}, &park[threadIdx.x]);
     bool to_slow[2];
     HD_UNROLL for (int k = 0; k < 2; k++) {
         const uint32_t i = 2 * t + k;
@@ -327,46 +327,52 @@ HD void sum_step(gej& acc, bool& started, ge cur, uint32_t ec) {
     started = started || nz;
 }
 
-template <int WAVES, int WP>
-__global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const ge* __restrict__ gtab,
-                                                          const ge* __restrict__ tab, SplitRows rows) {
+template <int WAVES, int WP, int PF>
+__global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* __restrict__ gtab,
+                                                          const gp* __restrict__ tab, SplitRows rows) {
     constexpr int NG = FbL<HD_FB_WG>::NWIN, NT = NG + FbL<WP>::NWIN;
+    static_assert(PF == 1 || PF == 2, "prefetch depth");
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t a = rows.aux[i];
     if ((a & 0xFFu) != HD_FAST_LIVE) return;
-    const ge* __restrict__ ptab = tab + (size_t)(a >> 8) * FbL<WP>::TAB;
+    const gp* __restrict__ ptab = tab + (size_t)(a >> 8) * FbL<WP>::TAB;
     const uint32_t* __restrict__ dp = rows.dig + i;
-    uint32_t e = *dp;
+    uint32_t e = dp[0];
     gej acc;
     {
-        ge p0 = gtab[e & HD_REF_IDX];
+        ge p0;
+        gp_unpack(p0, gtab[e & HD_REF_IDX]);
         if (e & HD_REF_NEG) fe_neg(p0.y, p0.y);
         fe_norm_weak(p0.y);
         gej_set_ge(acc, p0);
     }
     bool started = !(e & HD_REF_ZERO);
     if (!started) gej_set_inf(acc);
-    dp += n;
-    e = *dp;
-    ge t = gtab[e & HD_REF_IDX];
-    HD_NOUNROLL for (int j = 1; j < NG; j++) {
-        const ge cur = t;
-        const uint32_t ec = e;
-        dp += n;
-        e = *dp;
-        t = (j + 1 < NG ? gtab : ptab)[e & HD_REF_IDX];
-        sum_step(acc, started, cur, ec);
+    // the next PF windows' points, packed (16 words each) until used
+    uint32_t c1 = dp[n], c2 = 0;
+    gp q1 = gtab[c1 & HD_REF_IDX], q2;
+    if (PF == 2) {
+        c2 = dp[2 * (size_t)n];
+        q2 = (2 < NG ? gtab : ptab)[c2 & HD_REF_IDX];
     }
-    HD_NOUNROLL for (int j = NG; j < NT; j++) {
-        const ge cur = t;
-        const uint32_t ec = e;
-        if (j + 1 < NT) {
-            dp += n;
-            e = *dp;
-            t = ptab[e & HD_REF_IDX];
+    HD_NOUNROLL for (int j = 1; j < NT; j++) {
+        const gp cur = q1;
+        const uint32_t ec = c1;
+        if (PF == 2) {
+            q1 = q2;
+            c1 = c2;
+            if (j + 2 < NT) {
+                c2 = dp[(size_t)(j + 2) * n];
+                q2 = (j + 2 < NG ? gtab : ptab)[c2 & HD_REF_IDX];
+            }
+        } else if (j + 1 < NT) {
+            c1 = dp[(size_t)(j + 1) * n];
+            q1 = (j + 1 < NG ? gtab : ptab)[c1 & HD_REF_IDX];
         }
-        sum_step(acc, started, cur, ec);
+        ge g;
+        gp_unpack(g, cur);
+        sum_step(acc, started, g, ec);
     }
     // infinity, or a degenerate addition on the way (Z = 0): full recovery
     if (!started || gej_is_inf(acc)) {
@@ -490,7 +496,7 @@ __global__ __launch_bounds__(256) void k_fb_bases(const uint32_t* __restrict__ l
 template <int W>
 __global__ __launch_bounds__(256) void k_fb_entries(const uint32_t* __restrict__ list,
                                                     const uint32_t* __restrict__ count, const ge* __restrict__ base,
-                                                    ge* __restrict__ tab) {
+                                                    gp* __restrict__ tab) {
     constexpr uint32_t TAB = FbL<W>::TAB;
     const uint64_t total = (uint64_t)*count * TAB;
     for (uint64_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
@@ -500,7 +506,9 @@ __global__ __launch_bounds__(256) void k_fb_entries(const uint32_t* __restrict__
         fb_entry_pos<W>(e, j, d);
         ge o;
         fb_entry(o, base[(size_t)slot * FbL<W>::NWIN + j], d);
-        tab[(size_t)slot * TAB + e] = o;
+        gp q;
+        gp_pack(q, o);
+        tab[(size_t)slot * TAB + e] = q;
     }
 }
 
@@ -512,7 +520,9 @@ __global__ void k_fb_ready(const uint32_t* __restrict__ list, const uint32_t* __
 // per-key table geometry of width wp
 size_t fb_tab_entries(int wp) { return wp == HD_FB_WW ? FbL<HD_FB_WW>::TAB : FbL<HD_FB_W>::TAB; }
 int fb_nwin(int wp) { return wp == HD_FB_WW ? FbL<HD_FB_WW>::NWIN : FbL<HD_FB_W>::NWIN; }
-double fb_slot_bytes(int wp) { return (double)sizeof(ge) * (double)(fb_tab_entries(wp) + fb_nwin(wp) + 1) + 8; }
+double fb_slot_bytes(int wp) {
+    return (double)sizeof(gp) * (double)fb_tab_entries(wp) + (double)sizeof(ge) * (fb_nwin(wp) + 1) + 8;
+}
 
 // table bytes held by all contexts of a device (the budget is per device)
 std::mutex g_fb_bytes_mutex;
@@ -533,7 +543,8 @@ void fb_free_tables(hd_ctx* ctx) {
     void* ptrs[] = {f->tab, f->base, f->pub, f->state, f->list};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
-    f->tab = f->base = f->pub = nullptr;
+    f->tab = nullptr;
+    f->base = f->pub = nullptr;
     f->state = f->list = nullptr;
     f->nslots = 0;
     fb_account(ctx, 0, f->bytes);
@@ -544,9 +555,10 @@ int fb_grow_slots(hd_ctx* ctx, uint32_t want) {
     if (want <= f->nslots) return HD_OK;
     const uint32_t n = std::min(f->max_slots, std::max(want, 2 * f->nslots));
     const size_t TAB = fb_tab_entries(f->wp), NWIN = (size_t)fb_nwin(f->wp);
-    ge *tab = nullptr, *base = nullptr, *pub = nullptr;
+    gp* tab = nullptr;
+    ge *base = nullptr, *pub = nullptr;
     uint32_t *state = nullptr, *list = nullptr;
-    FBCHK(hipMalloc(&tab, sizeof(ge) * TAB * (size_t)n), "fb tables");
+    FBCHK(hipMalloc(&tab, sizeof(gp) * TAB * (size_t)n), "fb tables");
     FBCHK(hipMalloc(&base, sizeof(ge) * NWIN * (size_t)n), "fb bases");
     FBCHK(hipMalloc(&pub, sizeof(ge) * (size_t)n), "fb keys");
     FBCHK(hipMalloc(&state, 4 * (size_t)n), "fb state");
@@ -554,7 +566,7 @@ int fb_grow_slots(hd_ctx* ctx, uint32_t want) {
     FBCHK(hipMemset(state, 0, 4 * (size_t)n), "fb state clear");
     if (f->nslots) {
         const size_t k = f->nslots;
-        FBCHK(hipMemcpy(tab, f->tab, sizeof(ge) * TAB * k, hipMemcpyDeviceToDevice), "fb copy");
+        FBCHK(hipMemcpy(tab, f->tab, sizeof(gp) * TAB * k, hipMemcpyDeviceToDevice), "fb copy");
         FBCHK(hipMemcpy(base, f->base, sizeof(ge) * NWIN * k, hipMemcpyDeviceToDevice), "fb copy");
         FBCHK(hipMemcpy(pub, f->pub, sizeof(ge) * k, hipMemcpyDeviceToDevice), "fb copy");
         FBCHK(hipMemcpy(state, f->state, 4 * k, hipMemcpyDeviceToDevice), "fb copy");
@@ -592,9 +604,9 @@ int fb_learn(hd_ctx* ctx, hipStream_t s) {
 // The G table (W = HD_FB_WG) is built once per device and process and shared
 // by every context on that device.
 static std::mutex g_fb_g_mutex;
-static std::map<int, ge*> g_fb_g_tables;
+static std::map<int, gp*> g_fb_g_tables;
 
-static int fb_g_table(hd_ctx* ctx, const ge** out) {
+static int fb_g_table(hd_ctx* ctx, const gp** out) {
     std::lock_guard<std::mutex> lock(g_fb_g_mutex);
     auto it = g_fb_g_tables.find(ctx->device);
     if (it != g_fb_g_tables.end()) {
@@ -608,9 +620,10 @@ static int fb_g_table(hd_ctx* ctx, const ge** out) {
                             0xFD17B448u, 0xA6855419u, 0x9C47D08Fu, 0xFB10D4B8u};
     fe_from_be(g.x, GX);
     fe_from_be(g.y, GY);
-    ge *tab = nullptr, *base = nullptr, *pub = nullptr;
+    gp* tab = nullptr;
+    ge *base = nullptr, *pub = nullptr;
     uint32_t* cl = nullptr;  // [0] = list {0}, [1] = count 1
-    FBCHK(hipMalloc(&tab, sizeof(ge) * (size_t)FbL<HD_FB_WG>::TAB), "G table");
+    FBCHK(hipMalloc(&tab, sizeof(gp) * (size_t)FbL<HD_FB_WG>::TAB), "G table");
     FBCHK(hipMalloc(&base, sizeof(ge) * FbL<HD_FB_WG>::NWIN), "G bases");
     FBCHK(hipMalloc(&pub, sizeof(ge)), "G point");
     FBCHK(hipMalloc(&cl, 8), "G list");
@@ -742,14 +755,20 @@ int hd_fb_clear_keys(hd_ctx* ctx) {
     return HD_OK;
 }
 
-// k_fast_sums occupancy (HD_SUM_WAVES: 2, 3 = the default, or 4)
+// k_fast_sums occupancy (HD_SUM_WAVES: 2 or 3, the default) and prefetch
+// depth (HD_SUM_PF: 1, the default, or 2 windows ahead)
 template <int WP>
-static void launch_sums(uint32_t blocks, hipStream_t s, uint32_t n, const ge* gtab, const ge* tab,
+static void launch_sums(uint32_t blocks, hipStream_t s, uint32_t n, const gp* gtab, const gp* tab,
                         const SplitRows& rows) {
     static const int w = getenv("HD_SUM_WAVES") ? atoi(getenv("HD_SUM_WAVES")) : 3;
-    if (w == 2) k_fast_sums<2, WP><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
-    else if (w == 4) k_fast_sums<4, WP><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
-    else k_fast_sums<3, WP><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
+    static const int pf = getenv("HD_SUM_PF") ? atoi(getenv("HD_SUM_PF")) : 1;
+    if (pf == 2) {
+        if (w == 3) k_fast_sums<3, WP, 2><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
+        else k_fast_sums<2, WP, 2><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
+    } else {
+        if (w == 2) k_fast_sums<2, WP, 1><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
+        else k_fast_sums<3, WP, 1><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
+    }
 }
 
 template <int K, int WP>

@@ -60,6 +60,34 @@ struct FbL {
 #define HD_FB_LEARNED 2u   // key known, tables not built yet
 #define HD_FB_READY 3u     // tables built
 
+// A table point as the device stores it: canonical affine coordinates as 8
+// little-endian words each, 64 B aligned -- one 64-B HBM access per random
+// read instead of the two or three a 72-B radix-2^29 entry straddles.  The
+// reader unpacks to radix 2^29 (a few shifts per limb).
+struct alignas(64) gp {
+    uint32_t x[8], y[8];
+};
+HD void gp_pack(gp& o, const ge& a) {   // a canonical (gej_to_ge output)
+    fe_to_le(o.x, a.x);
+    fe_to_le(o.y, a.y);
+}
+HD void gp_unpack(ge& o, const gp& a) {
+    fe_from_le(o.x, a.x);
+    fe_from_le(o.y, a.y);
+}
+// a packed table read as affine points (fb_accumulate / verify_fast2 take any
+// indexable table)
+struct GpTab {
+    const gp* p;
+    HD ge operator[](size_t i) const {
+        const gp v = p[i];
+        ge o;
+        gp_unpack(o, v);
+        return o;
+    }
+    HD GpTab operator+(size_t k) const { return GpTab{p + k}; }
+};
+
 // a + b for a finite Jacobian a and an affine b, with no exceptional cases:
 // the madd of gej_add_ge (8M + 3S, Z3 = 2 Z1 H) without its a = inf and
 // a = +-b branches.  If a = +-b then H = 0 and Z3 = 0, and since every later

@@ -55,8 +55,8 @@ VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=1 << 20, help="messages per GPU")
     ap.add_argument("--signers", type=int, default=100)
     ap.add_argument("--adv", type=int, default=0, help="adversarial percentage (C5)")

@@ -174,13 +174,15 @@ __global__ __launch_bounds__(256, WAVES) void k_verify_fast(DevBatch b, const ui
 
 // ---- the split check: K messages per lane share each inversion ----------
 // k_verify_fast inverts s and Z once per two messages.  The split form runs
-// the same check in three kernels so that one inversion of each kind serves
+// the same check in four kernels so that one inversion of each kind serves
 // K messages of a lane (Montgomery's trick over K), with the per-message
 // state in word-major HBM rows between them (lane t reads word w of message
 // i at w * n + i, coalesced):
-//   k_fast_scalars  K per lane: lookup, digest, early checks; prefix products
-//                   of s, one inversion mod n, then u1 = m/s, u2 = r/s
-//   k_fast_sums     one per lane: u1 G + u2 P (29 mixed additions)
+//   k_fast_prep     one per lane: lookup, digest, early checks; m and r
+//   k_fast_scalars  K per lane: prefix products of s, one inversion mod n,
+//                   then u1 = m/s, u2 = r/s as window digits
+//   k_fast_sums     one per lane: u1 G + u2 P (the first window's point
+//                   loaded, one mixed addition per further window)
 //   k_fast_final    K per lane: prefix products of Z, one inversion mod p,
 //                   the comparison, the outputs and the fallback list
 // Message i of lane t is i = j T + t (j < K, T = ceil(n / K)), so every step
@@ -220,12 +222,64 @@ HD uint32_t fb_ref(int d, int w) {
     return d == 0 ? (base | HD_REF_ZERO) : ((base + ad - 1) | (d < 0 ? HD_REF_NEG : 0u));
 }
 
+// one message per lane (occupancy hides the lookup's dependent loads): type,
+// admitted lookup, key state, digest, the early checks; m and r to the rows
+__global__ __launch_bounds__(256) void k_fast_prep(DevBatch b, const uint8_t* __restrict__ digest_in,
+                                                   const uint32_t* __restrict__ state,
+                                                   const int32_t* __restrict__ adm_slot,
+                                                   const uint32_t* __restrict__ adm, uint32_t n_adm, int adm_steps,
+                                                   SplitRows rows) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = b.n;
+    if (i >= n) return;
+    FastSrc src{b, i, digest_in};
+    const uint32_t type = src.type();
+    uint32_t code = HD_NEEDS_SLOW, slot = 0;
+    int32_t idx = -1;
+    if (type < 1 || type > 3) {
+        code = V_BAD_TYPE;
+    } else {
+        uint32_t from_be[8];
+        HD_UNROLL for (int w = 0; w < 8; w++) from_be[w] = src.from(w);
+        idx = admitted_find(adm, n_adm, adm_steps, from_be);
+        const int32_t sl = idx >= 0 ? adm_slot[idx] : -1;
+        if (sl >= 0 && state[sl] == HD_FB_READY) {
+            slot = (uint32_t)sl;
+            FastIn in;
+            if (digest_in) {
+                HD_UNROLL for (int w = 0; w < 8; w++) in.digest_be[w] = load_be32(digest_in + 32 * (size_t)i + 4 * w);
+            } else {
+                uint32_t value_be[8];
+                HD_UNROLL for (int w = 0; w < 8; w++) value_be[w] = src.value(w);
+                if (type == T_PROPOSE)
+                    sha256_propose(in.digest_be, b.height[i], b.round[i], b.valid_round ? b.valid_round[i] : -1,
+                                   value_be);
+                else
+                    sha256_vote(in.digest_be, b.height[i], b.round[i], value_be);
+            }
+            HD_UNROLL for (int w = 0; w < 8; w++) { in.r_be[w] = src.sig_r(w); in.s_be[w] = src.sig_s(w); }
+            in.v = src.sig_v();
+            in.ready = true;
+            sc r, s, m;
+            fe x;
+            uint8_t o;
+            if (fast_prefix(o, r, s, m, x, in)) {
+                code = HD_FAST_LIVE;
+                soa_store(rows.u1, n, i, m.v);
+                soa_store(rows.u2, n, i, r.v);
+            } else {
+                code = o;
+            }
+        }
+    }
+    rows.aux[i] = slot << 8 | code;
+    rows.idx[i] = idx;
+}
+
+// K per lane: prefix products of s over the lane's live messages, one
+// inversion mod n, then u1 = m / s and u2 = r / s as window digits
 template <int K, int WP>
-__global__ __launch_bounds__(256) void k_fast_scalars(DevBatch b, const uint8_t* __restrict__ digest_in,
-                                                      const uint32_t* __restrict__ state,
-                                                      const int32_t* __restrict__ adm_slot,
-                                                      const uint32_t* __restrict__ adm, uint32_t n_adm,
-                                                      int adm_steps, uint32_t T, SplitRows rows) {
+__global__ __launch_bounds__(256) void k_fast_scalars(DevBatch b, uint32_t T, SplitRows rows) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
     const uint32_t n = b.n;
@@ -235,50 +289,13 @@ __global__ __launch_bounds__(256) void k_fast_scalars(DevBatch b, const uint8_t*
     HD_NOUNROLL for (int j = 0; j < K; j++) {
         const uint32_t i = (uint32_t)j * T + t;
         if (i >= n) break;
-        FastSrc src{b, i, digest_in};
-        const uint32_t type = src.type();
-        uint32_t code = HD_NEEDS_SLOW, slot = 0;
-        int32_t idx = -1;
-        if (type < 1 || type > 3) {
-            code = V_BAD_TYPE;
-        } else {
-            uint32_t from_be[8];
-            HD_UNROLL for (int w = 0; w < 8; w++) from_be[w] = src.from(w);
-            idx = admitted_find(adm, n_adm, adm_steps, from_be);
-            const int32_t sl = idx >= 0 ? adm_slot[idx] : -1;
-            if (sl >= 0 && state[sl] == HD_FB_READY) {
-                slot = (uint32_t)sl;
-                FastIn in;
-                if (digest_in) {
-                    HD_UNROLL for (int w = 0; w < 8; w++) in.digest_be[w] = load_be32(digest_in + 32 * (size_t)i + 4 * w);
-                } else {
-                    uint32_t value_be[8];
-                    HD_UNROLL for (int w = 0; w < 8; w++) value_be[w] = src.value(w);
-                    if (type == T_PROPOSE)
-                        sha256_propose(in.digest_be, b.height[i], b.round[i],
-                                       b.valid_round ? b.valid_round[i] : -1, value_be);
-                    else
-                        sha256_vote(in.digest_be, b.height[i], b.round[i], value_be);
-                }
-                HD_UNROLL for (int w = 0; w < 8; w++) { in.r_be[w] = src.sig_r(w); in.s_be[w] = src.sig_s(w); }
-                in.v = src.sig_v();
-                in.ready = true;
-                sc r, s, m;
-                fe x;
-                uint8_t o;
-                if (fast_prefix(o, r, s, m, x, in)) {
-                    code = HD_FAST_LIVE;
-                    live |= 1u << j;
-                    soa_store(rows.u1, n, i, m.v);
-                    soa_store(rows.u2, n, i, r.v);
-                    sc_mul(acc, acc, s);
-                } else {
-                    code = o;
-                }
-            }
+        if ((rows.aux[i] & 0xFFu) == HD_FAST_LIVE) {
+            FastSrc src{b, i, nullptr};
+            sc s;
+            HD_UNROLL for (int w = 0; w < 8; w++) s.v[w] = src.sig_s(7 - w);
+            sc_mul(acc, acc, s);
+            live |= 1u << j;
         }
-        rows.aux[i] = slot << 8 | code;
-        rows.idx[i] = idx;
         soa_store(rows.pre, n, i, acc.v);
     }
     if (!live) return;
@@ -294,7 +311,7 @@ __global__ __launch_bounds__(256) void k_fast_scalars(DevBatch b, const uint8_t*
             HD_UNROLL for (int w = 0; w < 8; w++) prev.v[w] = w == 0 ? 1u : 0u;
         }
         sc_mul(sinv, inv, prev);
-        FastSrc src{b, i, digest_in};
+        FastSrc src{b, i, nullptr};
         HD_UNROLL for (int w = 0; w < 8; w++) s.v[w] = src.sig_s(7 - w);
         sc_mul(inv, inv, s);
         // u1 = m / s and u2 = r / s leave as their window digits: table
@@ -433,7 +450,7 @@ __global__ __launch_bounds__(256) void k_fast_final(DevBatch b, uint32_t T, Spli
                 const uint32_t sv = src.sig_v();
                 sc r_, s_;
                 fe x;
-                (void)sig_prefix(r_, s_, x, r_be, s_be, sv);   // VALID here: k_fast_scalars passed it
+                (void)sig_prefix(r_, s_, x, r_be, s_be, sv);   // VALID here: k_fast_prep passed it
                 v = fast_final(s, zi, x, sv);
             }
             if (v != HD_NEEDS_SLOW) {
@@ -778,8 +795,9 @@ static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest
     const uint32_t n = b.n;
     const uint32_t T = (n + (uint32_t)K - 1) / (uint32_t)K;
     const uint32_t tb = (T + 255) / 256;
-    k_fast_scalars<K, WP><<<tb, 256, 0, s>>>(b, d_digest, f->state, f->adm_slot, ctx->d_adm, ctx->n_adm,
-                                             ctx->adm_steps, T, rows);
+    k_fast_prep<<<(n + 255) / 256, 256, 0, s>>>(b, d_digest, f->state, f->adm_slot, ctx->d_adm, ctx->n_adm,
+                                                ctx->adm_steps, rows);
+    k_fast_scalars<K, WP><<<tb, 256, 0, s>>>(b, T, rows);
     launch_sums<WP>((n + 255) / 256, s, n, f->gtab, f->tab, rows);
     k_fast_final<K><<<tb, 256, 0, s>>>(b, T, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer, f->slow,
                                        f->counts + 1);

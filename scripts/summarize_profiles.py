@@ -67,9 +67,9 @@ def kernel_pmc(match, outname, skip_first=False):
 
 
 # the known-key check: its three kernels, and their sum per verify call
-parts = [kernel_pmc(k, "pmc_%s.json" % k, skip_first=True) for k in ("k_fast_scalars", "k_fast_sums", "k_fast_final")]
+parts = [kernel_pmc(k, "pmc_%s.json" % k, skip_first=True) for k in ("k_fast_prep", "k_fast_scalars", "k_fast_sums", "k_fast_final")]
 if all(parts) and all("hbm_bytes_raw" in p for p in parts):
-    tot = {"kernels": ["k_fast_scalars", "k_fast_sums", "k_fast_final"],
+    tot = {"kernels": ["k_fast_prep", "k_fast_scalars", "k_fast_sums", "k_fast_final"],
            "hbm_bytes_raw": sum(p["hbm_bytes_raw"] for p in parts),
            "hbm_bytes_corrected": sum(p["hbm_bytes_corrected"] for p in parts)}
     if all("kernel_stats" in p for p in parts):

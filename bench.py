@@ -222,6 +222,8 @@ def main():
         # the known-key check for the rest
         geom = v.fastpath_geometry()
         w_fast = fast_ops_per_msg(*geom)
+        if os.environ.get("HD_VERIFY_FASTPATH", "1") == "0":
+            fallback = B                 # fast path off: every message takes the full recovery
         w_msg = ((B - fallback) * w_fast + fallback * W_OPS_PER_MSG) / B
         achieved = B * w_msg / (k_ms * 1e-3)
         out = {

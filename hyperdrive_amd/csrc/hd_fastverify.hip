@@ -366,13 +366,16 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
     }
     bool started = !(e & HD_REF_ZERO);
     if (!started) gej_set_inf(acc);
-    // the next PF windows' points, packed (16 words each) until used
-    uint32_t c1 = dp[n], c2 = 0;
+    // The next PF windows' points, packed (16 words each) until used; the
+    // digit of the window after those is read one addition earlier still, so
+    // no load waits on another load inside an addition.
+    uint32_t c1 = dp[n], c2 = 0, dn = 0;
     gp q1 = gtab[c1 & HD_REF_IDX], q2;
     if (PF == 2) {
         c2 = dp[2 * (size_t)n];
         q2 = (2 < NG ? gtab : ptab)[c2 & HD_REF_IDX];
     }
+    if (PF + 1 < NT) dn = dp[(size_t)(PF + 1) * n];
     HD_NOUNROLL for (int j = 1; j < NT; j++) {
         const gp cur = q1;
         const uint32_t ec = c1;
@@ -380,13 +383,14 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
             q1 = q2;
             c1 = c2;
             if (j + 2 < NT) {
-                c2 = dp[(size_t)(j + 2) * n];
+                c2 = dn;
                 q2 = (j + 2 < NG ? gtab : ptab)[c2 & HD_REF_IDX];
             }
         } else if (j + 1 < NT) {
-            c1 = dp[(size_t)(j + 1) * n];
+            c1 = dn;
             q1 = (j + 1 < NG ? gtab : ptab)[c1 & HD_REF_IDX];
         }
+        if (j + PF + 1 < NT) dn = dp[(size_t)(j + PF + 1) * n];
         ge g;
         gp_unpack(g, cur);
         sum_step(acc, started, g, ec);

@@ -79,13 +79,13 @@ HD void gp_unpack(ge& o, const gp& a) {
 // indexable table)
 struct GpTab {
     const gp* p;
-    HD ge operator[](size_t i) const {
+    HD_MEMBER ge operator[](size_t i) const {
         const gp v = p[i];
         ge o;
         gp_unpack(o, v);
         return o;
     }
-    HD GpTab operator+(size_t k) const { return GpTab{p + k}; }
+    HD_MEMBER GpTab operator+(size_t k) const { return GpTab{p + k}; }
 };
 
 // a + b for a finite Jacobian a and an affine b, with no exceptional cases:

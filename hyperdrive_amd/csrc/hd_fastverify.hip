@@ -689,13 +689,13 @@ void hd_fb_release(hd_ctx* ctx) {
     ctx->fb = nullptr;
 }
 
-// messages per lane of the split check (HD_FAST_K: 8, the default, or 16; 0
-// = the paired single-kernel check k_verify_fast)
+// messages per lane of the split check (HD_FAST_K: 4, 8, the default, or 16;
+// 0 = the paired single-kernel check k_verify_fast)
 static int fast_split_k() {
     static const int k = [] {
         const char* e = getenv("HD_FAST_K");
         const int v = e ? atoi(e) : 8;
-        return v <= 0 ? 0 : v <= 8 ? 8 : 16;
+        return v <= 0 ? 0 : v <= 4 ? 4 : v <= 8 ? 8 : 16;
     }();
     return k;
 }
@@ -828,12 +828,14 @@ int hd_fb_verify(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_
         rows.pre = f->rows + 18 * (size_t)n;
         rows.xyz = f->rows + 27 * (size_t)n;
         rows.dig = f->rows + 54 * (size_t)n;
-        const bool k16 = fast_split_k() == 16;
+        const int k = fast_split_k();
         if (f->wp == HD_FB_WW) {
-            if (k16) launch_split<16, HD_FB_WW>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, rows, s);
+            if (k == 16) launch_split<16, HD_FB_WW>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, rows, s);
+            else if (k == 4) launch_split<4, HD_FB_WW>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, rows, s);
             else launch_split<8, HD_FB_WW>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, rows, s);
         } else {
-            if (k16) launch_split<16, HD_FB_W>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, rows, s);
+            if (k == 16) launch_split<16, HD_FB_W>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, rows, s);
+            else if (k == 4) launch_split<4, HD_FB_W>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, rows, s);
             else launch_split<8, HD_FB_W>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, rows, s);
         }
         FBCHK(hipGetLastError(), "split check launch");

@@ -126,11 +126,14 @@ def main():
                     db.sig.data_ptr() + 65 * lo)
     full = db.c_struct()
     assert B % 32 == 0
-    # double-buffered outputs: the tally of step k (its own stream) overlaps
-    # the verification of step k+1; every step's verify and tally complete
-    # inside the timed region
-    verdicts = [torch.empty(B, dtype=torch.uint8, device=dev) for _ in range(2)]
-    bitmaps = [torch.zeros(B // 32, dtype=torch.int32, device=dev) for _ in range(2)]
+    # triple-buffered outputs: the tally of step k (its own stream; the call
+    # returns once its host outputs are complete) runs while the verifications
+    # of steps k+1 and k+2 are queued, so a slow host sync never drains the
+    # verify queue; every step's verify and tally complete inside the timed
+    # region
+    NBUF = 3
+    verdicts = [torch.empty(B, dtype=torch.uint8, device=dev) for _ in range(NBUF)]
+    bitmaps = [torch.zeros(B // 32, dtype=torch.int32, device=dev) for _ in range(NBUF)]
     lib = _lib.load()
     t_out, t_arr = v._tally_struct(total)
     ts = torch.cuda.Stream(device=dev)
@@ -139,7 +142,7 @@ def main():
     tally_info = {}
 
     def verify(k, record=False):
-        buf = k % 2
+        buf = k % NBUF
         if record:
             ev_k[k][0].record(ws)
         v.verify_batch_device(shard, verdicts[buf].data_ptr(), None, None, bitmaps[buf].data_ptr(), stream)
@@ -166,12 +169,15 @@ def main():
         tally_info["n_counts"] = t_out.n_counts
 
     def run(steps, record):
-        pending = None
+        # buffer k % NBUF is rewritten by verify(k + NBUF), queued only after
+        # tally(k) has returned (hd_tally_device_bitmap synchronises its stream)
+        pending = []
         for k in range(steps):
-            nxt = verify(k, record)
-            tally(pending)
-            pending = nxt
-        tally(pending)
+            pending.append(verify(k, record))
+            if len(pending) == NBUF:
+                tally(pending.pop(0))
+        while pending:
+            tally(pending.pop(0))
 
     # context setup, outside the timed region (like the generator tables): one
     # verification of this rank's shard teaches the context the keys of the

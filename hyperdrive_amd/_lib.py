@@ -116,10 +116,12 @@ SIGNATURES = {
     "hd_mq_insert_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                            ctypes.c_void_p]),
     "hd_mq_insert_verified_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
-                                                    ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
+                                                    ctypes.c_int64, ctypes.c_void_p]),
     "hd_mq_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
-    "hd_mq_consume": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(HdBatchOut), ctypes.c_void_p,
-                                     ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
+    "hd_mq_senders": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
+    "hd_mq_consume": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_uint32,
+                                     ctypes.POINTER(HdBatchOut), ctypes.c_void_p, ctypes.c_uint32,
+                                     ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
     "hd_mq_drop_below": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     # include/hd_digest.h
     "hd_digest_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(HdBatch),
@@ -162,6 +164,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             "`python -m hyperdrive_amd.build` (there is no CPU fallback)")
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
+        if "HD_LIB" in os.environ and not hasattr(lib, name):
+            continue   # an older build named by HD_LIB (A/B runs): only what it exports
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -26,7 +26,8 @@ ARCH = os.environ.get("HD_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 
 CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-          "-I" + INCLUDE] + ["-D%s=%s" % (k, os.environ[k]) for k in ("HD_FB_W", "HD_FB_WG") if os.environ.get(k)]
+          "-I" + INCLUDE] + ["-D%s=%s" % (k, os.environ[k]) for k in ("HD_FB_W", "HD_FB_WG") if os.environ.get(k)] \
+    + os.environ.get("HD_EXTRA_CFLAGS", "").split()   # A/B builds (e.g. into HD_BUILD_LIB under _lib/var/)
 
 
 def _sources():

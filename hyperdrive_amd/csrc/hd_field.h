@@ -37,26 +37,43 @@ struct sc { uint32_t v[8]; };  // mod n
 #define HD_C3 0x45512319u
 
 // ------------------------------------------------------------ 256-bit core
+// 96-bit column accumulator (acc, hi) += a * b.  On the device this is one
+// v_mad_u64_u32 whose carry-out lands in VCC plus one v_addc_co_u32 that adds
+// it to the third word: the C formulation (a 64-bit product plus two 32-bit
+// addends) compiles to a mad, a 64-bit add and register moves to build
+// {x, 0} operand pairs, about twice the cycles per product.
+HD void macc96(uint64_t& acc, uint32_t& hi, uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(HD_NO_MACC_ASM)
+    asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+        : "+v"(acc), "+v"(hi)
+        : "v"(a), "v"(b)
+        : "vcc");
+#else
+    const uint64_t p = (uint64_t)a * b;
+    const uint64_t s = acc + p;
+    hi += s < p ? 1u : 0u;
+    acc = s;
+#endif
+}
+// next column: (acc, hi) >>= 32
+HD void col96_shift(uint64_t& acc, uint32_t& hi) {
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+}
+
+// t = a b, product scanning (one 96-bit accumulator per column)
 HD void mul_256(uint32_t t[16], const uint32_t a[8], const uint32_t b[8]) {
-    // row 0
-    {
-        uint64_t c = 0;
-        HD_UNROLL for (int j = 0; j < 8; j++) {
-            uint64_t p = (uint64_t)a[0] * b[j] + c;
-            t[j] = (uint32_t)p;
-            c = p >> 32;
+    uint64_t acc = 0;
+    uint32_t hi = 0;
+    HD_UNROLL for (int k = 0; k < 15; k++) {
+        HD_UNROLL for (int i = 0; i < 8; i++) {
+            const int j = k - i;
+            if (j >= 0 && j < 8) macc96(acc, hi, a[i], b[j]);
         }
-        t[8] = (uint32_t)c;
+        t[k] = (uint32_t)acc;
+        col96_shift(acc, hi);
     }
-    HD_UNROLL for (int i = 1; i < 8; i++) {
-        uint64_t c = 0;
-        HD_UNROLL for (int j = 0; j < 8; j++) {
-            uint64_t p = (uint64_t)a[i] * b[j] + t[i + j] + c;
-            t[i + j] = (uint32_t)p;
-            c = p >> 32;
-        }
-        t[i + 8] = (uint32_t)c;
-    }
+    t[15] = (uint32_t)acc;
 }
 
 HD void sqr_256(uint32_t t[16], const uint32_t a[8]) {
@@ -569,21 +586,21 @@ HD void sc_from_be_reduce(sc& r, const uint32_t w[8]) {
 }
 
 // P[0 .. na+4] = a[0..na-1] * c  (c = 2^256 - n: 4 limbs + implicit c4 = 1)
+// (product scanning; the c4 = 1 term is a multiply by 1 into the same column)
 template <int NA>
 HD void mul_by_c(uint32_t* P, const uint32_t* a) {
-    const uint32_t C[4] = {HD_C0, HD_C1, HD_C2, HD_C3};
-    HD_UNROLL for (int k = 0; k < 5; k++) P[k] = 0;
-    HD_UNROLL for (int i = 0; i < NA; i++) {
-        uint64_t cy = 0;
-        HD_UNROLL for (int j = 0; j < 4; j++) {
-            uint64_t p = (uint64_t)a[i] * C[j] + P[i + j] + cy;
-            P[i + j] = (uint32_t)p;
-            cy = p >> 32;
+    const uint32_t C[5] = {HD_C0, HD_C1, HD_C2, HD_C3, 1u};
+    uint64_t acc = 0;
+    uint32_t hi = 0;
+    HD_UNROLL for (int k = 0; k < NA + 4; k++) {
+        HD_UNROLL for (int j = 0; j < 5; j++) {
+            const int i = k - j;
+            if (i >= 0 && i < NA) macc96(acc, hi, a[i], C[j]);
         }
-        uint64_t p = (uint64_t)a[i] + P[i + 4] + cy;  // c4 = 1
-        P[i + 4] = (uint32_t)p;
-        P[i + 5] = (uint32_t)(p >> 32);
+        P[k] = (uint32_t)acc;
+        col96_shift(acc, hi);
     }
+    P[NA + 4] = (uint32_t)acc;
 }
 
 // r = t mod n for a 512-bit t (three folds with c, libsecp256k1

@@ -1,20 +1,33 @@
 // hd_mq.hip -- bulk MessageQueue (include/hd_mq.h; mq/mq.go:19-143).
 //
-// The queue is one SoA pool of messages kept sorted by (sender, height,
-// round, arrival).  A batch insert appends the batch's messages after the
-// pool (so arrival order == position for equal keys), re-sorts with stable
-// LSD radix passes over (round, height, sender) -- keys rebased to the batch's
-// min and cut to their significant bits, so a typical insert costs a handful
-// of 8-bit digit passes -- and keeps each sender's first max_capacity
+// Senders.  mq.go keys its queues by the message's From (a 32-byte
+// id.Signatory, mq.go:107-113).  The queue interns every From it sees into a
+// dense sender id, assigned in order of first insertion and never reused: a
+// device hash table (id per slot, keys compared against the interned 32-byte
+// Froms) plus the array of interned Froms.  A batch looks its Froms up
+// read-only; the Froms it introduces are deduplicated in a batch-local table
+// (the slot's claim word keeps the lowest batch position, compared against
+// the batch's own bytes), numbered in batch order and inserted into the hash
+// table with one CAS each (they are distinct and new, so no comparison is
+// needed there).
+//
+// Messages.  The queue is one SoA pool of messages kept sorted by (sender id,
+// height, round, arrival).  A batch insert appends the batch's messages after
+// the pool (so arrival order == position for equal keys), re-sorts with
+// stable LSD radix passes over (round, height, sender) -- keys rebased to the
+// batch's min and cut to their significant bits, so a typical insert costs a
+// handful of 8-bit digit passes -- and keeps each sender's first max_capacity
 // elements: exactly the result of inserting one message at a time with
 // mq.go:133-142's truncation.  Consume(h) and DropMessagesBelowHeight(h) are
 // order-preserving partitions (each sender's consumed messages are a prefix of
-// its run, mq.go:38-41).
+// its run, mq.go:38-41); Consume delivers only senders in procsAllowed
+// (mq.go:49-51), evaluated against the set given at that call.
 #include <hip/hip_runtime.h>
 
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <new>
 
 #include "../../include/hd_mq.h"
@@ -23,6 +36,8 @@
 using namespace hd;
 
 namespace {
+
+static const uint32_t kEmpty = 0xFFFFFFFFu;
 
 struct Pool {
     uint32_t n = 0, cap = 0;
@@ -62,51 +77,190 @@ int pool_reserve(hd_ctx* ctx, Pool& p, uint32_t need) {
     return HD_OK;
 }
 
+// ---------------------------------------------------------------- senders
+// The interned Froms (8 little-endian words each, the bytes as given) and
+// the hash table of their ids.
+struct Dict {
+    const uint32_t* keys;
+    const uint32_t* slots;
+    uint32_t mask;
+    uint64_t seed;
+};
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 30;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27;
+    x *= 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    return x;
+}
+// From is a SHA-256 output, but the seed (per queue) keeps crafted signatories
+// from lining up in one probe chain
+__device__ __forceinline__ uint32_t key_hash(const uint4& a, const uint4& b, uint64_t seed) {
+    const uint64_t x = ((uint64_t)a.y << 32 | a.x) ^ mix64(((uint64_t)a.w << 32 | a.z) ^ seed) ^
+                       ((uint64_t)b.y << 32 | b.x) * 0x9E3779B97F4A7C15ull ^ ((uint64_t)b.w << 32 | b.z);
+    return (uint32_t)mix64(x ^ seed);
+}
+__device__ __forceinline__ bool key_eq(const uint4& a, const uint4& b, const uint32_t* k) {
+    const uint4 c = reinterpret_cast<const uint4*>(k)[0], d = reinterpret_cast<const uint4*>(k)[1];
+    return ((a.x ^ c.x) | (a.y ^ c.y) | (a.z ^ c.z) | (a.w ^ c.w) | (b.x ^ d.x) | (b.y ^ d.y) | (b.z ^ d.z) |
+            (b.w ^ d.w)) == 0;
+}
+__device__ __forceinline__ void load_key(const uint8_t* p, uint4& a, uint4& b) {
+    a = reinterpret_cast<const uint4*>(p)[0];
+    b = reinterpret_cast<const uint4*>(p)[1];
+}
+// id of an interned From, or kEmpty
+__device__ __forceinline__ uint32_t dict_find(const Dict& d, const uint4& a, const uint4& b) {
+    uint32_t s = key_hash(a, b, d.seed) & d.mask;
+    while (true) {
+        const uint32_t id = d.slots[s];
+        if (id == kEmpty || key_eq(a, b, d.keys + 8 * (size_t)id)) return id;
+        s = (s + 1) & d.mask;
+    }
+}
+// put a From known to be absent into the table (the keys are distinct)
+__device__ __forceinline__ void dict_put(uint32_t* slots, uint32_t mask, uint64_t seed, const uint4& a, const uint4& b,
+                                         uint32_t id) {
+    uint32_t s = key_hash(a, b, seed) & mask;
+    while (atomicCAS(&slots[s], kEmpty, id) != kEmpty) s = (s + 1) & mask;
+}
+
+// insert flag of a verified message: authenticated (recovered == From: VALID
+// or NOT_ADMITTED) and filterHeight (replica.go:247-249)
+__global__ void k_mq_ingress(uint32_t n, const uint8_t* __restrict__ verdict, const int64_t* __restrict__ height,
+                             int64_t min_height, uint8_t* __restrict__ flag) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const uint8_t v = verdict[i];
+        flag[i] = (v == HD_VERDICT_VALID || v == HD_VERDICT_NOT_ADMITTED) && height[i] >= min_height;
+    }
+}
+__global__ void k_mq_flag_nz(uint32_t n, const uint8_t* __restrict__ in, uint8_t* __restrict__ flag) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flag[i] = in ? in[i] != 0 : 1;
+}
+
+// Sender of each insertable message (position e of newidx): an interned id,
+// or -- for a From the queue has not seen -- a slot of the batch-local table
+// whose claim word ends as the lowest position with that From.
+__global__ void k_mq_lookup(uint32_t m, const uint32_t* __restrict__ newidx, const uint8_t* __restrict__ from32,
+                            Dict d, uint32_t* __restrict__ lclaim, uint32_t lmask, uint32_t* __restrict__ sid,
+                            uint32_t* __restrict__ lslot) {
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m) return;
+    uint4 a, b;
+    load_key(from32 + 32 * (size_t)newidx[e], a, b);
+    const uint32_t id = dict_find(d, a, b);
+    sid[e] = id;
+    if (id != kEmpty) {
+        lslot[e] = kEmpty;
+        return;
+    }
+    uint32_t s = key_hash(a, b, d.seed ^ 0x5A5A5A5Aull) & lmask;
+    while (true) {
+        uint32_t c = lclaim[s];
+        if (c == kEmpty) {
+            c = atomicCAS(&lclaim[s], kEmpty, e);
+            if (c == kEmpty) break;
+        }
+        uint4 x, y;
+        load_key(from32 + 32 * (size_t)newidx[c], x, y);
+        if (((a.x ^ x.x) | (a.y ^ x.y) | (a.z ^ x.z) | (a.w ^ x.w) | (b.x ^ y.x) | (b.y ^ y.y) | (b.z ^ y.z) |
+             (b.w ^ y.w)) == 0) {
+            if (e < c) atomicMin(&lclaim[s], e);
+            break;
+        }
+        s = (s + 1) & lmask;
+    }
+    lslot[e] = s;
+}
+// first occurrence of a new From in the batch
+__global__ void k_mq_newflag(uint32_t m, const uint32_t* __restrict__ lslot, const uint32_t* __restrict__ lclaim,
+                             uint8_t* __restrict__ flag) {
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < m) flag[e] = lslot[e] != kEmpty && lclaim[lslot[e]] == e;
+}
+// new sender k (batch order) gets id base + k
+__global__ void k_mq_assign(uint32_t r, const uint32_t* __restrict__ reps, const uint32_t* __restrict__ newidx,
+                            const uint8_t* __restrict__ from32, uint32_t base, uint32_t* __restrict__ keys,
+                            uint32_t* __restrict__ slots, uint32_t mask, uint64_t seed,
+                            const uint32_t* __restrict__ lslot, uint32_t* __restrict__ lid) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= r) return;
+    const uint32_t e = reps[k], id = base + k;
+    uint4 a, b;
+    load_key(from32 + 32 * (size_t)newidx[e], a, b);
+    reinterpret_cast<uint4*>(keys + 8 * (size_t)id)[0] = a;
+    reinterpret_cast<uint4*>(keys + 8 * (size_t)id)[1] = b;
+    dict_put(slots, mask, seed, a, b, id);
+    lid[lslot[e]] = id;
+}
+__global__ void k_mq_sid(uint32_t m, const uint32_t* __restrict__ lslot, const uint32_t* __restrict__ lid,
+                         uint32_t* __restrict__ sid) {
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < m && lslot[e] != kEmpty) sid[e] = lid[lslot[e]];
+}
+// rebuild the hash table at a new capacity from the interned keys
+__global__ void k_mq_rehash(uint32_t n, const uint32_t* __restrict__ keys, uint32_t* __restrict__ slots, uint32_t mask,
+                            uint64_t seed) {
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= n) return;
+    const uint4 a = reinterpret_cast<const uint4*>(keys + 8 * (size_t)id)[0];
+    const uint4 b = reinterpret_cast<const uint4*>(keys + 8 * (size_t)id)[1];
+    dict_put(slots, mask, seed, a, b, id);
+}
+// procsAllowed -> allow[id] for the interned senders.  The list is raw
+// 32-byte signatories, or (be_words) the ctx's admitted table of 8 big-endian
+// words per signatory.
+__global__ void k_mq_allow(uint32_t na, const uint32_t* __restrict__ list, int be_words, Dict d,
+                           uint8_t* __restrict__ allow) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= na) return;
+    uint32_t w[8];
+    for (int j = 0; j < 8; j++) {
+        const uint32_t x = list[8 * (size_t)k + j];
+        w[j] = be_words ? __builtin_bswap32(x) : x;
+    }
+    const uint4 a = make_uint4(w[0], w[1], w[2], w[3]), b = make_uint4(w[4], w[5], w[6], w[7]);
+    const uint32_t id = dict_find(d, a, b);
+    if (id != kEmpty) allow[id] = 1;
+}
+
 // element e of the merged sequence: e < M -> pool[e]; else batch[newidx[e - M]]
+// with sender nsid[e - M]
 struct MqSrc {
     Pool p;
     DevBatch b;
     const uint32_t* newidx;
-    const int32_t* bsender;
+    const uint32_t* nsid;
     uint32_t M;
 };
 
-__device__ __forceinline__ void src_keys(const MqSrc& s, uint32_t e, int32_t& snd, int64_t& h, int64_t& r) {
+__device__ __forceinline__ void src_keys(const MqSrc& s, uint32_t e, uint32_t& snd, int64_t& h, int64_t& r) {
     if (e < s.M) {
-        snd = s.p.sender[e];
+        snd = (uint32_t)s.p.sender[e];
         h = s.p.h[e];
         r = s.p.r[e];
     } else {
         const uint32_t i = s.newidx[e - s.M];
-        snd = s.bsender[i];
+        snd = s.nsid[e - s.M];
         h = s.b.height[i];
         r = s.b.round[i];
     }
-}
-
-__global__ void k_mq_flag_new(uint32_t n, const int32_t* __restrict__ sender, uint8_t* __restrict__ flag) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) flag[i] = sender[i] >= 0;
-}
-
-// Replica.Run ingress (replica.go:117-131): a verified message enters the
-// queue iff VALID and filterHeight passes (height >= current, replica.go:247-249)
-__global__ void k_mq_ingress(uint32_t n, const uint8_t* __restrict__ verdict, const int32_t* __restrict__ signer,
-                             const int64_t* __restrict__ height, int64_t min_height, int32_t* __restrict__ snd) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) snd[i] = (verdict[i] == HD_VERDICT_VALID && height[i] >= min_height) ? signer[i] : -1;
 }
 
 __global__ void k_mq_keys(MqSrc s, uint32_t T, int64_t* __restrict__ hk, int64_t* __restrict__ rk,
                           uint32_t* __restrict__ sk, uint32_t* __restrict__ iota) {
     const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= T) return;
-    int32_t snd;
+    uint32_t snd;
     int64_t h, r;
     src_keys(s, e, snd, h, r);
     hk[e] = h;
     rk[e] = r;
-    sk[e] = (uint32_t)snd;
+    sk[e] = snd;
     iota[e] = e;
 }
 
@@ -152,7 +306,7 @@ __global__ void k_mq_gather(MqSrc s, uint32_t n, const uint32_t* __restrict__ se
         for (int w = 0; w < 65; w++) d.sig[65 * (size_t)k + w] = s.p.sig[65 * (size_t)e + w];
     } else {
         const uint32_t i = s.newidx[e - s.M];
-        d.sender[k] = s.bsender[i];
+        d.sender[k] = (int32_t)s.nsid[e - s.M];
         d.type[k] = s.b.type[i];
         d.h[k] = s.b.height[i];
         d.r[k] = s.b.round[i];
@@ -171,14 +325,17 @@ __global__ void k_mq_compose(uint32_t n, const uint32_t* __restrict__ perm, cons
     if (k < n) ids[k] = perm[sel[k]];
 }
 
-// partition predicate over the pool: flag[e] = pool.h[e] <= h (consume) or
-// pool.h[e] < h (drop); inv = the complement
-__global__ void k_mq_pred(uint32_t n, const int64_t* __restrict__ ph, int64_t h, int strict, uint8_t* __restrict__ flag,
-                          uint8_t* __restrict__ inv) {
+// partition predicates over the pool.  Consume (strict = 0): removed = height
+// <= h, delivered = removed and the sender allowed (allow may be NULL: all);
+// drop (strict = 1): removed = height < h.  inv = kept.
+__global__ void k_mq_pred(uint32_t n, const int64_t* __restrict__ ph, const int32_t* __restrict__ psnd, int64_t h,
+                          int strict, const uint8_t* __restrict__ allow, uint8_t* __restrict__ removed,
+                          uint8_t* __restrict__ deliver, uint8_t* __restrict__ inv) {
     const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n) return;
     const bool f = strict ? ph[e] < h : ph[e] <= h;
-    flag[e] = f;
+    removed[e] = f;
+    if (deliver) deliver[e] = f && (!allow || allow[psnd[e]]);
     inv[e] = !f;
 }
 
@@ -193,13 +350,21 @@ int bits_of(uint64_t range) {
 }  // namespace
 
 enum MqSlot { MQ_FLAG, MQ_NEWIDX, MQ_NSEL, MQ_HK, MQ_RK, MQ_SK, MQ_PERM0, MQ_PERM1, MQ_K64A, MQ_K64B, MQ_K32A, MQ_K32B,
-              MQ_HEAD, MQ_KEEP, MQ_SEL, MQ_RED, MQ_TMP, MQ_SND, MQ__N };
+              MQ_HEAD, MQ_KEEP, MQ_SEL, MQ_RED, MQ_TMP, MQ_SID, MQ_LSLOT, MQ_LCLAIM, MQ_LID, MQ_REPS, MQ_ALLOW,
+              MQ_LIST, MQ_DELIV, MQ_SEL2, MQ__N };
 
 struct hd_mq {
     hd_ctx* ctx = nullptr;
     uint32_t max_cap = 1000;
     Pool pool, spare;
     DevBuf buf[MQ__N];
+    // sender dictionary
+    uint32_t nsend = 0;
+    uint32_t* keys = nullptr;   // kcap x 8 words
+    size_t kcap_bytes = 0;
+    uint32_t* slots = nullptr;  // tcap ids
+    uint32_t tcap = 0;
+    uint64_t seed = 0;
 };
 
 #define QCHK(expr, what)                                           \
@@ -217,6 +382,8 @@ static void* qbuf(hd_mq* q, int slot, size_t bytes, int* rc) {
     }
     return b.p;
 }
+
+static Dict dict_of(const hd_mq* q) { return Dict{q->keys, q->slots, q->tcap - 1, q->seed}; }
 
 template <typename T>
 static int dev_minmax(hd_mq* q, const T* d, uint32_t n, T* mn, T* mx, hipStream_t s) {
@@ -313,59 +480,93 @@ static int pool_filter(hd_mq* q, const uint8_t* keep, hipStream_t s) {
     return HD_OK;
 }
 
-extern "C" {
-
-int hd_mq_create(hd_ctx* ctx, uint32_t max_capacity, hd_mq** out) {
-    if (!ctx || !out || max_capacity == 0) return HD_EINVAL;
-    hd_mq* q = new (std::nothrow) hd_mq();
-    if (!q) return HD_ENOMEM;
-    q->ctx = ctx;
-    q->max_cap = max_capacity;
-    *out = q;
+// the hash table holds at least 2 (nsend + more) slots (load <= 1/2)
+static int dict_reserve(hd_mq* q, uint32_t more, hipStream_t s) {
+    const uint64_t want = 2 * ((uint64_t)q->nsend + more);
+    if (want > (1ull << 31)) return HD_EINVAL;
+    if (q->tcap >= want && q->slots) return HD_OK;
+    uint32_t cap = std::max<uint32_t>(q->tcap, 1024u);
+    while (cap < want) cap <<= 1;
+    uint32_t* slots = nullptr;
+    QCHK(hipMalloc(&slots, 4 * (size_t)cap), "hipMalloc mq senders");
+    QCHK(hipMemsetAsync(slots, 0xFF, 4 * (size_t)cap, s), "clear mq senders");
+    if (q->nsend) k_mq_rehash<<<nblk(q->nsend), 256, 0, s>>>(q->nsend, q->keys, slots, cap - 1, q->seed);
+    QCHK(hipGetLastError(), "mq rehash");
+    QCHK(hipStreamSynchronize(s), "mq rehash sync");
+    if (q->slots) (void)hipFree(q->slots);
+    q->slots = slots;
+    q->tcap = cap;
     return HD_OK;
 }
 
-int hd_mq_destroy(hd_mq* q) {
-    if (!q) return HD_EINVAL;
-    (void)hipSetDevice(q->ctx->device);
-    (void)hipStreamSynchronize(q->ctx->stream);
-    if (q->pool.base) (void)hipFree(q->pool.base);
-    if (q->spare.base) (void)hipFree(q->spare.base);
-    for (auto& b : q->buf)
-        if (b.p) (void)hipFree(b.p);
-    delete q;
+// interned key storage for `n` senders (contents kept)
+static int keys_reserve(hd_mq* q, uint32_t n, hipStream_t s) {
+    const size_t need = 32 * (size_t)std::max(n, 1u);
+    if (need <= q->kcap_bytes) return HD_OK;
+    const size_t cap = std::max(need, 2 * q->kcap_bytes);
+    uint32_t* k = nullptr;
+    QCHK(hipMalloc(&k, cap), "hipMalloc mq keys");
+    if (q->nsend) QCHK(hipMemcpyAsync(k, q->keys, 32 * (size_t)q->nsend, hipMemcpyDeviceToDevice, s), "mq keys copy");
+    QCHK(hipStreamSynchronize(s), "mq keys sync");
+    if (q->keys) (void)hipFree(q->keys);
+    q->keys = k;
+    q->kcap_bytes = cap;
     return HD_OK;
 }
 
-int hd_mq_size(hd_mq* q, uint64_t* n) {
-    if (!q || !n) return HD_EINVAL;
-    *n = q->pool.n;
+// sender ids of the m insertable messages (newidx), interning new Froms in
+// batch order
+static int intern_senders(hd_mq* q, const hd_batch* b, const uint32_t* newidx, uint32_t m, uint32_t** sid_out,
+                          hipStream_t s) {
+    int rc = dict_reserve(q, m, s);
+    if (rc) return rc;
+    uint32_t lcap = 1024;
+    while (lcap < 2 * m) lcap <<= 1;
+    uint32_t* sid = (uint32_t*)qbuf(q, MQ_SID, 4 * (size_t)m, &rc);
+    uint32_t* lslot = (uint32_t*)qbuf(q, MQ_LSLOT, 4 * (size_t)m, &rc);
+    uint32_t* lclaim = (uint32_t*)qbuf(q, MQ_LCLAIM, 4 * (size_t)lcap, &rc);
+    uint32_t* lid = (uint32_t*)qbuf(q, MQ_LID, 4 * (size_t)lcap, &rc);
+    uint8_t* nflag = (uint8_t*)qbuf(q, MQ_KEEP, m, &rc);
+    uint32_t* reps = (uint32_t*)qbuf(q, MQ_REPS, 4 * (size_t)m, &rc);
+    if (rc) return rc;
+    QCHK(hipMemsetAsync(lclaim, 0xFF, 4 * (size_t)lcap, s), "clear batch senders");
+    k_mq_lookup<<<nblk(m), 256, 0, s>>>(m, newidx, b->from32, dict_of(q), lclaim, lcap - 1, sid, lslot);
+    k_mq_newflag<<<nblk(m), 256, 0, s>>>(m, lslot, lclaim, nflag);
+    QCHK(hipGetLastError(), "mq lookup");
+    uint32_t r = 0;
+    rc = select_idx(q, nflag, m, reps, &r, s);
+    if (rc) return rc;
+    if (r) {
+        rc = keys_reserve(q, q->nsend + r, s);
+        if (rc) return rc;
+        k_mq_assign<<<nblk(r), 256, 0, s>>>(r, reps, newidx, b->from32, q->nsend, q->keys, q->slots, q->tcap - 1,
+                                            q->seed, lslot, lid);
+        k_mq_sid<<<nblk(m), 256, 0, s>>>(m, lslot, lid, sid);
+        QCHK(hipGetLastError(), "mq assign");
+        q->nsend += r;
+    }
+    *sid_out = sid;
     return HD_OK;
 }
 
-int hd_mq_insert_device(hd_mq* q, const hd_batch* d_batch, const int32_t* d_sender, void* stream) {
-    if (!q || !d_batch) return HD_EINVAL;
+static int mq_insert_flagged(hd_mq* q, const hd_batch* d_batch, const uint8_t* flag, hipStream_t s) {
     const uint32_t nb = d_batch->n;
-    if (nb == 0) return HD_OK;  // empty device tensors may have NULL data pointers
-    if (!d_sender) return HD_EINVAL;
-    if (!d_batch->type || !d_batch->height || !d_batch->round || !d_batch->value32 || !d_batch->from32)
-        return HD_EINVAL;
-    (void)hipSetDevice(q->ctx->device);
-    hipStream_t s = stream ? (hipStream_t)stream : q->ctx->stream;
     int rc = 0;
     // 1. the batch's insertable messages, in batch order
-    uint8_t* flag = (uint8_t*)qbuf(q, MQ_FLAG, nb, &rc);
     uint32_t* newidx = (uint32_t*)qbuf(q, MQ_NEWIDX, 4 * (size_t)nb, &rc);
     if (rc) return rc;
-    k_mq_flag_new<<<nblk(nb), 256, 0, s>>>(nb, d_sender, flag);
     uint32_t m = 0;
     rc = select_idx(q, flag, nb, newidx, &m, s);
     if (rc || m == 0) return rc;
-    // 2. merged sequence: pool (sorted) then the new messages (arrival order)
+    // 2. their sender queues (the From of each message)
+    uint32_t* nsid = nullptr;
+    rc = intern_senders(q, d_batch, newidx, m, &nsid, s);
+    if (rc) return rc;
+    // 3. merged sequence: pool (sorted) then the new messages (arrival order)
     const uint32_t M = q->pool.n, T = M + m;
     DevBatch b{nb, d_batch->type, d_batch->height, d_batch->round, d_batch->valid_round, d_batch->value32,
                d_batch->from32, d_batch->sig65};
-    MqSrc src{q->pool, b, newidx, d_sender, M};
+    MqSrc src{q->pool, b, newidx, nsid, M};
     int64_t* hk = (int64_t*)qbuf(q, MQ_HK, 8 * (size_t)T, &rc);
     int64_t* rk = (int64_t*)qbuf(q, MQ_RK, 8 * (size_t)T, &rc);
     uint32_t* sk = (uint32_t*)qbuf(q, MQ_SK, 4 * (size_t)T, &rc);
@@ -373,13 +574,13 @@ int hd_mq_insert_device(hd_mq* q, const hd_batch* d_batch, const int32_t* d_send
     uint32_t* p1 = (uint32_t*)qbuf(q, MQ_PERM1, 4 * (size_t)T, &rc);
     if (rc) return rc;
     k_mq_keys<<<nblk(T), 256, 0, s>>>(src, T, hk, rk, sk, p0);
-    // 3. stable LSD passes: round, height, sender (mq.go:120-128 order; the
+    // 4. stable LSD passes: round, height, sender (mq.go:120-128 order; the
     //    stability keeps arrival order among equal keys)
     hipcub::DoubleBuffer<uint32_t> perm(p0, p1);
     if ((rc = sort_pass64(q, perm, rk, T, s))) return rc;
     if ((rc = sort_pass64(q, perm, hk, T, s))) return rc;
     if ((rc = sort_pass32(q, perm, sk, T, s))) return rc;
-    // 4. per-sender capacity: keep the first max_cap of every sender run
+    // 5. per-sender capacity: keep the first max_cap of every sender run
     uint32_t* head = (uint32_t*)qbuf(q, MQ_HEAD, 4 * (size_t)T, &rc);
     uint8_t* keep = (uint8_t*)qbuf(q, MQ_KEEP, T, &rc);
     uint32_t* sel = (uint32_t*)qbuf(q, MQ_SEL, 4 * (size_t)T, &rc);
@@ -409,42 +610,129 @@ int hd_mq_insert_device(hd_mq* q, const hd_batch* d_batch, const int32_t* d_send
     return HD_OK;
 }
 
-int hd_mq_insert_verified_device(hd_mq* q, const hd_batch* d_batch, const uint8_t* d_verdict, const int32_t* d_signer,
-                                 int64_t min_height, void* stream) {
+extern "C" {
+
+int hd_mq_create(hd_ctx* ctx, uint32_t max_capacity, hd_mq** out) {
+    if (!ctx || !out || max_capacity == 0) return HD_EINVAL;
+    hd_mq* q = new (std::nothrow) hd_mq();
+    if (!q) return HD_ENOMEM;
+    q->ctx = ctx;
+    q->max_cap = max_capacity;
+    q->seed = (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count() * 0x9E3779B97F4A7C15ull ^
+              (uint64_t)(uintptr_t)q;
+    *out = q;
+    return HD_OK;
+}
+
+int hd_mq_destroy(hd_mq* q) {
+    if (!q) return HD_EINVAL;
+    (void)hipSetDevice(q->ctx->device);
+    (void)hipStreamSynchronize(q->ctx->stream);
+    if (q->pool.base) (void)hipFree(q->pool.base);
+    if (q->spare.base) (void)hipFree(q->spare.base);
+    if (q->keys) (void)hipFree(q->keys);
+    if (q->slots) (void)hipFree(q->slots);
+    for (auto& b : q->buf)
+        if (b.p) (void)hipFree(b.p);
+    delete q;
+    return HD_OK;
+}
+
+int hd_mq_size(hd_mq* q, uint64_t* n) {
+    if (!q || !n) return HD_EINVAL;
+    *n = q->pool.n;
+    return HD_OK;
+}
+
+int hd_mq_senders(hd_mq* q, uint32_t* n) {
+    if (!q || !n) return HD_EINVAL;
+    *n = q->nsend;
+    return HD_OK;
+}
+
+int hd_mq_insert_device(hd_mq* q, const hd_batch* d_batch, const uint8_t* d_insert, void* stream) {
     if (!q || !d_batch) return HD_EINVAL;
     const uint32_t nb = d_batch->n;
-    if (nb == 0) return HD_OK;
-    if (!d_verdict || !d_signer) return HD_EINVAL;
-    if (!d_batch->height) return HD_EINVAL;
+    if (nb == 0) return HD_OK;  // empty device tensors may have NULL data pointers
+    if (!d_batch->type || !d_batch->height || !d_batch->round || !d_batch->value32 || !d_batch->from32)
+        return HD_EINVAL;
     (void)hipSetDevice(q->ctx->device);
     hipStream_t s = stream ? (hipStream_t)stream : q->ctx->stream;
     int rc = 0;
-    int32_t* snd = (int32_t*)qbuf(q, MQ_SND, 4 * (size_t)nb, &rc);
+    uint8_t* flag = (uint8_t*)qbuf(q, MQ_FLAG, nb, &rc);
     if (rc) return rc;
-    k_mq_ingress<<<nblk(nb), 256, 0, s>>>(nb, d_verdict, d_signer, d_batch->height, min_height, snd);
-    QCHK(hipGetLastError(), "k_mq_ingress");
-    return hd_mq_insert_device(q, d_batch, snd, stream);
+    k_mq_flag_nz<<<nblk(nb), 256, 0, s>>>(nb, d_insert, flag);
+    QCHK(hipGetLastError(), "k_mq_flag_nz");
+    return mq_insert_flagged(q, d_batch, flag, s);
 }
 
-int hd_mq_consume(hd_mq* q, int64_t h, const hd_batch_out* out, int32_t* out_sender, uint32_t cap, uint32_t* n_out) {
+int hd_mq_insert_verified_device(hd_mq* q, const hd_batch* d_batch, const uint8_t* d_verdict, int64_t min_height,
+                                 void* stream) {
+    if (!q || !d_batch) return HD_EINVAL;
+    const uint32_t nb = d_batch->n;
+    if (nb == 0) return HD_OK;
+    if (!d_verdict) return HD_EINVAL;
+    if (!d_batch->type || !d_batch->height || !d_batch->round || !d_batch->value32 || !d_batch->from32)
+        return HD_EINVAL;
+    (void)hipSetDevice(q->ctx->device);
+    hipStream_t s = stream ? (hipStream_t)stream : q->ctx->stream;
+    int rc = 0;
+    uint8_t* flag = (uint8_t*)qbuf(q, MQ_FLAG, nb, &rc);
+    if (rc) return rc;
+    k_mq_ingress<<<nblk(nb), 256, 0, s>>>(nb, d_verdict, d_batch->height, min_height, flag);
+    QCHK(hipGetLastError(), "k_mq_ingress");
+    return mq_insert_flagged(q, d_batch, flag, s);
+}
+
+int hd_mq_consume(hd_mq* q, int64_t h, const uint8_t* allowed32, uint32_t n_allowed, const hd_batch_out* out,
+                  int32_t* out_sender, uint32_t cap, uint32_t* n_out, uint32_t* n_removed) {
     if (!q || !out || !n_out) return HD_EINVAL;
     if (!out->type || !out->height || !out->round || !out->value32 || !out->from32) return HD_EINVAL;
+    if (allowed32 == nullptr && n_allowed != 0) return HD_EINVAL;
     *n_out = 0;
+    if (n_removed) *n_removed = 0;
     const uint32_t M = q->pool.n;
     if (M == 0) return HD_OK;
     (void)hipSetDevice(q->ctx->device);
     hipStream_t s = q->ctx->stream;
     int rc = 0;
-    uint8_t* flag = (uint8_t*)qbuf(q, MQ_FLAG, M, &rc);
+    // procsAllowed as one flag per sender queue
+    uint8_t* allow = (uint8_t*)qbuf(q, MQ_ALLOW, q->nsend, &rc);
+    if (rc) return rc;
+    QCHK(hipMemsetAsync(allow, 0, q->nsend, s), "clear allow");
+    const uint32_t* list = nullptr;
+    uint32_t na = 0;
+    int be = 0;
+    if (allowed32) {
+        na = n_allowed;
+        if (na) {
+            uint32_t* d = (uint32_t*)qbuf(q, MQ_LIST, 32 * (size_t)na, &rc);
+            if (rc) return rc;
+            QCHK(hipMemcpyAsync(d, allowed32, 32 * (size_t)na, hipMemcpyHostToDevice, s), "allowed upload");
+            list = d;
+        }
+    } else {
+        na = q->ctx->n_adm;   // the ctx's admitted set now (sorted, big-endian words)
+        list = q->ctx->d_adm;
+        be = 1;
+    }
+    if (na) k_mq_allow<<<nblk(na), 256, 0, s>>>(na, list, be, dict_of(q), allow);
+    uint8_t* removed = (uint8_t*)qbuf(q, MQ_FLAG, M, &rc);
+    uint8_t* deliver = (uint8_t*)qbuf(q, MQ_DELIV, M, &rc);
     uint8_t* inv = (uint8_t*)qbuf(q, MQ_KEEP, M, &rc);
     uint32_t* sel = (uint32_t*)qbuf(q, MQ_SEL, 4 * (size_t)M, &rc);
+    uint32_t* sel2 = (uint32_t*)qbuf(q, MQ_SEL2, 4 * (size_t)M, &rc);
     if (rc) return rc;
-    k_mq_pred<<<nblk(M), 256, 0, s>>>(M, q->pool.h, h, 0, flag, inv);
-    uint32_t c = 0;
-    rc = select_idx(q, flag, M, sel, &c, s);
+    k_mq_pred<<<nblk(M), 256, 0, s>>>(M, q->pool.h, q->pool.sender, h, 0, allow, removed, deliver, inv);
+    QCHK(hipGetLastError(), "k_mq_pred");
+    uint32_t nr = 0, c = 0;
+    rc = select_idx(q, removed, M, sel2, &nr, s);
+    if (rc) return rc;
+    rc = select_idx(q, deliver, M, sel, &c, s);
     if (rc) return rc;
     *n_out = c;
     if (c > cap) return HD_ECAP;
+    if (n_removed) *n_removed = nr;
     if (c) {
         rc = pool_reserve(q->ctx, q->spare, c);
         if (rc) return rc;
@@ -462,7 +750,7 @@ int hd_mq_consume(hd_mq* q, int64_t h, const hd_batch_out* out, int32_t* out_sen
         if (out->adv_class) memset(out->adv_class, 0, c);
         QCHK(hipStreamSynchronize(s), "consume sync");
     }
-    return pool_filter(q, inv, s);
+    return nr ? pool_filter(q, inv, s) : HD_OK;
 }
 
 int hd_mq_drop_below(hd_mq* q, int64_t h) {
@@ -475,7 +763,8 @@ int hd_mq_drop_below(hd_mq* q, int64_t h) {
     uint8_t* flag = (uint8_t*)qbuf(q, MQ_FLAG, M, &rc);
     uint8_t* inv = (uint8_t*)qbuf(q, MQ_KEEP, M, &rc);
     if (rc) return rc;
-    k_mq_pred<<<nblk(M), 256, 0, s>>>(M, q->pool.h, h, 1, flag, inv);
+    k_mq_pred<<<nblk(M), 256, 0, s>>>(M, q->pool.h, q->pool.sender, h, 1, nullptr, flag, nullptr, inv);
+    QCHK(hipGetLastError(), "k_mq_pred");
     return pool_filter(q, inv, s);
 }
 

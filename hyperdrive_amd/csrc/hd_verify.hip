@@ -128,7 +128,7 @@ int hd_dev_grow(hd_ctx* ctx, void** p, size_t* cap, size_t need) {
 
 extern "C" {
 
-int hd_abi_version(void) { return 1; }
+int hd_abi_version(void) { return 2; }
 
 const char* hd_strerror(int code) {
     int k = -code;

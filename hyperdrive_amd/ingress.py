@@ -11,9 +11,17 @@ for a whole batch:
 
     ing = Ingress(verifier, height=h)
     ing.push_wire(PREVOTE, buf, n)          # unmarshal + verify + filterHeight + mq insert (GPU)
-    res = ing.flush()                       # mq.Consume(h) + vote-log inserts (host table)
+    res = ing.flush()                       # mq.Consume(h, procsAllowed) + vote-log inserts (host table)
     res.proposes                            # handed to the CPU's insertPropose (scheduler/validator)
-    ing.reset_height(h + 1)                 # ResetHeight: logs emptied, mq.DropMessagesBelowHeight
+    ing.reset_height(h + 1, signatories)    # ResetHeight: logs emptied, mq.DropMessagesBelowHeight,
+                                            # a new signatory set rebuilds procsAllowed (replica.go:132-145)
+
+Membership follows the reference: every *authenticated* message
+(recovered signatory == From: verdict VALID or NOT_ADMITTED) with height >=
+the current height is buffered, in the queue of its From; procsAllowed -- the
+verifier's admitted set at flush time -- is applied when the queue is
+consumed (mq/mq.go:49-51).  A message buffered while its sender was not
+admitted is delivered after a reset_height that admits it.
 
 Batch semantics: a flush consumes everything buffered at the current height
 in one go; the reference may advance the height in the middle of a flush
@@ -36,17 +44,19 @@ from .votes import VoteLog
 
 @dataclass
 class FlushResult:
-    consumed: Batch            # every message consumed, in consumption order
-    senders: np.ndarray        # int32 admitted index per consumed message
+    consumed: Batch            # every message delivered (sender in procsAllowed), in consumption order
+    senders: np.ndarray        # int32 sender-queue id per delivered message (queue creation order)
     vote_status: np.ndarray    # HD_VOTE_* per consumed message (NOT_VOTE for proposes)
     double_of: np.ndarray      # batch index of the logged vote for DOUBLE, else votes.NO_INDEX
     proposes: np.ndarray       # indices (into consumed) of the proposes, for the CPU
+    removed: int = 0           # messages consumed, delivered or dropped by procsAllowed (Consume's n)
 
 
 class Ingress:
     def __init__(self, v: Verifier, height: int = 1, max_capacity: int = 1000):
         self.v = v
         self.height = int(height)
+        self.f = None              # set by reset_height(signatories=...): len(signatories) // 3 (replica.go:138)
         self.mq = MessageQueue(v, max_capacity)
         self.votes = VoteLog(self.height)
 
@@ -55,19 +65,19 @@ class Ingress:
         self.votes.close()
 
     def push_device(self, batch: DeviceBatch, stream=None):
-        """Verify a device batch and buffer its VALID messages with height >=
-        the current height.  Returns the device verdict tensor."""
+        """Verify a device batch and buffer its authenticated messages (VALID
+        or NOT_ADMITTED) with height >= the current height.  Returns the
+        device verdict tensor."""
         torch = _torch()
         dev = batch.height.device
         n = batch.n
         verdict = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
-        signer = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
         if n == 0:
             return verdict[:0]
         ws = stream or work_stream(dev)
         ws.wait_stream(torch.cuda.current_stream(ws.device))
-        self.v.verify_batch_device(batch.c_struct(), verdict.data_ptr(), None, signer.data_ptr(), None, ws.cuda_stream)
-        self.mq.insert_verified_device(batch, verdict, signer, self.height, stream=ws)
+        self.v.verify_batch_device(batch.c_struct(), verdict.data_ptr(), None, None, None, ws.cuda_stream)
+        self.mq.insert_verified_device(batch, verdict, self.height, stream=ws)
         return verdict[:n]
 
     def push_wire(self, mtype: int, buf, n: int, with_sig: bool = True, stream=None):
@@ -82,14 +92,22 @@ class Ingress:
         return self.push_device(db, stream=stream)
 
     def flush(self) -> FlushResult:
-        b, senders = self.mq.consume(self.height)
+        """mq.Consume(CurrentHeight, ..., procsAllowed) with procsAllowed = the
+        verifier's admitted set now, then the vote-log inserts."""
+        b, senders = self.mq.consume(self.height, allowed=None)
         status, double_of = self.votes.insert_batch(b)
-        return FlushResult(b, senders, status, double_of, np.flatnonzero(b.type == PROPOSE))
+        return FlushResult(b, senders, status, double_of, np.flatnonzero(b.type == PROPOSE), self.mq.last_removed)
 
-    def reset_height(self, height: int) -> None:
+    def reset_height(self, height: int, signatories=None) -> None:
+        """ResetHeightMessage (replica.go:132-145): the logs restart at
+        `height`, lower heights leave the queue, and a non-empty signatory
+        set replaces procsAllowed (and the verifier's admitted set)."""
         self.height = int(height)
         self.votes.reset(self.height)
         self.mq.drop_below(self.height)
+        if signatories is not None and len(signatories):
+            self.v.set_signatories(signatories)
+            self.f = len(signatories) // 3
 
 
 __all__ = ["Ingress", "FlushResult"]

@@ -1,14 +1,19 @@
 """Bulk MessageQueue on the GPU (include/hd_mq.h; mq/mq.go).
 
     q = MessageQueue(verifier, max_capacity=1000)      # mq.New
-    q.insert_device(dbatch, d_sender)                  # InsertPrevote/... for a whole batch
-    msgs, senders = q.consume(height)                  # Consume(h): host Batch + sender ids
+    q.insert_device(dbatch)                            # InsertPrevote/... for a whole batch (queue = From)
+    q.insert_verified_device(dbatch, verdict, h)       # Replica.Run ingress: authenticated, filterHeight
+    msgs, senders = q.consume(height, allowed)         # Consume(h, ..., procsAllowed)
     q.drop_below(height)                               # DropMessagesBelowHeight
+
+Queues are keyed by the message's From (mq.go:107-113); ``allowed`` is
+procsAllowed, applied at consume time (mq.go:49-51): a list / array of
+32-byte signatories, or None for the verifier's current admitted set.
 """
 from __future__ import annotations
 
 import ctypes
-from typing import Tuple
+from typing import Optional, Tuple
 
 import numpy as np
 
@@ -16,6 +21,14 @@ from . import _lib
 from ._lib import HdBatchOut
 from .device import DeviceBatch, _torch, work_stream
 from .verify import Batch, Verifier
+
+
+def _sig_array(allowed) -> np.ndarray:
+    if isinstance(allowed, np.ndarray):
+        a = np.ascontiguousarray(allowed, dtype=np.uint8).reshape(-1, 32)
+    else:
+        a = np.frombuffer(b"".join(bytes(x) for x in allowed), dtype=np.uint8).reshape(-1, 32)
+    return np.ascontiguousarray(a)
 
 
 class MessageQueue:
@@ -28,6 +41,7 @@ class MessageQueue:
             raise _lib.HDError(rc, "hd_mq_create")
         self._q = h
         self.max_capacity = max_capacity
+        self.last_removed = 0        # Consume's n (delivered + dropped by procsAllowed) of the last consume
         _lib.track(self)
 
     def close(self):
@@ -45,25 +59,31 @@ class MessageQueue:
         if rc != 0:
             raise _lib.HDError(rc, where, self._lib.hd_ctx_last_error(self._v.handle).decode())
 
-    def insert_device(self, batch: DeviceBatch, sender, stream=None) -> None:
-        """Insert every message i with sender[i] >= 0 (an int32 device tensor), in
-        batch order."""
+    def insert_device(self, batch: DeviceBatch, insert=None, stream=None) -> None:
+        """Insert every message i with insert[i] != 0 (a uint8/bool device
+        tensor; None = all), in batch order, into the queue of its From."""
         torch = _torch()
         ws = stream or work_stream(batch.height.device)
         ws.wait_stream(torch.cuda.current_stream(ws.device))
         cs = batch.c_struct()
-        self._check(self._lib.hd_mq_insert_device(self._q, ctypes.byref(cs), sender.data_ptr(), ws.cuda_stream),
+        ptr = None
+        if insert is not None:
+            if insert.dtype == torch.bool:
+                insert = insert.to(torch.uint8)
+            ptr = insert.data_ptr()
+        self._check(self._lib.hd_mq_insert_device(self._q, ctypes.byref(cs), ptr, ws.cuda_stream),
                     "hd_mq_insert_device")
 
-    def insert_verified_device(self, batch: DeviceBatch, verdict, signer, min_height: int, stream=None) -> None:
-        """Replica ingress: insert the VALID messages with height >= min_height
-        (filterHeight), sender = signer[i] (device tensors from verify)."""
+    def insert_verified_device(self, batch: DeviceBatch, verdict, min_height: int, stream=None) -> None:
+        """Replica ingress: insert the authenticated messages (verdict VALID or
+        NOT_ADMITTED) with height >= min_height (filterHeight); membership is
+        checked at consume time."""
         torch = _torch()
         ws = stream or work_stream(batch.height.device)
         ws.wait_stream(torch.cuda.current_stream(ws.device))
         cs = batch.c_struct()
         self._check(self._lib.hd_mq_insert_verified_device(self._q, ctypes.byref(cs), verdict.data_ptr(),
-                                                           signer.data_ptr(), int(min_height), ws.cuda_stream),
+                                                           int(min_height), ws.cuda_stream),
                     "hd_mq_insert_verified_device")
 
     def __len__(self) -> int:
@@ -71,9 +91,19 @@ class MessageQueue:
         self._check(self._lib.hd_mq_size(self._q, ctypes.byref(n)), "hd_mq_size")
         return int(n.value)
 
-    def consume(self, height: int) -> Tuple[Batch, np.ndarray]:
-        """Remove and return every message with height <= `height`, senders
-        ascending, each sender's messages by (height, round, arrival)."""
+    @property
+    def senders(self) -> int:
+        """Sender queues created so far (distinct Froms ever inserted)."""
+        n = ctypes.c_uint32()
+        self._check(self._lib.hd_mq_senders(self._q, ctypes.byref(n)), "hd_mq_senders")
+        return int(n.value)
+
+    def consume(self, height: int, allowed=None) -> Tuple[Batch, np.ndarray]:
+        """Remove every message with height <= `height`; return those of
+        senders in `allowed` (procsAllowed; None = the verifier's admitted set
+        now), sender queues in creation order, each by (height, round,
+        arrival), with their sender-queue ids.  ``last_removed`` is set to the
+        number removed, delivered or not."""
         cap = len(self)
         n = max(cap, 1)
         a = dict(type=np.zeros(n, np.uint8), height=np.zeros(n, np.int64), round=np.zeros(n, np.int64),
@@ -83,10 +113,16 @@ class MessageQueue:
         p = lambda x: x.ctypes.data
         out = HdBatchOut(p(a["type"]), p(a["height"]), p(a["round"]), p(a["valid_round"]), p(a["value"]),
                          p(a["frm"]), p(a["sig"]), None)
-        got = ctypes.c_uint32()
-        self._check(self._lib.hd_mq_consume(self._q, int(height), ctypes.byref(out), p(snd), cap, ctypes.byref(got)),
-                    "hd_mq_consume")
+        got, removed = ctypes.c_uint32(), ctypes.c_uint32()
+        if allowed is None:
+            al, na = None, 0
+        else:
+            arr = _sig_array(allowed)
+            al, na = (p(arr) if len(arr) else p(np.zeros((1, 32), np.uint8))), len(arr)
+        self._check(self._lib.hd_mq_consume(self._q, int(height), al, na, ctypes.byref(out), p(snd), cap,
+                                            ctypes.byref(got), ctypes.byref(removed)), "hd_mq_consume")
         k = int(got.value)
+        self.last_removed = int(removed.value)
         b = Batch(a["type"][:k], a["height"][:k], a["round"][:k], a["valid_round"][:k], a["value"][:k], a["frm"][:k],
                   a["sig"][:k])
         return b, snd[:k].copy()

@@ -12,8 +12,11 @@ product never imports it.
                              delivered) but counted in n
   drop_below  mq.go:70-83    remove every message with height < h
 
-Sender iteration order: the reference walks a Go map (unspecified order); this
-restatement (like the GPU queue) walks senders in ascending key order.
+Senders are the queue keys (the reference's map key is the message's From,
+mq.go:107-113; any hashable here).  Sender iteration order: the reference walks
+a Go map (unspecified order); this restatement, like the GPU queue, walks the
+sender queues in the order they were created (a sender's first insert; the
+map entry, and so its place, outlives an emptied queue, as in mq.go).
 A message is any tuple whose [0] is height and [1] is round.
 """
 from __future__ import annotations
@@ -40,7 +43,7 @@ class MessageQueue:
     def consume(self, h: int, allowed: Optional[Set[Hashable]] = None) -> Tuple[int, List[Tuple[Hashable, tuple]]]:
         n = 0
         out = []
-        for sender in sorted(self.queues):
+        for sender in list(self.queues):                     # creation order (dicts keep insertion order)
             q = self.queues[sender]
             k = 0
             while k < len(q) and q[k][0] <= h:                # mq.go:38-41

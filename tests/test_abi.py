@@ -56,7 +56,7 @@ def test_strerror_without_gpu():
     assert lib.hd_strerror(0) == b"ok"
     assert lib.hd_strerror(-1) == b"invalid argument"
     assert lib.hd_strerror(-4) == b"tally capacity too small"
-    assert lib.hd_abi_version() == 1
+    assert lib.hd_abi_version() == 2
     # NULL arguments are rejected before any device work
     assert lib.hd_ctx_create(0, None) == -1
     assert lib.hd_verify_batch(None, None, None, None, None) == -1

@@ -8,7 +8,16 @@ The workload is the seeded adversarial generator (30 % invalid across the C5
 classes) over many heights, plus re-sent duplicates and double votes, so
 every branch of the chain is exercised: invalid verdicts dropped, heights
 below the current one filtered, future heights buffered, per-sender
-capacity truncation, first-wins / duplicate / double-vote statuses."""
+capacity truncation, first-wins / duplicate / double-vote statuses.
+
+Membership is the reference's: the restatement chain inserts
+every AUTHENTICATED message (the C oracle's verdict VALID or NOT_ADMITTED:
+recovered signatory == From) into mq_oracle keyed by From, and applies
+procsAllowed only in mq_oracle.consume(allowed=...) (mq.go:49-51).  The
+admitted set starts at five of the seven signers and is replaced mid-stream
+by a ResetHeight with a new signatory set (replica.go:132-145): messages
+buffered from the two signers admitted only then are delivered after it,
+those of the signers it removes are dropped at consume."""
 import numpy as np
 import pytest
 
@@ -51,43 +60,58 @@ def test_wire_to_vote_logs_matches_restatements(verifier, coracle, cap):
     jitter = np.arange(n) + rng.integers(-50, 51, n) * 2 * S
     order = np.concatenate([np.argsort(jitter, kind="stable"), extra])
     # arrival = per-type wire buffers pushed in this order: prevotes, precommits
-    adm = {sigs[k].tobytes(): k for k in range(S)}
+    first, later = sigs[:5], sigs[2:]        # admitted sets before / after the ResetHeight
+    verifier.set_signatories(first)
     ing = Ingress(verifier, height=H0, max_capacity=cap)
     try:
-        _run(ing, hb, order, sigs, adm, H0, cap, coracle)
+        _run(ing, hb, order, first, later, H0, cap, coracle)
     finally:
         ing.close()
 
 
-def _run(ing, hb, order, sigs, adm, H0, cap, coracle):
+def _run(ing, hb, order, first, later, H0, cap, coracle):
     import torch
+    from hyperdrive_amd.verify import Batch
     mq = MQO.MessageQueue(cap)
-    arrival = []
     for t in (2, 3):
         idx = order[hb.type[order] == t]
         buf = SC.marshal_array(t, hb.height[idx], hb.round[idx], None, hb.value[idx], hb.frm[idx], hb.sig[idx])
         d = torch.frombuffer(bytearray(buf), dtype=torch.uint8).cuda()
         vg = ing.push_wire(t, d, len(idx)).cpu().numpy()
-        from hyperdrive_amd.verify import Batch
         sub = Batch(hb.type[idx], hb.height[idx], hb.round[idx], None, hb.value[idx], hb.frm[idx], hb.sig[idx])
-        vc, _ = coracle.verify(sub, sigs, True, threads=8)
+        vc, _ = coracle.verify(sub, first, True, threads=8)
         assert vg.tolist() == vc.tolist()
+        assert (vc == 6).sum() > 0              # authenticated senders outside the admitted set
         for k, i in enumerate(idx):
-            if vc[k] == 0 and hb.height[i] >= H0:
-                mq.insert(adm[hb.frm[i].tobytes()], _rows(hb, [i])[0])
-        arrival += list(idx)
+            # authenticated (VALID or NOT_ADMITTED) and filterHeight: mq.Insert*
+            if vc[k] in (0, 6) and hb.height[i] >= H0:
+                mq.insert(hb.frm[i].tobytes(), _rows(hb, [i])[0])
     assert len(ing.mq) == len(mq)
     votes = VO.VoteLogs(H0)
+    allowed = {x.tobytes() for x in first}
+    ids = {}
+    late = {x.tobytes() for x in later} - allowed
+    delivered_late = 0
     for step in range(3):
         h = H0 + step
         if step:
-            ing.reset_height(h)
+            # step 1: ResetHeight with a new signatory set; step 2: without
+            sigset = later if step == 1 else None
+            ing.reset_height(h, sigset)
             mq.drop_below(h)
             votes.reset(h)
+            if sigset is not None:
+                allowed = {x.tobytes() for x in sigset}
+                assert ing.f == len(sigset) // 3
         res = ing.flush()
-        n_o, want = mq.consume(h)
-        got = [(int(res.senders[k]), r) for k, r in enumerate(_rows(res.consumed, range(len(res.consumed))))]
-        assert got == want and len(res.consumed) == n_o
+        n_o, want = mq.consume(h, allowed=allowed)
+        rows = _rows(res.consumed, range(len(res.consumed)))
+        assert [(m[5], m) for m in rows] == want and len(res.consumed) == len(want)
+        assert res.removed == n_o
+        for m, sid in zip(rows, res.senders.tolist()):
+            assert ids.setdefault(m[5], sid) == sid
+        if step:
+            delivered_late += sum(1 for m in rows if m[5] in late)
         for k, (s, m) in enumerate(want):
             st, _ = votes.insert(m[2], m[0], m[1], m[4], m[5])
             assert res.vote_status[k] == st
@@ -97,3 +121,6 @@ def _run(ing, hb, order, sigs, adm, H0, cap, coracle):
                 for (s, m) in want:
                     assert ing.votes.count(t, r, m[4]) == votes.count(t, r, m[4])
         assert len(want) > 0
+    # messages buffered while their sender was not admitted were delivered
+    # after the ResetHeight that admitted it
+    assert delivered_late > 0

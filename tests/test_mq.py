@@ -5,10 +5,14 @@ CPU: the restatement reproduces the reference's own mq_test.go behaviours --
 max capacity 1 (mq_test.go:642-714), excess dropped (716-793), ordering by
 height and round (334-608), drop below height (611-639), procsAllowed at
 consume (119-331).
-GPU: random insert / consume / drop sequences give exactly the restatement's
-consumed messages (all fields, order included) for capacities 1, 3, 25 and
-1000; a 1M-message batch from 100 senders keeps every sender's 1000 smallest
-(height, round, arrival) messages."""
+GPU: queues are keyed by From (the 32 bytes, mq.go:107-113) and procsAllowed
+is applied at consume time (mq.go:49-51).  Random insert / consume (with
+random procsAllowed subsets) / drop sequences give exactly the restatement's
+delivered messages (all fields, order included) and its Consume count n, for
+capacities 1, 3, 25 and 1000; the four whitelist scenarios of
+mq_test.go:119-331 (allowed, not allowed, removed later, added later) run
+through the GPU queue; a 1M-message batch from 100 senders keeps every
+sender's 1000 smallest (height, round, arrival) messages."""
 import random
 
 import numpy as np
@@ -74,6 +78,35 @@ def test_oracle_procs_allowed_at_consume():
     assert n == 2 and [s for s, _ in out] == ["in"]
 
 
+def test_oracle_whitelist_changes_between_consumes():
+    # mq_test.go:207-331: removed from / added to procsAllowed between two consumes
+    q = OracleMQ(1000)
+    q.insert("s", _msg(5, 0, "low"))
+    q.insert("s", _msg(9, 0, "high"))
+    n, out = q.consume(5, allowed={"s"})
+    assert n == 1 and [m[2] for _, m in out] == ["low"]
+    n, out = q.consume(9, allowed=set())
+    assert n == 1 and out == []
+    q.insert("t", _msg(5, 0, "a"))
+    q.insert("t", _msg(9, 0, "b"))
+    n, out = q.consume(5, allowed=set())
+    assert n == 1 and out == []
+    n, out = q.consume(9, allowed={"t"})
+    assert n == 1 and [m[2] for _, m in out] == ["b"]
+
+
+def test_oracle_queue_creation_order():
+    q = OracleMQ(10)
+    for s in ("c", "a", "b"):
+        q.insert(s, _msg(1, 0))
+    q.consume(1)
+    q.insert("a", _msg(2, 0))
+    q.insert("d", _msg(2, 0))
+    q.insert("c", _msg(2, 0))
+    n, out = q.consume(2)
+    assert [s for s, _ in out] == ["c", "a", "d"]
+
+
 # ---------------------------------------------------------------- GPU
 @pytest.fixture(scope="module")
 def verifier(gpu):
@@ -82,7 +115,13 @@ def verifier(gpu):
     v.close()
 
 
-def _batch(rng, n, S, hmax, rmax, neg_pct=10):
+def _senders(rng, S):
+    return rng.integers(0, 256, (S, 32), dtype=np.uint8)
+
+
+def _batch(rng, n, keys, hmax, rmax, skip_pct=10):
+    """Random messages from the senders `keys` (S x 32 Froms); ~skip_pct %
+    are not inserted (insert flag 0)."""
     import torch
     from hyperdrive_amd.device import DeviceBatch
     typ = rng.integers(1, 4, n).astype(np.uint8)
@@ -90,20 +129,28 @@ def _batch(rng, n, S, hmax, rmax, neg_pct=10):
     r = rng.integers(0, rmax, n).astype(np.int64)
     vr = rng.integers(-1, 3, n).astype(np.int64)
     value = rng.integers(0, 256, (n, 32), dtype=np.uint8)
-    frm = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    frm = keys[rng.integers(0, len(keys), n)]
     sig = rng.integers(0, 256, (n, 65), dtype=np.uint8)
-    snd = rng.integers(0, S, n).astype(np.int32)
-    snd[rng.random(n) < neg_pct / 100] = -1
+    ins = (rng.random(n) >= skip_pct / 100).astype(np.uint8)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
     db = DeviceBatch(n, t(typ), t(h), t(r), t(vr), t(value), t(frm), t(sig))
     host = [(int(h[i]), int(r[i]), int(typ[i]), int(vr[i]), value[i].tobytes(), frm[i].tobytes(), sig[i].tobytes())
             for i in range(n)]
-    return db, t(snd), host, snd
+    return db, t(ins), host, ins
 
 
-def _as_tuples(b, snd):
-    return [(int(snd[k]), (int(b.height[k]), int(b.round[k]), int(b.type[k]), int(b.valid_round[k]),
-                           b.value[k].tobytes(), b.frm[k].tobytes(), b.sig[k].tobytes())) for k in range(len(b))]
+def _rows(b):
+    return [(int(b.height[k]), int(b.round[k]), int(b.type[k]), int(b.valid_round[k]), b.value[k].tobytes(),
+             b.frm[k].tobytes(), b.sig[k].tobytes()) for k in range(len(b))]
+
+
+def _check_consumed(b, snd, want, ids):
+    """GPU (rows, sender ids) == oracle [(From, row)]; sender ids name the
+    queues in creation order (ids: From -> id seen so far, extended here)."""
+    rows = _rows(b)
+    assert [(m[5], m) for m in rows] == want
+    for m, k in zip(rows, snd.tolist()):
+        assert ids.setdefault(m[5], k) == k
 
 
 @pytest.mark.gpu
@@ -111,61 +158,120 @@ def _as_tuples(b, snd):
 def test_random_sequences_match_oracle(verifier, cap):
     from hyperdrive_amd.mq import MessageQueue
     rng = np.random.default_rng(cap)
+    keys = _senders(rng, 7)
     q = MessageQueue(verifier, cap)
     o = OracleMQ(cap)
+    ids = {}
     for step in range(12):
-        db, d_snd, host, snd = _batch(rng, int(rng.integers(1, 3000)), 7, 6, 4)
-        q.insert_device(db, d_snd)
+        db, d_ins, host, ins = _batch(rng, int(rng.integers(1, 3000)), keys, 6, 4)
+        q.insert_device(db, d_ins)
         for i, m in enumerate(host):
-            if snd[i] >= 0:
-                o.insert(int(snd[i]), m)
+            if ins[i]:
+                o.insert(m[5], m)
         assert len(q) == len(o)
         op = step % 3
         if op == 1:
             hh = int(rng.integers(0, 6))
-            b, s = q.consume(hh)
-            n, want = o.consume(hh)
-            assert _as_tuples(b, s) == want and len(b) == n
+            allowed = keys[rng.random(len(keys)) < 0.6]
+            b, s = q.consume(hh, allowed)
+            n, want = o.consume(hh, allowed={k.tobytes() for k in allowed})
+            _check_consumed(b, s, want, ids)
+            assert q.last_removed == n
         elif op == 2:
             hh = int(rng.integers(0, 6))
             q.drop_below(hh)
             o.drop_below(hh)
-    b, s = q.consume(10 ** 9)
+    # the creation order of the queues is the order of first insertion
+    assert sorted(ids.values()) == list(range(len(ids)))
+    b, s = q.consume(10 ** 9, keys)
     n, want = o.consume(10 ** 9)
-    assert _as_tuples(b, s) == want
+    _check_consumed(b, s, want, ids)
+    assert q.senders == len(o.queues)
     q.close()
+
+
+def _one(h, r, frm, tag):
+    import torch
+    from hyperdrive_amd.device import DeviceBatch
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    val = np.zeros((1, 32), np.uint8)
+    val[0, 0] = tag
+    f = np.frombuffer(frm, np.uint8).reshape(1, 32)
+    return DeviceBatch(1, t(np.array([1], np.uint8)), t(np.array([h], np.int64)), t(np.array([r], np.int64)),
+                       t(np.array([-1], np.int64)), t(val), t(f), t(np.zeros((1, 65), np.uint8)))
 
 
 @pytest.mark.gpu
 def test_capacity_one_on_gpu(verifier):
     """mq_test.go:642-714 through the GPU queue."""
-    import torch
-    from hyperdrive_amd.device import DeviceBatch
     from hyperdrive_amd.mq import MessageQueue
-
-    def one(h, r, sender, tag):
-        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
-        val = np.zeros((1, 32), np.uint8)
-        val[0, 0] = tag
-        db = DeviceBatch(1, t(np.array([1], np.uint8)), t(np.array([h], np.int64)), t(np.array([r], np.int64)),
-                         t(np.array([-1], np.int64)), t(val), t(np.zeros((1, 32), np.uint8)),
-                         t(np.zeros((1, 65), np.uint8)))
-        return db, t(np.array([sender], np.int32))
-
+    A, B = bytes([1]) * 32, bytes([2]) * 32
     q = MessageQueue(verifier, 1)
-    q.insert_device(*one(1, 1, 0, 1))
-    q.insert_device(*one(1, 2, 1, 2))
-    b, s = q.consume(1)
+    q.insert_device(_one(1, 1, A, 1))
+    q.insert_device(_one(1, 2, B, 2))
+    b, s = q.consume(1, [A, B])
     assert len(b) == 2
-    q.insert_device(*one(1, 1, 0, 1))
-    q.insert_device(*one(1, 2, 0, 3))
-    b, s = q.consume(1)
+    q.insert_device(_one(1, 1, A, 1))
+    q.insert_device(_one(1, 2, A, 3))
+    b, s = q.consume(1, [A])
     assert len(b) == 1 and b.value[0, 0] == 1
-    q.insert_device(*one(1, 1, 0, 1))
-    q.insert_device(*one(1, 0, 0, 4))
-    b, s = q.consume(1)
+    q.insert_device(_one(1, 1, A, 1))
+    q.insert_device(_one(1, 0, A, 4))
+    b, s = q.consume(1, [A])
     assert len(b) == 1 and b.value[0, 0] == 4
     q.close()
+
+
+@pytest.mark.gpu
+def test_whitelist_scenarios_on_gpu(verifier):
+    """mq_test.go:119-331: the sender whitelisted, not whitelisted, removed
+    from and added to procsAllowed between two consumes.  Consume's n counts
+    the message either way; only allowed senders' messages are delivered."""
+    from hyperdrive_amd.mq import MessageQueue
+    rng = np.random.default_rng(5)
+    for case in ("allowed", "denied", "removed", "added"):
+        for _ in range(4):
+            snd = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+            h = int(rng.integers(0, 1 << 62))
+            hi = h + 1 + int(rng.integers(0, 100))
+            r = int(rng.integers(0, 1 << 62))
+            q = MessageQueue(verifier, 1000)
+            q.insert_device(_one(h, r, snd, 1))
+            if case in ("removed", "added"):
+                q.insert_device(_one(hi, r, snd, 2))
+            first = [snd] if case in ("allowed", "removed") else []
+            b, _ = q.consume(h, first)
+            assert q.last_removed == 1 and len(b) == (1 if first else 0)
+            if case in ("removed", "added"):
+                second = [] if case == "removed" else [snd]
+                b, _ = q.consume(hi, second)
+                assert q.last_removed == 1 and len(b) == (1 if second else 0)
+                if second:
+                    assert b.value[0, 0] == 2
+            assert len(q) == 0
+            q.close()
+
+
+@pytest.mark.gpu
+def test_consume_uses_admitted_set_at_call(gpu):
+    """allowed=None is the verifier's admitted set as it is at the consume
+    (replica.go:136-143 rebuilds procsAllowed; mq.go:49 reads it then)."""
+    from hyperdrive_amd.mq import MessageQueue
+    v = gpu.Verifier(0)
+    A, B = bytes([7]) * 32, bytes([9]) * 32
+    v.set_signatories([A])
+    q = MessageQueue(v, 10)
+    q.insert_device(_one(1, 0, A, 1))
+    q.insert_device(_one(1, 0, B, 2))
+    q.insert_device(_one(2, 0, A, 3))
+    q.insert_device(_one(2, 0, B, 4))
+    b, s = q.consume(1)
+    assert b.value[:, 0].tolist() == [1] and q.last_removed == 2
+    v.set_signatories([B])
+    b, s = q.consume(2)
+    assert b.value[:, 0].tolist() == [4] and q.last_removed == 2 and s.tolist() == [1]
+    q.close()
+    v.close()
 
 
 @pytest.mark.gpu
@@ -180,19 +286,21 @@ def test_million_message_insert(verifier):
     h = rng.integers(1, 5000, n).astype(np.int64)
     r = rng.integers(0, 4, n).astype(np.int64)
     snd = (np.arange(n) % S).astype(np.int32)
+    keys = _senders(rng, S)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
     tag = np.zeros((n, 32), np.uint8)
     tag[:, :4] = np.arange(n, dtype=np.uint32).view(np.uint8).reshape(n, 4)
     db = DeviceBatch(n, t(np.full(n, 2, np.uint8)), t(h), t(r), t(np.full(n, -1, np.int64)), t(tag),
-                     t(np.zeros((n, 32), np.uint8)), t(np.zeros((n, 65), np.uint8)))
+                     t(keys[snd]), t(np.zeros((n, 65), np.uint8)))
     q = MessageQueue(verifier, 1000)
-    q.insert_device(db, t(snd))
-    assert len(q) == S * 1000
-    b, s = q.consume(10 ** 9)
+    q.insert_device(db)
+    assert len(q) == S * 1000 and q.senders == S
+    b, s = q.consume(10 ** 9, keys)
     idx = b.value[:, :4].copy().view(np.uint32).ravel()
-    order = np.lexsort((np.arange(n), r, h, snd))           # sender, h, r, arrival
+    order = np.lexsort((np.arange(n), r, h, snd))           # sender (= creation order), h, r, arrival
     keep = np.concatenate([order[snd[order] == k][:1000] for k in range(S)])
     assert idx.tolist() == keep.tolist()
+    assert s.tolist() == snd[keep].tolist()
     q.close()
 
 
@@ -206,16 +314,18 @@ def test_extreme_keys_and_empty_inputs(verifier):
     from hyperdrive_amd.mq import MessageQueue
     rng = np.random.default_rng(77)
     ext = np.array([-(1 << 63), -(1 << 62), -2, -1, 0, 1, 2, (1 << 62), (1 << 63) - 1], dtype=np.int64)
+    keys = _senders(rng, 4)
     q = MessageQueue(verifier, 5)
     o = OracleMQ(5)
-    b, s = q.consume(0)
+    ids = {}
+    b, s = q.consume(0, keys)
     assert len(b) == 0 and len(s) == 0 and len(q) == 0
     q.drop_below(1 << 40)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
     empty = DeviceBatch(0, t(np.zeros(0, np.uint8)), t(np.zeros(0, np.int64)), t(np.zeros(0, np.int64)),
                         t(np.zeros(0, np.int64)), t(np.zeros((0, 32), np.uint8)), t(np.zeros((0, 32), np.uint8)),
                         t(np.zeros((0, 65), np.uint8)))
-    q.insert_device(empty, t(np.zeros(0, np.int32)))
+    q.insert_device(empty, t(np.zeros(0, np.uint8)))
     for step in range(6):
         n = 400
         h = rng.choice(ext, n)
@@ -225,21 +335,23 @@ def test_extreme_keys_and_empty_inputs(verifier):
         snd = rng.integers(-1, 4, n).astype(np.int32)
         if step == 3:
             snd[:] = -1                                    # nothing insertable
-        db = DeviceBatch(n, t(typ), t(h), t(r), t(np.full(n, -1, np.int64)), t(val), t(np.zeros((n, 32), np.uint8)),
+        frm = keys[np.maximum(snd, 0)]
+        db = DeviceBatch(n, t(typ), t(h), t(r), t(np.full(n, -1, np.int64)), t(val), t(frm),
                          t(np.zeros((n, 65), np.uint8)))
-        q.insert_device(db, t(snd))
+        q.insert_device(db, t((snd >= 0).astype(np.uint8)))
         for i in range(n):
             if snd[i] >= 0:
-                o.insert(int(snd[i]), (int(h[i]), int(r[i]), int(typ[i]), -1, val[i].tobytes(), bytes(32),
-                                       bytes(65)))
+                o.insert(frm[i].tobytes(), (int(h[i]), int(r[i]), int(typ[i]), -1, val[i].tobytes(),
+                                            frm[i].tobytes(), bytes(65)))
         assert len(q) == len(o)
     hh = int(ext[4])
-    b, s = q.consume(hh)
+    b, s = q.consume(hh, keys)
     n_o, want = o.consume(hh)
-    assert _as_tuples(b, s) == want
+    _check_consumed(b, s, want, ids)
     q.drop_below(int(ext[7]))
     o.drop_below(int(ext[7]))
-    b, s = q.consume((1 << 63) - 1)
+    b, s = q.consume((1 << 63) - 1, keys)
     n_o, want = o.consume((1 << 63) - 1)
-    assert _as_tuples(b, s) == want and len(q) == 0
+    _check_consumed(b, s, want, ids)
+    assert len(q) == 0
     q.close()

@@ -69,6 +69,7 @@ class HdTallyOut(ctypes.Structure):
         ("hr_precommits", ctypes.c_void_p),
         ("hr_any", ctypes.c_void_p),
         ("dup", ctypes.c_void_p),
+        ("hr_rep", ctypes.c_void_p),
     ]
 
 
@@ -83,14 +84,22 @@ SIGNATURES = {
                                              ctypes.POINTER(ctypes.c_uint32)]),
     "hd_ctx_fastpath_geometry": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
                                                 ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "hd_ctx_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "hd_ctx_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
+                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32),
+                                           ctypes.POINTER(ctypes.c_double)]),
     "hd_verify_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_void_p]),
     "hd_verify_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "hd_tally": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                 ctypes.POINTER(HdTallyOut)]),
-    "hd_tally_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p, ctypes.c_void_p,
+    "hd_tally_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                        ctypes.POINTER(HdTallyOut), ctypes.c_void_p]),
+    "hd_tally_device_bitmap_part": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
+                                                   ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(HdTallyOut),
+                                                   ctypes.c_void_p]),
+    "hd_tally_partition_of": (ctypes.c_uint32, [ctypes.c_int64, ctypes.c_int64, ctypes.c_uint32]),
     "hd_tally_device_bitmap": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                               ctypes.POINTER(HdTallyOut), ctypes.c_void_p]),
     "hd_process_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
@@ -136,11 +145,13 @@ SIGNATURES = {
     "hd_votes_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "hd_votes_reset": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     "hd_votes_height": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]),
+    "hd_votes_set_f": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
     "hd_votes_insert": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint8, ctypes.c_int64, ctypes.c_int64,
-                                       ctypes.c_char_p, ctypes.c_char_p, c_u8p, ctypes.c_void_p]),
+                                       ctypes.c_char_p, ctypes.c_char_p, c_u8p, ctypes.c_void_p, c_u8p]),
     "hd_votes_insert_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
-                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
-    "hd_votes_trace_propose": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p]),
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.POINTER(ctypes.c_uint32)]),
+    "hd_votes_trace_propose": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p, c_u8p]),
     "hd_votes_count": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint8, ctypes.c_int64, ctypes.c_char_p,
                                       ctypes.POINTER(ctypes.c_uint32)]),
     "hd_votes_len": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint8, ctypes.c_int64,

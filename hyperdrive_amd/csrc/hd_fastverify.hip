@@ -53,6 +53,17 @@ struct FbWork {
     size_t cap_slow = 0;
     uint32_t* rows = nullptr;     // the split check's per-message rows (SplitRows, 83 words per message)
     size_t cap_rows = 0;
+    // The scratch above (rows, slow, counts) is per context: a verify call
+    // on another stream than the previous one first waits for that call's
+    // end, so calls of one context never overlap on the device whatever
+    // streams the caller uses (hd_verify_batch_device is asynchronous).
+    hipEvent_t done = nullptr;
+    hipStream_t last = nullptr;
+    bool any = false;
+    // hd_ctx_profile: event pairs around whole calls and around k_fast_sums
+    bool prof = false;
+    std::vector<hipEvent_t> ev_call, ev_sums;
+    size_t n_call = 0, n_sums = 0;   // pairs in use
     std::unordered_map<std::string, uint32_t> slot_of;  // signatory -> slot
     std::vector<uint32_t> free_slots;
     uint32_t used = 1;            // slots handed out so far (slot 0 = G)
@@ -690,6 +701,9 @@ void hd_fb_release(hd_ctx* ctx) {
     if (!ctx || !ctx->fb) return;
     FbWork* f = ctx->fb;
     fb_free_tables(ctx);
+    if (f->done) (void)hipEventDestroy(f->done);
+    for (hipEvent_t e : f->ev_call) (void)hipEventDestroy(e);
+    for (hipEvent_t e : f->ev_sums) (void)hipEventDestroy(e);
     void* ptrs[] = {f->counts, f->slow, f->adm_slot, f->rows};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -784,6 +798,23 @@ int hd_fb_clear_keys(hd_ctx* ctx) {
     return HD_OK;
 }
 
+// the next free event pair of a profile record (created on first use), or
+// NULL when profiling is off or the event could not be created
+static hipEvent_t* fb_prof_pair(std::vector<hipEvent_t>& ev, size_t& used, bool on) {
+    if (!on) return nullptr;
+    if (2 * (used + 1) > ev.size()) {
+        hipEvent_t a = nullptr, b = nullptr;
+        if (hipEventCreate(&a) != hipSuccess) return nullptr;
+        if (hipEventCreate(&b) != hipSuccess) {
+            (void)hipEventDestroy(a);
+            return nullptr;
+        }
+        ev.push_back(a);
+        ev.push_back(b);
+    }
+    return &ev[2 * used++];
+}
+
 // k_fast_sums occupancy (HD_SUM_WAVES: 2 or 3, the default) and prefetch
 // depth (HD_SUM_PF: 1, the default, or 2 windows ahead)
 template <int WP>
@@ -810,13 +841,34 @@ static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest
     k_fast_prep<<<(n + 255) / 256, 256, 0, s>>>(b, d_digest, f->state, f->adm_slot, ctx->d_adm, ctx->n_adm,
                                                 ctx->adm_steps, rows);
     k_fast_scalars<K, WP><<<tb, 256, 0, s>>>(b, T, rows);
+    hipEvent_t* pe = fb_prof_pair(f->ev_sums, f->n_sums, f->prof);
+    if (pe) (void)hipEventRecord(pe[0], s);
     launch_sums<WP>((n + 255) / 256, s, n, f->gtab, f->tab, rows);
+    if (pe) (void)hipEventRecord(pe[1], s);
     k_fast_final<K><<<tb, 256, 0, s>>>(b, T, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer, f->slow,
                                        f->counts + 1);
 }
 
+static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict,
+                          uint8_t* d_rec32, int32_t* d_signer, uint32_t* d_bitmap, hipStream_t s);
+
 int hd_fb_verify(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict, uint8_t* d_rec32,
                  int32_t* d_signer, uint32_t* d_bitmap, hipStream_t s) {
+    FbWork* f = ctx->fb;
+    if (!f->done) FBCHK(hipEventCreateWithFlags(&f->done, hipEventDisableTiming), "fb event");
+    if (f->any && f->last != s) FBCHK(hipStreamWaitEvent(s, f->done, 0), "fb stream order");
+    hipEvent_t* pe = fb_prof_pair(f->ev_call, f->n_call, f->prof);
+    if (pe) (void)hipEventRecord(pe[0], s);
+    const int rc = fb_verify_impl(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, s);
+    if (pe) (void)hipEventRecord(pe[1], s);
+    FBCHK(hipEventRecord(f->done, s), "fb event record");
+    f->last = s;
+    f->any = true;
+    return rc;
+}
+
+static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict,
+                          uint8_t* d_rec32, int32_t* d_signer, uint32_t* d_bitmap, hipStream_t s) {
     FbWork* f = ctx->fb;
     int rc = hd_dev_grow(ctx, (void**)&f->slow, &f->cap_slow, 4 * (size_t)b.n);
     if (rc) return rc;
@@ -916,6 +968,43 @@ int hd_ctx_fastpath_geometry(hd_ctx* ctx, int* g_windows, int* key_windows, int*
     if (g_windows) *g_windows = FbL<HD_FB_WG>::NWIN;
     if (key_windows) *key_windows = fb_nwin(ctx->fb ? ctx->fb->wp : HD_FB_W);
     if (msgs_per_inversion) *msgs_per_inversion = k > 0 ? k : 2;
+    return HD_OK;
+}
+
+int hd_ctx_profile(hd_ctx* ctx, int enable) {
+    if (!ctx) return HD_EINVAL;
+    if (!ctx->fb) return enable ? HD_EINVAL : HD_OK;   // the profile covers the known-key path's calls
+    ctx->fb->prof = enable != 0;
+    return HD_OK;
+}
+
+int hd_ctx_profile_read(hd_ctx* ctx, uint32_t* calls, double* verify_ms, uint32_t* sums_launches, double* sums_ms) {
+    if (!ctx) return HD_EINVAL;
+    double tc = 0, ts = 0;
+    uint32_t nc = 0, ns = 0;
+    if (ctx->fb) {
+        FbWork* f = ctx->fb;
+        (void)hipSetDevice(ctx->device);
+        for (size_t k = 0; k < f->n_call; k++) {
+            float ms = 0;
+            FBCHK(hipEventSynchronize(f->ev_call[2 * k + 1]), "profile sync");
+            FBCHK(hipEventElapsedTime(&ms, f->ev_call[2 * k], f->ev_call[2 * k + 1]), "profile read");
+            tc += ms;
+        }
+        for (size_t k = 0; k < f->n_sums; k++) {
+            float ms = 0;
+            FBCHK(hipEventSynchronize(f->ev_sums[2 * k + 1]), "profile sync");
+            FBCHK(hipEventElapsedTime(&ms, f->ev_sums[2 * k], f->ev_sums[2 * k + 1]), "profile read");
+            ts += ms;
+        }
+        nc = (uint32_t)f->n_call;
+        ns = (uint32_t)f->n_sums;
+        f->n_call = f->n_sums = 0;
+    }
+    if (calls) *calls = nc;
+    if (verify_ms) *verify_ms = tc;
+    if (sums_launches) *sums_launches = ns;
+    if (sums_ms) *sums_ms = ts;
     return HD_OK;
 }
 

@@ -86,20 +86,15 @@ HD void ecmult_gen(gej& out, const sc& k, GTab gtab) {
 }
 
 template <typename GTab>
-HD void pubkey_signatory(uint32_t out_be[8], const sc& sk, bool compressed, GTab gtab) {
+HD void pubkey_signatory(uint32_t out_be[8], const sc& sk, int pkfmt, GTab gtab) {
     gej P;
     ecmult_gen(P, sk, gtab);
     fe x, y;
     gej_to_ge(x, y, P);
-    uint32_t xb[8];
+    uint32_t xb[8], yb[8];
     fe_to_be(xb, x);
-    if (compressed) {
-        sha256_pub33(out_be, 2u | (y.n[0] & 1u), xb);
-    } else {
-        uint32_t yb[8];
-        fe_to_be(yb, y);
-        sha256_pub65(out_be, xb, yb);
-    }
+    fe_to_be(yb, y);
+    sha256_pubkey(out_be, pkfmt, xb, yb, y.n[0] & 1u);
 }
 
 HD void sc_to_bytes(uint8_t b[32], const sc& a) {

@@ -15,7 +15,7 @@ struct BeWords {  // 32-byte strings addressed as big-endian words
     __device__ __forceinline__ uint32_t operator[](size_t k) const { return load_be32(p + 4 * k); }
 };
 
-__global__ __launch_bounds__(256) void k_keys(uint32_t S, int compressed, const ge* __restrict__ gtab,
+__global__ __launch_bounds__(256) void k_keys(uint32_t S, int pkfmt, const ge* __restrict__ gtab,
                                               uint8_t* sigs32, uint8_t* foreign32) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= S + HD_NONADMITTED_KEYS) return;
@@ -23,7 +23,7 @@ __global__ __launch_bounds__(256) void k_keys(uint32_t S, int compressed, const 
     sc sk;
     signer_sk(sk, idx);
     uint32_t o[8];
-    pubkey_signatory(o, sk, compressed != 0, gtab);
+    pubkey_signatory(o, sk, pkfmt, gtab);
     uint8_t* dst = j < S ? sigs32 + 32 * (size_t)j : foreign32 + 32 * (size_t)(j - S);
     for (int w = 0; w < 8; w++) store_be32(dst + 4 * w, o[w]);
 }
@@ -58,7 +58,7 @@ int hd_gen_keys(hd_ctx* ctx, uint32_t S, uint8_t* signatories32, uint8_t* foreig
     hipError_t e = hipMalloc(&d, bytes);
     if (e != hipSuccess) return hd_ctx_fail(ctx, e, "gen_keys alloc");
     uint32_t total = S + HD_NONADMITTED_KEYS;
-    k_keys<<<(total + 255) / 256, 256, 0, ctx->stream>>>(S, ctx->compressed ? 1 : 0, ctx->d_gtab, d, d + 32 * (size_t)S);
+    k_keys<<<(total + 255) / 256, 256, 0, ctx->stream>>>(S, ctx->pkfmt, ctx->d_gtab, d, d + 32 * (size_t)S);
     e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpyAsync(signatories32, d, 32 * (size_t)S, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess)

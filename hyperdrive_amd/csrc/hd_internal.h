@@ -36,7 +36,7 @@ struct hd_ctx {
     int n_cu = 256;
     int verify_waves = 3;   // register budget of k_verify (waves per SIMD)
     hipStream_t stream = nullptr;
-    bool compressed = true;
+    int pkfmt = HD_PUBKEY_COMPRESSED;   // id.NewSignatory's pubkey encoding (hd_ctx_set_pubkey_format)
     hd::ge* d_gtab = nullptr;
     uint32_t* d_adm = nullptr;      // sorted admitted signatories, 8 BE words each
     int32_t* d_adm_perm = nullptr;  // sorted index -> caller's index

@@ -4,8 +4,9 @@
 //     (process/message.go:172-186, 270-284 -- identical for Prevote/Precommit)
 //   * propose digest   SHA-256(BE64 h || BE64 r || BE64 vr || value) 56 B, 2 blocks
 //     (process/message.go:60-78)
-//   * signatory        SHA-256(SEC1 pubkey)  33 B (1 block) / 65 B (2 blocks)
-//     [renproject/id v0.4.2 NewSignatory]
+//   * signatory        SHA-256(pubkey)  SEC1 compressed 33 B (1 block), SEC1
+//     uncompressed 65 B (2 blocks) or raw X || Y 64 B (2 blocks)
+//     [renproject/id v0.4.2 NewSignatory; the encoding is a context setting]
 // plus a small streaming context used only by the synthetic-workload signer
 // (HMAC-SHA256 for RFC6979 nonces).
 #pragma once
@@ -113,6 +114,27 @@ HD void sha256_pub65(uint32_t out[8], const uint32_t x_be[8], const uint32_t y_b
     w[15] = 65 * 8;
     sha256_compress(st, w);
     HD_UNROLL for (int i = 0; i < 8; i++) out[i] = st[i];
+}
+
+// Raw pubkey X || Y, 64 bytes -> 2 blocks (the second is padding only).
+HD void sha256_pub64(uint32_t out[8], const uint32_t x_be[8], const uint32_t y_be[8]) {
+    uint32_t st[8], w[16];
+    sha256_init(st);
+    HD_UNROLL for (int i = 0; i < 8; i++) { w[i] = x_be[i]; w[8 + i] = y_be[i]; }
+    sha256_compress(st, w);
+    w[0] = 0x80000000u;
+    HD_UNROLL for (int i = 1; i < 15; i++) w[i] = 0;
+    w[15] = 64 * 8;
+    sha256_compress(st, w);
+    HD_UNROLL for (int i = 0; i < 8; i++) out[i] = st[i];
+}
+
+// The signatory of an affine key in pubkey format `fmt` (include/hd_verify.h
+// HD_PUBKEY_*: 0 uncompressed, 1 compressed, 2 raw X || Y); y_odd = Y mod 2.
+HD void sha256_pubkey(uint32_t out[8], int fmt, const uint32_t x_be[8], const uint32_t y_be[8], uint32_t y_odd) {
+    if (fmt == 1) sha256_pub33(out, 2u | (y_odd & 1u), x_be);
+    else if (fmt == 2) sha256_pub64(out, x_be, y_be);
+    else sha256_pub65(out, x_be, y_be);
 }
 
 // ---------------------------------------------------------------------------

@@ -58,7 +58,7 @@ struct CTab {   // (G slot, type, value)
     uint32_t* n;
 };
 
-__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+HD uint64_t mix64(uint64_t x) {
     x ^= x >> 30;
     x *= 0xBF58476D1CE4E5B9ull;
     x ^= x >> 27;
@@ -67,11 +67,38 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
     return x;
 }
 
+HD uint64_t hash_hr(int64_t h, int64_t r) {
+    return mix64((uint64_t)h * 0x9E3779B97F4A7C15ull ^ mix64((uint64_t)r));
+}
+// partition of a round among nparts (the high half of its hash; the table
+// probes use the low bits)
+HD uint32_t part_of(uint64_t hhr, uint32_t nparts) { return nparts > 1 ? (uint32_t)((hhr >> 32) % nparts) : 0u; }
+
+struct Part {
+    uint32_t part, nparts;
+};
+
 __device__ __forceinline__ bool candidate(const DevBatch& b, const uint8_t* verdict, const uint32_t* bitmap,
-                                          uint32_t i) {
+                                          uint32_t i, Part p) {
     const uint8_t t = b.type[i];
     if (t != T_PREVOTE && t != T_PRECOMMIT) return false;
-    return verdict ? verdict[i] == V_VALID : ((bitmap[i >> 5] >> (i & 31)) & 1u);
+    if (!(verdict ? verdict[i] == V_VALID : ((bitmap[i >> 5] >> (i & 31)) & 1u))) return false;
+    return p.nparts <= 1 || part_of(hash_hr(b.height[i], b.round[i]), p.nparts) == p.part;
+}
+
+// candidates of the partition (sizes the hash tables): one atomic per block
+__global__ __launch_bounds__(256) void k_tally_count(DevBatch b, const uint8_t* __restrict__ verdict,
+                                                     const uint32_t* __restrict__ bitmap, Part p,
+                                                     uint32_t* __restrict__ count) {
+    __shared__ uint32_t c;
+    if (threadIdx.x == 0) c = 0;
+    __syncthreads();
+    uint32_t mine = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += gridDim.x * blockDim.x)
+        mine += candidate(b, verdict, bitmap, i, p) ? 1u : 0u;
+    if (mine) atomicAdd(&c, mine);
+    __syncthreads();
+    if (threadIdx.x == 0 && c) atomicAdd(count, c);
 }
 
 __device__ __forceinline__ bool eq32(const uint8_t* a, const uint8_t* b) {
@@ -147,9 +174,6 @@ __device__ __forceinline__ int64_t shfl64(int64_t v, int src) {
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
-__device__ __forceinline__ uint64_t hash_hr(int64_t h, int64_t r) {
-    return mix64((uint64_t)h * 0x9E3779B97F4A7C15ull ^ mix64((uint64_t)r));
-}
 __device__ __forceinline__ uint64_t hash_log(uint64_t hhr, const uint8_t* from, uint32_t t) {
     return mix64(hhr ^ *reinterpret_cast<const uint64_t*>(from) ^ (uint64_t)t);
 }
@@ -158,11 +182,11 @@ __device__ __forceinline__ uint64_t hash_log(uint64_t hhr, const uint8_t* from, 
 // the lowest index of the key); a new D slot counts a distinct signer of
 // that type in the round.
 __global__ void k_tally_logs(DevBatch b, const uint8_t* __restrict__ verdict, const uint32_t* __restrict__ bitmap,
-                             GTab G, uint32_t* __restrict__ D, uint32_t mask, uint32_t* __restrict__ gslot,
+                             Part p, GTab G, uint32_t* __restrict__ D, uint32_t mask, uint32_t* __restrict__ gslot,
                              uint32_t* __restrict__ dslot, uint8_t* __restrict__ dup) {
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += stride) {
-        if (!candidate(b, verdict, bitmap, i)) {
+        if (!candidate(b, verdict, bitmap, i, p)) {
             if (dup) dup[i] = 3;
             gslot[i] = kEmpty;
             continue;
@@ -291,10 +315,12 @@ __global__ __launch_bounds__(256) void k_tally_used(uint32_t cap, const uint32_t
 
 __global__ void k_tally_emit_hr(uint32_t n_hr, const uint32_t* __restrict__ slot, GTab G, const int64_t* __restrict__ h,
                                 const int64_t* __restrict__ r, int64_t* __restrict__ oh, int64_t* __restrict__ orr,
-                                uint32_t* __restrict__ oprev, uint32_t* __restrict__ oprec, uint32_t* __restrict__ oany) {
+                                uint32_t* __restrict__ oprev, uint32_t* __restrict__ oprec, uint32_t* __restrict__ oany,
+                                uint32_t* __restrict__ orep) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_hr) return;
     const uint32_t s = slot[k], i = G.claim[s];
+    orep[k] = i;
     oh[k] = h[i];
     orr[k] = r[i];
     oprev[k] = G.nprev[s];
@@ -373,14 +399,27 @@ static int used_sorted(hd_ctx* ctx, uint32_t cap, const uint32_t* claim, uint32_
 }
 
 static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdict, const uint32_t* d_bitmap,
-                        hd_tally_out* out, hipStream_t s) {
+                        Part part, hd_tally_out* out, hipStream_t s) {
     const uint32_t n = hb->n;
     if (!ctx->tally) ctx->tally = new TallyWork();
     DevBatch b{n, hb->type, hb->height, hb->round, hb->valid_round, hb->value32, hb->from32, hb->sig65};
-    uint32_t cap = 1024;
-    while (cap < 2 * n) cap <<= 1;  // load factor <= 1/2: probes terminate
-    const uint32_t mask = cap - 1;
     int rc = 0;
+    const uint32_t grid = std::min<uint32_t>(nblk(n), (uint32_t)ctx->n_cu * 16u);
+    // the tables hold at most one key per candidate: size them by this
+    // partition's candidates (one counting pass), load factor <= 1/2 so
+    // probes terminate
+    uint32_t n_cand = n;
+    {
+        uint32_t* cnt = (uint32_t*)tbuf(ctx, T_NSEL, 64, &rc);
+        if (rc) return rc;
+        TCHK(hipMemsetAsync(cnt + 1, 0, 4, s), "clear candidate count");
+        k_tally_count<<<grid, 256, 0, s>>>(b, d_verdict, d_bitmap, part, cnt + 1);
+        TCHK(hipMemcpyAsync(&n_cand, cnt + 1, 4, hipMemcpyDeviceToHost, s), "candidate count");
+        TCHK(hipStreamSynchronize(s), "candidate count sync");
+    }
+    uint32_t cap = 1024;
+    while (cap < 2 * n_cand) cap <<= 1;
+    const uint32_t mask = cap - 1;
     uint32_t* g = (uint32_t*)tbuf(ctx, T_G, 20 * (size_t)cap, &rc);  // 16 B used; staging for the outputs
     uint32_t* d = (uint32_t*)tbuf(ctx, T_D, 4 * (size_t)cap, &rc);
     uint32_t* c = (uint32_t*)tbuf(ctx, T_C, 8 * (size_t)cap, &rc);
@@ -388,6 +427,11 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     uint32_t* dslot = (uint32_t*)tbuf(ctx, T_DSLOT, 4 * (size_t)n, &rc);
     uint8_t* d_dup = out->dup ? (uint8_t*)tbuf(ctx, T_DUP, n, &rc) : nullptr;
     if (rc) return rc;
+    if (n_cand == 0) {   // nothing to tally here (dup: every message 3)
+        out->n_hr = out->n_counts = 0;
+        if (out->dup) memset(out->dup, 3, n);
+        return HD_OK;
+    }
     GTab G{g, g + cap, g + 2 * (size_t)cap, g + 3 * (size_t)cap};
     CTab C{c, c + cap};
     // claim words := empty; counters := 0
@@ -396,8 +440,7 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     TCHK(hipMemsetAsync(d, 0xFF, 4 * (size_t)cap, s), "clear D");
     TCHK(hipMemsetAsync(c, 0xFF, 4 * (size_t)cap, s), "clear C");
     TCHK(hipMemsetAsync(C.n, 0, 4 * (size_t)cap, s), "clear C counters");
-    const uint32_t grid = std::min<uint32_t>(nblk(n), (uint32_t)ctx->n_cu * 16u);
-    k_tally_logs<<<grid, 256, 0, s>>>(b, d_verdict, d_bitmap, G, d, mask, gslot, dslot, d_dup);
+    k_tally_logs<<<grid, 256, 0, s>>>(b, d_verdict, d_bitmap, part, G, d, mask, gslot, dslot, d_dup);
     k_tally_values<<<grid, 256, 0, s>>>(b, d, G, C, mask, gslot, dslot, d_dup);
     TCHK(hipGetLastError(), "tally kernels");
 
@@ -407,20 +450,23 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     if (rc) return rc;
     out->n_hr = n_hr;
     if (n_hr && n_hr <= out->cap_hr) {
-        char* st = (char*)tbuf(ctx, T_SEL, 28 * (size_t)n_hr, &rc);
+        char* st = (char*)tbuf(ctx, T_SEL, 32 * (size_t)n_hr, &rc);
         if (rc) return rc;
         int64_t* o_h = reinterpret_cast<int64_t*>(st);
         int64_t* o_r = o_h + n_hr;
         uint32_t* o_prev = reinterpret_cast<uint32_t*>(o_r + n_hr);
         uint32_t* o_prec = o_prev + n_hr;
         uint32_t* o_any = o_prec + n_hr;
-        k_tally_emit_hr<<<nblk(n_hr), 256, 0, s>>>(n_hr, order, G, b.height, b.round, o_h, o_r, o_prev, o_prec, o_any);
+        uint32_t* o_rep = o_any + n_hr;
+        k_tally_emit_hr<<<nblk(n_hr), 256, 0, s>>>(n_hr, order, G, b.height, b.round, o_h, o_r, o_prev, o_prec, o_any,
+                                                   o_rep);
         struct Cp { void* dst; const void* src; size_t sz; } cp[] = {
             {out->hr_height, o_h, 8 * (size_t)n_hr},     {out->hr_round, o_r, 8 * (size_t)n_hr},
             {out->hr_prevotes, o_prev, 4 * (size_t)n_hr}, {out->hr_precommits, o_prec, 4 * (size_t)n_hr},
-            {out->hr_any, o_any, 4 * (size_t)n_hr},
+            {out->hr_any, o_any, 4 * (size_t)n_hr},       {out->hr_rep, o_rep, 4 * (size_t)n_hr},
         };
-        for (auto& x : cp) TCHK(hipMemcpyAsync(x.dst, x.src, x.sz, hipMemcpyDeviceToHost, s), "hr download");
+        for (auto& x : cp)
+            if (x.dst) TCHK(hipMemcpyAsync(x.dst, x.src, x.sz, hipMemcpyDeviceToHost, s), "hr download");
     }
     // (the count sort below reuses the sort buffers: same stream, so the
     // per-round emit above has consumed `order` before they are rewritten)
@@ -477,28 +523,36 @@ int hd_tally(hd_ctx* ctx, const hd_batch* batch, const uint8_t* verdict, hd_tall
     if (rc) return rc;
     uint8_t* d_v = (uint8_t*)ctx->bufs[BUF_VERDICT].p;
     TCHK(hipMemcpyAsync(d_v, verdict, batch->n, hipMemcpyHostToDevice, ctx->stream), "verdict upload");
-    return tally_device(ctx, &db, d_v, nullptr, out, ctx->stream);
+    return tally_device(ctx, &db, d_v, nullptr, Part{0, 1}, out, ctx->stream);
 }
 
-int hd_tally_device(hd_ctx* ctx, const hd_batch* dbatch, const uint8_t* d_verdict, const int32_t* d_signer,
-                    hd_tally_out* out, void* stream) {
-    (void)d_signer;  // logs are keyed by From itself (equal to the signer for VALID messages)
+int hd_tally_device(hd_ctx* ctx, const hd_batch* dbatch, const uint8_t* d_verdict, hd_tally_out* out, void* stream) {
     if (!ctx || !dbatch || !tally_out_ok(out)) return HD_EINVAL;
     if (dbatch->n && !d_verdict) return HD_EINVAL;
     out->n_counts = out->n_hr = 0;
     if (dbatch->n == 0) return HD_OK;
     (void)hipSetDevice(ctx->device);
-    return tally_device(ctx, dbatch, d_verdict, nullptr, out, stream ? (hipStream_t)stream : ctx->stream);
+    return tally_device(ctx, dbatch, d_verdict, nullptr, Part{0, 1}, out, stream ? (hipStream_t)stream : ctx->stream);
 }
 
 int hd_tally_device_bitmap(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* d_valid_bitmap, hd_tally_out* out,
                            void* stream) {
-    if (!ctx || !dbatch || !tally_out_ok(out)) return HD_EINVAL;
+    return hd_tally_device_bitmap_part(ctx, dbatch, d_valid_bitmap, 0, 1, out, stream);
+}
+
+int hd_tally_device_bitmap_part(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* d_valid_bitmap, uint32_t part,
+                                uint32_t nparts, hd_tally_out* out, void* stream) {
+    if (!ctx || !dbatch || !tally_out_ok(out) || nparts == 0 || part >= nparts) return HD_EINVAL;
     if (dbatch->n && !d_valid_bitmap) return HD_EINVAL;
     out->n_counts = out->n_hr = 0;
     if (dbatch->n == 0) return HD_OK;
     (void)hipSetDevice(ctx->device);
-    return tally_device(ctx, dbatch, nullptr, d_valid_bitmap, out, stream ? (hipStream_t)stream : ctx->stream);
+    return tally_device(ctx, dbatch, nullptr, d_valid_bitmap, Part{part, nparts}, out,
+                        stream ? (hipStream_t)stream : ctx->stream);
+}
+
+uint32_t hd_tally_partition_of(int64_t height, int64_t round, uint32_t nparts) {
+    return part_of(hash_hr(height, round), nparts);
 }
 
 int hd_process_batch(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8_t* recovered32,
@@ -512,7 +566,7 @@ int hd_process_batch(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8
     if (rc) return rc;
     rc = hd_verify_uploaded(ctx, &db, verdict, recovered32, valid_bitmap);
     if (rc) return rc;
-    return tally_device(ctx, &db, (const uint8_t*)ctx->bufs[BUF_VERDICT].p, nullptr, tally, ctx->stream);
+    return tally_device(ctx, &db, (const uint8_t*)ctx->bufs[BUF_VERDICT].p, nullptr, Part{0, 1}, tally, ctx->stream);
 }
 
 }  // extern "C"

@@ -53,7 +53,7 @@ struct DevSrc {
 // known-key fast path's leftovers); with ctl.adm_slot, a VALID message whose
 // signatory has no known key yet publishes its recovered key to the
 // signatory's table slot (first writer wins, hd_fixedbase.h states).
-template <bool COMPRESSED, int WAVES>
+template <int PKFMT, int WAVES>
 __global__ __launch_bounds__(256, WAVES) void k_verify(DevBatch b, const ge* __restrict__ gtab_g,
                                                 const uint32_t* __restrict__ adm, const int32_t* __restrict__ adm_perm,
                                                 uint32_t n_adm, int adm_steps, uint8_t* __restrict__ verdict,
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256, WAVES) void k_verify(DevBatch b, const ge* __r
             uint32_t rec[8];
             int32_t s;
             ge q;
-            v = verify_msg_src(src, gtab_g, adm, n_adm, adm_steps, COMPRESSED, rec, s, ctl.adm_slot ? &q : nullptr);
+            v = verify_msg_src(src, gtab_g, adm, n_adm, adm_steps, PKFMT, rec, s, ctl.adm_slot ? &q : nullptr);
             verdict[i] = v;
             if (rec32) {
                 uint8_t* o = rec32 + 32 * (size_t)i;
@@ -200,11 +200,10 @@ int hd_ctx_destroy(hd_ctx* ctx) {
     return HD_OK;
 }
 
-int hd_ctx_set_pubkey_format(hd_ctx* ctx, int compressed) {
-    if (!ctx) return HD_EINVAL;
-    const bool c = compressed != 0;
-    if (c != ctx->compressed) {
-        ctx->compressed = c;
+int hd_ctx_set_pubkey_format(hd_ctx* ctx, int format) {
+    if (!ctx || format < HD_PUBKEY_UNCOMPRESSED || format > HD_PUBKEY_RAW64) return HD_EINVAL;
+    if (format != ctx->pkfmt) {
+        ctx->pkfmt = format;
         // keys were learned under the other signatory derivation
         if (ctx->fb) return hd_fb_clear_keys(ctx);
     }
@@ -265,14 +264,14 @@ int hd_launch_slow(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint
                                           d_verdict, d_rec32, d_signer, d_bitmap, d_digest, ctl)
     // waves/SIMD the kernel is register-allocated for (HD_VERIFY_WAVES = 2/3/4, default 3)
     const int w = ctx->verify_waves;
-    if (ctx->compressed) {
-        if (w == 2) HD_LAUNCH_VERIFY(true, 2);
-        else if (w == 4) HD_LAUNCH_VERIFY(true, 4);
-        else HD_LAUNCH_VERIFY(true, 3);
+    if (ctx->pkfmt == HD_PUBKEY_COMPRESSED) {
+        if (w == 2) HD_LAUNCH_VERIFY(1, 2);
+        else if (w == 4) HD_LAUNCH_VERIFY(1, 4);
+        else HD_LAUNCH_VERIFY(1, 3);
+    } else if (ctx->pkfmt == HD_PUBKEY_RAW64) {
+        HD_LAUNCH_VERIFY(2, 3);
     } else {
-        if (w == 2) HD_LAUNCH_VERIFY(false, 2);
-        else if (w == 4) HD_LAUNCH_VERIFY(false, 4);
-        else HD_LAUNCH_VERIFY(false, 3);
+        HD_LAUNCH_VERIFY(0, 3);
     }
 #undef HD_LAUNCH_VERIFY
     hipError_t e = hipGetLastError();

@@ -64,7 +64,7 @@ HD int32_t admitted_find(AdmTab adm, uint32_t n, int steps, const uint32_t key[8
 // the recovered signatory (zeros when recovery failed); signer the
 // admitted-table index; qout (optional) the recovered key of a VALID message.
 template <typename Src, typename GTab, typename AdmTab>
-HD uint8_t verify_msg_src(const Src& src, GTab gtab, AdmTab adm, uint32_t n_adm, int adm_steps, bool compressed,
+HD uint8_t verify_msg_src(const Src& src, GTab gtab, AdmTab adm, uint32_t n_adm, int adm_steps, int pkfmt,
                           uint32_t rec_be[8], int32_t& signer, ge* qout = nullptr) {
     signer = -1;
     HD_UNROLL for (int i = 0; i < 8; i++) rec_be[i] = 0;
@@ -88,14 +88,11 @@ HD uint8_t verify_msg_src(const Src& src, GTab gtab, AdmTab adm, uint32_t n_adm,
         verdict = recover(qx, qy, d, r_be, s_be, src.sig_v(), gtab);
     }
     if (verdict != V_VALID) return verdict;
-    uint32_t xb[8];
-    fe_to_be(xb, qx);
-    if (compressed) {
-        sha256_pub33(rec_be, 2u | (qy.n[0] & 1u), xb);
-    } else {
-        uint32_t yb[8];
+    {
+        uint32_t xb[8], yb[8];
+        fe_to_be(xb, qx);
         fe_to_be(yb, qy);
-        sha256_pub65(rec_be, xb, yb);
+        sha256_pubkey(rec_be, pkfmt, xb, yb, qy.n[0] & 1u);
     }
     uint32_t from_be[8];
     uint32_t diff = 0;
@@ -131,10 +128,10 @@ struct MsgSrc {
 };
 
 template <typename GTab, typename AdmTab>
-HD uint8_t verify_msg(const MsgIn& m, GTab gtab, AdmTab adm, uint32_t n_adm, int adm_steps, bool compressed,
+HD uint8_t verify_msg(const MsgIn& m, GTab gtab, AdmTab adm, uint32_t n_adm, int adm_steps, int pkfmt,
                       uint32_t rec_be[8], int32_t& signer) {
     MsgSrc src{m};
-    return verify_msg_src(src, gtab, adm, n_adm, adm_steps, compressed, rec_be, signer);
+    return verify_msg_src(src, gtab, adm, n_adm, adm_steps, pkfmt, rec_be, signer);
 }
 
 }  // namespace hd

@@ -157,10 +157,13 @@ struct RoundLog {
         std::fill(traced.begin(), traced.end(), 0);
         trace_len = 0;
     }
-    void trace(uint32_t id) {
+    // true when `id` is new to the trace
+    bool trace(uint32_t id) {
         uint8_t& b = at(traced, id);
-        trace_len += !b;
+        const bool fresh = !b;
+        trace_len += fresh;
         b = 1;
+        return fresh;
     }
 };
 
@@ -173,6 +176,7 @@ inline int type_ix(uint8_t type) {
 struct hd_votes {
     int64_t height = 0;
     uint32_t epoch = 0;
+    uint32_t f = UINT32_MAX;     // quorum events off until hd_votes_set_f
     // signatories seen at this height -> dense id; the per-round logs are
     // arrays over these ids, so a vote costs one probe of this (small, hot)
     // table instead of probes of per-round tables keyed by 32-byte From
@@ -228,7 +232,8 @@ struct hd_votes {
 
     // insertPrevote / insertPrecommit (process.go:823-855, 860-892)
     uint8_t insert(int ti, int64_t h, int64_t r, const Key32& value, const Key32& from, uint32_t origin,
-                   const Logged** prior) {
+                   const Logged** prior, uint8_t* ev) {
+        *ev = 0;
         if (h != height) return HD_VOTE_WRONG_HEIGHT;
         RoundLog* l = get_or_make(r);
         TypeLog& t = l->t[ti];
@@ -248,7 +253,11 @@ struct hd_votes {
         t.counts[*s]++;
         t.len++;
         e = Logged{*s + 1, origin, epoch};
-        l->trace(id);
+        const bool traced = l->trace(id);
+        if (f != UINT32_MAX) {
+            if (t.len == 2 * (uint64_t)f + 1) *ev |= ti == 0 ? HD_VOTE_EV_PREVOTE_2F1 : HD_VOTE_EV_PRECOMMIT_2F1;
+            if (traced && l->trace_len == (uint64_t)f + 1) *ev |= HD_VOTE_EV_TRACE_F1;
+        }
         return HD_VOTE_INSERTED;
     }
 
@@ -280,6 +289,12 @@ int hd_votes_create(int64_t height, hd_votes** out) {
     return HD_OK;
 }
 
+int hd_votes_set_f(hd_votes* v, uint32_t f) {
+    if (!v) return HD_EINVAL;
+    v->f = f;
+    return HD_OK;
+}
+
 int hd_votes_destroy(hd_votes* v) {
     delete v;
     return HD_OK;
@@ -298,26 +313,28 @@ int hd_votes_height(const hd_votes* v, int64_t* height) {
 }
 
 int hd_votes_insert(hd_votes* v, uint8_t type, int64_t height, int64_t round, const uint8_t* value32,
-                    const uint8_t* from32, uint8_t* status, uint8_t* existing_value32) {
+                    const uint8_t* from32, uint8_t* status, uint8_t* existing_value32, uint8_t* events) {
     const int ti = type_ix(type);
     if (!v || ti < 0 || !value32 || !from32 || !status) return HD_EINVAL;
     const Logged* prior = nullptr;
+    uint8_t ev = 0;
     v->epoch++;
     HD_TRY_ALLOC(*status = v->insert(ti, height, round, Key32::load(value32), Key32::load(from32), UINT32_MAX,
-                                     &prior));
+                                     &prior, &ev));
+    if (events) *events = ev;
     if (*status == HD_VOTE_DOUBLE && existing_value32)
         memcpy(existing_value32, v->get(round)->t[ti].values[prior->slot - 1].w, 32);
     return HD_OK;
 }
 
 int hd_votes_insert_batch(hd_votes* v, const hd_batch* b, const uint8_t* verdict, uint8_t* status,
-                          uint32_t* double_of, uint32_t* n_inserted) {
+                          uint32_t* double_of, uint8_t* events, uint32_t* n_inserted) {
     if (!v || !b) return HD_EINVAL;
     if (b->n && (!b->type || !b->height || !b->round || !b->value32 || !b->from32)) return HD_EINVAL;
     const uint32_t epoch = ++v->epoch;
     uint32_t ins = 0;
     for (uint32_t i = 0; i < b->n; ++i) {
-        uint8_t st;
+        uint8_t st, ev = 0;
         uint32_t dof = UINT32_MAX;
         const int ti = type_ix(b->type[i]);
         if (verdict && verdict[i] != HD_VERDICT_VALID) {
@@ -327,20 +344,24 @@ int hd_votes_insert_batch(hd_votes* v, const hd_batch* b, const uint8_t* verdict
         } else {
             const Logged* prior = nullptr;
             HD_TRY_ALLOC(st = v->insert(ti, b->height[i], b->round[i], Key32::load(b->value32 + 32 * size_t(i)),
-                                        Key32::load(b->from32 + 32 * size_t(i)), i, &prior));
+                                        Key32::load(b->from32 + 32 * size_t(i)), i, &prior, &ev));
             if (st == HD_VOTE_INSERTED) ins++;
             if (st == HD_VOTE_DOUBLE && prior->epoch == epoch) dof = prior->origin;
         }
         if (status) status[i] = st;
         if (double_of) double_of[i] = dof;
+        if (events) events[i] = ev;
     }
     if (n_inserted) *n_inserted = ins;
     return HD_OK;
 }
 
-int hd_votes_trace_propose(hd_votes* v, int64_t round, const uint8_t* from32) {
+int hd_votes_trace_propose(hd_votes* v, int64_t round, const uint8_t* from32, uint8_t* events) {
     if (!v || !from32) return HD_EINVAL;
-    HD_TRY_ALLOC(v->get_or_make(round)->trace(v->id_of(Key32::load(from32))));
+    RoundLog* l = nullptr;
+    bool fresh = false;
+    HD_TRY_ALLOC(l = v->get_or_make(round); fresh = l->trace(v->id_of(Key32::load(from32))));
+    if (events) *events = (fresh && v->f != UINT32_MAX && l->trace_len == (uint64_t)v->f + 1) ? HD_VOTE_EV_TRACE_F1 : 0;
     return HD_OK;
 }
 

@@ -30,9 +30,13 @@ def decide(tally, height: int, round_: int, f: int, propose_value: Optional[byte
 
     - timeout_prevote   L34 ``len(PrevoteLogs[r]) >= 2f+1``         process.go:534
     - precommit_nil     L44 #prevotes for NilValue >= 2f+1          process.go:626-632
-    - timeout_precommit_reached  L47 ``len(PrecommitLogs[r]) == 2f+1`` is evaluated
-      by the automaton at the crossing; the batch reports whether the log
-      reached 2f+1                                                  process.go:658
+    - timeout_precommit_reached  L47: the log reached 2f+1 at some insert of
+      the batch (``>=``: true iff the equality ``len == 2f+1`` held at the
+      crossing insert; the per-insert crossing is hd_votes' EV_PRECOMMIT_2F1)
+                                                                    process.go:658
+    - timeout_precommit_exact  L47 as StartRound evaluates it on entering the
+      round: ``len(PrecommitLogs[r]) == 2f+1`` exactly (more than 2f+1
+      buffered precommits never fire it)                   process.go:310, 658
     - skip              L55 |TraceLogs[r]| >= f+1 (votes + valid propose signer) process.go:751
     - precommit_value   L36 #prevotes for propose.Value >= 2f+1     process.go:574-582
     - commit            L49 #precommits for propose.Value >= 2f+1   process.go:696-702
@@ -46,6 +50,7 @@ def decide(tally, height: int, round_: int, f: int, propose_value: Optional[byte
         "timeout_prevote": tally.distinct.get((height, round_, PREVOTE), 0) >= q,
         "precommit_nil": pv(NIL_VALUE) >= q,
         "timeout_precommit_reached": tally.distinct.get((height, round_, PRECOMMIT), 0) >= q,
+        "timeout_precommit_exact": tally.distinct.get((height, round_, PRECOMMIT), 0) == q,
         "skip": tally.distinct_any.get((height, round_), 0) + (1 if propose_signer_new else 0) >= f + 1,
         "precommit_value": False,
         "commit": False,
@@ -69,7 +74,8 @@ def decide_votes(votes, round_: int, f: int, propose_value: Optional[bytes] = No
     out = {
         "timeout_prevote": votes.len(PREVOTE, round_) >= q,                 # process.go:534
         "precommit_nil": votes.count(PREVOTE, round_, NIL_VALUE) >= q,     # 626-632
-        "timeout_precommit_reached": votes.len(PRECOMMIT, round_) >= q,    # 658
+        "timeout_precommit_reached": votes.len(PRECOMMIT, round_) >= q,    # 658 (crossed at some insert)
+        "timeout_precommit_exact": votes.len(PRECOMMIT, round_) == q,      # 310 + 658 (StartRound's ==)
         "skip": votes.trace_len(round_) >= f + 1,                          # 751
         "precommit_value": False,
         "commit": False,

@@ -5,12 +5,26 @@ in the CPU tests).  Verification is embarrassingly parallel per message, so
 rank k verifies the contiguous index range ``shard_range(n, k, world)`` of a
 batch whose metadata is replicated on every rank; the only exchange is an
 all-gather of the per-rank valid bitmaps (n/32 words in total, latency-bound
-over xGMI).  The tally then needs the global first-wins order, so every rank
-tallies the whole batch from the gathered bitmap (hd_tally_device_bitmap).
+over xGMI).
+
+The tally is partitioned too.  First-wins is per (height, round, type,
+signer), so the rank that owns an (height, round) -- ``partition_of`` -- sees
+every duplicate of its keys: rank k tallies only its rounds
+(hd_tally_device_bitmap_part) from the replicated metadata and the gathered
+bitmap, and the small per-rank count tables are all-gathered and merged in
+first-batch-index order (``gather_tally``), which is exactly the single-GPU
+tally's output order.
 """
 from __future__ import annotations
 
-from typing import Tuple
+import ctypes
+from typing import Dict, List, Tuple
+
+import numpy as np
+
+# rows of a packed tally part (int64 columns)
+COUNT_COLS = ("count_height", "count_round", "count_type", "count_rep", "count_n")
+HR_COLS = ("hr_height", "hr_round", "hr_prevotes", "hr_precommits", "hr_any", "hr_rep")
 
 
 def shard_range(n: int, rank: int, world: int, align: int = 32) -> Tuple[int, int]:
@@ -46,3 +60,64 @@ def gather_bitmaps(local_bits, n: int, world: int, group=None):
     dist.all_gather_into_tensor(out, padded, group=group)
     parts = [out[r * width: r * width + per_words[r]] for r in range(world)]
     return torch.cat(parts)[: (n + 31) // 32]
+
+
+def partition_of(height: int, round_: int, nparts: int) -> int:
+    """The rank that tallies (height, round) among nparts
+    (include/hd_verify.h hd_tally_partition_of; a host function of the
+    library, no device needed)."""
+    from . import _lib
+    return int(_lib.load().hd_tally_partition_of(int(height), int(round_), int(nparts)))
+
+
+def tally_part(v, dbatch, d_bitmap: int, part: int, nparts: int, stream=None) -> Dict[str, np.ndarray]:
+    """This rank's partition of the tally of a device batch (all messages,
+    replicated) given the gathered valid bitmap: the packed rows
+    {"counts": [k, 5] int64, "hr": [m, 6] int64} (COUNT_COLS / HR_COLS)."""
+    from . import _lib
+    lib = _lib.load()
+    t, a = v._tally_struct(dbatch.n)
+    rc = lib.hd_tally_device_bitmap_part(v.handle, ctypes.byref(dbatch), d_bitmap, part, nparts, ctypes.byref(t),
+                                         stream)
+    if rc != 0:
+        raise _lib.HDError(rc, "hd_tally_device_bitmap_part", lib.hd_ctx_last_error(v.handle).decode())
+    return pack_tally(a, t.n_counts, t.n_hr)
+
+
+def pack_tally(a, n_counts: int, n_hr: int) -> Dict[str, np.ndarray]:
+    return {"counts": np.stack([a[c][:n_counts].astype(np.int64) for c in COUNT_COLS], 1).reshape(n_counts, 5),
+            "hr": np.stack([a[c][:n_hr].astype(np.int64) for c in HR_COLS], 1).reshape(n_hr, 6)}
+
+
+def merge_tally_parts(parts: List[Dict[str, np.ndarray]]) -> Dict[str, np.ndarray]:
+    """The union of the partitions' rows in first-batch-index order (the
+    order of the unpartitioned hd_tally outputs)."""
+    out = {}
+    for key, rep_col in (("counts", 3), ("hr", 5)):
+        rows = np.concatenate([p[key] for p in parts]) if parts else np.zeros((0, 5 if key == "counts" else 6),
+                                                                               np.int64)
+        out[key] = rows[np.argsort(rows[:, rep_col], kind="stable")]
+    return out
+
+
+def gather_tally(local: Dict[str, np.ndarray], world: int, device=None, group=None) -> Dict[str, np.ndarray]:
+    """All-gather every rank's packed tally partition (sizes first, then the
+    rows padded to the largest) and merge them.  device: where the
+    collective runs (a CUDA device for RCCL, None = CPU for gloo)."""
+    import torch
+    import torch.distributed as dist
+    sizes = torch.tensor([local["counts"].shape[0], local["hr"].shape[0]], dtype=torch.int64, device=device)
+    all_sizes = torch.empty(2 * world, dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(all_sizes, sizes, group=group)
+    all_sizes = all_sizes.view(world, 2).cpu().numpy()
+    parts = [dict() for _ in range(world)]
+    for j, (key, cols) in enumerate((("counts", 5), ("hr", 6))):
+        width = max(1, int(all_sizes[:, j].max()))
+        pad = np.zeros((width, cols), np.int64)
+        pad[: local[key].shape[0]] = local[key]
+        out = torch.empty(world * width * cols, dtype=torch.int64, device=device)
+        dist.all_gather_into_tensor(out, torch.from_numpy(pad.ravel()).to(device), group=group)
+        got = out.view(world, width, cols).cpu().numpy()
+        for r in range(world):
+            parts[r][key] = got[r, : int(all_sizes[r, j])]
+    return merge_tally_parts(parts)

@@ -113,7 +113,10 @@ class Verifier:
     """One context per caller thread (the reference's Process is
     single-goroutine, process/process.go:100-101)."""
 
-    def __init__(self, device: int = 0, compressed: bool = True):
+    def __init__(self, device: int = 0, compressed=True):
+        """compressed: the pubkey encoding of id.NewSignatory -- True / 1 SEC1
+        compressed (33 B, default), False / 0 SEC1 uncompressed (65 B),
+        2 raw X || Y (64 B) (include/hd_verify.h HD_PUBKEY_*)."""
         self._lib = _lib.load()
         h = ctypes.c_void_p()
         rc = self._lib.hd_ctx_create(device, ctypes.byref(h))
@@ -123,7 +126,7 @@ class Verifier:
         self._close_rank = 1          # closed after the queues / tables that use it
         _lib.track(self)
         self.device = device
-        self._check(self._lib.hd_ctx_set_pubkey_format(self._ctx, 1 if compressed else 0), "set_pubkey_format")
+        self._check(self._lib.hd_ctx_set_pubkey_format(self._ctx, int(compressed)), "set_pubkey_format")
         self.n_signatories = 0
 
     def _check(self, rc: int, where: str):
@@ -160,6 +163,20 @@ class Verifier:
     def set_fastpath(self, enable: bool) -> None:
         """Known-key fast path on/off (include/hd_verify.h hd_ctx_set_fastpath)."""
         self._check(self._lib.hd_ctx_set_fastpath(self._ctx, 1 if enable else 0), "hd_ctx_set_fastpath")
+
+    def profile(self, enable: bool) -> None:
+        """Record HIP events around every verify call and its k_fast_sums
+        launch (include/hd_verify.h hd_ctx_profile)."""
+        self._check(self._lib.hd_ctx_profile(self._ctx, 1 if enable else 0), "hd_ctx_profile")
+
+    def profile_read(self):
+        """(calls, verify ms summed, k_fast_sums launches, their ms summed)
+        since the last read."""
+        c, s = ctypes.c_uint32(), ctypes.c_uint32()
+        vm, sm = ctypes.c_double(), ctypes.c_double()
+        self._check(self._lib.hd_ctx_profile_read(self._ctx, ctypes.byref(c), ctypes.byref(vm), ctypes.byref(s),
+                                                  ctypes.byref(sm)), "hd_ctx_profile_read")
+        return c.value, vm.value, s.value, sm.value
 
     def fastpath_stats(self) -> Tuple[int, int]:
         """(signatories with built key tables, messages of the last verify
@@ -205,7 +222,7 @@ class Verifier:
             count_n=np.zeros(max(n, 1), np.uint32), hr_height=np.zeros(max(n, 1), np.int64),
             hr_round=np.zeros(max(n, 1), np.int64), hr_prevotes=np.zeros(max(n, 1), np.uint32),
             hr_precommits=np.zeros(max(n, 1), np.uint32), hr_any=np.zeros(max(n, 1), np.uint32),
-            dup=np.zeros(max(n, 1), np.uint8))
+            dup=np.zeros(max(n, 1), np.uint8), hr_rep=np.zeros(max(n, 1), np.uint32))
         t = HdTallyOut()
         t.cap_counts = n
         t.cap_hr = n

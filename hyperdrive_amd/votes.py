@@ -10,6 +10,10 @@ process.go (L28/L36/L44/L47/L49/L55) are O(1) lookups instead of O(n) loops:
     v.trace_propose(r, frm)                  # valid propose signer -> TraceLogs
     v.count(PREVOTE, r, value); v.len(PRECOMMIT, r); v.trace_len(r)
     v.reset(h + 1)                           # new height (process.go:718-724)
+
+With ``set_f(f)``, each insert also reports the thresholds it made a log reach
+exactly (``last_events``; EV_PRECOMMIT_2F1 is L47's equality crossing,
+process.go:658).
 """
 from __future__ import annotations
 
@@ -22,6 +26,7 @@ from . import _lib
 from .verify import PRECOMMIT, PREVOTE, Batch, _ptr
 
 INSERTED, WRONG_HEIGHT, DUPLICATE, DOUBLE, NOT_VOTE, SKIPPED = range(6)
+EV_PREVOTE_2F1, EV_PRECOMMIT_2F1, EV_TRACE_F1 = 1, 2, 4     # include/hd_votes.h HD_VOTE_EV_*
 STATUS_NAMES = ["INSERTED", "WRONG_HEIGHT", "DUPLICATE", "DOUBLE", "NOT_VOTE", "SKIPPED"]
 NO_INDEX = 0xFFFFFFFF
 
@@ -39,6 +44,7 @@ class VoteLog:
         h = ctypes.c_void_p()
         self._check(self._lib.hd_votes_create(int(height), ctypes.byref(h)), "hd_votes_create")
         self._v = h
+        self.last_events = 0      # HD_VOTE_EV_* of the last insert / trace_propose (array after insert_batch)
         _lib.track(self)
 
     def _check(self, rc: int, where: str):
@@ -62,15 +68,20 @@ class VoteLog:
         self._check(self._lib.hd_votes_height(self._v, ctypes.byref(h)), "hd_votes_height")
         return h.value
 
+    def set_f(self, f: int) -> None:
+        """f for the quorum-crossing events (len(signatories) // 3)."""
+        self._check(self._lib.hd_votes_set_f(self._v, int(f)), "hd_votes_set_f")
+
     def reset(self, height: int) -> None:
         self._check(self._lib.hd_votes_reset(self._v, int(height)), "hd_votes_reset")
 
     def insert(self, mtype: int, height: int, round_: int, value, frm) -> Tuple[int, Optional[bytes]]:
         """(status, logged value if status == DOUBLE else None)."""
-        st = ctypes.c_uint8()
+        st, ev = ctypes.c_uint8(), ctypes.c_uint8()
         prev = ctypes.create_string_buffer(32)
         self._check(self._lib.hd_votes_insert(self._v, mtype, int(height), int(round_), _b32(value), _b32(frm),
-                                              ctypes.byref(st), prev), "hd_votes_insert")
+                                              ctypes.byref(st), prev, ctypes.byref(ev)), "hd_votes_insert")
+        self.last_events = ev.value
         return st.value, (prev.raw if st.value == DOUBLE else None)
 
     def insert_batch(self, batch: Batch, verdict: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray]:
@@ -80,6 +91,7 @@ class VoteLog:
         n = len(batch)
         status = np.zeros(n, np.uint8)
         double_of = np.zeros(n, np.uint32)
+        events = np.zeros(n, np.uint8)
         if verdict is not None:
             verdict = np.ascontiguousarray(verdict, np.uint8)
             if len(verdict) != n:
@@ -87,11 +99,16 @@ class VoteLog:
         cs = batch.c_struct()
         ins = ctypes.c_uint32()
         self._check(self._lib.hd_votes_insert_batch(self._v, ctypes.byref(cs), _ptr(verdict), _ptr(status),
-                                                    _ptr(double_of), ctypes.byref(ins)), "hd_votes_insert_batch")
+                                                    _ptr(double_of), _ptr(events), ctypes.byref(ins)),
+                    "hd_votes_insert_batch")
+        self.last_events = events
         return status, double_of
 
     def trace_propose(self, round_: int, frm) -> None:
-        self._check(self._lib.hd_votes_trace_propose(self._v, int(round_), _b32(frm)), "hd_votes_trace_propose")
+        ev = ctypes.c_uint8()
+        self._check(self._lib.hd_votes_trace_propose(self._v, int(round_), _b32(frm), ctypes.byref(ev)),
+                    "hd_votes_trace_propose")
+        self.last_events = ev.value
 
     def count(self, mtype: int, round_: int, value) -> int:
         n = ctypes.c_uint32()
@@ -118,4 +135,4 @@ class VoteLog:
 
 
 __all__ = ["VoteLog", "PREVOTE", "PRECOMMIT", "INSERTED", "WRONG_HEIGHT", "DUPLICATE", "DOUBLE", "NOT_VOTE",
-           "SKIPPED", "NO_INDEX", "STATUS_NAMES"]
+           "SKIPPED", "NO_INDEX", "STATUS_NAMES", "EV_PREVOTE_2F1", "EV_PRECOMMIT_2F1", "EV_TRACE_F1"]

@@ -85,9 +85,16 @@ typedef struct {
 /* ---- context --------------------------------------------------------- */
 int hd_ctx_create(int device, hd_ctx** out);
 int hd_ctx_destroy(hd_ctx* ctx);
-/* 1 (default): signatory = SHA-256(33-byte compressed pubkey);
- * 0: SHA-256(65-byte uncompressed pubkey).  [renproject/id v0.4.2] */
-int hd_ctx_set_pubkey_format(hd_ctx* ctx, int compressed);
+/* The pubkey encoding id.NewSignatory hashes [renproject/id v0.4.2; not
+ * confirmable in this container, SURVEY §8(c)]:
+ *   HD_PUBKEY_COMPRESSED   (1, default) SHA-256(02|03 || X), 33 bytes
+ *   HD_PUBKEY_UNCOMPRESSED (0)          SHA-256(04 || X || Y), 65 bytes
+ *   HD_PUBKEY_RAW64        (2)          SHA-256(X || Y), 64 bytes (X, Y 32-byte big-endian)
+ * Changing it drops the learned keys of the known-key fast path. */
+#define HD_PUBKEY_UNCOMPRESSED 0
+#define HD_PUBKEY_COMPRESSED 1
+#define HD_PUBKEY_RAW64 2
+int hd_ctx_set_pubkey_format(hd_ctx* ctx, int format);
 /* Admitted set = procsAllowed.  sigs32: n x 32 bytes, any order, duplicates
  * allowed.  Signer indices reported by the library index this array. */
 int hd_set_signatories(hd_ctx* ctx, const uint8_t* sigs32, uint32_t n);
@@ -112,6 +119,15 @@ int hd_ctx_fastpath_stats(hd_ctx* ctx, uint32_t* known_keys, uint32_t* last_fall
  * each kind (8 or 16 for the split check, 2 for the paired kernel).
  * Host-only (no device access); any pointer may be NULL. */
 int hd_ctx_fastpath_geometry(hd_ctx* ctx, int* g_windows, int* key_windows, int* msgs_per_inversion);
+/* Device-time profile for roofline reports.  While enabled, every verify
+ * call of the context records HIP events on its stream around the whole call
+ * and around the known-key check's sums kernel (k_fast_sums, the dominant
+ * kernel).  hd_ctx_profile_read waits for the recorded events, returns the
+ * calls recorded since the last read with their summed milliseconds (either
+ * pointer may be NULL; sums_ms covers the calls that ran the kernel, counted
+ * in *sums_launches) and clears the record. */
+int hd_ctx_profile(hd_ctx* ctx, int enable);
+int hd_ctx_profile_read(hd_ctx* ctx, uint32_t* calls, double* verify_ms, uint32_t* sums_launches, double* sums_ms);
 
 /* ---- verification ------------------------------------------------------
  * verdict:     n bytes (HD_VERDICT_*), required.
@@ -125,7 +141,9 @@ int hd_verify_batch(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8_
 /* Same, with every pointer (batch fields and outputs) in device memory of the
  * ctx's device; signer (n x int32 or NULL) receives the index of From in the
  * hd_set_signatories array for VALID messages, -1 otherwise.  Enqueued on
- * `stream` (a hipStream_t, NULL = the ctx's stream); asynchronous. */
+ * `stream` (a hipStream_t, NULL = the ctx's stream); asynchronous.  Calls on
+ * one context share its scratch: a call on another stream than the previous
+ * call's first waits (on the device) for that call to finish. */
 int hd_verify_batch_device(hd_ctx* ctx, const hd_batch* dbatch, uint8_t* d_verdict, uint8_t* d_recovered32,
                            int32_t* d_signer, uint32_t* d_valid_bitmap, void* stream);
 
@@ -135,7 +153,10 @@ int hd_verify_batch_device(hd_ctx* ctx, const hd_batch* dbatch, uint8_t* d_verdi
  * (first-wins, process.go:834-847); later ones are duplicates: identical
  * value -> dropped silently, different value -> what the reference hands to
  * Catcher.CatchDoublePrevote/Precommit (process.go:838-843, 875-880).
- * All output arrays are caller-owned with the given capacities. */
+ * All output arrays are caller-owned with the given capacities.
+ * Values are grouped by their 32 bytes themselves (count_rep names a message
+ * carrying the value), so the caller-interned value_id argument SURVEY §8(b)
+ * sketches is not needed and not taken. */
 typedef struct {
     /* (height, round, type, value) groups, in the batch order of each group's
      * first message (deterministic) */
@@ -156,23 +177,36 @@ typedef struct {
     uint32_t* hr_precommits; /* len(PrecommitLogs[r]) */
     uint32_t* hr_any;        /* distinct vote signers (TraceLogs[r] without proposes) */
     /* n bytes or NULL: 0 logged, 1 identical duplicate, 2 conflicting
-     * duplicate (double vote), 3 not a candidate */
+     * duplicate (double vote), 3 not a candidate (of this partition) */
     uint8_t* dup;
+    /* cap_hr entries or NULL: batch index of each round's first candidate */
+    uint32_t* hr_rep;
 } hd_tally_out;
 
 int hd_tally(hd_ctx* ctx, const hd_batch* batch, const uint8_t* verdict, hd_tally_out* out);
 
-/* Same on device-resident inputs (pointers as in hd_verify_batch_device);
- * d_signer is accepted for ABI stability and ignored: the logs are keyed by
- * From itself, which equals the recovered signatory of every VALID message.
- * Results land in the host arrays of `out`; synchronises `stream`. */
-int hd_tally_device(hd_ctx* ctx, const hd_batch* dbatch, const uint8_t* d_verdict, const int32_t* d_signer,
-                    hd_tally_out* out, void* stream);
+/* Same on device-resident inputs (pointers as in hd_verify_batch_device).
+ * The logs are keyed by From itself, which equals the recovered signatory of
+ * every VALID message.  Results land in the host arrays of `out`;
+ * synchronises `stream`. */
+int hd_tally_device(hd_ctx* ctx, const hd_batch* dbatch, const uint8_t* d_verdict, hd_tally_out* out, void* stream);
 
 /* Same, with validity given as the valid bitmap of hd_verify_batch_device
  * (e.g. after an all-gather of per-GPU bitmaps over RCCL). */
 int hd_tally_device_bitmap(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* d_valid_bitmap, hd_tally_out* out,
                            void* stream);
+
+/* Partitioned tally for G GPUs: only candidates with
+ * hd_tally_partition_of(height, round, nparts) == part are tallied.
+ * First-wins is per (height, round, type, signer), so the owner of an
+ * (height, round) sees every duplicate of its keys and the partitions' groups
+ * are exactly the unpartitioned tally's: their union, ordered by count_rep /
+ * hr_rep, is the single-GPU output, and dup merges by taking the minimum over
+ * partitions (a non-owner reports 3). */
+int hd_tally_device_bitmap_part(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* d_valid_bitmap, uint32_t part,
+                                uint32_t nparts, hd_tally_out* out, void* stream);
+/* the partition of an (height, round) among nparts (host function) */
+uint32_t hd_tally_partition_of(int64_t height, int64_t round, uint32_t nparts);
 
 /* verify + tally with one upload of the batch */
 int hd_process_batch(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8_t* recovered32,

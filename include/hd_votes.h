@@ -11,6 +11,15 @@
  *   T2/T5        len(PrevoteLogs[r]) / len(PrecommitLogs[r])  hd_votes_len
  *   T7           len(TraceLogs[r])                         hd_votes_trace_len
  *
+ * and, with f set (hd_votes_set_f), each insert reports the thresholds it
+ * made a log reach exactly (HD_VOTE_EV_*).  L47 is an EQUALITY,
+ * len(PrecommitLogs[CurrentRound]) == 2f+1 (process.go:658), tried after every
+ * precommit insert (process.go:268) and at StartRound (process.go:310): it
+ * fires on the insert that makes the log exactly 2f+1 when that round is the
+ * current one, and a round entered with more than 2f+1 buffered precommits
+ * never fires it.  A batch insert loses the intermediate lengths, so the
+ * crossing is reported per message.
+ *
  * Insertion follows insertPrevote / insertPrecommit (process.go:823-892):
  * accepted iff height == the table's height; first wins per (round, From); a
  * later vote from the same From in the same round is an identical duplicate
@@ -46,8 +55,16 @@ typedef struct hd_votes hd_votes;
 #define HD_VOTE_NOT_VOTE 4     /* type is not Prevote/Precommit (batch insert only)     */
 #define HD_VOTE_SKIPPED 5      /* verdict != VALID (batch insert only)                  */
 
+/* quorum events of one insert (bit mask) */
+#define HD_VOTE_EV_PREVOTE_2F1 1u   /* len(PrevoteLogs[r]) became 2f+1 (L34's >= first true, process.go:534)  */
+#define HD_VOTE_EV_PRECOMMIT_2F1 2u /* len(PrecommitLogs[r]) became 2f+1: L47's == (process.go:658)        */
+#define HD_VOTE_EV_TRACE_F1 4u      /* len(TraceLogs[r]) became f+1 (L55's >= first true, process.go:751)   */
+
 /* an empty table for `height` (NewProcess / State, state.go:66-78) */
 int hd_votes_create(int64_t height, hd_votes** out);
+/* f of the quorum events (replica.go:54, 138: len(signatories) / 3;
+ * UINT32_MAX, the initial value, reports none).  Kept across resets. */
+int hd_votes_set_f(hd_votes* v, uint32_t f);
 int hd_votes_destroy(hd_votes* v);
 
 /* empty every log and move to `height`: the reset of
@@ -57,21 +74,25 @@ int hd_votes_reset(hd_votes* v, int64_t height);
 int hd_votes_height(const hd_votes* v, int64_t* height);
 
 /* insertPrevote / insertPrecommit of one vote.  existing_value32 (may be
- * NULL) receives the logged value when *status == HD_VOTE_DOUBLE. */
+ * NULL) receives the logged value when *status == HD_VOTE_DOUBLE; events
+ * (may be NULL) the HD_VOTE_EV_* this insert caused. */
 int hd_votes_insert(hd_votes* v, uint8_t type, int64_t height, int64_t round, const uint8_t* value32,
-                    const uint8_t* from32, uint8_t* status, uint8_t* existing_value32);
+                    const uint8_t* from32, uint8_t* status, uint8_t* existing_value32, uint8_t* events);
 
 /* the votes of a HOST batch in batch (= arrival) order: message i is
  * inserted iff verdict == NULL or verdict[i] == HD_VERDICT_VALID, and its
  * type is Prevote or Precommit.  status (N, may be NULL) gets each message's
  * HD_VOTE_*; double_of (N, may be NULL) gets, for HD_VOTE_DOUBLE, the batch
  * index of the logged vote if it came from this batch, else UINT32_MAX;
+ * events (N, may be NULL) gets each message's HD_VOTE_EV_* mask;
  * *n_inserted (may be NULL) counts HD_VOTE_INSERTED. */
 int hd_votes_insert_batch(hd_votes* v, const hd_batch* batch, const uint8_t* verdict, uint8_t* status,
-                          uint32_t* double_of, uint32_t* n_inserted);
+                          uint32_t* double_of, uint8_t* events, uint32_t* n_inserted);
 
-/* TraceLogs[round][from] = true for an accepted VALID propose (process.go:810-815) */
-int hd_votes_trace_propose(hd_votes* v, int64_t round, const uint8_t* from32);
+/* TraceLogs[round][from] = true for an accepted VALID propose
+ * (process.go:810-815); events (may be NULL): HD_VOTE_EV_TRACE_F1 if this
+ * made the trace reach f+1 */
+int hd_votes_trace_propose(hd_votes* v, int64_t round, const uint8_t* from32, uint8_t* events);
 
 /* #votes of `type` in `round` whose value equals value32 (T1/T3/T4/T6) */
 int hd_votes_count(const hd_votes* v, uint8_t type, int64_t round, const uint8_t* value32, uint32_t* n);

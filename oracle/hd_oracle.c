@@ -13,7 +13,8 @@
  *   - digest preimage + SHA-256: process/message.go:53-78, 165-186, 263-284
  *   - recovery: go-ethereum v1.9.5 crypto/secp256k1 (checkSignature V < 4) ->
  *     libsecp256k1 parse_compact / ecdsa_sig_recover; high-S accepted
- *   - signatory: SHA-256 of SEC1 compressed (or uncompressed) pubkey
+ *   - signatory: SHA-256 of the pubkey encoding `compressed` selects:
+ *     1 SEC1 compressed (33 B), 0 SEC1 uncompressed (65 B), 2 raw X || Y (64 B)
  *     [renproject/id v0.4.2]
  *   - membership: procsAllowed at mq/mq.go:49-51
  * Parity anchoring: tests/test_oracle.py (KATs + OpenSSL + pyoracle).
@@ -481,10 +482,14 @@ static void* run_job(void* arg) {
         if (v != V_VALID) { j->verdict[i] = (uint8_t)v; continue; }
         uint8_t pk[65], sg[32];
         size_t pl;
-        if (j->compressed) {
+        if (j->compressed == 1) {
             pk[0] = 2 | (uint8_t)(qy.v[0] & 1);
             u256_to_be(pk + 1, &qx);
             pl = 33;
+        } else if (j->compressed == 2) {
+            u256_to_be(pk, &qx);
+            u256_to_be(pk + 32, &qy);
+            pl = 64;
         } else {
             pk[0] = 4;
             u256_to_be(pk + 1, &qx);

@@ -17,7 +17,8 @@ What it restates (reference = tuanggolt/hyperdrive @ /root/reference, Go):
   261, 324``) = go-ethereum v1.9.5 ``crypto.SigToPub`` -> cgo libsecp256k1
   ``secp256k1_ext_ecdsa_recover`` semantics, restated in ``recover()`` below,
   followed by ``id.NewSignatory`` = SHA-256 over the SEC1 *compressed* pubkey
-  (33 B; ``compressed=False`` switches to the 65 B uncompressed encoding).
+  (33 B; ``compressed=False`` switches to the 65 B uncompressed encoding,
+  ``compressed=2`` to the raw 64 B X || Y).
 * ``id.PrivKey.Sign`` (``message_test.go:150``) = libsecp256k1
   ``secp256k1_ecdsa_sign_recoverable`` with the RFC6979 HMAC-SHA256 nonce,
   low-S normalisation, V = recid.  Used only to build inputs.
@@ -150,8 +151,16 @@ def lift_x(x: int, odd: int) -> Point:
     return (x, y)
 
 
-def pubkey_bytes(q: Tuple[int, int], compressed: bool = True) -> bytes:
+PUBKEY_UNCOMPRESSED, PUBKEY_COMPRESSED, PUBKEY_RAW64 = 0, 1, 2   # include/hd_verify.h HD_PUBKEY_*
+
+
+def pubkey_bytes(q: Tuple[int, int], compressed=True) -> bytes:
+    """The pubkey encoding id.NewSignatory hashes.  `compressed`: True / 1 =
+    SEC1 compressed (33 B), False / 0 = SEC1 uncompressed (65 B), 2 = raw
+    X || Y (64 B)."""
     x, y = q
+    if int(compressed) == PUBKEY_RAW64:
+        return x.to_bytes(32, "big") + y.to_bytes(32, "big")
     if compressed:
         return bytes([2 | (y & 1)]) + x.to_bytes(32, "big")
     return b"\x04" + x.to_bytes(32, "big") + y.to_bytes(32, "big")
@@ -539,8 +548,13 @@ def decide_round(t: Tally, h: int, r: int, f: int, propose_value: Optional[bytes
         "timeout_prevote": t.distinct.get((h, r, PREVOTE), 0) >= q,
         # L44 process.go:626-632
         "precommit_nil": pv(NIL_VALUE) >= q,
-        # L47 process.go:658 (equality: fires on the exact crossing)
+        # L47 process.go:658 is `len(PrecommitLogs[cur]) == 2f+1`, tried after
+        # every precommit insert: over a batch's final logs it held at some
+        # insert iff the final length is >= 2f+1 ("reached") ...
         "timeout_precommit_reached": t.distinct.get((h, r, PRECOMMIT), 0) >= q,
+        # ... while StartRound (process.go:310) evaluates it once on entering
+        # the round: only exactly 2f+1 buffered precommits fire it ("exact")
+        "timeout_precommit_exact": t.distinct.get((h, r, PRECOMMIT), 0) == q,
         # L55 process.go:751 (votes plus a valid propose from a new signer)
         "skip": t.distinct_any.get((h, r), 0) + (1 if propose_signer_new else 0) >= f + 1,
         "precommit_value": False,

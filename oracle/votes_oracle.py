@@ -16,6 +16,10 @@ product never imports it.
   counts        process.go:486-491 (L28), 574-579 (L36), 626-631 (L44),
                 696-701 (L49): a loop over the round's log comparing values
   lengths       process.go:534 (L34), 658 (L47), 751 (L55)
+  crossings     with f set: the insert that makes len(PrecommitLogs[r]) ==
+                2f+1 (L47's equality, tried after every precommit insert,
+                process.go:268), len(PrevoteLogs[r]) == 2f+1 (L34) or
+                |TraceLogs[r]| == f+1 (L55) reports it (last_events)
   reset         process.go:718-724         every log emptied at a new height
 
 A vote is (value: bytes32); Prevote.Equal compares height, round, value and
@@ -28,10 +32,13 @@ from typing import Dict, Optional, Tuple
 
 PREVOTE, PRECOMMIT = 2, 3
 INSERTED, WRONG_HEIGHT, DUPLICATE, DOUBLE = 0, 1, 2, 3
+EV_PREVOTE_2F1, EV_PRECOMMIT_2F1, EV_TRACE_F1 = 1, 2, 4
 
 
 class VoteLogs:
-    def __init__(self, height: int = 0):
+    def __init__(self, height: int = 0, f: Optional[int] = None):
+        self.f = f
+        self.last_events = 0
         self.reset(height)
 
     def reset(self, height: int) -> None:
@@ -40,6 +47,7 @@ class VoteLogs:
         self.trace: Dict[int, Dict[bytes, bool]] = {}
 
     def insert(self, mtype: int, height: int, round_: int, value: bytes, frm: bytes) -> Tuple[int, Optional[bytes]]:
+        self.last_events = 0
         if height != self.height:
             return WRONG_HEIGHT, None
         log = self.logs[mtype].setdefault(round_, {})
@@ -47,11 +55,21 @@ class VoteLogs:
             prior = log[frm]
             return (DUPLICATE, None) if prior == value else (DOUBLE, prior)
         log[frm] = value
-        self.trace.setdefault(round_, {})[frm] = True
+        tr = self.trace.setdefault(round_, {})
+        fresh = frm not in tr
+        tr[frm] = True
+        if self.f is not None:
+            if len(log) == 2 * self.f + 1:                    # process.go:534 / 658
+                self.last_events |= EV_PREVOTE_2F1 if mtype == PREVOTE else EV_PRECOMMIT_2F1
+            if fresh and len(tr) == self.f + 1:               # process.go:751
+                self.last_events |= EV_TRACE_F1
         return INSERTED, None
 
     def trace_propose(self, round_: int, frm: bytes) -> None:
-        self.trace.setdefault(round_, {})[frm] = True
+        tr = self.trace.setdefault(round_, {})
+        fresh = frm not in tr
+        tr[frm] = True
+        self.last_events = EV_TRACE_F1 if (self.f is not None and fresh and len(tr) == self.f + 1) else 0
 
     def count(self, mtype: int, round_: int, value: bytes) -> int:
         n = 0

@@ -41,12 +41,14 @@ sys.path.insert(0, ROOT)
 
 import hd_pyoracle as O  # noqa: E402
 
-# (name, generator kind, n, signatories, adversarial %, start, compressed)
+# (name, generator kind, n, signatories, adversarial %, start, pubkey format:
+#  True = SEC1 compressed, False = SEC1 uncompressed, 2 = raw X || Y)
 CASES = [
     ("votes_allclasses", O.GEN_VOTES, 260, 10, 100, 0, True),
     ("votes_mix30", O.GEN_VOTES, 200, 10, 30, 0, True),
     ("rounds_mix40", O.GEN_ROUNDS, 150, 7, 40, 0, True),
     ("votes_uncompressed", O.GEN_VOTES, 120, 10, 60, 0, False),
+    ("votes_raw64", O.GEN_VOTES, 120, 10, 60, 0, O.PUBKEY_RAW64),
     ("votes_100signers_tail", O.GEN_VOTES, 64, 100, 30, 999_936, True),
 ]
 

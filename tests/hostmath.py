@@ -90,7 +90,7 @@ class HostMath:
     def keys(self, S: int, compressed: bool = True):
         sigs = np.zeros((S, 32), np.uint8)
         foreign = np.zeros((16, 32), np.uint8)
-        self.L.hdh_keys(S, 1 if compressed else 0, _p(sigs), _p(foreign))
+        self.L.hdh_keys(S, int(compressed), _p(sigs), _p(foreign))
         return sigs, foreign
 
     def gen(self, kind: int, start: int, n: int, S: int, adv_pct: int, keys):
@@ -115,6 +115,6 @@ class HostMath:
         sgn = np.zeros(n, np.int32)
         adm = np.ascontiguousarray(admitted_sorted, dtype=np.uint8).reshape(-1, 32)
         self.L.hdh_verify(n, _p(batch.type), _p(batch.height), _p(batch.round), _p(batch.valid_round),
-                          _p(batch.value), _p(batch.frm), _p(batch.sig), _p(adm), len(adm), 1 if compressed else 0,
+                          _p(batch.value), _p(batch.frm), _p(batch.sig), _p(adm), len(adm), int(compressed),
                           _p(ver), _p(rec), _p(sgn))
         return ver, rec, sgn

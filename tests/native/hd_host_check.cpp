@@ -116,7 +116,7 @@ void hdh_keys(uint32_t S, int compressed, uint8_t* sigs32, uint8_t* foreign32) {
         sc sk;
         signer_sk(sk, idx);
         uint32_t o[8];
-        pubkey_signatory(o, sk, compressed != 0, gtab());
+        pubkey_signatory(o, sk, compressed, gtab());
         uint8_t* dst = j < S ? sigs32 + 32 * j : foreign32 + 32 * (j - S);
         for (int i = 0; i < 8; i++) store_be32(dst + 4 * i, o[i]);
     }
@@ -158,7 +158,7 @@ int hdh_verify(uint32_t n, const uint8_t* type, const int64_t* h, const int64_t*
         m.v = sig65[65 * (size_t)i + 64];
         uint32_t rec[8];
         int32_t s;
-        verdict[i] = verify_msg(m, gtab(), aw.data(), n_adm, steps, compressed != 0, rec, s);
+        verdict[i] = verify_msg(m, gtab(), aw.data(), n_adm, steps, compressed, rec, s);
         signer[i] = s;
         for (int w = 0; w < 8; w++) store_be32(rec32 + 32 * (size_t)i + 4 * w, rec[w]);
     }

@@ -45,6 +45,6 @@ class COracle:
         adm = np.ascontiguousarray(admitted, dtype=np.uint8).reshape(-1, 32)
         rc = self.lib.oracle_verify_batch(n, _p(batch.type), _p(batch.height), _p(batch.round),
                                           _p(batch.valid_round), _p(batch.value), _p(batch.frm), _p(batch.sig),
-                                          _p(adm), len(adm), 1 if compressed else 0, _p(verdict), _p(rec), threads)
+                                          _p(adm), len(adm), int(compressed), _p(verdict), _p(rec), threads)
         assert rc == 0
         return verdict, rec

@@ -66,6 +66,19 @@ def scenarios(seed: int = 1):
         s.expect.append((5, 1, v, True, {"commit": True, "timeout_precommit_reached": True}))
         s.expect.append((5, 1, v, False, {"commit": False}))   # invalid propose never commits (687-694)
         out.append(s)
+        # a round holding more than 2f+1 precommits: StartRound's L47 equality
+        # (process.go:310, 658) does not fire, though the log passed 2f+1
+        s = Scenario(f"precommits_over_2f1_f{f}", f)
+        for k in range(2 * f + 3):
+            s.vote(PC, 6, 2, k, v)
+        s.expect.append((6, 2, v, True, {"timeout_precommit_reached": True, "timeout_precommit_exact": False}))
+        out.append(s)
+        s = Scenario(f"precommits_exact_2f1_f{f}", f)
+        for k in range(2 * f + 1):
+            s.vote(PC, 6, 2, k, O.canonical_value(6, 7) if k % 3 == 0 else v)
+        s.expect.append((6, 2, v, True, {"timeout_precommit_reached": True, "timeout_precommit_exact": True,
+                                         "commit": False}))
+        out.append(s)
         s = Scenario(f"mixed_f{f}", f)
         for k in range(2 * f + 1):
             s.vote(PC, 5, 1, k, v if k % 2 == 0 else O.canonical_value(5, 99))

@@ -37,7 +37,7 @@ def tally_from_json(tj):
 
 
 def test_golden_cases_present():
-    assert len(CASES) >= 6, CASES
+    assert len(CASES) >= 7, CASES
 
 
 def test_kats(oracle, coracle):
@@ -59,7 +59,7 @@ def test_kats(oracle, coracle):
 @pytest.mark.parametrize("name", CASES)
 def test_c_oracle_and_host_headers_reproduce_fixture(coracle, hostmath, name):
     b, z, _ = load_case(name)
-    compressed = bool(z["compressed"])
+    compressed = int(z["compressed"])
     cv, crec = coracle.verify(b, z["admitted"], compressed, threads=4)
     assert cv.tolist() == z["verdict"].tolist()
     assert crec.tobytes() == z["recovered"].tobytes()
@@ -74,7 +74,7 @@ def test_python_oracle_reproduces_fixture(oracle, name):
     b, z, tj = load_case(name)
     ob = from_np(b)
     adm = [bytes(r) for r in z["admitted"]]
-    vs, recs = oracle.verify_batch(ob, adm, bool(z["compressed"]))
+    vs, recs = oracle.verify_batch(ob, adm, int(z["compressed"]))
     assert vs == z["verdict"].tolist()
     assert b"".join(recs) == z["recovered"].tobytes()
 
@@ -97,24 +97,45 @@ def test_fixture_tally_and_openssl(oracle, name):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", CASES)
 def test_gpu_matches_golden(gpu, name):
+    """Each fixture is verified twice on one context.  Pass 1 finds no known
+    key, so every message takes the full recovery, which teaches the context
+    the keys of the admitted signers it saw VALID.  Pass 2 then runs the
+    known-key check (hd_fixedbase.h) on those signers' messages: its fallback
+    count may not exceed the fixture's non-VALID messages plus the VALID ones
+    of signers it could not have learned, and both passes must equal the
+    golden verdicts, recovered signatories, bitmap, tally and decisions."""
     from hyperdrive_amd import quorum
     b, z, tj = load_case(name)
-    v = gpu.Verifier(0, compressed=bool(z["compressed"]))
+    v = gpu.Verifier(0, compressed=int(z["compressed"]))
     try:
         v.set_signatories(z["admitted"])
-        res, tal = v.process_batch(b)
-        assert res.verdict.tolist() == z["verdict"].tolist()
-        assert res.recovered.tobytes() == z["recovered"].tobytes()
-        bits = np.unpackbits(res.valid_bitmap.view(np.uint8), bitorder="little")[: len(b)]
-        assert bits.tolist() == (z["verdict"] == 0).astype(int).tolist()
-        count, distinct, distinct_any, dup = tally_from_json(tj)
-        assert tal.count == count
-        assert tal.distinct == distinct
-        assert tal.distinct_any == distinct_any
-        assert tal.dup.tolist() == dup
-        for d in tj["decisions"]:
-            pv = bytes.fromhex(d["propose_value"]) if d["propose_value"] else None
-            got = quorum.decide(tal, d["h"], d["r"], tj["f"], pv, pv is not None)
-            assert got == d["decision"], d
+        for rnd in range(2):
+            res, tal = v.process_batch(b)
+            assert res.verdict.tolist() == z["verdict"].tolist(), rnd
+            assert res.recovered.tobytes() == z["recovered"].tobytes(), rnd
+            bits = np.unpackbits(res.valid_bitmap.view(np.uint8), bitorder="little")[: len(b)]
+            assert bits.tolist() == (z["verdict"] == 0).astype(int).tolist()
+            count, distinct, distinct_any, dup = tally_from_json(tj)
+            assert tal.count == count
+            assert tal.distinct == distinct
+            assert tal.distinct_any == distinct_any
+            assert tal.dup.tolist() == dup
+            for d in tj["decisions"]:
+                pv = bytes.fromhex(d["propose_value"]) if d["propose_value"] else None
+                got = quorum.decide(tal, d["h"], d["r"], tj["f"], pv, pv is not None)
+                assert got == d["decision"], d
+            known, fallback = v.fastpath_stats()
+            valid = z["verdict"] == 0
+            if rnd == 0:
+                # every VALID signer's key is learned from its first VALID message
+                learned = len({b.frm[i].tobytes() for i in np.flatnonzero(valid)})
+                assert known == learned
+                assert fallback == len(b) - int((z["verdict"] == 7).sum())    # BAD_TYPE is decided up front
+            else:
+                # the known-key check decided every VALID message (a zero
+                # window digit, ~2^-20 per message, would also fall back)
+                assert fallback <= int((~valid).sum()), (fallback, int((~valid).sum()))
+                if valid.any():
+                    assert fallback < len(b)
     finally:
         v.close()

@@ -116,3 +116,48 @@ def test_bitmap_entry_equals_verdict_entry(verifier, oracle):
     got = verifier._tally_result(hb, t, a)
     assert got.count == ref.count and got.distinct == ref.distinct and got.distinct_any == ref.distinct_any
     assert got.dup.tolist() == ref.dup.tolist()
+
+
+@pytest.mark.parametrize("kind,n,S,adv", [(0, 65536, 100, 30), (1, 128064, 1000, 10)])
+def test_partitioned_tally_merges_to_the_whole(verifier, kind, n, S, adv):
+    """hd_tally_device_bitmap_part over nparts = 2, 3 and 8 partitions of the
+    rounds (what each of G ranks runs after the bitmap all-gather): the
+    partitions' rows are disjoint, their merge in first-batch-index order is
+    exactly the unpartitioned tally (count and round tables, hr_rep
+    included), the min-merged dup flags equal its dup, and every row sits in
+    the partition hd_tally_partition_of names."""
+    import ctypes
+    import torch
+    from hyperdrive_amd import _lib
+    from hyperdrive_amd.device import generate, work_stream
+    from hyperdrive_amd.shard import merge_tally_parts, pack_tally, partition_of
+    ks = verifier.gen_keys(S)
+    verifier.set_signatories(ks[0])
+    db, _, _ = generate(verifier, kind, n, S, adv, keys=ks)
+    hb = db.to_host()
+    res = verifier.verify_batch(hb)
+    bm = torch.from_numpy(res.valid_bitmap.view(np.int32)).cuda()
+    lib = _lib.load()
+    cs = db.c_struct()
+    ws = work_stream().cuda_stream
+    torch.cuda.synchronize()
+    t, a = verifier._tally_struct(n)
+    assert lib.hd_tally_device_bitmap(verifier.handle, ctypes.byref(cs), bm.data_ptr(), ctypes.byref(t), ws) == 0
+    whole = pack_tally(a, t.n_counts, t.n_hr)
+    whole_dup = a["dup"][:n].copy()
+    for nparts in (2, 3, 8):
+        parts, dup = [], np.full(n, 3, np.uint8)
+        for p in range(nparts):
+            t, a = verifier._tally_struct(n)
+            assert lib.hd_tally_device_bitmap_part(verifier.handle, ctypes.byref(cs), bm.data_ptr(), p, nparts,
+                                                   ctypes.byref(t), ws) == 0
+            part = pack_tally(a, t.n_counts, t.n_hr)
+            for row in part["hr"][:20]:
+                assert partition_of(row[0], row[1], nparts) == p
+            parts.append(part)
+            dup = np.minimum(dup, a["dup"][:n])
+        merged = merge_tally_parts(parts)
+        assert np.array_equal(merged["counts"], whole["counts"]), nparts
+        assert np.array_equal(merged["hr"], whole["hr"]), nparts
+        assert np.array_equal(dup, whole_dup), nparts
+        assert sum(len(p["hr"]) for p in parts) == len(whole["hr"])

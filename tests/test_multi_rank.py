@@ -1,6 +1,9 @@
 """Multi-rank sharding on CPU: world_size 2 (and 3) gloo process groups run the
 shard/all-gather logic of the multi-GPU path on oracle-verified bitmaps and
-reproduce the single-rank bitmap and tally exactly."""
+reproduce the single-rank bitmap and tally exactly; the partitioned tally --
+each rank tallies only the rounds hd_tally_partition_of gives it, the packed
+count tables are all-gathered and merged (shard.gather_tally) -- equals the
+single-rank tally rows."""
 import os
 import socket
 
@@ -10,7 +13,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from hyperdrive_amd.shard import gather_bitmaps, shard_range
+from hyperdrive_amd.shard import gather_bitmaps, gather_tally, partition_of, shard_range
 
 
 def _free_port():
@@ -84,3 +87,76 @@ def test_sharded_tally_equals_global(oracle):
         lo, hi = shard_range(len(verdicts), r, world)
         gathered += verdicts[lo:hi]
     assert oracle.tally(sc.b, gathered) == full
+
+
+def tally_rows(b, verdicts, part=0, nparts=1):
+    """Packed tally rows (shard.COUNT_COLS / HR_COLS) restated from the
+    first-wins rule (process.go:823-892) over the candidates of one partition:
+    a round's rep is its first candidate, a value group's rep its first
+    winner, rows in rep order."""
+    hr, cnt, seen = {}, {}, set()
+    for i in range(len(b)):
+        t, h, r = b.mtype[i], b.height[i], b.round[i]
+        if verdicts[i] != 0 or t not in (2, 3) or partition_of(h, r, nparts) != part:
+            continue
+        g = hr.setdefault((h, r), {"rep": i, 2: 0, 3: 0, "any": set()})
+        key = (h, r, t, b.frm[i])
+        if key in seen:
+            continue                                   # first wins
+        seen.add(key)
+        g[t] += 1
+        g["any"].add(b.frm[i])
+        c = cnt.setdefault((h, r, t, b.value[i]), [i, 0])
+        c[1] += 1
+    counts = sorted([h, r, t, c[0], c[1]] for (h, r, t, _), c in cnt.items())
+    counts.sort(key=lambda row: row[3])
+    hrs = sorted(([h, r, g[2], g[3], len(g["any"]), g["rep"]] for (h, r), g in hr.items()), key=lambda row: row[5])
+    return {"counts": np.array(counts, np.int64).reshape(-1, 5), "hr": np.array(hrs, np.int64).reshape(-1, 6)}
+
+
+def test_tally_rows_restatement_matches_oracle(oracle):
+    """The row restatement above agrees with the oracle's tally."""
+    from tally_cases import scenarios
+    sc = [s for s in scenarios() if s.name == "random_mix"][0]
+    verdicts = [0 if i % 7 else 5 for i in range(len(sc.b))]
+    t = oracle.tally(sc.b, verdicts)
+    rows = tally_rows(sc.b, verdicts)
+    assert {(h, r, ty, sc.b.value[rep]): n for h, r, ty, rep, n in rows["counts"].tolist()} == t.count
+    assert {(h, r): a for h, r, _, _, a, _ in rows["hr"].tolist()} == t.distinct_any
+
+
+def _tally_worker(rank, world, port, out_q):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__))))
+    from tally_cases import scenarios
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sc = [s for s in scenarios() if s.name == "random_mix"][0]
+    verdicts = [0 if i % 7 else 5 for i in range(len(sc.b))]
+    local = tally_rows(sc.b, verdicts, rank, world)
+    merged = gather_tally(local, world)
+    out_q.put((rank, merged["counts"].tolist(), merged["hr"].tolist(), len(local["hr"])))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_partitioned_tally_equals_single_rank(world):
+    from tally_cases import scenarios
+    sc = [s for s in scenarios() if s.name == "random_mix"][0]
+    verdicts = [0 if i % 7 else 5 for i in range(len(sc.b))]
+    want = tally_rows(sc.b, verdicts)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tally_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, counts, hrs, n_local in res:
+        assert counts == want["counts"].tolist() and hrs == want["hr"].tolist()
+        assert 0 < n_local < len(want["hr"])             # every rank tallied a strict share of the rounds

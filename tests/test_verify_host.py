@@ -7,7 +7,7 @@ import pytest
 from util import from_np, to_np
 
 
-@pytest.mark.parametrize("compressed", [True, False])
+@pytest.mark.parametrize("compressed", [True, False, 2])
 @pytest.mark.parametrize("kind,S,n,adv", [(0, 10, 140, 70), (1, 7, 70, 50)])
 def test_verify_matches_oracle(oracle, hostmath, compressed, kind, S, n, adv):
     keys = oracle.KeyCache(compressed)

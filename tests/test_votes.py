@@ -8,7 +8,10 @@ against the restatement of process.go's logs and O(n) counting loops
 - the process_test-style threshold scenarios (tests/tally_cases.py) give the
   same predicates through quorum.decide_votes as through the restatement;
 - C3-sized (1000 signers x 64 rounds) logs, resets reuse memory correctly;
-- argument errors are HD_EINVAL, verdicts gate insertion, proposes are not votes."""
+- argument errors are HD_EINVAL, verdicts gate insertion, proposes are not votes;
+- with f set, every insert's quorum-crossing events (L47's == 2f+1 on the
+  precommit log, process.go:658; L34; L55) equal the restatement's, and a
+  round holding more than 2f+1 precommits reports exactly one crossing."""
 import random
 
 import numpy as np
@@ -51,8 +54,10 @@ def test_random_sequences_match_restatement(V, seed):
     signers = [_sig(i) for i in range(12)]
     values = [_val(i) for i in range(4)]
     rounds = list(range(-1, 5))
+    f = 1 + seed
     v = V.VoteLog(7)
-    o = VO.VoteLogs(7)
+    v.set_f(f)
+    o = VO.VoteLogs(7, f)
     for step in range(600):
         op = rng.random()
         if op < 0.85:
@@ -60,10 +65,12 @@ def test_random_sequences_match_restatement(V, seed):
             h = rng.choice([7, 7, 7, 7, 8, 6]) + (o.height - 7)
             args = (t, h, rng.choice(rounds), rng.choice(values), rng.choice(signers))
             assert v.insert(*args) == o.insert(*args)
+            assert v.last_events == o.last_events
         elif op < 0.97:
             r, s = rng.choice(rounds), rng.choice(signers)
             v.trace_propose(r, s)
             o.trace_propose(r, s)
+            assert v.last_events == o.last_events
         else:
             h = o.height + rng.choice([0, 1])
             v.reset(h)
@@ -90,8 +97,10 @@ def test_batch_insert_equals_sequential(V):
     verdict = np.where(rng.random(n) < 0.1, 5, 0).astype(np.uint8)
     b = Batch(typ, h, r, None, val, frm, np.zeros((n, 65), np.uint8))
     v = V.VoteLog(3)
+    v.set_f(40)
     status, double_of = v.insert_batch(b, verdict)
-    o = VO.VoteLogs(3)
+    events = v.last_events.copy()
+    o = VO.VoteLogs(3, 40)
     first = {}
     for i in range(n):
         if verdict[i] != 0:
@@ -103,6 +112,7 @@ def test_batch_insert_equals_sequential(V):
         key = (int(typ[i]), int(r[i]), frm[i].tobytes())
         st, prior = o.insert(int(typ[i]), int(h[i]), int(r[i]), val[i].tobytes(), frm[i].tobytes())
         assert status[i] == st, i
+        assert events[i] == o.last_events, i
         if st == VO.INSERTED:
             first[key] = i
         if st == VO.DOUBLE:
@@ -114,6 +124,7 @@ def test_batch_insert_equals_sequential(V):
     ok = (verdict == 0) & np.isin(typ, [2, 3]) & (h == 3)
     assert set(s2[ok].tolist()) <= {V.DUPLICATE, V.DOUBLE}
     assert (d2 == V.NO_INDEX).all()
+    assert int((events != 0).sum()) > 0
     _compare_all(v, o, range(6), [frm[i].tobytes() for i in range(0, n, 97)], [_val(0), _val(1), _val(2)])
 
 
@@ -195,3 +206,36 @@ def test_errors_and_edges(V):
     assert v.insert(2, 0, (1 << 63) - 1, _val(2), _sig(1)) == (V.DOUBLE, _val(1))
     assert v.insert(2, 1, 0, _val(1), _sig(1)) == (V.WRONG_HEIGHT, None)
     v.close()
+
+
+def test_precommit_crossing_reported_once(V):
+    """L47 (process.go:658) is len(PrecommitLogs[r]) == 2f+1: over 2f+3
+    precommits of one round (duplicates and a double vote among them) exactly
+    the insert of the (2f+1)-th distinct signer crosses; the prevote log and
+    the trace report their own crossings; a round entered afterwards holds
+    2f+3 > 2f+1 logs, so StartRound's equality (quorum 'timeout_precommit_exact')
+    is false while 'timeout_precommit_reached' is true."""
+    from hyperdrive_amd import quorum
+    for f in (1, 5, 33):
+        v = V.VoteLog(9)
+        v.set_f(f)
+        o = VO.VoteLogs(9, f)
+        crossed = []
+        for k in range(2 * f + 3):
+            for frm in (_sig(k), _sig(k)):                     # an identical duplicate each time
+                st, _ = v.insert(VO.PRECOMMIT, 9, 2, _val(1), frm)
+                o.insert(VO.PRECOMMIT, 9, 2, _val(1), frm)
+                assert v.last_events == o.last_events
+                if v.last_events & V.EV_PRECOMMIT_2F1:
+                    crossed.append(k)
+        st, _ = v.insert(VO.PRECOMMIT, 9, 2, _val(2), _sig(0))   # double vote: no event
+        assert st == V.DOUBLE and v.last_events == 0
+        assert crossed == [2 * f]
+        d = quorum.decide_votes(v, 2, f)
+        assert d["timeout_precommit_reached"] and not d["timeout_precommit_exact"]
+        v.reset(10)
+        for k in range(2 * f + 1):
+            v.insert(VO.PRECOMMIT, 10, 0, _val(1), _sig(k))
+        d = quorum.decide_votes(v, 0, f)
+        assert d["timeout_precommit_reached"] and d["timeout_precommit_exact"]
+        v.close()

@@ -83,6 +83,9 @@ def parse():
     ap.add_argument("--no-aux", action="store_true", help="skip the SURVEY §8(f) side measurements")
     ap.add_argument("--no-sub", action="store_true", help="skip the C3 / C5 sub-benchmarks")
     ap.add_argument("--sub-steps", type=int, default=8)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, one GPU per rank) or gloo: a rehearsal of the N > 1 path with ranks "
+                         "sharing the visible GPUs and host-side collectives")
     return ap.parse_args()
 
 
@@ -210,8 +213,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "gloo":
+            local = local % torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         dist = None
         torch.cuda.set_device(0)
@@ -255,7 +263,7 @@ def main():
     calls, verify_ms, sums_launches, sums_ms = v.profile_read()
     v.profile(False)
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     verdict, recovered, bitmap = pipe.last(args.steps)

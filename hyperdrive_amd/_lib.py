@@ -104,6 +104,14 @@ SIGNATURES = {
                                               ctypes.POINTER(HdTallyOut), ctypes.c_void_p]),
     "hd_process_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(HdTallyOut)]),
+    "hd_multi_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "hd_multi_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "hd_multi_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "hd_multi_ctx": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_int]),
+    "hd_multi_set_signatories": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
+    "hd_multi_set_pubkey_format": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "hd_multi_verify_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "hd_gen_keys": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
     "hd_gen_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
                                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,

@@ -24,6 +24,7 @@ LIB = os.environ.get("HD_BUILD_LIB", os.path.join(LIBDIR, "libhdverify.so"))
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 ARCH = os.environ.get("HD_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
+ROCM_LIB = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib")
 
 CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
           "-I" + INCLUDE] + ["-D%s=%s" % (k, os.environ[k]) for k in ("HD_FB_W", "HD_FB_WG") if os.environ.get(k)] \
@@ -69,7 +70,9 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
         objs = list(ex.map(lambda s: _compile(s, force), srcs))
     if force or _mtime(LIB) < max(_mtime(o) for o in objs):
         tmp = LIB + ".tmp"
-        r = subprocess.run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", *objs, "-o", tmp],
+        # librccl: the hd_multi_* exchange (hd_multi.hip)
+        r = subprocess.run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", *objs, "-L" + ROCM_LIB, "-lrccl",
+                            "-Wl,-rpath," + ROCM_LIB, "-o", tmp],
                            capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")

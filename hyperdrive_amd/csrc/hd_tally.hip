@@ -86,19 +86,17 @@ __device__ __forceinline__ bool candidate(const DevBatch& b, const uint8_t* verd
     return p.nparts <= 1 || part_of(hash_hr(b.height[i], b.round[i]), p.nparts) == p.part;
 }
 
-// candidates of the partition (sizes the hash tables): one atomic per block
+// candidates of the partition (sizes the hash tables): a wavefront sum,
+// then one global atomic per wavefront (a shared-memory atomic from every
+// lane serialises the block: measured 114 us per 1M messages)
 __global__ __launch_bounds__(256) void k_tally_count(DevBatch b, const uint8_t* __restrict__ verdict,
                                                      const uint32_t* __restrict__ bitmap, Part p,
                                                      uint32_t* __restrict__ count) {
-    __shared__ uint32_t c;
-    if (threadIdx.x == 0) c = 0;
-    __syncthreads();
     uint32_t mine = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += gridDim.x * blockDim.x)
         mine += candidate(b, verdict, bitmap, i, p) ? 1u : 0u;
-    if (mine) atomicAdd(&c, mine);
-    __syncthreads();
-    if (threadIdx.x == 0 && c) atomicAdd(count, c);
+    HD_UNROLL for (int off = 32; off > 0; off >>= 1) mine += (uint32_t)__shfl_xor((int)mine, off, 64);
+    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(count, mine);
 }
 
 __device__ __forceinline__ bool eq32(const uint8_t* a, const uint8_t* b) {

@@ -47,6 +47,9 @@ def gather_bitmaps(local_bits, n: int, world: int, group=None):
     alignment), so the concatenation is exactly the global bitmap."""
     import torch
     import torch.distributed as dist
+    if local_bits.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo moves host tensors only (CPU rehearsal of the multi-GPU path)
+        return gather_bitmaps(local_bits.cpu(), n, world, group).to(local_bits.device)
     per_words = [(shard_range(n, r, world)[1] - shard_range(n, r, world)[0] + 31) // 32 for r in range(world)]
     if len(set(per_words)) == 1:
         out = torch.empty(per_words[0] * world, dtype=local_bits.dtype, device=local_bits.device)
@@ -106,6 +109,8 @@ def gather_tally(local: Dict[str, np.ndarray], world: int, device=None, group=No
     collective runs (a CUDA device for RCCL, None = CPU for gloo)."""
     import torch
     import torch.distributed as dist
+    if dist.get_backend(group) == "gloo":
+        device = None
     sizes = torch.tensor([local["counts"].shape[0], local["hr"].shape[0]], dtype=torch.int64, device=device)
     all_sizes = torch.empty(2 * world, dtype=torch.int64, device=device)
     dist.all_gather_into_tensor(all_sizes, sizes, group=group)

@@ -215,7 +215,8 @@ class Verifier:
                                                      d_signer, d_bitmap, stream), "hd_verify_batch_device")
 
     # ---- tally -------------------------------------------------------
-    def _tally_struct(self, n: int):
+    @staticmethod
+    def _tally_struct(n: int):
         arrs = dict(
             count_height=np.zeros(max(n, 1), np.int64), count_round=np.zeros(max(n, 1), np.int64),
             count_type=np.zeros(max(n, 1), np.uint8), count_rep=np.zeros(max(n, 1), np.uint32),

@@ -212,6 +212,31 @@ uint32_t hd_tally_partition_of(int64_t height, int64_t round, uint32_t nparts);
 int hd_process_batch(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8_t* recovered32,
                      uint32_t* valid_bitmap, hd_tally_out* tally);
 
+/* ---- multi-GPU in one process ----------------------
+ * A context per device plus an RCCL communicator over the devices
+ * (ncclCommInitAll); for one caller (a Replica) that owns several GPUs.
+ * hd_multi_verify_batch = hd_process_batch over the devices: message i is
+ * verified on the device whose contiguous 32-aligned shard holds i; the
+ * per-device valid bitmaps are all-gathered in place over RCCL (xGMI), so
+ * every device holds the whole bitmap; with `tally` non-NULL every device
+ * tallies the rounds hd_tally_partition_of gives it and the host merges the
+ * tables into the single-device output (same rows, same order).  Host
+ * buffers, synchronous; outputs as hd_verify_batch / hd_tally.  devices:
+ * ngpus ordinals (NULL: 0 .. ngpus-1); a device listed twice gets two
+ * contexts and the bitmap exchange uses device copies (RCCL takes one rank
+ * per device).  Not thread-safe (one hd_multi per caller thread). */
+typedef struct hd_multi hd_multi;
+int hd_multi_create(int ngpus, const int* devices, hd_multi** out);
+int hd_multi_destroy(hd_multi* m);
+/* number of devices; whether the exchange runs over RCCL (else copies) */
+int hd_multi_size(hd_multi* m, int* ngpus, int* uses_rccl);
+/* the context of device slot k (fast-path stats etc.), NULL if out of range */
+hd_ctx* hd_multi_ctx(hd_multi* m, int k);
+int hd_multi_set_signatories(hd_multi* m, const uint8_t* sigs32, uint32_t n);
+int hd_multi_set_pubkey_format(hd_multi* m, int format);
+int hd_multi_verify_batch(hd_multi* m, const hd_batch* batch, uint8_t* verdict, uint8_t* recovered32,
+                          uint32_t* valid_bitmap, hd_tally_out* tally);
+
 /* ---- synthetic workload (seeded; benchmarks/tests) --------
  * kind 0: votes (signer = i % S, type = 2 + (i/S)%2, h = 1 + i/(2S), r = 0)
  * kind 1: rounds (h = 1; per round 1 Propose + S Prevotes + S Precommits)

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_tally.py tests/test_gpu_verify.py tests/test_golden.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/t4.log 2>&1 || { tail -30 gpurun_out/t4.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_multi_gpu.py tests/test_gpu_tally.py tests/test_gpu_verify.py tests/test_golden.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/t4.log 2>&1 || { tail -30 gpurun_out/t4.log; exit 1; }
 tail -2 gpurun_out/t4.log
 timeout -k 10 600 python bench.py > gpurun_out/bench_r2.json 2> gpurun_out/bench_r2.err || { tail -20 gpurun_out/bench_r2.err; exit 2; }
 cat gpurun_out/bench_r2.json

@@ -487,6 +487,110 @@ HD_FEMUL void fe_mul_impl(fe& out, const fe& a, const fe& b) {
 }
 HD void fe_mul(fe& r, const fe& a, const fe& b) { fe_mul_impl<false>(r, a, b); }
 HD void fe_sqr(fe& r, const fe& a) { fe_mul_impl<true>(r, a, a); }
+
+// Two independent products (or squares: SA / SB) computed side by side, the
+// mads of the two alternating column by column.  One product's column is a
+// chain of dependent v_mad_u64_u32 (a 64-bit accumulator); a wave running one
+// chain stalls between its links (and gfx950 needs a wait state between a
+// mad and a dependent one: the compiler pads with s_nop), so two chains in
+// flight hide each other's latency.  Same arithmetic, same limb bounds and
+// outputs as two fe_mul_impl calls (the HD_BOUNDS build runs exactly those).
+template <bool SA, bool SB>
+HD void fe_mul2_impl(fe& outA, const fe& a0, const fe& a1, fe& outB, const fe& b0, const fe& b1) {
+#ifdef HD_BOUND_CHECKS
+    fe_mul_impl<SA>(outA, a0, a1);
+    fe_mul_impl<SB>(outB, b0, b1);
+#else
+    fe rA, rB;  // outputs may alias inputs
+    uint32_t xa[9], ya[9], xb[9], yb[9], a2a[8], a2b[8];
+    HD_UNROLL for (int i = 0; i < 9; i++) {
+        xa[i] = i == 8 ? opaque_u32(a0.n[i]) : a0.n[i];
+        xb[i] = i == 8 ? opaque_u32(b0.n[i]) : b0.n[i];
+        if (!SA) ya[i] = i == 8 ? opaque_u32(a1.n[i]) : a1.n[i];
+        if (!SB) yb[i] = i == 8 ? opaque_u32(b1.n[i]) : b1.n[i];
+    }
+    if (SA) {
+        HD_UNROLL for (int i = 0; i < 8; i++) a2a[i] = xa[i] << 1;
+    }
+    if (SB) {
+        HD_UNROLL for (int i = 0; i < 8; i++) a2b[i] = xb[i] << 1;
+    }
+    const uint32_t K1 = opaque_u32(0x7A20u), K2 = opaque_u32(256u);
+    uint64_t chiA = 0, cloA = 0, chiB = 0, cloB = 0;
+    uint32_t hprevA = 0, hprevB = 0;
+    HD_UNROLL for (int k = 0; k < 9; k++) {
+        uint64_t dA = chiA, dB = chiB;
+        HD_UNROLL for (int i = k + 1; i < 9; i++) {
+            const int j = k + 9 - i;
+            if (SA) {
+                if (i < j) dA = mad64(a2a[i], xa[j], dA);
+                else if (i == j) dA = mad64(xa[i], xa[i], dA);
+            } else {
+                dA = mad64(xa[i], ya[j], dA);
+            }
+            if (SB) {
+                if (i < j) dB = mad64(a2b[i], xb[j], dB);
+                else if (i == j) dB = mad64(xb[i], xb[i], dB);
+            } else {
+                dB = mad64(xb[i], yb[j], dB);
+            }
+        }
+        const uint32_t hA = opaque_u32((uint32_t)dA & HD_M29), hB = opaque_u32((uint32_t)dB & HD_M29);
+        chiA = dA >> 29;
+        chiB = dB >> 29;
+        uint64_t cA = mad64(hA, K1, cloA), cB = mad64(hB, K1, cloB);
+        if (k > 0) {
+            cA = mad64(hprevA, K2, cA);
+            cB = mad64(hprevB, K2, cB);
+        }
+        HD_UNROLL for (int i = 0; i <= k; i++) {
+            const int j = k - i;
+            if (SA) {
+                if (i < j) cA = mad64(a2a[i], xa[j], cA);
+                else if (i == j) cA = mad64(xa[i], xa[i], cA);
+            } else {
+                cA = mad64(xa[i], ya[j], cA);
+            }
+            if (SB) {
+                if (i < j) cB = mad64(a2b[i], xb[j], cB);
+                else if (i == j) cB = mad64(xb[i], xb[i], cB);
+            } else {
+                cB = mad64(xb[i], yb[j], cB);
+            }
+        }
+        rA.n[k] = (uint32_t)cA & HD_M29;
+        rB.n[k] = (uint32_t)cB & HD_M29;
+        cloA = cA >> 29;
+        cloB = cB >> 29;
+        hprevA = hA;
+        hprevB = hB;
+    }
+    // the final folds, as fe_mul_impl
+    const uint64_t uA = ((cloA + ((uint64_t)hprevA << 8)) << 5) + (rA.n[8] >> 24);
+    const uint64_t uB = ((cloB + ((uint64_t)hprevB << 8)) << 5) + (rB.n[8] >> 24);
+    rA.n[8] &= HD_M24;
+    rB.n[8] &= HD_M24;
+    uint64_t fA = mad64((uint32_t)uA, 977u, rA.n[0]), fB = mad64((uint32_t)uB, 977u, rB.n[0]);
+    fA += (uint64_t)((uint32_t)(uA >> 32) * 977u) << 32;
+    fB += (uint64_t)((uint32_t)(uB >> 32) * 977u) << 32;
+    rA.n[0] = (uint32_t)fA & HD_M29;
+    rB.n[0] = (uint32_t)fB & HD_M29;
+    const uint64_t gA = (fA >> 29) + (uA << 3) + rA.n[1], gB = (fB >> 29) + (uB << 3) + rB.n[1];
+    rA.n[1] = (uint32_t)gA & HD_M29;
+    rB.n[1] = (uint32_t)gB & HD_M29;
+    rA.n[2] += (uint32_t)(gA >> 29);
+    rB.n[2] += (uint32_t)(gB >> 29);
+    outA = rA;
+    outB = rB;
+#endif
+}
+// ra = a0 a1 and rb = b0 b1 (mul2), squares (sqr2), or a product and a square
+HD void fe_mul2(fe& ra, const fe& a0, const fe& a1, fe& rb, const fe& b0, const fe& b1) {
+    fe_mul2_impl<false, false>(ra, a0, a1, rb, b0, b1);
+}
+HD void fe_mul_sqr(fe& ra, const fe& a0, const fe& a1, fe& rb, const fe& b) {
+    fe_mul2_impl<false, true>(ra, a0, a1, rb, b, b);
+}
 HD void fe_sqr_n(fe& r, const fe& a, int n) {
     r = a;
     HD_NOUNROLL for (int i = 0; i < n; i++) fe_sqr(r, r);

@@ -5,11 +5,14 @@
 // SIMD design note: per-lane wNAF sparsity buys nothing on a 64-wide
 // wavefront -- some lane always has a non-zero digit, so every lane would pay
 // every addition.  The ladder therefore uses *uniform* Booth-recoded fixed
-// windows: a 4-bit window for the variable point R (table 1R..8R, Jacobian,
-// per-lane, scratch) and an 8-bit window for G (table 1G..128G, affine, staged
-// in LDS by the kernel).  Every lane runs the identical sequence of
-// doublings/additions; a zero digit is a per-lane select, and the exceptional
-// cases of the addition law (P = inf, P = +-T) are rare branches.
+// windows over the GLV halves: 4-bit windows for the variable point R and
+// lambda R (tables 1R..8R, per lane, made affine on an isomorphic curve, in
+// scratch) and 12-bit windows for G and lambda G (1G..2048G, affine, 288 KiB
+// read through L2 -- it does not fit the 160 KiB LDS next to the kernel's
+// occupancy, and L2 hits measured as fast).  Every lane runs
+// the identical sequence of doublings/additions; a zero digit is a per-lane
+// select, and the exceptional cases of the addition law (P = inf, P = +-T)
+// are rare branches.
 //
 // Jacobian infinity is Z == 0 (mod p), tested on the normalised value.
 #pragma once

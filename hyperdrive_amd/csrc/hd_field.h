@@ -374,45 +374,66 @@ HD bool fe_eq(const fe& a, const fe& b) {  // b <= 2p limb-wise (T)
 #ifdef HD_BOUND_CHECKS
 // Interval image of fe_mul_impl: per-limb maxima of the output, and a check
 // that no 64-bit column accumulator can overflow for ANY inputs within the
-// input bounds.  Mirrors the device algorithm step by step.
+// input bounds.  Mirrors the device algorithm step by step (every step is
+// monotone in its inputs, so upper bounds propagate).
 static void fe_mul_bounds(uint64_t* ob, const uint64_t* A, const uint64_t* B) {
     typedef unsigned __int128 u128;
-    const u128 LIM = (u128)1 << 64;
-    u128 chi = 0, clo = 0;
-    uint64_t hprev = 0, r[9];
+    const u128 LIM = (u128)1 << 64, W32 = ((u128)1 << 32) - 1;
+    u128 dhi = 0, clo = 0, c = 0, hprev = 0;
+    uint64_t r[9];
     for (int k = 0; k < 9; k++) {
-        u128 d = chi;
+        u128 d = k > 0 ? dhi * 8u : 0;
         for (int i = k + 1; i < 9; i++) d += (u128)A[i] * B[k + 9 - i];
         HD_BREQ(d < LIM, "fe_mul: high column overflow");
-        const uint64_t hk = d > HD_M29 ? HD_M29 : (uint64_t)d;
-        chi = d >> 29;
-        u128 c = clo + (u128)hk * 0x7A20u + (k > 0 ? (u128)hprev * 256u : 0);
+        const u128 hk = d < W32 ? d : W32;
+        dhi = d >> 32;
+        c = clo + hk * 0x7A20u + (k > 0 ? hprev * 256u : 0);
         for (int i = 0; i <= k; i++) c += (u128)A[i] * B[k - i];
         HD_BREQ(c < LIM, "fe_mul: low column overflow");
         r[k] = c > HD_M29 ? HD_M29 : (uint64_t)c;
         clo = c >> 29;
         hprev = hk;
     }
-    HD_BREQ(chi == 0, "fe_mul: carry out of the top column");
-    const u128 W = clo + (u128)hprev * 256u;
-    const u128 u = (W << 5) + (r[8] >> 24);
-    HD_BREQ(u < ((u128)1 << 42), "fe_mul: final fold too large");
-    const u128 x = u * 977u + r[0];
-    const u128 y = (x >> 29) + (u << 3) + r[1];
+    HD_BREQ(dhi == 0, "fe_mul: carry out of the top column");
+    const u128 u = (c >> 24) + (hprev << 13);
+    HD_BREQ(u < ((u128)1 << 48), "fe_mul: final fold too large");
+    const u128 ulo = u < W32 ? u : W32, uhi = u >> 32;
+    const u128 f0 = ulo * 977u + r[0];
+    HD_BREQ(f0 < LIM, "fe_mul: fold overflow");
+    const u128 f1 = (f0 >> 29) + r[1] + uhi * 7816u + (u << 3);
+    HD_BREQ(f1 < LIM && (f1 >> 29) < ((u128)1 << 32), "fe_mul: fold overflow");
     for (int i = 0; i < 9; i++) ob[i] = r[i];
     ob[0] = HD_M29;
     ob[1] = HD_M29;
-    ob[2] = r[2] + (uint64_t)(y >> 29);
+    ob[2] = r[2] + (uint64_t)(f1 >> 29);
     ob[8] = HD_M24;
     for (int i = 0; i < 9; i++) HD_BREQ(ob[i] <= fe_t_limb(i), "fe_mul: output not tight");
 }
 #endif
 
+// A constant multiplier in an SGPR (the VOP3 mad reads one scalar operand):
+// no per-product v_mov to materialise it in a VGPR.
+HD uint32_t opaque_s32(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(HD_NO_LAUNDER)
+    asm("" : "+s"(x));
+#endif
+    return x;
+}
+
 // Product scanning with the high half folded in as it is produced: column k
 // (weight 2^(29k)) and column k+9 (weight 2^(29k) 2^261, 2^261 == 2^8 2^29 +
 // 0x7A20 mod p) are accumulated side by side, so only two 64-bit accumulator
-// chains are live.  hk (29 bits of column k+9) adds hk * 0x7A20 to column k
-// and hk * 2^8 to column k+1.  Output T.
+// chains are live.
+//  * A high column d is split at its register boundary, not at 29 bits:
+//    hk = d mod 2^32 adds hk * 0x7A20 to column k and hk * 2^8 to column
+//    k+1, and d >> 32 (weight 2^32 2^(29(k+9)) = 2^3 2^(29(k+10))) enters the
+//    next high column as one mad by 8.  The split costs no instruction
+//    (mask + 64-bit shift before).
+//  * A low column c leaves c mod 2^29 as the output limb and c >> 29 as the
+//    next column's carry.
+//  * Column 8's accumulator and the top high part fold at weight 2^256:
+//    u = (c8 >> 24) + h8 2^13, then u (2^32 + 977) into limbs 0..2.
+// Output T.
 #ifdef HD_FE_NOINLINE
 #define HD_FEMUL __host__ __device__ __noinline__
 #else
@@ -441,11 +462,13 @@ HD_FEMUL void fe_mul_impl(fe& out, const fe& a, const fe& b) {
     if (SQR) {
         HD_UNROLL for (int i = 0; i < 8; i++) a2[i] = x[i] << 1;
     }
-    const uint32_t K1 = opaque_u32(0x7A20u), K2 = opaque_u32(256u);
-    uint64_t chi = 0, clo = 0;
-    uint32_t hprev = 0;
+    // (K8 and K13 are opaque too: a known power of two turns the one mad
+    // into a 64-bit shift, two masks and an add)
+    const uint32_t K1 = opaque_s32(0x7A20u), K2 = opaque_s32(256u), K8 = opaque_s32(8u), K13 = opaque_s32(1u << 13);
+    uint64_t clo = 0, c = 0;
+    uint32_t dhi = 0, hprev = 0;
     HD_UNROLL for (int k = 0; k < 9; k++) {
-        uint64_t d = chi;
+        uint64_t d = 0;
         HD_UNROLL for (int i = k + 1; i < 9; i++) {
             const int j = k + 9 - i;
             if (SQR) {
@@ -455,9 +478,10 @@ HD_FEMUL void fe_mul_impl(fe& out, const fe& a, const fe& b) {
                 d = mad64(x[i], y[j], d);
             }
         }
-        const uint32_t hk = opaque_u32((uint32_t)d & HD_M29);
-        chi = d >> 29;
-        uint64_t c = mad64(hk, K1, clo);
+        if (k > 0) d = mad64(dhi, K8, d);
+        const uint32_t hk = (uint32_t)d;
+        dhi = (uint32_t)(d >> 32);
+        c = mad64(hk, K1, clo);
         if (k > 0) c = mad64(hprev, K2, c);
         HD_UNROLL for (int i = 0; i <= k; i++) {
             const int j = k - i;
@@ -468,129 +492,30 @@ HD_FEMUL void fe_mul_impl(fe& out, const fe& a, const fe& b) {
                 c = mad64(x[i], y[j], c);
             }
         }
-        r.n[k] = (uint32_t)c & HD_M29;
-        clo = c >> 29;
+        if (k < 8) {
+            r.n[k] = (uint32_t)c & HD_M29;
+            clo = c >> 29;
+        }
         hprev = hk;
     }
-    // weight 2^261: W = clo + h8 2^8; weight 2^256: u = 32 W + (r8 >> 24) (< 2^42)
-    const uint64_t u = ((clo + ((uint64_t)hprev << 8)) << 5) + (r.n[8] >> 24);
-    r.n[8] &= HD_M24;
-    // fold u (2^32 + 977): u 977 + r0, then u 2^32 = 8 u 2^29 into limb 1
-    uint64_t f0 = mad64((uint32_t)u, 977u, r.n[0]);
-    f0 += (uint64_t)((uint32_t)(u >> 32) * 977u) << 32;
+    // weight 2^256: u = (c8 >> 24) + h8 2^13 (< 2^48); limb 8 keeps c8's low 24 bits
+    r.n[8] = (uint32_t)c & HD_M24;
+    const uint64_t u = mad64(hprev, K13, c >> 24);
+    // u (2^32 + 977): u 977 into limb 0, u 2^32 = 8 u 2^29 into limb 1
+    const uint64_t f0 = mad64((uint32_t)u, 977u, r.n[0]);
+    const uint64_t g = mad64((uint32_t)(u >> 32), 977u * 8u, (f0 >> 29) + r.n[1]);
+    const uint64_t f1 = g + (u << 3);
     r.n[0] = (uint32_t)f0 & HD_M29;
-    const uint64_t f1 = (f0 >> 29) + (u << 3) + r.n[1];
     r.n[1] = (uint32_t)f1 & HD_M29;
-    r.n[2] += (uint32_t)(f1 >> 29);
+    // laundered: left alone the backend keeps limb 2 as the 64-bit sum and
+    // multiplies both of its halves in the next product
+    r.n[2] = opaque_u32(r.n[2] + (uint32_t)(f1 >> 29));
     HD_B(for (int i = 0; i < 9; i++) r.b[i] = ob[i];)
     out = r;
 }
 HD void fe_mul(fe& r, const fe& a, const fe& b) { fe_mul_impl<false>(r, a, b); }
 HD void fe_sqr(fe& r, const fe& a) { fe_mul_impl<true>(r, a, a); }
 
-// Two independent products (or squares: SA / SB) computed side by side, the
-// mads of the two alternating column by column.  One product's column is a
-// chain of dependent v_mad_u64_u32 (a 64-bit accumulator); a wave running one
-// chain stalls between its links (and gfx950 needs a wait state between a
-// mad and a dependent one: the compiler pads with s_nop), so two chains in
-// flight hide each other's latency.  Same arithmetic, same limb bounds and
-// outputs as two fe_mul_impl calls (the HD_BOUNDS build runs exactly those).
-template <bool SA, bool SB>
-HD void fe_mul2_impl(fe& outA, const fe& a0, const fe& a1, fe& outB, const fe& b0, const fe& b1) {
-#ifdef HD_BOUND_CHECKS
-    fe_mul_impl<SA>(outA, a0, a1);
-    fe_mul_impl<SB>(outB, b0, b1);
-#else
-    fe rA, rB;  // outputs may alias inputs
-    uint32_t xa[9], ya[9], xb[9], yb[9], a2a[8], a2b[8];
-    HD_UNROLL for (int i = 0; i < 9; i++) {
-        xa[i] = i == 8 ? opaque_u32(a0.n[i]) : a0.n[i];
-        xb[i] = i == 8 ? opaque_u32(b0.n[i]) : b0.n[i];
-        if (!SA) ya[i] = i == 8 ? opaque_u32(a1.n[i]) : a1.n[i];
-        if (!SB) yb[i] = i == 8 ? opaque_u32(b1.n[i]) : b1.n[i];
-    }
-    if (SA) {
-        HD_UNROLL for (int i = 0; i < 8; i++) a2a[i] = xa[i] << 1;
-    }
-    if (SB) {
-        HD_UNROLL for (int i = 0; i < 8; i++) a2b[i] = xb[i] << 1;
-    }
-    const uint32_t K1 = opaque_u32(0x7A20u), K2 = opaque_u32(256u);
-    uint64_t chiA = 0, cloA = 0, chiB = 0, cloB = 0;
-    uint32_t hprevA = 0, hprevB = 0;
-    HD_UNROLL for (int k = 0; k < 9; k++) {
-        uint64_t dA = chiA, dB = chiB;
-        HD_UNROLL for (int i = k + 1; i < 9; i++) {
-            const int j = k + 9 - i;
-            if (SA) {
-                if (i < j) dA = mad64(a2a[i], xa[j], dA);
-                else if (i == j) dA = mad64(xa[i], xa[i], dA);
-            } else {
-                dA = mad64(xa[i], ya[j], dA);
-            }
-            if (SB) {
-                if (i < j) dB = mad64(a2b[i], xb[j], dB);
-                else if (i == j) dB = mad64(xb[i], xb[i], dB);
-            } else {
-                dB = mad64(xb[i], yb[j], dB);
-            }
-        }
-        const uint32_t hA = opaque_u32((uint32_t)dA & HD_M29), hB = opaque_u32((uint32_t)dB & HD_M29);
-        chiA = dA >> 29;
-        chiB = dB >> 29;
-        uint64_t cA = mad64(hA, K1, cloA), cB = mad64(hB, K1, cloB);
-        if (k > 0) {
-            cA = mad64(hprevA, K2, cA);
-            cB = mad64(hprevB, K2, cB);
-        }
-        HD_UNROLL for (int i = 0; i <= k; i++) {
-            const int j = k - i;
-            if (SA) {
-                if (i < j) cA = mad64(a2a[i], xa[j], cA);
-                else if (i == j) cA = mad64(xa[i], xa[i], cA);
-            } else {
-                cA = mad64(xa[i], ya[j], cA);
-            }
-            if (SB) {
-                if (i < j) cB = mad64(a2b[i], xb[j], cB);
-                else if (i == j) cB = mad64(xb[i], xb[i], cB);
-            } else {
-                cB = mad64(xb[i], yb[j], cB);
-            }
-        }
-        rA.n[k] = (uint32_t)cA & HD_M29;
-        rB.n[k] = (uint32_t)cB & HD_M29;
-        cloA = cA >> 29;
-        cloB = cB >> 29;
-        hprevA = hA;
-        hprevB = hB;
-    }
-    // the final folds, as fe_mul_impl
-    const uint64_t uA = ((cloA + ((uint64_t)hprevA << 8)) << 5) + (rA.n[8] >> 24);
-    const uint64_t uB = ((cloB + ((uint64_t)hprevB << 8)) << 5) + (rB.n[8] >> 24);
-    rA.n[8] &= HD_M24;
-    rB.n[8] &= HD_M24;
-    uint64_t fA = mad64((uint32_t)uA, 977u, rA.n[0]), fB = mad64((uint32_t)uB, 977u, rB.n[0]);
-    fA += (uint64_t)((uint32_t)(uA >> 32) * 977u) << 32;
-    fB += (uint64_t)((uint32_t)(uB >> 32) * 977u) << 32;
-    rA.n[0] = (uint32_t)fA & HD_M29;
-    rB.n[0] = (uint32_t)fB & HD_M29;
-    const uint64_t gA = (fA >> 29) + (uA << 3) + rA.n[1], gB = (fB >> 29) + (uB << 3) + rB.n[1];
-    rA.n[1] = (uint32_t)gA & HD_M29;
-    rB.n[1] = (uint32_t)gB & HD_M29;
-    rA.n[2] += (uint32_t)(gA >> 29);
-    rB.n[2] += (uint32_t)(gB >> 29);
-    outA = rA;
-    outB = rB;
-#endif
-}
-// ra = a0 a1 and rb = b0 b1 (mul2), squares (sqr2), or a product and a square
-HD void fe_mul2(fe& ra, const fe& a0, const fe& a1, fe& rb, const fe& b0, const fe& b1) {
-    fe_mul2_impl<false, false>(ra, a0, a1, rb, b0, b1);
-}
-HD void fe_mul_sqr(fe& ra, const fe& a0, const fe& a1, fe& rb, const fe& b) {
-    fe_mul2_impl<false, true>(ra, a0, a1, rb, b, b);
-}
 HD void fe_sqr_n(fe& r, const fe& a, int n) {
     r = a;
     HD_NOUNROLL for (int i = 0; i < n; i++) fe_sqr(r, r);

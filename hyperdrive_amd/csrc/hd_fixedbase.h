@@ -36,9 +36,6 @@ namespace hd {
 #ifndef HD_FB_WG
 #define HD_FB_WG 24   // the one shared G table: 11 windows, 10 x 2^23 + 2^16 points (6.0 GB)
 #endif
-#ifndef HD_ADD_PAIRS
-#define HD_ADD_PAIRS 0   // 1: gej_add_ge_nx issues its multiplications in pairs (fe_mul2); A/B: no gain, the sums loop is issue-bound
-#endif
 
 // Windows 0 .. NWIN-2 take signed Booth digits |d| <= 2^(W-1); the top window
 // takes the remaining TOPBITS bits plus the Booth carry unsigned,
@@ -101,35 +98,6 @@ HD void gej_add_ge_nx(gej& r, const gej& a, const ge& b) {
     HD_REQUIRE_T(a.y, "gej_add_ge_nx: y");
     HD_REQUIRE_T(a.z, "gej_add_ge_nx: z");
     HD_REQUIRE_T(b.x, "gej_add_ge_nx: b.x");
-#if HD_ADD_PAIRS
-    // The same formula with its independent multiplications issued in pairs
-    // (fe_mul2: two mad chains in flight per wave); 1 square + 5 pairs.
-    fe z1z1, u2, s2, h, R, t;
-    gej o;
-    fe hh, i4, j, v;
-    fe_sqr(z1z1, a.z);                          // T
-    fe_mul2(u2, b.x, z1z1, s2, b.y, a.z);       // T, T (2T x T)
-    fe_sub_k<2>(h, u2, a.x);
-    fe_norm_weak(h);                            // H = U2 - X1       T
-    fe_add(t, a.z, a.z);
-    fe_mul2(s2, s2, z1z1, o.z, t, h);           // S2 T; Z3 = 2 Z1 H T
-    fe_sub_k<2>(R, s2, a.y);                    // r = S2 - Y1       3T
-    fe_norm_weak(R);
-    fe_add(R, R, R);                            // 2r                2T
-    fe_mul2_impl<true, true>(hh, h, h, o.x, R, R);   // H^2, (2r)^2  T, T
-    fe_mul_int(i4, hh, 4);                      // I = 4 H^2         4T
-    fe_mul2(j, h, i4, v, a.x, i4);              // J = H I, V = X1 I T, T
-    fe_add(t, v, v);
-    fe_add(t, t, j);                            // 2V + J            3T
-    fe_sub_k<4>(o.x, o.x, t);
-    fe_norm_weak(o.x);                          // X3                T
-    fe_sub_k<2>(t, v, o.x);                     // V - X3            3T
-    fe_mul2(t, R, t, j, a.y, j);                // r (V - X3) T (2T x 3T); Y1 J T
-    fe_add(j, j, j);                            // 2 Y1 J            2T
-    fe_sub_k<3>(o.y, t, j);
-    fe_norm_weak(o.y);                          // Y3                T
-    r = o;
-#else
     fe z1z1, u2, s2, h, R, t;
     fe_sqr(z1z1, a.z);         // T
     fe_mul(u2, b.x, z1z1);     // T
@@ -160,7 +128,6 @@ HD void gej_add_ge_nx(gej& r, const gej& a, const ge& b) {
     fe_sub_k<3>(o.y, t, j);
     fe_norm_weak(o.y);         // Y3                T
     r = o;
-#endif
 }
 
 // Booth digit j of u for the table width: bits [W j - 1, W j + W - 1] of u

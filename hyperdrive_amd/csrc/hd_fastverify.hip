@@ -2,23 +2,28 @@
 // the tables it runs on (hd_fixedbase.h).
 //
 // Per batch, stream-ordered, no host synchronisation:
-//   k_verify_fast   one message per lane: a message whose claimed From is an
+//   k_fast_prep / k_fast_scalars / k_fast_sums / k_fast_final
+//                   the split known-key check (the default, see "the split
+//                   check" below): a message whose claimed From is an
 //                   admitted signatory with a known key is checked with two
-//                   fixed-base multiplications (29 mixed additions, no
+//                   fixed-base multiplications (23 mixed additions, no
 //                   doublings, no square root); VALID / early exact verdicts
 //                   are final, everything else is appended to a list
+//   k_verify_fast   the older single-kernel form (two messages per lane,
+//                   HD_FAST_K=0), kept for A/B
 //   k_verify        (hd_verify.hip) the full libsecp256k1-semantics recovery
 //                   over that list only; VALID messages of signatories without
 //                   a known key publish the recovered key to their slot
 //   k_fb_bitmap     the valid bitmap from the final verdicts
-//   k_fb_list / k_fb_bases / k_fb_entries / k_fb_ready
-//                   build the tables of newly learned keys (HD_FB_NWIN window
-//                   bases, then HD_FB_NWIN x HD_FB_N affine multiples, one per
-//                   lane); with nothing learned each exits at once
+//   k_fb_list / k_fb_bases / k_fb_runs / k_fb_ready
+//                   build the tables of newly learned keys (window bases,
+//                   then the affine multiples by segments of consecutive
+//                   entries, one addition per entry); with nothing learned
+//                   each exits at once
 // Table memory is capped by HD_FB_MAX_BYTES (default 64 GiB of the 288 GB):
 // signatories beyond the cap always take the full recovery.
-// G has one table with wider windows (HD_FB_WG bits: 13 additions for u1
-// instead of 16), built once per device and process (fb_g_table).
+// G has one table with wider windows (HD_FB_WG bits), built once per device
+// and process (fb_g_table).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -53,6 +58,7 @@ struct FbWork {
     size_t cap_slow = 0;
     uint32_t* rows = nullptr;     // the split check's per-message rows (SplitRows, 83 words per message)
     size_t cap_rows = 0;
+    uint32_t* zr = nullptr;       // the table builder's z ratios (k_fb_runs: HD_FB_RUN x 9 words per thread)
     // The scratch above (rows, slow, counts) is per context: a verify call
     // on another stream than the previous one first waits for that call's
     // end, so calls of one context never overlap on the device whatever
@@ -533,22 +539,95 @@ __global__ __launch_bounds__(256) void k_fb_bases(const uint32_t* __restrict__ l
     }
 }
 
+// Table entries by segments of HD_FB_SEG consecutive multiples of one window
+// base B: a lane computes the segment's first point d0 B once (double-and-add)
+// and walks the rest with one mixed addition each, in blocks of HD_FB_RUN:
+// the forward walk keeps each step's z ratio (Z_{k+1} = Z_k zr_k) and parks
+// the Jacobian X, Y canonically in the entry's own 64-B table slot; one
+// inversion of the block's last Z, then the backward walk makes each entry
+// affine (1/Z_k = 1/Z_{k+1} zr_k).  Per entry one addition and ~5 products
+// plus a share of one inversion, instead of a double-and-add and an
+// inversion per entry (fb_entry, the definition the host tests check).
+// The walk never adds B to +-B: its first point is d0 B with d0 >= 2 (d = 1
+// is B itself, written directly), so (d0 + k) B = +-B cannot occur.
+#define HD_FB_RUN 32
+#define HD_FB_SEG 512
 template <int W>
-__global__ __launch_bounds__(256) void k_fb_entries(const uint32_t* __restrict__ list,
-                                                    const uint32_t* __restrict__ count, const ge* __restrict__ base,
-                                                    gp* __restrict__ tab) {
-    constexpr uint32_t TAB = FbL<W>::TAB;
-    const uint64_t total = (uint64_t)*count * TAB;
-    for (uint64_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t slot = list[t / TAB], e = (uint32_t)(t % TAB);
-        int j;
-        uint32_t d;
-        fb_entry_pos<W>(e, j, d);
-        ge o;
-        fb_entry(o, base[(size_t)slot * FbL<W>::NWIN + j], d);
-        gp q;
-        gp_pack(q, o);
-        tab[(size_t)slot * TAB + e] = q;
+__global__ __launch_bounds__(256) void k_fb_runs(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
+                                                 const ge* __restrict__ base, gp* __restrict__ tab,
+                                                 uint32_t* __restrict__ zr_scratch) {
+    constexpr uint32_t N = FbL<W>::N, NW = FbL<W>::NWIN, TAB = FbL<W>::TAB;
+    constexpr uint32_t SW = N / HD_FB_SEG;                                  // segments per full window
+    constexpr uint32_t SB = (NW - 1) * SW + FbL<W>::NTOP / HD_FB_SEG;      // segments per base
+    static_assert(N % HD_FB_SEG == 0 && FbL<W>::NTOP % HD_FB_SEG == 0 && HD_FB_SEG % HD_FB_RUN == 0, "segments");
+    const uint32_t T = gridDim.x * blockDim.x;
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t total = (uint64_t)*count * SB;
+    for (uint64_t g = tid; g < total; g += T) {
+        const uint32_t slot = list[g / SB];
+        const uint32_t rem = (uint32_t)(g % SB);
+        const uint32_t j = min(rem / SW, NW - 1);
+        const uint32_t d0 = 1 + (rem - j * SW) * HD_FB_SEG;
+        const ge B = base[(size_t)slot * NW + j];
+        gp* out = tab + (size_t)slot * TAB + (size_t)j * N + (d0 - 1);
+        gej a;
+        uint32_t k0 = 0;   // first entry of the segment the walk produces
+        if (d0 == 1) {
+            gp q;
+            gp_pack(q, B);   // bases are canonical affine
+            out[0] = q;
+            gej b;
+            gej_set_ge(b, B);
+            gej_dbl(a, b);
+            k0 = 1;
+        } else {
+            fb_mul_small(a, B, d0);
+        }
+        for (uint32_t blk = 0; blk < HD_FB_SEG; blk += HD_FB_RUN) {
+            const uint32_t lo = blk + (blk == 0 ? k0 : 0), hi = blk + HD_FB_RUN;
+            HD_NOUNROLL for (uint32_t k = lo; k < hi; k++) {
+                if (k > lo) {
+                    fe zr;
+                    gej_add_ge_zr(a, a, B, zr);
+                    HD_UNROLL for (int w = 0; w < 9; w++)
+                        zr_scratch[((size_t)(k - 1 - blk) * 9 + w) * T + tid] = zr.n[w];
+                }
+                fe x = a.x, y = a.y;
+                fe_normalize(x);
+                fe_normalize(y);
+                gp q;
+                fe_to_le(q.x, x);
+                fe_to_le(q.y, y);
+                out[k] = q;
+            }
+            fe zinv;
+            fe_inv_divsteps(zinv, a.z);
+            HD_NOUNROLL for (uint32_t k = hi; k-- > lo;) {
+                ge p;
+                gp_unpack(p, out[k]);
+                fe z2, ax, ay;
+                fe_sqr(z2, zinv);
+                fe_mul(ax, p.x, z2);
+                fe_mul(z2, z2, zinv);
+                fe_mul(ay, p.y, z2);
+                fe_normalize(ax);
+                fe_normalize(ay);
+                gp q;
+                fe_to_le(q.x, ax);
+                fe_to_le(q.y, ay);
+                out[k] = q;
+                if (k > lo) {
+                    fe zr;
+                    HD_UNROLL for (int w = 0; w < 9; w++) zr.n[w] = zr_scratch[((size_t)(k - 1 - blk) * 9 + w) * T + tid];
+                    fe_mul(zinv, zinv, zr);
+                }
+            }
+            // the next block continues the walk from this block's last point
+            if (hi < HD_FB_SEG) {
+                fe zr;
+                gej_add_ge_zr(a, a, B, zr);
+            }
+        }
     }
 }
 
@@ -622,6 +701,10 @@ int fb_grow_slots(hd_ctx* ctx, uint32_t want) {
     return HD_OK;
 }
 
+// k_fb_runs grid (4 blocks per CU) and its z-ratio scratch
+uint32_t fb_run_blocks(const hd_ctx* ctx) { return (uint32_t)std::max(ctx->n_cu, 1) * 4u; }
+size_t fb_run_scratch_bytes(const hd_ctx* ctx) { return (size_t)HD_FB_RUN * 9 * 4 * 256 * fb_run_blocks(ctx); }
+
 // build the tables of every LEARNED slot, stream-ordered
 int fb_learn(hd_ctx* ctx, hipStream_t s) {
     FbWork* f = ctx->fb;
@@ -629,10 +712,10 @@ int fb_learn(hd_ctx* ctx, hipStream_t s) {
     k_fb_list<<<1, 256, 0, s>>>(f->nslots, f->state, f->list, f->counts);
     if (f->wp == HD_FB_WW) {
         k_fb_bases<HD_FB_WW><<<g, 256, 0, s>>>(f->list, f->counts, f->pub, f->base);
-        k_fb_entries<HD_FB_WW><<<g * 2, 256, 0, s>>>(f->list, f->counts, f->base, f->tab);
+        k_fb_runs<HD_FB_WW><<<fb_run_blocks(ctx), 256, 0, s>>>(f->list, f->counts, f->base, f->tab, f->zr);
     } else {
         k_fb_bases<HD_FB_W><<<g, 256, 0, s>>>(f->list, f->counts, f->pub, f->base);
-        k_fb_entries<HD_FB_W><<<g * 2, 256, 0, s>>>(f->list, f->counts, f->base, f->tab);
+        k_fb_runs<HD_FB_W><<<fb_run_blocks(ctx), 256, 0, s>>>(f->list, f->counts, f->base, f->tab, f->zr);
     }
     k_fb_ready<<<1, 256, 0, s>>>(f->list, f->counts, f->state);
     FBCHK(hipGetLastError(), "fb table kernels");
@@ -670,9 +753,8 @@ static int fb_g_table(hd_ctx* ctx, const gp** out) {
     const uint32_t hl[2] = {0u, 1u};
     FBCHK(hipMemcpy(pub, &g, sizeof(ge), hipMemcpyHostToDevice), "G point");
     FBCHK(hipMemcpy(cl, hl, 8, hipMemcpyHostToDevice), "G list");
-    const uint32_t grid = (uint32_t)std::max(ctx->n_cu, 1) * 8u;
     k_fb_bases<HD_FB_WG><<<1, 64, 0, ctx->stream>>>(cl, cl + 1, pub, base);
-    k_fb_entries<HD_FB_WG><<<grid, 256, 0, ctx->stream>>>(cl, cl + 1, base, tab);
+    k_fb_runs<HD_FB_WG><<<fb_run_blocks(ctx), 256, 0, ctx->stream>>>(cl, cl + 1, base, tab, ctx->fb->zr);
     FBCHK(hipGetLastError(), "G table kernels");
     FBCHK(hipStreamSynchronize(ctx->stream), "G table build");
     (void)hipFree(base);
@@ -692,6 +774,7 @@ int hd_fb_init(hd_ctx* ctx) {
     if (const char* m = getenv("HD_FB_MAX_BYTES")) f->budget = atof(m);
     f->max_slots = (uint32_t)std::max(1.0, std::min(1e6, f->budget / fb_slot_bytes(f->wp)));
     FBCHK(hipMalloc(&f->counts, 8), "fb counts");
+    FBCHK(hipMalloc(&f->zr, fb_run_scratch_bytes(ctx)), "fb builder scratch");
     int rc = fb_grow_slots(ctx, 1);
     if (rc) return rc;
     return fb_g_table(ctx, &f->gtab);
@@ -704,7 +787,7 @@ void hd_fb_release(hd_ctx* ctx) {
     if (f->done) (void)hipEventDestroy(f->done);
     for (hipEvent_t e : f->ev_call) (void)hipEventDestroy(e);
     for (hipEvent_t e : f->ev_sums) (void)hipEventDestroy(e);
-    void* ptrs[] = {f->counts, f->slow, f->adm_slot, f->rows};
+    void* ptrs[] = {f->counts, f->slow, f->adm_slot, f->rows, f->zr};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete f;

@@ -359,17 +359,23 @@ HD void fb_window_base(ge& out, const ge& B, int W, int j) {
     gej_to_ge(out.x, out.y, a);
 }
 
-// d Bj for 1 <= d <= 2^(W-1) (2^TOPBITS in the top window), affine canonical
-// (double-and-add from the top bit)
-HD void fb_entry(ge& out, const ge& Bj, uint32_t d) {
+// d B (Jacobian) for 1 <= d < 2^32: double-and-add from the top bit
+HD void fb_mul_small(gej& a, const ge& B, uint32_t d) {
     int top = 31;
     while (top > 0 && !((d >> top) & 1u)) top--;
-    gej a;
-    gej_set_ge(a, Bj);
+    gej_set_ge(a, B);
     HD_NOUNROLL for (int b = top - 1; b >= 0; b--) {
         gej_dbl(a, a);
-        if ((d >> b) & 1u) gej_add_ge(a, a, Bj);
+        if ((d >> b) & 1u) gej_add_ge(a, a, B);
     }
+}
+
+// d Bj for 1 <= d <= 2^(W-1) (2^TOPBITS in the top window), affine canonical:
+// the entry definition (the device builds tables by runs, k_fb_runs; the
+// host tests check entries against this)
+HD void fb_entry(ge& out, const ge& Bj, uint32_t d) {
+    gej a;
+    fb_mul_small(a, Bj, d);
     gej_to_ge(out.x, out.y, a);
 }
 

@@ -24,6 +24,15 @@ def child():
     sigs, foreign = v.gen_keys(S)
     v.set_signatories(sigs)
     db, _, _ = generate(v, 0, N, S, adv, keys=(sigs, foreign))
+    if os.environ.get("AB_SORT"):
+        # messages grouped by signatory (probe of the table reads' locality)
+        key = db.frm[:, :8].to(torch.int64)
+        k = torch.zeros(N, dtype=torch.int64, device="cuda")
+        for b in range(7):
+            k = k * 256 + key[:, b]
+        perm = torch.argsort(k, stable=True)
+        for f in ("type", "height", "round", "valid_round", "value", "frm", "sig"):
+            setattr(db, f, getattr(db, f)[perm].contiguous())
     ws = work_stream()
     verdict = torch.empty(N, dtype=torch.uint8, device="cuda")
     cb = db.c_struct()

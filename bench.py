@@ -80,6 +80,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: the host cores this process may use")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-tally", action="store_true")
+    ap.add_argument("--stream-priority", choices=("high", "normal"), default="high",
+                    help="priority of the verify stream over the tally stream")
     ap.add_argument("--no-aux", action="store_true", help="skip the SURVEY §8(f) side measurements")
     ap.add_argument("--no-sub", action="store_true", help="skip the C3 / C5 sub-benchmarks")
     ap.add_argument("--sub-steps", type=int, default=8)
@@ -106,7 +108,7 @@ class Pipeline:
     runs on its own stream while the verifications of steps k+1 .. k+NBUF-1
     are queued, so the tally's host syncs never drain the verify queue; every
     step's verification and tally complete inside the timed region."""
-    NBUF = 3
+    NBUF = int(os.environ.get("HD_BENCH_NBUF", 3))
 
     def __init__(self, v, db, total, B, rank, world, dist, ws, ts, tally=True):
         import torch
@@ -127,9 +129,14 @@ class Pipeline:
         self.verdicts = [torch.empty(B, dtype=torch.uint8, device=dev) for _ in range(self.NBUF)]
         self.recovered = [torch.empty((B, 32), dtype=torch.uint8, device=dev) for _ in range(self.NBUF)]
         self.bitmaps = [torch.zeros(B // 32, dtype=torch.int32, device=dev) for _ in range(self.NBUF)]
-        self.t_out, self.t_arr = v._tally_struct(total)
+        self.t_out, self.t_arr = v._tally_struct(total, pinned=True)
+        self.t_part = None
+        if world > 1:
+            from hyperdrive_amd.shard import tally_out
+            self.t_part = tally_out(v, total, pinned=True)
         self.tally_info = {}
         self.last_tally = None
+        self.host_trace = [] if os.environ.get("HD_BENCH_HOSTTRACE") else None
 
     def verify(self, k):
         import torch
@@ -164,7 +171,8 @@ class Pipeline:
             self.last_tally = (self.t_out, self.t_arr)
         else:
             # this rank's rounds, then the merged count tables of all ranks
-            local = tally_part(self.v, self.full, gathered.data_ptr(), self.rank, self.world, self.ts.cuda_stream)
+            local = tally_part(self.v, self.full, gathered.data_ptr(), self.rank, self.world, self.ts.cuda_stream,
+                               out=self.t_part)
             with torch.cuda.stream(self.ts):
                 merged = gather_tally(local, self.world, device=gathered.device)
             self.tally_info = {"n_hr": len(merged["hr"]), "n_counts": len(merged["counts"]),
@@ -175,10 +183,15 @@ class Pipeline:
         """steps verifications + tallies; buffer k % NBUF is rewritten by
         verify(k + NBUF), queued only after tally(k) returned (the tally
         synchronises its stream)."""
+        tr = self.host_trace
         pending = []
         for k in range(steps):
+            if tr is not None:
+                tr.append(("v", k, time.perf_counter()))
             pending.append(self.verify(k))
             if len(pending) == self.NBUF:
+                if tr is not None:
+                    tr.append(("t", k, time.perf_counter()))
                 self.tally(pending.pop(0))
         while pending:
             self.tally(pending.pop(0))
@@ -233,6 +246,8 @@ def main():
     t0 = time.perf_counter()
     v = hd.Verifier(dev.index)                  # builds the device's shared G table (5.4 GB, once per process)
     ctx_s = time.perf_counter() - t0
+    # the library's stream (created before anything else uses work_stream)
+    ws = work_stream(dev, priority=-1 if args.stream_priority == "high" else 0)
     sigs, foreign = v.gen_keys(S)
     v.set_signatories(sigs)
     t0 = time.perf_counter()
@@ -240,7 +255,6 @@ def main():
     db, _, _ = generate(v, 0, total, S, args.adv, keys=(sigs, foreign), device=str(dev))
     gen_s = time.perf_counter() - t0
 
-    ws = work_stream(dev)
     torch.cuda.set_stream(ws)          # torch ops (RCCL all-gather included) share the library's stream
     ts = torch.cuda.Stream(device=dev)
     pipe = Pipeline(v, db, total, B, rank, world, dist, ws, ts, tally=not args.no_tally)
@@ -259,7 +273,12 @@ def main():
     pipe.run(args.warmup)
     v.profile(True)
     v.profile_read()                    # clear
+    if pipe.host_trace is not None:
+        pipe.host_trace.clear()
     elapsed = timed(pipe, args.steps, dist, dev)
+    if pipe.host_trace:
+        t0h = pipe.host_trace[0][2]
+        print("host trace:", [(a, k, round((t - t0h) * 1e3, 3)) for a, k, t in pipe.host_trace], file=sys.stderr)
     calls, verify_ms, sums_launches, sums_ms = v.profile_read()
     v.profile(False)
     if dist is not None:

@@ -3,27 +3,29 @@
 // (process.go:486-494, 534, 574-582, 626-632, 658, 696-702, 751), for every
 // (height, round) in a batch at once.
 //
-// Candidates are VALID Prevotes / Precommits.  The tally is three group-bys,
-// done with open-addressing hash tables in HBM rather than sorts (a sort of
-// 1M 64-bit keys is ~0.2 ms per radix pass; a probe is a few L2 accesses):
+// Candidates are VALID Prevotes / Precommits.  Three group-bys:
 //
-//   G  (h, r)                 one slot per round: distinct prevote and
-//                             precommit signers, signers with both
-//   D  (h, r, type, From)     first-wins logs (process.go:834-847)
+//   G  (h, r)                 open-addressing hash table in HBM, one slot per
+//                             round: distinct prevote and precommit signers,
+//                             signers with both (probed once per wavefront:
+//                             lanes of a wavefront usually share their round)
+//   logs (h, r, type, From)   first-wins vote logs (process.go:834-847): for an
+//                             admitted From a dense cell (round rank, type,
+//                             admitted index) of an L2-resident word array,
+//                             first-wins = atomicMin of the batch index; a From
+//                             outside the admitted set takes the hashed table D
 //   C  (G slot, type, value)  count of first-wins votes per value
 //                             (process.go:574-579 and the other count loops)
 //
-// A slot's `claim` word holds the LOWEST batch index of its key: a new key
-// claims an empty slot by CAS, an equal key with a lower index lowers it by
-// atomicMin.  Keys are never copied -- a probe compares against the
+// A hash slot's `claim` word holds the LOWEST batch index of its key: a new
+// key claims an empty slot by CAS, an equal key with a lower index lowers it
+// by atomicMin.  Keys are never copied -- a probe compares against the
 // claimer's fields in the (immutable) batch, so there is no torn-key window.
-// Device-scope atomics execute at the memory side on gfx950 (tens of ns, ~11
-// ns per op on one word), so everything else is read-only probing and
-// wavefront-aggregated adds: the distinct signers of a round over both types
-// (TraceLogs[r] restricted to votes, process.go:744-754) are prevotes +
-// precommits - signers with both, found by probing D for the opposite type.
+// The distinct signers of a round over both types (TraceLogs[r] restricted to
+// votes, process.go:744-754) are prevotes + precommits - signers with both.
 // Counts are integer atomics, hence deterministic; outputs are ordered by the
-// batch index of each group's first message.
+// batch index of each group's first message (an index-addressed scatter and
+// an ordered compaction, no sort).
 // Non-winners compare their value with the winner's: identical -> dropped
 // silently, different -> the double vote handed to Catcher.CatchDouble*
 // (process.go:838-843, 875-880).
@@ -32,6 +34,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "hd_internal.h"
@@ -43,7 +46,11 @@ static const uint32_t kEmpty = 0xFFFFFFFFu;
 
 struct TallyWork {
     DevBuf b[12];
+    void* host = nullptr;   // pinned download stage (hipHostMalloc)
+    size_t host_cap = 0;
 };
+// T_G: the hash tables; T_C: the dense log cells; T_SEL: the output stage;
+// T_SORTK / T_SORTV: order marks / compacted order
 enum TSlot { T_G, T_D, T_C, T_GSLOT, T_DSLOT, T_NSEL, T_SEL, T_SORTK, T_SORTV, T_TMP, T_DUP };
 
 // table layouts (structure of arrays inside one allocation, capacity cap)
@@ -86,17 +93,24 @@ __device__ __forceinline__ bool candidate(const DevBatch& b, const uint8_t* verd
     return p.nparts <= 1 || part_of(hash_hr(b.height[i], b.round[i]), p.nparts) == p.part;
 }
 
-// candidates of the partition (sizes the hash tables): a wavefront sum,
-// then one global atomic per wavefront (a shared-memory atomic from every
-// lane serialises the block: measured 114 us per 1M messages)
+// candidates of the partition (sizes the hash tables of a partitioned tally):
+// a block sum, then one global atomic per block -- same-word atomics
+// serialise at the memory side (~11 ns each), so one per wavefront over 1M
+// messages cost 180 us
 __global__ __launch_bounds__(256) void k_tally_count(DevBatch b, const uint8_t* __restrict__ verdict,
                                                      const uint32_t* __restrict__ bitmap, Part p,
                                                      uint32_t* __restrict__ count) {
+    __shared__ uint32_t part_sums[4];
     uint32_t mine = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += gridDim.x * blockDim.x)
         mine += candidate(b, verdict, bitmap, i, p) ? 1u : 0u;
     HD_UNROLL for (int off = 32; off > 0; off >>= 1) mine += (uint32_t)__shfl_xor((int)mine, off, 64);
-    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(count, mine);
+    if ((threadIdx.x & 63) == 0) part_sums[threadIdx.x >> 6] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t t = part_sums[0] + part_sums[1] + part_sums[2] + part_sums[3];
+        if (t) atomicAdd(count, t);
+    }
 }
 
 __device__ __forceinline__ bool eq32(const uint8_t* a, const uint8_t* b) {
@@ -176,12 +190,12 @@ __device__ __forceinline__ uint64_t hash_log(uint64_t hhr, const uint8_t* from, 
     return mix64(hhr ^ *reinterpret_cast<const uint64_t*>(from) ^ (uint64_t)t);
 }
 
-// pass 1: every candidate -> its round (G) and its log entry (D, first-wins:
-// the lowest index of the key); a new D slot counts a distinct signer of
-// that type in the round.
-__global__ void k_tally_logs(DevBatch b, const uint8_t* __restrict__ verdict, const uint32_t* __restrict__ bitmap,
-                             Part p, GTab G, uint32_t* __restrict__ D, uint32_t mask, uint32_t* __restrict__ gslot,
-                             uint32_t* __restrict__ dslot, uint8_t* __restrict__ dup) {
+// pass 1: every candidate -> its round (G slot).  Lanes of a wavefront
+// usually share their round, so the first active lane probes for all lanes
+// with its (h, r) (first_active_lane / shfl64).
+__global__ void k_tally_rounds(DevBatch b, const uint8_t* __restrict__ verdict, const uint32_t* __restrict__ bitmap,
+                               Part p, GTab G, uint32_t mask, uint32_t* __restrict__ gslot,
+                               uint8_t* __restrict__ dup) {
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += stride) {
         if (!candidate(b, verdict, bitmap, i, p)) {
@@ -190,68 +204,75 @@ __global__ void k_tally_logs(DevBatch b, const uint8_t* __restrict__ verdict, co
             continue;
         }
         const int64_t h = b.height[i], r = b.round[i];
-        const uint8_t t = b.type[i];
-        const uint8_t* from = b.from32 + 32 * (size_t)i;
-        const uint64_t hhr = hash_hr(h, r);
-        bool created;
         const int lead = first_active_lane();
         const bool follower = shfl64(h, lead) == h && shfl64(r, lead) == r && (int)(threadIdx.x & 63) != lead;
         uint32_t g = kEmpty;
+        bool created;
         if (!follower)
-            g = probe(G.claim, mask, hhr, i, [&](uint32_t c) { return b.height[c] == h && b.round[c] == r; },
-                      created);
-        {
-            const uint32_t gl = (uint32_t)__shfl((int)g, lead, 64);
-            if (follower) g = gl;
-        }
-        const uint32_t d = probe(D, mask, hash_log(hhr, from, t), i,
-                                 [&](uint32_t c) {
-                                     return b.type[c] == t && b.height[c] == h && b.round[c] == r &&
-                                            eq32(b.from32 + 32 * (size_t)c, from);
-                                 },
-                                 created);
-        wave_add(G.nprev, g, created && t == T_PREVOTE);
-        wave_add(G.nprec, g, created && t == T_PRECOMMIT);
-        gslot[i] = g;
-        dslot[i] = d;
+            g = probe(G.claim, mask, hash_hr(h, r), i,
+                      [&](uint32_t c) { return b.height[c] == h && b.round[c] == r; }, created);
+        const uint32_t gl = (uint32_t)__shfl((int)g, lead, 64);
+        gslot[i] = follower ? gl : g;
     }
 }
 
-// pass 2: winners count their value (C) and, for prevotes, whether the same
-// signer also has a precommit log in the round; the rest are classified
-// against the winner's value.
-__global__ void k_tally_values(DevBatch b, const uint32_t* __restrict__ D, GTab G, CTab C, uint32_t mask,
-                               const uint32_t* __restrict__ gslot, const uint32_t* __restrict__ dslot,
-                               uint8_t* __restrict__ dup) {
+// Dense vote logs.  A candidate's log key (h, r, type, From) is, for an
+// admitted From, the cell (round rank, type, admitted index) of an array of
+// n_rounds x 2 x S words -- a few MB, L2-resident -- and first-wins is one
+// atomicMin of the batch index into that cell: no hashing, no key compares
+// against the batch.  A From outside the context's admitted set (possible
+// when the caller's verdicts predate a set change) takes the hashed table D
+// instead; a signatory's prevote and precommit always take the same path.
+// ref[i]: the cell index, or HD_REF_HASHED | the D slot.
+#define HD_REF_HASHED 0x80000000u
+__global__ void k_tally_logs(DevBatch b, const uint32_t* __restrict__ gslot, const uint32_t* __restrict__ rank_of,
+                             const uint32_t* __restrict__ adm, uint32_t S, int adm_steps, uint32_t* __restrict__ Dd,
+                             uint32_t* __restrict__ D, uint32_t mask, uint32_t* __restrict__ ref) {
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += stride) {
         const uint32_t g = gslot[i];
         if (g == kEmpty) continue;
-        const uint32_t w = D[dslot[i]];
-        const uint8_t* value = b.value32 + 32 * (size_t)i;
-        if (w != i) {
-            if (dup) dup[i] = eq32(b.value32 + 32 * (size_t)w, value) ? 1 : 2;
-            continue;
-        }
-        if (dup) dup[i] = 0;
         const uint8_t t = b.type[i];
-        const int64_t h = b.height[i], r = b.round[i];
         const uint8_t* from = b.from32 + 32 * (size_t)i;
-        bool both = false;
-        if (t == T_PREVOTE) {
-            const uint32_t o = find(D, mask, hash_log(hash_hr(h, r), from, T_PRECOMMIT), [&](uint32_t c) {
-                return b.type[c] == T_PRECOMMIT && b.height[c] == h && b.round[c] == r &&
-                       eq32(b.from32 + 32 * (size_t)c, from);
-            });
-            both = o != kEmpty;
+        int32_t signer = -1;
+        if (Dd) {
+            uint32_t from_be[8];
+            HD_UNROLL for (int w = 0; w < 8; w++) from_be[w] = load_be32(from + 4 * w);
+            signer = admitted_find(adm, S, adm_steps, from_be);
         }
-        wave_add(G.nboth, g, both);
-        const uint64_t hv = *reinterpret_cast<const uint64_t*>(value) ^ *reinterpret_cast<const uint64_t*>(value + 8);
-        bool created;
-        // same (round, type, value) as the wave's first active winner: share its slot
-        const int lead = first_active_lane();
-        const uint4* vw = reinterpret_cast<const uint4*>(value);
-        const uint4 v0 = vw[0], v1 = vw[1];
+        if (signer >= 0) {
+            const uint32_t cell = (rank_of[g] * 2u + (t == T_PRECOMMIT ? 1u : 0u)) * S + (uint32_t)signer;
+            atomicMin(&Dd[cell], i);
+            ref[i] = cell;
+        } else {
+            const int64_t h = b.height[i], r = b.round[i];
+            bool created;
+            const uint32_t d = probe(D, mask, hash_log(hash_hr(h, r), from, t), i,
+                                     [&](uint32_t c) {
+                                         return b.type[c] == t && b.height[c] == h && b.round[c] == r &&
+                                                eq32(b.from32 + 32 * (size_t)c, from);
+                                     },
+                                     created);
+            ref[i] = HD_REF_HASHED | d;
+        }
+    }
+}
+
+// Per-value counts of a wavefront's winners: the distinct (round, type,
+// value) keys among the active lanes are handled one at a time -- the lowest
+// lane holding a key (the lowest batch index, so first-wins of the claim word
+// stays exact) probes C once and adds the number of lanes with that key in
+// one atomic.  A batch's votes repeat few values per round, so this is a few
+// probes and atomics per wavefront instead of one per lane on a handful of
+// hot words.
+__device__ __forceinline__ void count_value(CTab C, uint32_t mask, const DevBatch& b, const uint32_t* gslot,
+                                            uint32_t g, uint8_t t, uint32_t i, const uint8_t* value) {
+    const uint4* vw = reinterpret_cast<const uint4*>(value);
+    const uint4 v0 = vw[0], v1 = vw[1];
+    const int lane = threadIdx.x & 63;
+    unsigned long long pending = __ballot(true);
+    while (pending) {
+        const int lead = __ffsll((long long)pending) - 1;
         uint32_t diff = (uint32_t)__shfl((int)g, lead, 64) ^ g;
         diff |= (uint32_t)__shfl((int)t, lead, 64) ^ t;
         diff |= (uint32_t)__shfl((int)v0.x, lead, 64) ^ v0.x;
@@ -262,49 +283,125 @@ __global__ void k_tally_values(DevBatch b, const uint32_t* __restrict__ D, GTab 
         diff |= (uint32_t)__shfl((int)v1.y, lead, 64) ^ v1.y;
         diff |= (uint32_t)__shfl((int)v1.z, lead, 64) ^ v1.z;
         diff |= (uint32_t)__shfl((int)v1.w, lead, 64) ^ v1.w;
-        const bool follower = diff == 0 && (int)(threadIdx.x & 63) != lead;
-        uint32_t c = kEmpty;
-        if (!follower)
-            c = probe(C.claim, mask, mix64(hv ^ ((uint64_t)g << 1 | (t & 1u))), i,
-                      [&](uint32_t o) {
-                          return gslot[o] == g && b.type[o] == t && eq32(b.value32 + 32 * (size_t)o, value);
-                      },
-                      created);
-        {
-            const uint32_t cl = (uint32_t)__shfl((int)c, lead, 64);
-            if (follower) c = cl;
+        const unsigned long long same = __ballot(diff == 0 && ((pending >> lane) & 1ull));
+        if (lane == lead) {
+            const uint64_t hv = *reinterpret_cast<const uint64_t*>(value) ^
+                                *reinterpret_cast<const uint64_t*>(value + 8);
+            bool created;
+            const uint32_t c = probe(C.claim, mask, mix64(hv ^ ((uint64_t)g << 1 | (t & 1u))), i,
+                                     [&](uint32_t o) {
+                                         return gslot[o] == g && b.type[o] == t &&
+                                                eq32(b.value32 + 32 * (size_t)o, value);
+                                     },
+                                     created);
+            atomicAdd(&C.n[c], (uint32_t)__popcll(same));
         }
-        wave_add(C.n, c, true);
+        pending &= ~same;
     }
 }
 
-// occupied slots -> (lowest index, slot) pairs.  Each block compacts a
-// chunk of HD_USED_CHUNK slots in order and reserves its output range with
-// ONE atomic (same-word atomics serialise at the memory side).
-#define HD_USED_CHUNK 8192
-__global__ __launch_bounds__(256) void k_tally_used(uint32_t cap, const uint32_t* __restrict__ claim,
-                                                    uint32_t* __restrict__ key, uint32_t* __restrict__ val,
-                                                    uint32_t* __restrict__ count) {
+// pass 3: each log entry's winner (the lowest index of its key) counts as a
+// distinct signer of its type in the round and counts its value (C); a
+// prevote winner whose signer also has a precommit log in the round counts
+// in nboth.  The other candidates are classified against the winner's value.
+__global__ void k_tally_values(DevBatch b, const uint32_t* __restrict__ Dd, uint32_t S, const uint32_t* __restrict__ D,
+                               GTab G, CTab C, uint32_t mask, const uint32_t* __restrict__ gslot,
+                               const uint32_t* __restrict__ ref, uint8_t* __restrict__ dup) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += stride) {
+        const uint32_t g = gslot[i];
+        if (g == kEmpty) continue;
+        const uint32_t rf = ref[i];
+        const bool hashed = (rf & HD_REF_HASHED) != 0;
+        const uint32_t w = hashed ? D[rf & ~HD_REF_HASHED] : Dd[rf];
+        const uint8_t* value = b.value32 + 32 * (size_t)i;
+        if (w != i) {
+            if (dup) dup[i] = eq32(b.value32 + 32 * (size_t)w, value) ? 1 : 2;
+            continue;
+        }
+        if (dup) dup[i] = 0;
+        const uint8_t t = b.type[i];
+        wave_add(G.nprev, g, t == T_PREVOTE);
+        wave_add(G.nprec, g, t == T_PRECOMMIT);
+        bool both = false;
+        if (t == T_PREVOTE) {
+            if (!hashed) {
+                both = Dd[rf + S] != kEmpty;   // the same signer's precommit cell of the round
+            } else {
+                const int64_t h = b.height[i], r = b.round[i];
+                const uint8_t* from = b.from32 + 32 * (size_t)i;
+                const uint32_t o = find(D, mask, hash_log(hash_hr(h, r), from, T_PRECOMMIT), [&](uint32_t c) {
+                    return b.type[c] == T_PRECOMMIT && b.height[c] == h && b.round[c] == r &&
+                           eq32(b.from32 + 32 * (size_t)c, from);
+                });
+                both = o != kEmpty;
+            }
+        }
+        wave_add(G.nboth, g, both);
+        count_value(C, mask, b, gslot, g, t, i, value);
+    }
+}
+
+// Output order: the groups of a table sorted by their first batch index.
+// Each occupied slot's claim word IS that index (unique per table), so the
+// sort is a scatter into an index-addressed array (at[claim] = slot) and an
+// ordered compaction of it -- no radix sort.
+__global__ __launch_bounds__(256) void k_tally_mark(uint32_t cap, const uint32_t* __restrict__ claim,
+                                                    uint32_t* __restrict__ at) {
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += gridDim.x * blockDim.x) {
+        const uint32_t c = claim[s];
+        if (c != kEmpty) at[c] = s;
+    }
+}
+
+// ordered compaction of at (n entries) in chunks of HD_CHUNK: per-chunk
+// counts, then each chunk writes from the sum of the counts before it (a
+// block reads at most n / HD_CHUNK words); rank_of[slot] = output position
+#define HD_CHUNK 8192
+__global__ __launch_bounds__(256) void k_tally_chunk_counts(uint32_t n, const uint32_t* __restrict__ at,
+                                                            uint32_t* __restrict__ cnt) {
+    typedef hipcub::BlockReduce<uint32_t, 256> Red;
+    __shared__ typename Red::TempStorage ts;
+    const uint32_t lo = blockIdx.x * HD_CHUNK, hi = min(n, lo + HD_CHUNK);
+    uint32_t m = 0;
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += 256) m += at[i] != kEmpty ? 1u : 0u;
+    const uint32_t t = Red(ts).Sum(m);
+    if (threadIdx.x == 0) cnt[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(256) void k_tally_chunk_write(uint32_t n, const uint32_t* __restrict__ at,
+                                                           const uint32_t* __restrict__ cnt,
+                                                           uint32_t* __restrict__ order,
+                                                           uint32_t* __restrict__ rank_of,
+                                                           uint32_t* __restrict__ total) {
     typedef hipcub::BlockScan<uint32_t, 256> Scan;
+    typedef hipcub::BlockReduce<uint32_t, 256> Red;
     __shared__ typename Scan::TempStorage ts;
+    __shared__ typename Red::TempStorage rs;
     __shared__ uint32_t base;
-    const uint32_t lo = blockIdx.x * HD_USED_CHUNK;
-    const int per = HD_USED_CHUNK / 256;  // contiguous slots per thread
-    const uint32_t s0 = lo + threadIdx.x * per;
-    uint32_t mine = 0;
-    for (int k = 0; k < per; k++) mine += (s0 + k < cap && claim[s0 + k] != kEmpty) ? 1u : 0u;
-    uint32_t off = 0, total = 0;
-    Scan(ts).ExclusiveSum(mine, off, total);
-    if (threadIdx.x == 0) base = total ? atomicAdd(count, total) : 0u;
+    const uint32_t nch = (n + HD_CHUNK - 1) / HD_CHUNK;
+    uint32_t bsum = 0;
+    for (uint32_t k = threadIdx.x; k < blockIdx.x; k += 256) bsum += cnt[k];
+    bsum = Red(rs).Sum(bsum);
+    if (threadIdx.x == 0) {
+        base = bsum;
+        if (blockIdx.x == nch - 1) *total = bsum + cnt[blockIdx.x];
+    }
     __syncthreads();
+    constexpr uint32_t PER = HD_CHUNK / 256;   // contiguous entries per thread, in order
+    const uint32_t lo = blockIdx.x * HD_CHUNK + threadIdx.x * PER;
+    uint32_t mine = 0;
+    for (uint32_t k = 0; k < PER; k++) mine += (lo + k < n && at[lo + k] != kEmpty) ? 1u : 0u;
+    uint32_t off = 0;
+    Scan(ts).ExclusiveSum(mine, off);
     uint32_t o = base + off;
-    for (int k = 0; k < per && mine; k++) {
-        const uint32_t s = s0 + k;
-        if (s < cap) {
-            const uint32_t c = claim[s];
-            if (c != kEmpty) {
-                key[o] = c;
-                val[o] = s;
+    for (uint32_t k = 0; k < PER && mine; k++) {
+        const uint32_t i = lo + k;
+        if (i < n) {
+            const uint32_t v = at[i];
+            if (v != kEmpty) {
+                order[o] = v;
+                if (rank_of) rank_of[v] = o;
                 o++;
             }
         }
@@ -361,40 +458,29 @@ void hd_tally_release(hd_ctx* ctx) {
     if (!ctx || !ctx->tally) return;
     for (auto& b : ctx->tally->b)
         if (b.p) (void)hipFree(b.p);
+    if (ctx->tally->host) (void)hipHostFree(ctx->tally->host);
     delete ctx->tally;
     ctx->tally = nullptr;
 }
 
 static inline uint32_t nblk(uint32_t n) { return (n + 255) / 256; }
 
-// Sort the occupied slots of a table by their group's first batch index.
-// Returns the number of groups in *n_out (host) and the slot order in *order.
-static int used_sorted(hd_ctx* ctx, uint32_t cap, const uint32_t* claim, uint32_t** order, uint32_t* n_out,
-                       hipStream_t s) {
-    int rc = 0;
-    uint32_t* cnt = (uint32_t*)tbuf(ctx, T_NSEL, 64, &rc);
-    uint32_t* key = (uint32_t*)tbuf(ctx, T_SORTK, 8 * (size_t)cap, &rc);
-    uint32_t* val = (uint32_t*)tbuf(ctx, T_SORTV, 8 * (size_t)cap, &rc);
-    if (rc) return rc;
-    TCHK(hipMemsetAsync(cnt, 0, 4, s), "memset count");
-    k_tally_used<<<(cap + HD_USED_CHUNK - 1) / HD_USED_CHUNK, 256, 0, s>>>(cap, claim, key, val, cnt);
-    uint32_t n = 0;
-    TCHK(hipMemcpyAsync(&n, cnt, 4, hipMemcpyDeviceToHost, s), "group count");
-    TCHK(hipStreamSynchronize(s), "group count sync");
-    *n_out = n;
-    if (n == 0) {
-        *order = val;
-        return HD_OK;
-    }
-    hipcub::DoubleBuffer<uint32_t> kk(key, key + cap), vv(val, val + cap);
-    size_t need = 0;
-    TCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, need, kk, vv, n, 0, 32, s), "sort size");
-    void* tmp = tbuf(ctx, T_TMP, need, &rc);
-    if (rc) return rc;
-    TCHK(hipcub::DeviceRadixSort::SortPairs(tmp, need, kk, vv, n, 0, 32, s), "sort groups");
-    *order = vv.Current();
+// the groups of one table (claim words, capacity cap) in first-index order:
+// order[0 .. total), rank_of[slot] (optional); the count lands in *d_total.
+// `at` (n words) must be all-empty on entry.
+static int table_order(hd_ctx* ctx, uint32_t n, uint32_t cap, const uint32_t* claim, uint32_t* at, uint32_t* cnt,
+                       uint32_t* order, uint32_t* rank_of, uint32_t* d_total, hipStream_t s) {
+    const uint32_t nch = (n + HD_CHUNK - 1) / HD_CHUNK;
+    k_tally_mark<<<std::min<uint32_t>(nblk(cap), (uint32_t)ctx->n_cu * 8u), 256, 0, s>>>(cap, claim, at);
+    k_tally_chunk_counts<<<nch, 256, 0, s>>>(n, at, cnt);
+    k_tally_chunk_write<<<nch, 256, 0, s>>>(n, at, cnt, order, rank_of, d_total);
+    TCHK(hipGetLastError(), "tally order kernels");
     return HD_OK;
 }
+
+// dense log cells allowed (words): beyond this the hashed table takes every
+// candidate (e.g. a batch of a million single-message rounds)
+#define HD_TALLY_DENSE_MAX (64ull << 20)
 
 static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdict, const uint32_t* d_bitmap,
                         Part part, hd_tally_out* out, hipStream_t s) {
@@ -402,99 +488,132 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     if (!ctx->tally) ctx->tally = new TallyWork();
     DevBatch b{n, hb->type, hb->height, hb->round, hb->valid_round, hb->value32, hb->from32, hb->sig65};
     int rc = 0;
-    const uint32_t grid = std::min<uint32_t>(nblk(n), (uint32_t)ctx->n_cu * 16u);
-    // the tables hold at most one key per candidate: size them by this
-    // partition's candidates (one counting pass), load factor <= 1/2 so
-    // probes terminate
+    // blocks per CU of the probe passes (HD_TALLY_BPC, default 16)
+    static const uint32_t bpc = getenv("HD_TALLY_BPC") ? (uint32_t)std::max(1, atoi(getenv("HD_TALLY_BPC"))) : 16u;
+    const uint32_t grid = std::min<uint32_t>(nblk(n), (uint32_t)ctx->n_cu * bpc);
+    // the tables hold at most one key per candidate, load factor <= 1/2 so
+    // probes terminate.  A partition sizes them by its own candidates (one
+    // counting pass); the whole batch by n.
     uint32_t n_cand = n;
-    {
-        uint32_t* cnt = (uint32_t*)tbuf(ctx, T_NSEL, 64, &rc);
-        if (rc) return rc;
+    uint32_t* cnt = (uint32_t*)tbuf(ctx, T_NSEL, 64, &rc);
+    if (rc) return rc;
+    if (part.nparts > 1) {
         TCHK(hipMemsetAsync(cnt + 1, 0, 4, s), "clear candidate count");
-        k_tally_count<<<grid, 256, 0, s>>>(b, d_verdict, d_bitmap, part, cnt + 1);
+        k_tally_count<<<std::min<uint32_t>(nblk(n), (uint32_t)ctx->n_cu * 4u), 256, 0, s>>>(b, d_verdict, d_bitmap,
+                                                                                              part, cnt + 1);
         TCHK(hipMemcpyAsync(&n_cand, cnt + 1, 4, hipMemcpyDeviceToHost, s), "candidate count");
         TCHK(hipStreamSynchronize(s), "candidate count sync");
     }
     uint32_t cap = 1024;
     while (cap < 2 * n_cand) cap <<= 1;
     const uint32_t mask = cap - 1;
-    uint32_t* g = (uint32_t*)tbuf(ctx, T_G, 20 * (size_t)cap, &rc);  // 16 B used; staging for the outputs
-    uint32_t* d = (uint32_t*)tbuf(ctx, T_D, 4 * (size_t)cap, &rc);
-    uint32_t* c = (uint32_t*)tbuf(ctx, T_C, 8 * (size_t)cap, &rc);
+    const uint32_t nch = (n + HD_CHUNK - 1) / HD_CHUNK;
+    // one allocation for the tables: the claim words (G, C, D; := empty by one
+    // memset), then the counters (G x 3, C; := 0 by one memset), then rank_of
+    uint32_t* tabs = (uint32_t*)tbuf(ctx, T_G, 4 * 8 * (size_t)cap, &rc);
     uint32_t* gslot = (uint32_t*)tbuf(ctx, T_GSLOT, 4 * (size_t)n, &rc);
-    uint32_t* dslot = (uint32_t*)tbuf(ctx, T_DSLOT, 4 * (size_t)n, &rc);
+    uint32_t* ref = (uint32_t*)tbuf(ctx, T_DSLOT, 4 * (size_t)n, &rc);
     uint8_t* d_dup = out->dup ? (uint8_t*)tbuf(ctx, T_DUP, n, &rc) : nullptr;
+    uint32_t* at = (uint32_t*)tbuf(ctx, T_SORTK, 8 * (size_t)n, &rc);      // at_g | at_c
+    uint32_t* ord = (uint32_t*)tbuf(ctx, T_SORTV, 8 * (size_t)n, &rc);     // order_g | order_c
+    uint32_t* ccnt = (uint32_t*)tbuf(ctx, T_TMP, 4 * ((size_t)nch + 2), &rc);  // chunk counts, totals
     if (rc) return rc;
     if (n_cand == 0) {   // nothing to tally here (dup: every message 3)
         out->n_hr = out->n_counts = 0;
         if (out->dup) memset(out->dup, 3, n);
         return HD_OK;
     }
-    GTab G{g, g + cap, g + 2 * (size_t)cap, g + 3 * (size_t)cap};
-    CTab C{c, c + cap};
-    // claim words := empty; counters := 0
-    TCHK(hipMemsetAsync(g, 0xFF, 4 * (size_t)cap, s), "clear G");
-    TCHK(hipMemsetAsync(G.nprev, 0, 12 * (size_t)cap, s), "clear G counters");
-    TCHK(hipMemsetAsync(d, 0xFF, 4 * (size_t)cap, s), "clear D");
-    TCHK(hipMemsetAsync(c, 0xFF, 4 * (size_t)cap, s), "clear C");
-    TCHK(hipMemsetAsync(C.n, 0, 4 * (size_t)cap, s), "clear C counters");
-    k_tally_logs<<<grid, 256, 0, s>>>(b, d_verdict, d_bitmap, part, G, d, mask, gslot, dslot, d_dup);
-    k_tally_values<<<grid, 256, 0, s>>>(b, d, G, C, mask, gslot, dslot, d_dup);
-    TCHK(hipGetLastError(), "tally kernels");
-
-    uint32_t n_hr = 0, n_cnt = 0;
-    uint32_t* order = nullptr;
-    rc = used_sorted(ctx, cap, G.claim, &order, &n_hr, s);
+    const size_t K = cap;
+    GTab G{tabs, tabs + 3 * K, tabs + 4 * K, tabs + 5 * K};
+    CTab C{tabs + K, tabs + 6 * K};
+    uint32_t* d = tabs + 2 * K;
+    uint32_t* rank_of = tabs + 7 * K;
+    uint32_t* tot = ccnt + nch;
+    TCHK(hipMemsetAsync(tabs, 0xFF, 4 * 3 * K, s), "clear claims");
+    TCHK(hipMemsetAsync(tabs + 3 * K, 0, 4 * 4 * K, s), "clear counters");
+    TCHK(hipMemsetAsync(at, 0xFF, 8 * (size_t)n, s), "clear order marks");
+    // rounds, then their first-index order (the output order and the dense rank)
+    k_tally_rounds<<<grid, 256, 0, s>>>(b, d_verdict, d_bitmap, part, G, mask, gslot, d_dup);
+    rc = table_order(ctx, n, cap, G.claim, at, ccnt, ord, rank_of, tot, s);
     if (rc) return rc;
-    out->n_hr = n_hr;
-    if (n_hr && n_hr <= out->cap_hr) {
-        char* st = (char*)tbuf(ctx, T_SEL, 32 * (size_t)n_hr, &rc);
+    uint32_t n_hr = 0;
+    TCHK(hipMemcpyAsync(&n_hr, tot, 4, hipMemcpyDeviceToHost, s), "round count");
+    TCHK(hipStreamSynchronize(s), "round count sync");
+    // dense log cells (n_hr x 2 x S) for admitted signatories, the hashed D
+    // table for the rest
+    const uint32_t S = ctx->n_adm;
+    const size_t cells = (size_t)n_hr * 2 * S;
+    uint32_t* Dd = nullptr;
+    if (S > 0 && cells <= HD_TALLY_DENSE_MAX) {
+        Dd = (uint32_t*)tbuf(ctx, T_C, 4 * cells, &rc);
         if (rc) return rc;
-        int64_t* o_h = reinterpret_cast<int64_t*>(st);
-        int64_t* o_r = o_h + n_hr;
-        uint32_t* o_prev = reinterpret_cast<uint32_t*>(o_r + n_hr);
-        uint32_t* o_prec = o_prev + n_hr;
-        uint32_t* o_any = o_prec + n_hr;
-        uint32_t* o_rep = o_any + n_hr;
-        k_tally_emit_hr<<<nblk(n_hr), 256, 0, s>>>(n_hr, order, G, b.height, b.round, o_h, o_r, o_prev, o_prec, o_any,
-                                                   o_rep);
-        struct Cp { void* dst; const void* src; size_t sz; } cp[] = {
-            {out->hr_height, o_h, 8 * (size_t)n_hr},     {out->hr_round, o_r, 8 * (size_t)n_hr},
-            {out->hr_prevotes, o_prev, 4 * (size_t)n_hr}, {out->hr_precommits, o_prec, 4 * (size_t)n_hr},
-            {out->hr_any, o_any, 4 * (size_t)n_hr},       {out->hr_rep, o_rep, 4 * (size_t)n_hr},
-        };
-        for (auto& x : cp)
-            if (x.dst) TCHK(hipMemcpyAsync(x.dst, x.src, x.sz, hipMemcpyDeviceToHost, s), "hr download");
+        TCHK(hipMemsetAsync(Dd, 0xFF, 4 * cells, s), "clear dense logs");
     }
-    // (the count sort below reuses the sort buffers: same stream, so the
-    // per-round emit above has consumed `order` before they are rewritten)
-    rc = used_sorted(ctx, cap, C.claim, &order, &n_cnt, s);
+    k_tally_logs<<<grid, 256, 0, s>>>(b, gslot, rank_of, ctx->d_adm, S, ctx->adm_steps, Dd, d, mask, ref);
+    k_tally_values<<<grid, 256, 0, s>>>(b, Dd, S, d, G, C, mask, gslot, ref, d_dup);
+    TCHK(hipGetLastError(), "tally kernels");
+    rc = table_order(ctx, n, cap, C.claim, at + n, ccnt, ord + n, nullptr, tot + 1, s);
     if (rc) return rc;
+    uint32_t n_cnt = 0;
+    TCHK(hipMemcpyAsync(&n_cnt, tot + 1, 4, hipMemcpyDeviceToHost, s), "group counts");
+    TCHK(hipStreamSynchronize(s), "group count sync");
+    out->n_hr = n_hr;
     out->n_counts = n_cnt;
-    if (n_hr > out->cap_hr || n_cnt > out->cap_counts) {
-        TCHK(hipStreamSynchronize(s), "sync");
-        return HD_ECAP;
+    if (n_hr > out->cap_hr || n_cnt > out->cap_counts) return HD_ECAP;
+    // Every output into one device stage -- per-round rows (32 B each), the
+    // per-value rows (25 B each), the per-message classification -- and ONE
+    // download into a pinned host stage, then host copies into the caller's
+    // arrays (one blit instead of a dozen).
+    const size_t hr_bytes = 32 * (size_t)n_hr, cnt_bytes = 25 * (size_t)n_cnt;
+    const size_t dup_off = (hr_bytes + cnt_bytes + 63) & ~(size_t)63;
+    const size_t total = dup_off + (out->dup ? (size_t)n : 0);
+    char* st = (char*)tbuf(ctx, T_SEL, total + 64, &rc);
+    if (rc) return rc;
+    TallyWork* tw = ctx->tally;
+    if (tw->host_cap < total) {
+        if (tw->host) (void)hipHostFree(tw->host);
+        tw->host = nullptr;
+        tw->host_cap = 0;
+        TCHK(hipHostMalloc(&tw->host, total + (total >> 2), hipHostMallocDefault), "tally host stage");
+        tw->host_cap = total + (total >> 2);
     }
-    if (n_cnt) {
-        // staging for the counts: the G table (20 B x cap, cap >= 2 n_cnt) is
-        // no longer read once the per-round outputs are downloaded
-        TCHK(hipStreamSynchronize(s), "hr sync");
-        int64_t* c_h = reinterpret_cast<int64_t*>(g);
-        int64_t* c_r = c_h + n_cnt;
-        uint32_t* c_rep = reinterpret_cast<uint32_t*>(c_r + n_cnt);
-        uint32_t* c_n = c_rep + n_cnt;
-        uint8_t* c_t = reinterpret_cast<uint8_t*>(c_n + n_cnt);
-        k_tally_emit_counts<<<nblk(n_cnt), 256, 0, s>>>(n_cnt, order, C, b.height, b.round, b.type, c_h, c_r, c_t,
+    int64_t* o_h = reinterpret_cast<int64_t*>(st);
+    int64_t* o_r = o_h + n_hr;
+    uint32_t* o_prev = reinterpret_cast<uint32_t*>(o_r + n_hr);
+    uint32_t* o_prec = o_prev + n_hr;
+    uint32_t* o_any = o_prec + n_hr;
+    uint32_t* o_rep = o_any + n_hr;
+    int64_t* c_h = reinterpret_cast<int64_t*>(st + hr_bytes);
+    int64_t* c_r = c_h + n_cnt;
+    uint32_t* c_rep = reinterpret_cast<uint32_t*>(c_r + n_cnt);
+    uint32_t* c_n = c_rep + n_cnt;
+    uint8_t* c_t = reinterpret_cast<uint8_t*>(c_n + n_cnt);
+    if (n_hr)
+        k_tally_emit_hr<<<nblk(n_hr), 256, 0, s>>>(n_hr, ord, G, b.height, b.round, o_h, o_r, o_prev, o_prec, o_any,
+                                                   o_rep);
+    if (n_cnt)
+        k_tally_emit_counts<<<nblk(n_cnt), 256, 0, s>>>(n_cnt, ord + n, C, b.height, b.round, b.type, c_h, c_r, c_t,
                                                         c_rep, c_n);
-        struct Cp { void* dst; const void* src; size_t sz; } cp[] = {
-            {out->count_height, c_h, 8 * (size_t)n_cnt}, {out->count_round, c_r, 8 * (size_t)n_cnt},
-            {out->count_type, c_t, (size_t)n_cnt},       {out->count_rep, c_rep, 4 * (size_t)n_cnt},
-            {out->count_n, c_n, 4 * (size_t)n_cnt},
-        };
-        for (auto& x : cp) TCHK(hipMemcpyAsync(x.dst, x.src, x.sz, hipMemcpyDeviceToHost, s), "count download");
-    }
-    if (out->dup) TCHK(hipMemcpyAsync(out->dup, d_dup, (size_t)n, hipMemcpyDeviceToHost, s), "dup download");
+    TCHK(hipGetLastError(), "tally emit");
+    if (out->dup) TCHK(hipMemcpyAsync(st + dup_off, d_dup, (size_t)n, hipMemcpyDeviceToDevice, s), "dup stage");
+    TCHK(hipMemcpyAsync(tw->host, st, total, hipMemcpyDeviceToHost, s), "tally download");
     TCHK(hipStreamSynchronize(s), "tally sync");
+    const char* hst = (const char*)tw->host;
+    auto put = [&](void* dst, const void* dev_src, size_t sz) {
+        if (dst && sz) memcpy(dst, hst + ((const char*)dev_src - st), sz);
+    };
+    put(out->hr_height, o_h, 8 * (size_t)n_hr);
+    put(out->hr_round, o_r, 8 * (size_t)n_hr);
+    put(out->hr_prevotes, o_prev, 4 * (size_t)n_hr);
+    put(out->hr_precommits, o_prec, 4 * (size_t)n_hr);
+    put(out->hr_any, o_any, 4 * (size_t)n_hr);
+    put(out->hr_rep, o_rep, 4 * (size_t)n_hr);
+    put(out->count_height, c_h, 8 * (size_t)n_cnt);
+    put(out->count_round, c_r, 8 * (size_t)n_cnt);
+    put(out->count_type, c_t, (size_t)n_cnt);
+    put(out->count_rep, c_rep, 4 * (size_t)n_cnt);
+    put(out->count_n, c_n, 4 * (size_t)n_cnt);
+    if (out->dup) memcpy(out->dup, hst + dup_off, (size_t)n);
     return HD_OK;
 }
 

@@ -24,16 +24,19 @@ def _torch():
 _STREAMS = {}
 
 
-def work_stream(device=None):
+def work_stream(device=None, priority: int = 0):
     """A dedicated (non-default) torch stream per device for library launches.
 
     The C ABI reads a NULL stream as "the context's own stream", and torch's
     default stream has handle 0, so device work is always enqueued on an
-    explicit stream whose handle is non-zero."""
+    explicit stream whose handle is non-zero.  `priority` (torch convention:
+    lower is higher, -1 = high) applies when the stream is first created: a
+    high-priority verify stream keeps its workgroups ahead of side work (the
+    tally of an earlier batch) queued on normal streams."""
     torch = _torch()
     dev = torch.device("cuda", torch.cuda.current_device() if device is None else torch.device(device).index or 0)
     if dev not in _STREAMS:
-        _STREAMS[dev] = torch.cuda.Stream(device=dev)
+        _STREAMS[dev] = torch.cuda.Stream(device=dev, priority=priority)
     return _STREAMS[dev]
 
 

@@ -73,13 +73,22 @@ def partition_of(height: int, round_: int, nparts: int) -> int:
     return int(_lib.load().hd_tally_partition_of(int(height), int(round_), int(nparts)))
 
 
-def tally_part(v, dbatch, d_bitmap: int, part: int, nparts: int, stream=None) -> Dict[str, np.ndarray]:
+def tally_out(v, n: int, pinned: bool = False):
+    """A reusable output struct for tally_part over n messages (no per-message
+    dup classification: the partitions' packed rows do not carry it)."""
+    t, a = v._tally_struct(n, pinned=pinned)
+    t.dup = None
+    return t, a
+
+
+def tally_part(v, dbatch, d_bitmap: int, part: int, nparts: int, stream=None, out=None) -> Dict[str, np.ndarray]:
     """This rank's partition of the tally of a device batch (all messages,
     replicated) given the gathered valid bitmap: the packed rows
-    {"counts": [k, 5] int64, "hr": [m, 6] int64} (COUNT_COLS / HR_COLS)."""
+    {"counts": [k, 5] int64, "hr": [m, 6] int64} (COUNT_COLS / HR_COLS).
+    out: a struct from tally_out, reused across calls."""
     from . import _lib
     lib = _lib.load()
-    t, a = v._tally_struct(dbatch.n)
+    t, a = out if out is not None else tally_out(v, dbatch.n)
     rc = lib.hd_tally_device_bitmap_part(v.handle, ctypes.byref(dbatch), d_bitmap, part, nparts, ctypes.byref(t),
                                          stream)
     if rc != 0:

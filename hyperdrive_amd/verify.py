@@ -216,19 +216,33 @@ class Verifier:
 
     # ---- tally -------------------------------------------------------
     @staticmethod
-    def _tally_struct(n: int):
+    def _tally_struct(n: int, pinned: bool = False):
+        """Output arrays for n messages.  pinned: page-locked host memory (torch
+        pin_memory), so the library's device-to-host copies are plain DMA on
+        the tally's stream instead of staged pageable copies."""
+        keep = []
+
+        def mk(dtype):
+            if not pinned:
+                return np.zeros(max(n, 1), dtype)
+            import torch
+            tdt = {np.int64: torch.int64, np.uint8: torch.uint8, np.uint32: torch.int32}[dtype]
+            t = torch.zeros(max(n, 1), dtype=tdt, pin_memory=True)
+            keep.append(t)
+            return t.numpy().view(dtype)
+
         arrs = dict(
-            count_height=np.zeros(max(n, 1), np.int64), count_round=np.zeros(max(n, 1), np.int64),
-            count_type=np.zeros(max(n, 1), np.uint8), count_rep=np.zeros(max(n, 1), np.uint32),
-            count_n=np.zeros(max(n, 1), np.uint32), hr_height=np.zeros(max(n, 1), np.int64),
-            hr_round=np.zeros(max(n, 1), np.int64), hr_prevotes=np.zeros(max(n, 1), np.uint32),
-            hr_precommits=np.zeros(max(n, 1), np.uint32), hr_any=np.zeros(max(n, 1), np.uint32),
-            dup=np.zeros(max(n, 1), np.uint8), hr_rep=np.zeros(max(n, 1), np.uint32))
+            count_height=mk(np.int64), count_round=mk(np.int64), count_type=mk(np.uint8), count_rep=mk(np.uint32),
+            count_n=mk(np.uint32), hr_height=mk(np.int64), hr_round=mk(np.int64), hr_prevotes=mk(np.uint32),
+            hr_precommits=mk(np.uint32), hr_any=mk(np.uint32), dup=mk(np.uint8), hr_rep=mk(np.uint32))
+        if keep:
+            arrs["_pinned"] = keep
         t = HdTallyOut()
         t.cap_counts = n
         t.cap_hr = n
         for k, a in arrs.items():
-            setattr(t, k, _ptr(a))
+            if not k.startswith("_"):
+                setattr(t, k, _ptr(a))
         return t, arrs
 
     @staticmethod

@@ -1,0 +1,15 @@
+# Bench (no aux/sub/cpu) with and without the tally, interleaved.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for cfg in tally notally tally2 notally2; do
+  case $cfg in tally*) f="" ;; notally*) f="--no-tally" ;; esac
+  timeout -k 10 300 python3 bench.py --steps 40 --no-aux --no-sub --no-cpu $f > gpurun_out/b2_$cfg.json 2> gpurun_out/b2_$cfg.err || { tail -5 gpurun_out/b2_$cfg.err; exit 1; }
+  python3 - "$cfg" <<'PY'
+import json,sys
+for l in open(f'gpurun_out/b2_{sys.argv[1]}.json'):
+    if l.startswith('{"metric"'):
+        d=json.loads(l); r=d['roofline']
+        print(sys.argv[1], round(d['value']/1e6,1), 'M/s', round(d['ms_per_step'],3), 'ms/step', 'sums', round(r['kernel_ms'],3), 'call', round(r['verify_call']['ms'],3))
+PY
+done

@@ -62,6 +62,24 @@ def test_generated_batches_match_oracle(verifier, oracle, kind, n, S, adv):
         assert quorum.decide(tal, h, r, f, pv, True) == oracle.decide_round(ot, h, r, f, pv, True)
 
 
+def test_dense_and_hashed_logs(verifier, oracle):
+    """Half the signers admitted: their logs take the dense cells, the others
+    the hashed table, inside one tally (a VALID verdict for a From outside
+    the context's current set, as after a set change) -- same as the oracle."""
+    rng = np.random.default_rng(11)
+    n = 8000
+    sigs = [oracle.sha256(b"m" + bytes([k])) for k in range(40)]
+    vals = [oracle.sha256(b"w" + bytes([k])) for k in range(3)]
+    ob = oracle.Batch()
+    for i in range(n):
+        ob.append(int(rng.integers(2, 4)), int(rng.integers(0, 3)), int(rng.integers(0, 3)), -1,
+                  vals[int(rng.integers(0, 3))], sigs[int(rng.integers(0, 40))], bytes(65))
+    verdicts = [oracle.VALID if rng.random() < 0.95 else oracle.BAD_RS for _ in range(n)]
+    verifier.set_signatories(np.frombuffer(b"".join(sigs[:20]), np.uint8).reshape(20, 32))
+    tal = verifier.tally(to_np(ob), np.array(verdicts, np.uint8))
+    _same(tal, oracle.tally(ob, verdicts))
+
+
 def test_heavy_collisions(verifier, oracle):
     """3 rounds, 40 signers, every signer votes ~25 times per (round, type) with
     a few values: long probe chains in every table, most votes duplicates."""

@@ -369,6 +369,15 @@ HD void sum_step(gej& acc, bool& started, ge cur, uint32_t ec) {
     else sum_step_sel(acc, started, cur, nz);
 }
 
+// the first addition: the accumulator is still the first window's affine
+// point p0, so the cheaper affine + affine formula applies (4M + 2S)
+HD void sum_first(gej& acc, bool& started, const ge& p0, ge cur, uint32_t ec) {
+    if (ec & HD_REF_NEG) fe_neg(cur.y, cur.y);
+    const bool nz = !(ec & HD_REF_ZERO);
+    if (__ballot(!(started && nz)) == 0ull) gej_add_ge_z1(acc, p0, cur);
+    else sum_step_sel(acc, started, cur, nz);
+}
+
 template <int WAVES, int WP, int PF>
 __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* __restrict__ gtab,
                                                           const gp* __restrict__ tab, SplitRows rows) {
@@ -382,13 +391,11 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
     const uint32_t* __restrict__ dp = rows.dig + i;
     uint32_t e = dp[0];
     gej acc;
-    {
-        ge p0;
-        gp_unpack(p0, gtab[e & HD_REF_IDX]);
-        if (e & HD_REF_NEG) fe_neg(p0.y, p0.y);
-        fe_norm_weak(p0.y);
-        gej_set_ge(acc, p0);
-    }
+    ge p0;
+    gp_unpack(p0, gtab[e & HD_REF_IDX]);
+    if (e & HD_REF_NEG) fe_neg(p0.y, p0.y);
+    fe_norm_weak(p0.y);
+    gej_set_ge(acc, p0);
     bool started = !(e & HD_REF_ZERO);
     if (!started) gej_set_inf(acc);
     // The next PF windows' points, packed (16 words each) until used; the
@@ -401,9 +408,10 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
         q2 = (2 < NG ? gtab : ptab)[c2 & HD_REF_IDX];
     }
     if (PF + 1 < NT) dn = dp[(size_t)(PF + 1) * n];
-    HD_NOUNROLL for (int j = 1; j < NT; j++) {
-        const gp cur = q1;
-        const uint32_t ec = c1;
+    // window j's point and digit reference, advancing the prefetch queue
+    auto advance = [&](int j, gp& cur, uint32_t& ec) {
+        cur = q1;
+        ec = c1;
         if (PF == 2) {
             q1 = q2;
             c1 = c2;
@@ -416,6 +424,19 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
             q1 = (j + 1 < NG ? gtab : ptab)[c1 & HD_REF_IDX];
         }
         if (j + PF + 1 < NT) dn = dp[(size_t)(j + PF + 1) * n];
+    };
+    {
+        gp cur;
+        uint32_t ec;
+        advance(1, cur, ec);
+        ge g;
+        gp_unpack(g, cur);
+        sum_first(acc, started, p0, g, ec);
+    }
+    HD_NOUNROLL for (int j = 2; j < NT; j++) {
+        gp cur;
+        uint32_t ec;
+        advance(j, cur, ec);
         ge g;
         gp_unpack(g, cur);
         sum_step(acc, started, g, ec);

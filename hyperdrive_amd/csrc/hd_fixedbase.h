@@ -130,6 +130,42 @@ HD void gej_add_ge_nx(gej& r, const gej& a, const ge& b) {
     r = o;
 }
 
+// a + b for two affine points, no exceptional cases: gej_add_ge_nx with
+// Z1 = 1 (Z1Z1 = 1, U2 = X2, S2 = Y2), 4M + 2S instead of 8M + 3S -- the
+// first addition of a fixed-base sum, whose accumulator is still the first
+// window's table point.  a = +-b gives Z3 = 0, like gej_add_ge_nx.
+HD void gej_add_ge_z1(gej& r, const ge& a, const ge& b) {
+    HD_REQUIRE_T(a.x, "gej_add_ge_z1: a.x");
+    HD_REQUIRE_T(a.y, "gej_add_ge_z1: a.y");
+    HD_REQUIRE_T(b.x, "gej_add_ge_z1: b.x");
+    fe h, R, t;
+    fe_sub_k<2>(h, b.x, a.x);
+    fe_norm_weak(h);           // H = X2 - X1       T
+    fe_sub_k<2>(R, b.y, a.y);  // r = Y2 - Y1       3T (b.y <= 2T)
+    gej o;
+    fe_add(o.z, h, h);
+    fe_norm_weak(o.z);         // Z3 = 2 H          T
+    fe hh, i4, j, v;
+    fe_norm_weak(R);
+    fe_add(R, R, R);           // 2r                2T
+    fe_sqr(hh, h);             // T
+    fe_mul_int(i4, hh, 4);     // I = 4 H^2         4T
+    fe_mul(j, h, i4);          // J = H I           T
+    fe_mul(v, a.x, i4);        // V = X1 I          T
+    fe_sqr(o.x, R);            // T
+    fe_add(t, v, v);
+    fe_add(t, t, j);           // 2V + J            3T
+    fe_sub_k<4>(o.x, o.x, t);
+    fe_norm_weak(o.x);         // X3                T
+    fe_sub_k<2>(t, v, o.x);    // V - X3            3T
+    fe_mul(t, R, t);           // r (V - X3)        T (2T x 3T)
+    fe_mul(j, a.y, j);
+    fe_add(j, j, j);           // 2 Y1 J            2T
+    fe_sub_k<3>(o.y, t, j);
+    fe_norm_weak(o.y);         // Y3                T
+    r = o;
+}
+
 // Booth digit j of u for the table width: bits [W j - 1, W j + W - 1] of u
 // (bits outside [0, 256) read 0).  The words are picked with selects over
 // the 8 limbs instead of a runtime array index, which would put u in scratch.

@@ -272,6 +272,14 @@ extern "C" int hdh_bound_certify(const uint8_t* px, const uint8_t* py, const uin
     qn.y = Q.y; set_class(qn.y, 1);
     gej_add_ge_nx(r, a, qn);
     gej_add_ge_nx(r, aq, qq);           // a == -b: Z3 = 0, still in bounds
+    // the first addition of a fixed-base sum (two affine points), b.y T and 2T
+    {
+        ge pa = P; set_class(pa.x, 1); set_class(pa.y, 1);
+        ge qb = Q; set_class(qb.x, 1); set_class(qb.y, 1);
+        gej_add_ge_z1(r, pa, qb);
+        fe_neg(qb.y, Q.y); set_class(qb.y, 2);
+        gej_add_ge_z1(r, pa, qb);
+    }
     // isomorphic-curve additions (G side of the ladder) and the R table build
     fe zg = b.z; set_class(zg, 1);
     gej_add_ge_zinv(r, a, qn, zg);
@@ -385,6 +393,22 @@ extern "C" int hdh_fb_verify(const uint8_t* pub64, const uint8_t* digest, const 
     return verify_fast(d, r, sw, sig65[64], gt.data(), pt.data());
 }
 // one table entry d 2^(12 j) B (x || y big-endian), for the table-layout test
+// two affine points added with the first-step formula of the fixed-base sum
+// (gej_add_ge_z1); returns 1 when Z3 = 0 (a = +-b), else out = affine x || y
+extern "C" int hdh_add_affine(const uint8_t* ax, const uint8_t* ay, const uint8_t* bx, const uint8_t* by,
+                              uint8_t* out64) {
+    ge a, b;
+    fe_in(a.x, ax); fe_in(a.y, ay); fe_in(b.x, bx); fe_in(b.y, by);
+    gej r;
+    gej_add_ge_z1(r, a, b);
+    if (gej_is_inf(r)) return 1;
+    fe x, y;
+    gej_to_ge(x, y, r);
+    fe_out(out64, x);
+    fe_out(out64 + 32, y);
+    return 0;
+}
+
 extern "C" void hdh_fb_entry(const uint8_t* b64, int j, uint32_t d, uint8_t* out64) {
     ge B, bj, e;
     fe_in(B.x, b64);

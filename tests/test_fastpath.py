@@ -47,6 +47,28 @@ def test_table_entries_are_window_multiples(fb, oracle):
         assert out.raw == _pub64(want), (j, d)
 
 
+def test_first_step_addition(fb, oracle):
+    """gej_add_ge_z1 (the fixed-base sum's first addition, two affine points)
+    against oracle point addition; a = +-b yields Z3 = 0 (the check then hands
+    the message to the full recovery)."""
+    O = oracle
+    fb.hdh_add_affine.argtypes = [ctypes.c_char_p] * 4 + [ctypes.c_char_p]
+    fb.hdh_add_affine.restype = ctypes.c_int
+    rng = random.Random(5)
+    b32 = lambda v: v.to_bytes(32, "big")
+    for _ in range(40):
+        a = O.point_mul(rng.randrange(1, O.N), (O.GX, O.GY))
+        b = O.point_mul(rng.randrange(1, O.N), (O.GX, O.GY))
+        out = ctypes.create_string_buffer(64)
+        assert fb.hdh_add_affine(b32(a[0]), b32(a[1]), b32(b[0]), b32(b[1]), out) == 0
+        assert out.raw == _pub64(O.point_add(a, b))
+    a = O.point_mul(7, (O.GX, O.GY))
+    na = O.point_neg(a)
+    out = ctypes.create_string_buffer(64)
+    assert fb.hdh_add_affine(b32(a[0]), b32(a[1]), b32(na[0]), b32(na[1]), out) == 1
+    assert fb.hdh_add_affine(b32(a[0]), b32(a[1]), b32(a[0]), b32(a[1]), out) == 1
+
+
 def test_fast_path_agrees_with_recovery(fb, oracle):
     O = oracle
     rng = random.Random(12)

@@ -59,6 +59,13 @@ struct FbWork {
     uint32_t* rows = nullptr;     // the split check's per-message rows (SplitRows, 83 words per message)
     size_t cap_rows = 0;
     uint32_t* zr = nullptr;       // the table builder's z ratios (k_fb_runs: HD_FB_RUN x 9 words per thread)
+    // Mapped slots whose key is not READY, in pinned host memory the device
+    // also writes (k_fb_ready subtracts what it finished): 0 means nothing
+    // can be learned any more, so a verify call launches no table-build
+    // kernels.  Set exactly (after a device sync) whenever the admitted set
+    // or the key format changes; UINT32_MAX = unknown.
+    uint32_t* nr_host = nullptr;
+    uint32_t* nr_dev = nullptr;
     // The scratch above (rows, slow, counts) is per context: a verify call
     // on another stream than the previous one first waits for that call's
     // end, so calls of one context never overlap on the device whatever
@@ -451,12 +458,16 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
     soa_store(rows.xyz + 18 * (size_t)n, n, i, acc.z.n);
 }
 
+// T is a multiple of 64, so step j of a wavefront covers the 64 messages
+// j T + t0 .. j T + t0 + 63 (t0 = the wave's first lane, a multiple of 64):
+// two whole words of the valid bitmap, written from one ballot.  Messages
+// handed to the full recovery get bit 0 here; k_verify sets theirs.
 template <int K>
 __global__ __launch_bounds__(256) void k_fast_final(DevBatch b, uint32_t T, SplitRows rows,
                                                     const int32_t* __restrict__ adm_perm,
                                                     uint8_t* __restrict__ verdict, uint8_t* __restrict__ rec32,
                                                     int32_t* __restrict__ signer, uint32_t* __restrict__ slow,
-                                                    uint32_t* __restrict__ n_slow) {
+                                                    uint32_t* __restrict__ n_slow, uint32_t* __restrict__ bitmap) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
     const uint32_t n = b.n;
@@ -516,13 +527,21 @@ __global__ __launch_bounds__(256) void k_fast_final(DevBatch b, uint32_t T, Spli
         }
         const bool to_slow = present && v == HD_NEEDS_SLOW;
         const unsigned long long bal = __ballot(to_slow);
+        const uint32_t lane = threadIdx.x & 63u;
         if (bal) {
-            const uint32_t lane = threadIdx.x & 63u;
             const uint32_t leader = (uint32_t)__ffsll((long long)bal) - 1;
             uint32_t base = 0;
             if (lane == leader) base = atomicAdd(n_slow, (uint32_t)__popcll(bal));
             base = __shfl(base, (int)leader);
             if (to_slow) slow[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1))] = i;
+        }
+        if (bitmap) {
+            const unsigned long long ok = __ballot(present && v == V_VALID);
+            const uint32_t i0 = i - lane;   // multiple of 64
+            if (lane == 0 && i0 < n) {
+                bitmap[i0 >> 5] = (uint32_t)ok;
+                if (i0 + 32 < n) bitmap[(i0 >> 5) + 1] = (uint32_t)(ok >> 32);
+            }
         }
     }
 }
@@ -653,8 +672,13 @@ __global__ __launch_bounds__(256) void k_fb_runs(const uint32_t* __restrict__ li
 }
 
 __global__ void k_fb_ready(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
-                           uint32_t* __restrict__ state) {
-    for (uint32_t k = threadIdx.x; k < *count; k += blockDim.x) state[list[k]] = HD_FB_READY;
+                           uint32_t* __restrict__ state, uint32_t* not_ready) {
+    const uint32_t c = *count;
+    for (uint32_t k = threadIdx.x; k < c; k += blockDim.x) state[list[k]] = HD_FB_READY;
+    if (threadIdx.x == 0 && c && not_ready) {
+        const uint32_t v = *(volatile uint32_t*)not_ready;
+        *(volatile uint32_t*)not_ready = v >= c ? v - c : 0u;
+    }
 }
 
 // per-key table geometry of width wp
@@ -726,9 +750,11 @@ int fb_grow_slots(hd_ctx* ctx, uint32_t want) {
 uint32_t fb_run_blocks(const hd_ctx* ctx) { return (uint32_t)std::max(ctx->n_cu, 1) * 4u; }
 size_t fb_run_scratch_bytes(const hd_ctx* ctx) { return (size_t)HD_FB_RUN * 9 * 4 * 256 * fb_run_blocks(ctx); }
 
-// build the tables of every LEARNED slot, stream-ordered
+// build the tables of every LEARNED slot, stream-ordered (nothing to launch
+// once every mapped key is READY)
 int fb_learn(hd_ctx* ctx, hipStream_t s) {
     FbWork* f = ctx->fb;
+    if (f->nr_host && *(volatile uint32_t*)f->nr_host == 0) return HD_OK;
     const uint32_t g = (uint32_t)std::max(ctx->n_cu, 1) * 4u;
     k_fb_list<<<1, 256, 0, s>>>(f->nslots, f->state, f->list, f->counts);
     if (f->wp == HD_FB_WW) {
@@ -738,7 +764,7 @@ int fb_learn(hd_ctx* ctx, hipStream_t s) {
         k_fb_bases<HD_FB_W><<<g, 256, 0, s>>>(f->list, f->counts, f->pub, f->base);
         k_fb_runs<HD_FB_W><<<fb_run_blocks(ctx), 256, 0, s>>>(f->list, f->counts, f->base, f->tab, f->zr);
     }
-    k_fb_ready<<<1, 256, 0, s>>>(f->list, f->counts, f->state);
+    k_fb_ready<<<1, 256, 0, s>>>(f->list, f->counts, f->state, f->nr_dev);
     FBCHK(hipGetLastError(), "fb table kernels");
     return HD_OK;
 }
@@ -796,6 +822,9 @@ int hd_fb_init(hd_ctx* ctx) {
     f->max_slots = (uint32_t)std::max(1.0, std::min(1e6, f->budget / fb_slot_bytes(f->wp)));
     FBCHK(hipMalloc(&f->counts, 8), "fb counts");
     FBCHK(hipMalloc(&f->zr, fb_run_scratch_bytes(ctx)), "fb builder scratch");
+    FBCHK(hipHostMalloc((void**)&f->nr_host, 4, hipHostMallocMapped | hipHostMallocCoherent), "fb ready count");
+    *f->nr_host = 0xFFFFFFFFu;
+    FBCHK(hipHostGetDevicePointer((void**)&f->nr_dev, f->nr_host, 0), "fb ready count map");
     int rc = fb_grow_slots(ctx, 1);
     if (rc) return rc;
     return fb_g_table(ctx, &f->gtab);
@@ -811,6 +840,7 @@ void hd_fb_release(hd_ctx* ctx) {
     void* ptrs[] = {f->counts, f->slow, f->adm_slot, f->rows, f->zr};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    if (f->nr_host) (void)hipHostFree(f->nr_host);
     delete f;
     ctx->fb = nullptr;
 }
@@ -840,8 +870,24 @@ static int fb_pick_width(hd_ctx* ctx, uint32_t m) {
     return need <= f->budget - others ? HD_FB_WW : HD_FB_W;
 }
 
+// mapped slots whose state is not READY (device idle: called after a sync)
+static int fb_count_not_ready(hd_ctx* ctx) {
+    FbWork* f = ctx->fb;
+    uint32_t nr = 0;
+    if (!f->slot_of.empty()) {
+        std::vector<uint32_t> st(f->nslots);
+        FBCHK(hipMemcpy(st.data(), f->state, 4 * (size_t)f->nslots, hipMemcpyDeviceToHost), "fb state read");
+        for (const auto& kv : f->slot_of) nr += st[kv.second] != HD_FB_READY ? 1u : 0u;
+    }
+    *(volatile uint32_t*)f->nr_host = nr;
+    return HD_OK;
+}
+
 int hd_fb_map_signatories(hd_ctx* ctx, const uint8_t* sorted, uint32_t m) {
     FbWork* f = ctx->fb;
+    // no verify call of this context may still learn into a slot reassigned here
+    FBCHK(hipDeviceSynchronize(), "fb map sync");
+    *(volatile uint32_t*)f->nr_host = 0xFFFFFFFFu;
     const int wp = fb_pick_width(ctx, m);
     if (wp != f->wp) {
         // another table width: every key is learned again (full recovery)
@@ -892,14 +938,16 @@ int hd_fb_map_signatories(hd_ctx* ctx, const uint8_t* sorted, uint32_t m) {
     rc = hd_dev_grow(ctx, (void**)&f->adm_slot, &f->cap_adm_slot, 4 * adm_slot.size());
     if (rc) return rc;
     FBCHK(hipMemcpy(f->adm_slot, adm_slot.data(), 4 * adm_slot.size(), hipMemcpyHostToDevice), "fb adm_slot");
-    return HD_OK;
+    FBCHK(hipDeviceSynchronize(), "fb map done");
+    return fb_count_not_ready(ctx);
 }
 
 int hd_fb_clear_keys(hd_ctx* ctx) {
     FbWork* f = ctx->fb;
     FBCHK(hipDeviceSynchronize(), "fb clear sync");
     if (f->nslots > 1) FBCHK(hipMemset(f->state + 1, 0, 4 * (size_t)(f->nslots - 1)), "fb clear");
-    return HD_OK;
+    FBCHK(hipDeviceSynchronize(), "fb clear done");
+    return fb_count_not_ready(ctx);
 }
 
 // the next free event pair of a profile record (created on first use), or
@@ -937,10 +985,12 @@ static void launch_sums(uint32_t blocks, hipStream_t s, uint32_t n, const gp* gt
 
 template <int K, int WP>
 static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict,
-                         uint8_t* d_rec32, int32_t* d_signer, const SplitRows& rows, hipStream_t s) {
+                         uint8_t* d_rec32, int32_t* d_signer, uint32_t* d_bitmap, const SplitRows& rows,
+                         hipStream_t s) {
     FbWork* f = ctx->fb;
     const uint32_t n = b.n;
-    const uint32_t T = (n + (uint32_t)K - 1) / (uint32_t)K;
+    // lanes of the K-per-lane kernels, a multiple of 64 (k_fast_final's bitmap words)
+    const uint32_t T = ((n + (uint32_t)K - 1) / (uint32_t)K + 63u) & ~63u;
     const uint32_t tb = (T + 255) / 256;
     k_fast_prep<<<(n + 255) / 256, 256, 0, s>>>(b, d_digest, f->state, f->adm_slot, ctx->d_adm, ctx->n_adm,
                                                 ctx->adm_steps, rows);
@@ -950,7 +1000,7 @@ static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest
     launch_sums<WP>((n + 255) / 256, s, n, f->gtab, f->tab, rows);
     if (pe) (void)hipEventRecord(pe[1], s);
     k_fast_final<K><<<tb, 256, 0, s>>>(b, T, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer, f->slow,
-                                       f->counts + 1);
+                                       f->counts + 1, d_bitmap);
 }
 
 static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict,
@@ -994,23 +1044,21 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         rows.dig = f->rows + 54 * (size_t)n;
         const int k = fast_split_k();
         if (f->wp == HD_FB_WW) {
-            if (k == 16) launch_split<16, HD_FB_WW>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, rows, s);
-            else if (k == 4) launch_split<4, HD_FB_WW>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, rows, s);
-            else launch_split<8, HD_FB_WW>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, rows, s);
+            if (k == 16) launch_split<16, HD_FB_WW>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, s);
+            else if (k == 4) launch_split<4, HD_FB_WW>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, s);
+            else launch_split<8, HD_FB_WW>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, s);
         } else {
-            if (k == 16) launch_split<16, HD_FB_W>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, rows, s);
-            else if (k == 4) launch_split<4, HD_FB_W>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, rows, s);
-            else launch_split<8, HD_FB_W>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, rows, s);
+            if (k == 16) launch_split<16, HD_FB_W>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, s);
+            else if (k == 4) launch_split<4, HD_FB_W>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, s);
+            else launch_split<8, HD_FB_W>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, s);
         }
         FBCHK(hipGetLastError(), "split check launch");
-        const SlowCtl ctl{f->slow, f->counts + 1, f->adm_slot, f->state, f->pub};
+        // k_fast_final wrote the valid bitmap; the slow path sets the bits of
+        // its VALID messages
+        const SlowCtl ctl{f->slow, f->counts + 1, f->adm_slot, f->state, f->pub, d_bitmap};
         const uint32_t slow_blocks = std::min(blocks, (uint32_t)std::max(ctx->n_cu, 1) * 4u);
         rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl, slow_blocks, s);
         if (rc) return rc;
-        if (d_bitmap) {
-            k_fb_bitmap<<<((b.n + 31) / 32 + 255) / 256, 256, 0, s>>>(b.n, d_verdict, d_bitmap);
-            FBCHK(hipGetLastError(), "k_fb_bitmap launch");
-        }
         return fb_learn(ctx, s);
     }
     if (ctx->n_adm > 0 && f->adm_slot) {
@@ -1028,7 +1076,7 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         // the fallback list is usually short (its length is only known on the
         // device): a grid of 4 blocks per CU walks it, instead of one block
         // per 256 messages that would mostly start and exit
-        const SlowCtl ctl{f->slow, f->counts + 1, f->adm_slot, f->state, f->pub};
+        const SlowCtl ctl{f->slow, f->counts + 1, f->adm_slot, f->state, f->pub, nullptr};
         const uint32_t slow_blocks = std::min(blocks, (uint32_t)std::max(ctx->n_cu, 1) * 4u);
         rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl, slow_blocks, s);
         if (rc) return rc;
@@ -1040,7 +1088,7 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
     }
     // no admitted set: every message takes the full recovery (it ends in
     // NOT_ADMITTED at best), nothing to learn
-    const SlowCtl none{nullptr, nullptr, nullptr, nullptr, nullptr};
+    const SlowCtl none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     return hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, none, blocks, s);
 }
 

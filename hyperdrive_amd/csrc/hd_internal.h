@@ -72,6 +72,7 @@ struct SlowCtl {
     const int32_t* adm_slot;  // admitted sorted index -> table slot (-1 none), NULL: no learning
     uint32_t* fb_state;
     hd::ge* fb_pub;
+    uint32_t* bitmap_or;      // list mode: set the valid bit of each VALID message (the rest already written)
 };
 int hd_launch_slow(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict, uint8_t* d_rec32,
                    int32_t* d_signer, uint32_t* d_bitmap, const SlowCtl& ctl, uint32_t blocks, hipStream_t s);

@@ -79,6 +79,7 @@ __global__ __launch_bounds__(256, WAVES) void k_verify(DevBatch b, const ge* __r
                 HD_UNROLL for (int w = 0; w < 8; w++) store_be32(o + 4 * w, rec[w]);
             }
             if (signer) signer[i] = s >= 0 ? adm_perm[s] : -1;
+            if (ctl.bitmap_or && v == V_VALID) atomicOr(&ctl.bitmap_or[i >> 5], 1u << (i & 31));
             if (ctl.adm_slot && v == V_VALID) {
                 const int32_t slot = ctl.adm_slot[s];
                 if (slot >= 0 && ctl.fb_state[slot] == HD_FB_EMPTY &&
@@ -292,7 +293,7 @@ int launch_verify(hd_ctx* ctx, const hd_batch* db, const uint8_t* d_digest, uint
     // than a resident-sized grid looping over the batch (measured on 1M:
     // 13.2 ms vs 13.5 ms at 2x resident blocks, 14.3 ms at 1x)
     const uint32_t blocks = (db->n + 255) / 256;
-    const SlowCtl none{nullptr, nullptr, nullptr, nullptr, nullptr};
+    const SlowCtl none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     return hd_launch_slow(ctx, b, d_digest, d_verdict, d_recovered32, d_signer, d_valid_bitmap, none, blocks, s);
 }
 }  // namespace

@@ -37,6 +37,7 @@
 
 #include "../../include/hd_verify.h"
 #include "hd_fixedbase.h"
+#include "hd_scmont.h"
 #include "hd_internal.h"
 #include "hd_verify_msg.h"
 
@@ -301,14 +302,17 @@ __global__ __launch_bounds__(256) void k_fast_prep(DevBatch b, const uint8_t* __
 }
 
 // K per lane: prefix products of s over the lane's live messages, one
-// inversion mod n, then u1 = m / s and u2 = r / s as window digits
+// inversion mod n, then u1 = m / s and u2 = r / s as window digits.  The
+// products are Montgomery products in radix 2^29 (hd_scmont.h, R = 2^261):
+// with P_l = prod_{i<=l} s_i R^-l the l-th live prefix, inv = P_last^-1 R
+// gives, walking back, s_l^-1 R = M(inv_l, P_{l-1}) and inv_{l-1} =
+// M(inv_l, s_l), so that u = M(m, s^-1 R) = m / s comes out in plain form.
 template <int K, int WP>
 __global__ __launch_bounds__(256) void k_fast_scalars(DevBatch b, uint32_t T, SplitRows rows) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
     const uint32_t n = b.n;
-    sc acc;
-    HD_UNROLL for (int w = 0; w < 8; w++) acc.v[w] = w == 0 ? 1u : 0u;
+    sm acc;
     uint32_t live = 0;   // bit j: message j of this lane goes on
     HD_NOUNROLL for (int j = 0; j < K; j++) {
         const uint32_t i = (uint32_t)j * T + t;
@@ -317,35 +321,55 @@ __global__ __launch_bounds__(256) void k_fast_scalars(DevBatch b, uint32_t T, Sp
             FastSrc src{b, i, nullptr};
             sc s;
             HD_UNROLL for (int w = 0; w < 8; w++) s.v[w] = src.sig_s(7 - w);
-            sc_mul(acc, acc, s);
+            sm ss;
+            sm_from_sc(ss, s);
+            if (live) sm_mul(acc, acc, ss);
+            else acc = ss;
             live |= 1u << j;
         }
-        soa_store(rows.pre, n, i, acc.v);
+        if (live) soa_store(rows.pre, n, i, acc.n);
     }
     if (!live) return;
-    sc inv;
-    sc_inv_divsteps(inv, acc);   // a product of scalars in [1, n): never 0
+    sm inv;
+    {
+        sc p, pinv;
+        sm_to_sc(p, acc);
+        sc_inv_divsteps(pinv, p);   // a product of scalars in [1, n) times R^-k: never 0
+        sm_from_sc(inv, pinv);
+        sm r2;
+        sm_r2(r2);
+        sm_mul(inv, inv, r2);
+    }
     HD_NOUNROLL for (int j = K - 1; j >= 0; j--) {
         if (!((live >> j) & 1u)) continue;
         const uint32_t i = (uint32_t)j * T + t;
-        sc prev, sinv, s, u;
-        if (j > 0) {
-            soa_load(prev.v, rows.pre, n, i - T);
+        sm sinv;
+        if (live & ((1u << j) - 1u)) {   // a live message before this one
+            sm prev, ss;
+            soa_load(prev.n, rows.pre, n, i - T);
+            sm_mul(sinv, inv, prev);
+            FastSrc src{b, i, nullptr};
+            sc s;
+            HD_UNROLL for (int w = 0; w < 8; w++) s.v[w] = src.sig_s(7 - w);
+            sm_from_sc(ss, s);
+            sm_mul(inv, inv, ss);
         } else {
-            HD_UNROLL for (int w = 0; w < 8; w++) prev.v[w] = w == 0 ? 1u : 0u;
+            sinv = inv;
         }
-        sc_mul(sinv, inv, prev);
-        FastSrc src{b, i, nullptr};
-        HD_UNROLL for (int w = 0; w < 8; w++) s.v[w] = src.sig_s(7 - w);
-        sc_mul(inv, inv, s);
         // u1 = m / s and u2 = r / s leave as their window digits: table
         // references of the G windows, then of the P windows
+        sc u;
+        sm x;
         soa_load(u.v, rows.u1, n, i);
-        sc_mul(u, u, sinv);
+        sm_from_sc(x, u);
+        sm_mul(x, x, sinv);
+        sm_to_sc(u, x);
         HD_UNROLL for (int w = 0; w < FbL<HD_FB_WG>::NWIN; w++)
             rows.dig[(size_t)w * n + i] = fb_ref<HD_FB_WG>(fb_digit<HD_FB_WG>(u, w), w);
         soa_load(u.v, rows.u2, n, i);
-        sc_mul(u, u, sinv);
+        sm_from_sc(x, u);
+        sm_mul(x, x, sinv);
+        sm_to_sc(u, x);
         HD_UNROLL for (int w = 0; w < FbL<WP>::NWIN; w++)
             rows.dig[(size_t)(FbL<HD_FB_WG>::NWIN + w) * n + i] = fb_ref<WP>(fb_digit<WP>(u, w), w);
     }

@@ -6,6 +6,7 @@
 #include <vector>
 #include "../../hyperdrive_amd/csrc/hd_gen.h"
 #include "../../hyperdrive_amd/csrc/hd_fixedbase.h"
+#include "../../hyperdrive_amd/csrc/hd_scmont.h"
 #include "../../hyperdrive_amd/csrc/hd_keccak.h"
 #include "../../hyperdrive_amd/csrc/hd_modinv.h"
 
@@ -393,6 +394,39 @@ extern "C" int hdh_fb_verify(const uint8_t* pub64, const uint8_t* digest, const 
     return verify_fast(d, r, sw, sig65[64], gt.data(), pt.data());
 }
 // one table entry d 2^(12 j) B (x || y big-endian), for the table-layout test
+// scalar Montgomery product (hd_scmont.h): out = a b R^-1 mod n, canonical
+// (operands 32-byte big-endian);
+// raw9 != NULL also returns the 9 radix-2^29 limbs before the final reduction
+extern "C" void hdh_sm_mul(const uint8_t* a_le, const uint8_t* b_le, uint8_t* out_le, uint32_t* raw9) {
+    sc a, b, o;
+    le_in(a.v, a_le);
+    le_in(b.v, b_le);
+    sm x, y, r;
+    sm_from_sc(x, a);
+    sm_from_sc(y, b);
+    sm_mul(r, x, y);
+    if (raw9) for (int i = 0; i < 9; i++) raw9[i] = r.n[i];
+    sm_to_sc(o, r);
+    le_out(out_le, o.v);
+}
+// a chain of Montgomery products on radix-2^29 values kept below 2n:
+// x <- x * y_k for k steps (inputs canonical), result canonical
+extern "C" void hdh_sm_chain(const uint8_t* x_le, const uint8_t* ys_le, int k, uint8_t* out_le) {
+    sc a, o;
+    le_in(a.v, x_le);
+    sm x;
+    sm_from_sc(x, a);
+    for (int t = 0; t < k; t++) {
+        sc b;
+        le_in(b.v, ys_le + 32 * t);
+        sm y;
+        sm_from_sc(y, b);
+        sm_mul(x, x, y);
+    }
+    sm_to_sc(o, x);
+    le_out(out_le, o.v);
+}
+
 // two affine points added with the first-step formula of the fixed-base sum
 // (gej_add_ge_z1); returns 1 when Z3 = 0 (a = +-b), else out = affine x || y
 extern "C" int hdh_add_affine(const uint8_t* ax, const uint8_t* ay, const uint8_t* bx, const uint8_t* by,

@@ -47,6 +47,32 @@ def test_table_entries_are_window_multiples(fb, oracle):
         assert out.raw == _pub64(want), (j, d)
 
 
+def test_scalar_montgomery(fb, oracle):
+    """sm_mul (hd_scmont.h, k_fast_scalars' products): a b 2^-261 mod n for
+    random and extreme operands, and chains whose intermediate values stay in
+    [0, 2n) -- against Python integers."""
+    O = oracle
+    n = O.N
+    Rinv = pow(1 << 261, -1, n)
+    fb.hdh_sm_mul.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p]
+    fb.hdh_sm_chain.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p]
+    rng = random.Random(9)
+    vals = [0, 1, 2, n - 1, n - 2, (1 << 255), n >> 1] + [rng.randrange(n) for _ in range(60)]
+    out = ctypes.create_string_buffer(32)
+    for k in range(len(vals) - 1):
+        a, b = vals[k], vals[k + 1]
+        fb.hdh_sm_mul(a.to_bytes(32, "big"), b.to_bytes(32, "big"), out, None)
+        assert int.from_bytes(out.raw, "big") == a * b * Rinv % n, (a, b)
+    for t in range(20):
+        x = rng.randrange(1, n)
+        ys = [rng.randrange(1, n) if t % 3 else n - 1 for _ in range(12)]
+        fb.hdh_sm_chain(x.to_bytes(32, "big"), b"".join(y.to_bytes(32, "big") for y in ys), len(ys), out)
+        want = x
+        for y in ys:
+            want = want * y * Rinv % n
+        assert int.from_bytes(out.raw, "big") == want
+
+
 def test_first_step_addition(fb, oracle):
     """gej_add_ge_z1 (the fixed-base sum's first addition, two affine points)
     against oracle point addition; a = +-b yields Z3 = 0 (the check then hands

@@ -140,6 +140,17 @@ HD void modinv30(s30& x, const ModInfo30& mi) {
         zeta = divsteps30(zeta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
         update_de30(d, e, t, mi);
         update_fg30(f, g, t);
+#ifdef __HIP_DEVICE_COMPILE__
+        // Once g = 0 further divsteps only halve g = 0 and leave d fixed
+        // (their matrix is diag(2^30, 1) / 2^30), so a wavefront whose lanes
+        // all reached g = 0 stops: random 256-bit inputs need ~531 divsteps
+        // (the worst of 64 lanes ~550, 19 batches) of the 590 bound.
+        if (it >= 16) {
+            uint32_t nz = 0;
+            HD_UNROLL for (int i = 0; i < 9; i++) nz |= (uint32_t)g.v[i];
+            if (__ballot(nz != 0) == 0ull) break;
+        }
+#endif
     }
     normalize30(d, f.v[8], mi);
     x = d;

@@ -130,6 +130,8 @@ class Pipeline:
         self.recovered = [torch.empty((B, 32), dtype=torch.uint8, device=dev) for _ in range(self.NBUF)]
         self.bitmaps = [torch.zeros(B // 32, dtype=torch.int32, device=dev) for _ in range(self.NBUF)]
         self.t_out, self.t_arr = v._tally_struct(total, pinned=True)
+        if os.environ.get("HD_BENCH_NO_DUP"):      # A/B probe: skip the per-message classification download
+            self.t_out.dup = None
         self.t_part = None
         if world > 1:
             from hyperdrive_amd.shard import tally_out

@@ -96,7 +96,10 @@ int hd_ctx_destroy(hd_ctx* ctx);
 #define HD_PUBKEY_RAW64 2
 int hd_ctx_set_pubkey_format(hd_ctx* ctx, int format);
 /* Admitted set = procsAllowed.  sigs32: n x 32 bytes, any order, duplicates
- * allowed.  Signer indices reported by the library index this array. */
+ * allowed.  Signer indices reported by the library index this array.
+ * Blocking: waits for the context's device work in flight (a verify call
+ * still learning keys must not see its slots reassigned), so call it between
+ * batches, as ResetHeight does (replica/replica.go:136-144). */
 int hd_set_signatories(hd_ctx* ctx, const uint8_t* sigs32, uint32_t n);
 /* Known-key fast path (on by default; HD_VERIFY_FASTPATH=0 in the
  * environment turns it off for new contexts).  The first message of an

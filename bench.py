@@ -172,11 +172,20 @@ class Pipeline:
             self.tally_info = {"n_hr": self.t_out.n_hr, "n_counts": self.t_out.n_counts}
             self.last_tally = (self.t_out, self.t_arr)
         else:
-            # this rank's rounds, then the merged count tables of all ranks
-            local = tally_part(self.v, self.full, gathered.data_ptr(), self.rank, self.world, self.ts.cuda_stream,
-                               out=self.t_part)
-            with torch.cuda.stream(self.ts):
-                merged = gather_tally(local, self.world, device=gathered.device)
+            # this rank's rounds, then the merged count tables of all ranks:
+            # on the GPU over RCCL (exchange and merge stay on the device),
+            # through host arrays over gloo
+            if self.dist.get_backend() == "nccl":
+                from hyperdrive_amd.shard import gather_tally_device, tally_part_device
+                with torch.cuda.stream(self.ts):
+                    local = tally_part_device(self.v, self.full, gathered.data_ptr(), self.rank, self.world,
+                                              self.ts.cuda_stream, self.t_part, gathered.device)
+                    merged = gather_tally_device(local, self.world)
+            else:
+                local = tally_part(self.v, self.full, gathered.data_ptr(), self.rank, self.world, self.ts.cuda_stream,
+                                   out=self.t_part)
+                with torch.cuda.stream(self.ts):
+                    merged = gather_tally(local, self.world, device=gathered.device)
             self.tally_info = {"n_hr": len(merged["hr"]), "n_counts": len(merged["counts"]),
                                "n_hr_this_rank": len(local["hr"])}
             self.last_tally = merged

@@ -49,7 +49,8 @@ struct TallyWork {
     void* host = nullptr;   // pinned download stage (hipHostMalloc)
     size_t host_cap = 0;
 };
-// T_G: the hash tables; T_C: the dense log cells; T_SEL: the output stage;
+// T_G: the hash tables; T_C: the dense log cells; T_D: a partition's candidates;
+// T_SEL: the output stage;
 // T_SORTK / T_SORTV: order marks / compacted order
 enum TSlot { T_G, T_D, T_C, T_GSLOT, T_DSLOT, T_NSEL, T_SEL, T_SORTK, T_SORTV, T_TMP, T_DUP };
 
@@ -91,26 +92,6 @@ __device__ __forceinline__ bool candidate(const DevBatch& b, const uint8_t* verd
     if (t != T_PREVOTE && t != T_PRECOMMIT) return false;
     if (!(verdict ? verdict[i] == V_VALID : ((bitmap[i >> 5] >> (i & 31)) & 1u))) return false;
     return p.nparts <= 1 || part_of(hash_hr(b.height[i], b.round[i]), p.nparts) == p.part;
-}
-
-// candidates of the partition (sizes the hash tables of a partitioned tally):
-// a block sum, then one global atomic per block -- same-word atomics
-// serialise at the memory side (~11 ns each), so one per wavefront over 1M
-// messages cost 180 us
-__global__ __launch_bounds__(256) void k_tally_count(DevBatch b, const uint8_t* __restrict__ verdict,
-                                                     const uint32_t* __restrict__ bitmap, Part p,
-                                                     uint32_t* __restrict__ count) {
-    __shared__ uint32_t part_sums[4];
-    uint32_t mine = 0;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += gridDim.x * blockDim.x)
-        mine += candidate(b, verdict, bitmap, i, p) ? 1u : 0u;
-    HD_UNROLL for (int off = 32; off > 0; off >>= 1) mine += (uint32_t)__shfl_xor((int)mine, off, 64);
-    if ((threadIdx.x & 63) == 0) part_sums[threadIdx.x >> 6] = mine;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t t = part_sums[0] + part_sums[1] + part_sums[2] + part_sums[3];
-        if (t) atomicAdd(count, t);
-    }
 }
 
 __device__ __forceinline__ bool eq32(const uint8_t* a, const uint8_t* b) {
@@ -190,17 +171,38 @@ __device__ __forceinline__ uint64_t hash_log(uint64_t hhr, const uint8_t* from, 
     return mix64(hhr ^ *reinterpret_cast<const uint64_t*>(from) ^ (uint64_t)t);
 }
 
+// Items.  The whole-batch tally walks every message (item p = batch index
+// p); a partition's tally first compacts its candidates into cand[] (in
+// batch order, k_tally_flag + the ordered compaction below), so that every
+// later pass and every index array is sized by the partition's candidates,
+// not by the replicated batch (G ranks x the per-GPU batch).  Claim words
+// hold item numbers, which order like batch indices.
+__device__ __forceinline__ uint32_t msg_of(const uint32_t* cand, uint32_t p) { return cand ? cand[p] : p; }
+
+// a partition's candidates: at[i] = i, others empty; dup of the others = 3
+__global__ __launch_bounds__(256) void k_tally_flag(DevBatch b, const uint8_t* __restrict__ verdict,
+                                                    const uint32_t* __restrict__ bitmap, Part p,
+                                                    uint32_t* __restrict__ at, uint8_t* __restrict__ dup) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += gridDim.x * blockDim.x) {
+        const bool c = candidate(b, verdict, bitmap, i, p);
+        at[i] = c ? i : kEmpty;
+        if (dup && !c) dup[i] = 3;
+    }
+}
+
 // pass 1: every candidate -> its round (G slot).  Lanes of a wavefront
 // usually share their round, so the first active lane probes for all lanes
-// with its (h, r) (first_active_lane / shfl64).
-__global__ void k_tally_rounds(DevBatch b, const uint8_t* __restrict__ verdict, const uint32_t* __restrict__ bitmap,
-                               Part p, GTab G, uint32_t mask, uint32_t* __restrict__ gslot,
-                               uint8_t* __restrict__ dup) {
+// with its (h, r) (first_active_lane / shfl64).  Without cand[] the pass
+// also filters the candidates.
+__global__ void k_tally_rounds(DevBatch b, const uint32_t* __restrict__ cand, uint32_t m,
+                               const uint8_t* __restrict__ verdict, const uint32_t* __restrict__ bitmap, Part p,
+                               GTab G, uint32_t mask, uint32_t* __restrict__ gslot, uint8_t* __restrict__ dup) {
     const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += stride) {
-        if (!candidate(b, verdict, bitmap, i, p)) {
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < m; q += stride) {
+        const uint32_t i = msg_of(cand, q);
+        if (!cand && !candidate(b, verdict, bitmap, i, p)) {
             if (dup) dup[i] = 3;
-            gslot[i] = kEmpty;
+            gslot[q] = kEmpty;
             continue;
         }
         const int64_t h = b.height[i], r = b.round[i];
@@ -209,29 +211,35 @@ __global__ void k_tally_rounds(DevBatch b, const uint8_t* __restrict__ verdict, 
         uint32_t g = kEmpty;
         bool created;
         if (!follower)
-            g = probe(G.claim, mask, hash_hr(h, r), i,
-                      [&](uint32_t c) { return b.height[c] == h && b.round[c] == r; }, created);
+            g = probe(G.claim, mask, hash_hr(h, r), q,
+                      [&](uint32_t c) {
+                          const uint32_t ic = msg_of(cand, c);
+                          return b.height[ic] == h && b.round[ic] == r;
+                      },
+                      created);
         const uint32_t gl = (uint32_t)__shfl((int)g, lead, 64);
-        gslot[i] = follower ? gl : g;
+        gslot[q] = follower ? gl : g;
     }
 }
 
 // Dense vote logs.  A candidate's log key (h, r, type, From) is, for an
 // admitted From, the cell (round rank, type, admitted index) of an array of
 // n_rounds x 2 x S words -- a few MB, L2-resident -- and first-wins is one
-// atomicMin of the batch index into that cell: no hashing, no key compares
+// atomicMin of the item number into that cell: no hashing, no key compares
 // against the batch.  A From outside the context's admitted set (possible
 // when the caller's verdicts predate a set change) takes the hashed table D
 // instead; a signatory's prevote and precommit always take the same path.
-// ref[i]: the cell index, or HD_REF_HASHED | the D slot.
+// ref[q]: the cell index, or HD_REF_HASHED | the D slot.
 #define HD_REF_HASHED 0x80000000u
-__global__ void k_tally_logs(DevBatch b, const uint32_t* __restrict__ gslot, const uint32_t* __restrict__ rank_of,
+__global__ void k_tally_logs(DevBatch b, const uint32_t* __restrict__ cand, uint32_t m,
+                             const uint32_t* __restrict__ gslot, const uint32_t* __restrict__ rank_of,
                              const uint32_t* __restrict__ adm, uint32_t S, int adm_steps, uint32_t* __restrict__ Dd,
                              uint32_t* __restrict__ D, uint32_t mask, uint32_t* __restrict__ ref) {
     const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += stride) {
-        const uint32_t g = gslot[i];
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < m; q += stride) {
+        const uint32_t g = gslot[q];
         if (g == kEmpty) continue;
+        const uint32_t i = msg_of(cand, q);
         const uint8_t t = b.type[i];
         const uint8_t* from = b.from32 + 32 * (size_t)i;
         int32_t signer = -1;
@@ -242,31 +250,33 @@ __global__ void k_tally_logs(DevBatch b, const uint32_t* __restrict__ gslot, con
         }
         if (signer >= 0) {
             const uint32_t cell = (rank_of[g] * 2u + (t == T_PRECOMMIT ? 1u : 0u)) * S + (uint32_t)signer;
-            atomicMin(&Dd[cell], i);
-            ref[i] = cell;
+            atomicMin(&Dd[cell], q);
+            ref[q] = cell;
         } else {
             const int64_t h = b.height[i], r = b.round[i];
             bool created;
-            const uint32_t d = probe(D, mask, hash_log(hash_hr(h, r), from, t), i,
+            const uint32_t d = probe(D, mask, hash_log(hash_hr(h, r), from, t), q,
                                      [&](uint32_t c) {
-                                         return b.type[c] == t && b.height[c] == h && b.round[c] == r &&
-                                                eq32(b.from32 + 32 * (size_t)c, from);
+                                         const uint32_t ic = msg_of(cand, c);
+                                         return b.type[ic] == t && b.height[ic] == h && b.round[ic] == r &&
+                                                eq32(b.from32 + 32 * (size_t)ic, from);
                                      },
                                      created);
-            ref[i] = HD_REF_HASHED | d;
+            ref[q] = HD_REF_HASHED | d;
         }
     }
 }
 
 // Per-value counts of a wavefront's winners: the distinct (round, type,
 // value) keys among the active lanes are handled one at a time -- the lowest
-// lane holding a key (the lowest batch index, so first-wins of the claim word
-// stays exact) probes C once and adds the number of lanes with that key in
-// one atomic.  A batch's votes repeat few values per round, so this is a few
+// lane holding a key (the lowest item, so first-wins of the claim word stays
+// exact) probes C once and adds the number of lanes with that key in one
+// atomic.  A batch's votes repeat few values per round, so this is a few
 // probes and atomics per wavefront instead of one per lane on a handful of
 // hot words.
-__device__ __forceinline__ void count_value(CTab C, uint32_t mask, const DevBatch& b, const uint32_t* gslot,
-                                            uint32_t g, uint8_t t, uint32_t i, const uint8_t* value) {
+__device__ __forceinline__ void count_value(CTab C, uint32_t mask, const DevBatch& b, const uint32_t* cand,
+                                            const uint32_t* gslot, uint32_t g, uint8_t t, uint32_t q,
+                                            const uint8_t* value) {
     const uint4* vw = reinterpret_cast<const uint4*>(value);
     const uint4 v0 = vw[0], v1 = vw[1];
     const int lane = threadIdx.x & 63;
@@ -288,10 +298,11 @@ __device__ __forceinline__ void count_value(CTab C, uint32_t mask, const DevBatc
             const uint64_t hv = *reinterpret_cast<const uint64_t*>(value) ^
                                 *reinterpret_cast<const uint64_t*>(value + 8);
             bool created;
-            const uint32_t c = probe(C.claim, mask, mix64(hv ^ ((uint64_t)g << 1 | (t & 1u))), i,
+            const uint32_t c = probe(C.claim, mask, mix64(hv ^ ((uint64_t)g << 1 | (t & 1u))), q,
                                      [&](uint32_t o) {
-                                         return gslot[o] == g && b.type[o] == t &&
-                                                eq32(b.value32 + 32 * (size_t)o, value);
+                                         const uint32_t io = msg_of(cand, o);
+                                         return gslot[o] == g && b.type[io] == t &&
+                                                eq32(b.value32 + 32 * (size_t)io, value);
                                      },
                                      created);
             atomicAdd(&C.n[c], (uint32_t)__popcll(same));
@@ -300,23 +311,25 @@ __device__ __forceinline__ void count_value(CTab C, uint32_t mask, const DevBatc
     }
 }
 
-// pass 3: each log entry's winner (the lowest index of its key) counts as a
+// pass 3: each log entry's winner (the lowest item of its key) counts as a
 // distinct signer of its type in the round and counts its value (C); a
 // prevote winner whose signer also has a precommit log in the round counts
 // in nboth.  The other candidates are classified against the winner's value.
-__global__ void k_tally_values(DevBatch b, const uint32_t* __restrict__ Dd, uint32_t S, const uint32_t* __restrict__ D,
+__global__ void k_tally_values(DevBatch b, const uint32_t* __restrict__ cand, uint32_t m,
+                               const uint32_t* __restrict__ Dd, uint32_t S, const uint32_t* __restrict__ D,
                                GTab G, CTab C, uint32_t mask, const uint32_t* __restrict__ gslot,
                                const uint32_t* __restrict__ ref, uint8_t* __restrict__ dup) {
     const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += stride) {
-        const uint32_t g = gslot[i];
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < m; q += stride) {
+        const uint32_t g = gslot[q];
         if (g == kEmpty) continue;
-        const uint32_t rf = ref[i];
+        const uint32_t i = msg_of(cand, q);
+        const uint32_t rf = ref[q];
         const bool hashed = (rf & HD_REF_HASHED) != 0;
         const uint32_t w = hashed ? D[rf & ~HD_REF_HASHED] : Dd[rf];
         const uint8_t* value = b.value32 + 32 * (size_t)i;
-        if (w != i) {
-            if (dup) dup[i] = eq32(b.value32 + 32 * (size_t)w, value) ? 1 : 2;
+        if (w != q) {
+            if (dup) dup[i] = eq32(b.value32 + 32 * (size_t)msg_of(cand, w), value) ? 1 : 2;
             continue;
         }
         if (dup) dup[i] = 0;
@@ -331,14 +344,15 @@ __global__ void k_tally_values(DevBatch b, const uint32_t* __restrict__ Dd, uint
                 const int64_t h = b.height[i], r = b.round[i];
                 const uint8_t* from = b.from32 + 32 * (size_t)i;
                 const uint32_t o = find(D, mask, hash_log(hash_hr(h, r), from, T_PRECOMMIT), [&](uint32_t c) {
-                    return b.type[c] == T_PRECOMMIT && b.height[c] == h && b.round[c] == r &&
-                           eq32(b.from32 + 32 * (size_t)c, from);
+                    const uint32_t ic = msg_of(cand, c);
+                    return b.type[ic] == T_PRECOMMIT && b.height[ic] == h && b.round[ic] == r &&
+                           eq32(b.from32 + 32 * (size_t)ic, from);
                 });
                 both = o != kEmpty;
             }
         }
         wave_add(G.nboth, g, both);
-        count_value(C, mask, b, gslot, g, t, i, value);
+        count_value(C, mask, b, cand, gslot, g, t, q, value);
     }
 }
 
@@ -408,13 +422,14 @@ __global__ __launch_bounds__(256) void k_tally_chunk_write(uint32_t n, const uin
     }
 }
 
-__global__ void k_tally_emit_hr(uint32_t n_hr, const uint32_t* __restrict__ slot, GTab G, const int64_t* __restrict__ h,
+__global__ void k_tally_emit_hr(uint32_t n_hr, const uint32_t* __restrict__ slot, const uint32_t* __restrict__ cand,
+                                GTab G, const int64_t* __restrict__ h,
                                 const int64_t* __restrict__ r, int64_t* __restrict__ oh, int64_t* __restrict__ orr,
                                 uint32_t* __restrict__ oprev, uint32_t* __restrict__ oprec, uint32_t* __restrict__ oany,
                                 uint32_t* __restrict__ orep) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_hr) return;
-    const uint32_t s = slot[k], i = G.claim[s];
+    const uint32_t s = slot[k], i = msg_of(cand, G.claim[s]);
     orep[k] = i;
     oh[k] = h[i];
     orr[k] = r[i];
@@ -423,13 +438,14 @@ __global__ void k_tally_emit_hr(uint32_t n_hr, const uint32_t* __restrict__ slot
     oany[k] = G.nprev[s] + G.nprec[s] - G.nboth[s];
 }
 
-__global__ void k_tally_emit_counts(uint32_t n_c, const uint32_t* __restrict__ slot, CTab C, const int64_t* __restrict__ h,
+__global__ void k_tally_emit_counts(uint32_t n_c, const uint32_t* __restrict__ slot, const uint32_t* __restrict__ cand,
+                                    CTab C, const int64_t* __restrict__ h,
                                     const int64_t* __restrict__ r, const uint8_t* __restrict__ type,
                                     int64_t* __restrict__ oh, int64_t* __restrict__ orr, uint8_t* __restrict__ ot,
                                     uint32_t* __restrict__ orep, uint32_t* __restrict__ on) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_c) return;
-    const uint32_t s = slot[k], i = C.claim[s];
+    const uint32_t s = slot[k], i = msg_of(cand, C.claim[s]);
     oh[k] = h[i];
     orr[k] = r[i];
     ot[k] = type[i];
@@ -490,39 +506,47 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     int rc = 0;
     // blocks per CU of the probe passes (HD_TALLY_BPC, default 16)
     static const uint32_t bpc = getenv("HD_TALLY_BPC") ? (uint32_t)std::max(1, atoi(getenv("HD_TALLY_BPC"))) : 16u;
-    const uint32_t grid = std::min<uint32_t>(nblk(n), (uint32_t)ctx->n_cu * bpc);
-    // the tables hold at most one key per candidate, load factor <= 1/2 so
-    // probes terminate.  A partition sizes them by its own candidates (one
-    // counting pass); the whole batch by n.
-    uint32_t n_cand = n;
-    uint32_t* cnt = (uint32_t*)tbuf(ctx, T_NSEL, 64, &rc);
-    if (rc) return rc;
-    if (part.nparts > 1) {
-        TCHK(hipMemsetAsync(cnt + 1, 0, 4, s), "clear candidate count");
-        k_tally_count<<<std::min<uint32_t>(nblk(n), (uint32_t)ctx->n_cu * 4u), 256, 0, s>>>(b, d_verdict, d_bitmap,
-                                                                                              part, cnt + 1);
-        TCHK(hipMemcpyAsync(&n_cand, cnt + 1, 4, hipMemcpyDeviceToHost, s), "candidate count");
-        TCHK(hipStreamSynchronize(s), "candidate count sync");
-    }
-    uint32_t cap = 1024;
-    while (cap < 2 * n_cand) cap <<= 1;
-    const uint32_t mask = cap - 1;
-    const uint32_t nch = (n + HD_CHUNK - 1) / HD_CHUNK;
-    // one allocation for the tables: the claim words (G, C, D; := empty by one
-    // memset), then the counters (G x 3, C; := 0 by one memset), then rank_of
-    uint32_t* tabs = (uint32_t*)tbuf(ctx, T_G, 4 * 8 * (size_t)cap, &rc);
-    uint32_t* gslot = (uint32_t*)tbuf(ctx, T_GSLOT, 4 * (size_t)n, &rc);
-    uint32_t* ref = (uint32_t*)tbuf(ctx, T_DSLOT, 4 * (size_t)n, &rc);
     uint8_t* d_dup = out->dup ? (uint8_t*)tbuf(ctx, T_DUP, n, &rc) : nullptr;
-    uint32_t* at = (uint32_t*)tbuf(ctx, T_SORTK, 8 * (size_t)n, &rc);      // at_g | at_c
-    uint32_t* ord = (uint32_t*)tbuf(ctx, T_SORTV, 8 * (size_t)n, &rc);     // order_g | order_c
-    uint32_t* ccnt = (uint32_t*)tbuf(ctx, T_TMP, 4 * ((size_t)nch + 2), &rc);  // chunk counts, totals
+    uint32_t* at = (uint32_t*)tbuf(ctx, T_SORTK, 8 * (size_t)n, &rc);   // candidate flags; then at_g | at_c
+    uint32_t* ccnt = (uint32_t*)tbuf(ctx, T_TMP, 4 * ((size_t)(n + HD_CHUNK - 1) / HD_CHUNK + 2), &rc);
     if (rc) return rc;
-    if (n_cand == 0) {   // nothing to tally here (dup: every message 3)
+    // Items: the whole batch, or a partition's candidates compacted in batch
+    // order (the rest of the tally then scales with the partition, not with
+    // the replicated batch).
+    uint32_t m = n;
+    const uint32_t* cand = nullptr;
+    if (part.nparts > 1) {
+        uint32_t* cl = (uint32_t*)tbuf(ctx, T_D, 4 * (size_t)n, &rc);
+        if (rc) return rc;
+        const uint32_t nch = (n + HD_CHUNK - 1) / HD_CHUNK;
+        k_tally_flag<<<std::min<uint32_t>(nblk(n), (uint32_t)ctx->n_cu * 8u), 256, 0, s>>>(b, d_verdict, d_bitmap, part,
+                                                                                            at, d_dup);
+        k_tally_chunk_counts<<<nch, 256, 0, s>>>(n, at, ccnt);
+        k_tally_chunk_write<<<nch, 256, 0, s>>>(n, at, ccnt, cl, nullptr, ccnt + nch);
+        TCHK(hipGetLastError(), "tally candidate kernels");
+        TCHK(hipMemcpyAsync(&m, ccnt + nch, 4, hipMemcpyDeviceToHost, s), "candidate count");
+        TCHK(hipStreamSynchronize(s), "candidate count sync");
+        cand = cl;
+    }
+    if (m == 0) {   // nothing to tally here (dup: every message 3)
         out->n_hr = out->n_counts = 0;
         if (out->dup) memset(out->dup, 3, n);
         return HD_OK;
     }
+    const uint32_t grid = std::min<uint32_t>(nblk(m), (uint32_t)ctx->n_cu * bpc);
+    // the tables hold at most one key per item, load factor <= 1/2 so probes
+    // terminate
+    uint32_t cap = 1024;
+    while (cap < 2 * m) cap <<= 1;
+    const uint32_t mask = cap - 1;
+    const uint32_t nch = (m + HD_CHUNK - 1) / HD_CHUNK;
+    // one allocation for the tables: the claim words (G, C, D; := empty by one
+    // memset), then the counters (G x 3, C; := 0 by one memset), then rank_of
+    uint32_t* tabs = (uint32_t*)tbuf(ctx, T_G, 4 * 8 * (size_t)cap, &rc);
+    uint32_t* gslot = (uint32_t*)tbuf(ctx, T_GSLOT, 4 * (size_t)m, &rc);
+    uint32_t* ref = (uint32_t*)tbuf(ctx, T_DSLOT, 4 * (size_t)m, &rc);
+    uint32_t* ord = (uint32_t*)tbuf(ctx, T_SORTV, 8 * (size_t)m, &rc);     // order_g | order_c
+    if (rc) return rc;
     const size_t K = cap;
     GTab G{tabs, tabs + 3 * K, tabs + 4 * K, tabs + 5 * K};
     CTab C{tabs + K, tabs + 6 * K};
@@ -531,10 +555,10 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     uint32_t* tot = ccnt + nch;
     TCHK(hipMemsetAsync(tabs, 0xFF, 4 * 3 * K, s), "clear claims");
     TCHK(hipMemsetAsync(tabs + 3 * K, 0, 4 * 4 * K, s), "clear counters");
-    TCHK(hipMemsetAsync(at, 0xFF, 8 * (size_t)n, s), "clear order marks");
-    // rounds, then their first-index order (the output order and the dense rank)
-    k_tally_rounds<<<grid, 256, 0, s>>>(b, d_verdict, d_bitmap, part, G, mask, gslot, d_dup);
-    rc = table_order(ctx, n, cap, G.claim, at, ccnt, ord, rank_of, tot, s);
+    TCHK(hipMemsetAsync(at, 0xFF, 8 * (size_t)m, s), "clear order marks");
+    // rounds, then their first-item order (the output order and the dense rank)
+    k_tally_rounds<<<grid, 256, 0, s>>>(b, cand, m, d_verdict, d_bitmap, part, G, mask, gslot, d_dup);
+    rc = table_order(ctx, m, cap, G.claim, at, ccnt, ord, rank_of, tot, s);
     if (rc) return rc;
     uint32_t n_hr = 0;
     TCHK(hipMemcpyAsync(&n_hr, tot, 4, hipMemcpyDeviceToHost, s), "round count");
@@ -549,10 +573,10 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
         if (rc) return rc;
         TCHK(hipMemsetAsync(Dd, 0xFF, 4 * cells, s), "clear dense logs");
     }
-    k_tally_logs<<<grid, 256, 0, s>>>(b, gslot, rank_of, ctx->d_adm, S, ctx->adm_steps, Dd, d, mask, ref);
-    k_tally_values<<<grid, 256, 0, s>>>(b, Dd, S, d, G, C, mask, gslot, ref, d_dup);
+    k_tally_logs<<<grid, 256, 0, s>>>(b, cand, m, gslot, rank_of, ctx->d_adm, S, ctx->adm_steps, Dd, d, mask, ref);
+    k_tally_values<<<grid, 256, 0, s>>>(b, cand, m, Dd, S, d, G, C, mask, gslot, ref, d_dup);
     TCHK(hipGetLastError(), "tally kernels");
-    rc = table_order(ctx, n, cap, C.claim, at + n, ccnt, ord + n, nullptr, tot + 1, s);
+    rc = table_order(ctx, m, cap, C.claim, at + m, ccnt, ord + m, nullptr, tot + 1, s);
     if (rc) return rc;
     uint32_t n_cnt = 0;
     TCHK(hipMemcpyAsync(&n_cnt, tot + 1, 4, hipMemcpyDeviceToHost, s), "group counts");
@@ -589,11 +613,11 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     uint32_t* c_n = c_rep + n_cnt;
     uint8_t* c_t = reinterpret_cast<uint8_t*>(c_n + n_cnt);
     if (n_hr)
-        k_tally_emit_hr<<<nblk(n_hr), 256, 0, s>>>(n_hr, ord, G, b.height, b.round, o_h, o_r, o_prev, o_prec, o_any,
-                                                   o_rep);
+        k_tally_emit_hr<<<nblk(n_hr), 256, 0, s>>>(n_hr, ord, cand, G, b.height, b.round, o_h, o_r, o_prev, o_prec,
+                                                   o_any, o_rep);
     if (n_cnt)
-        k_tally_emit_counts<<<nblk(n_cnt), 256, 0, s>>>(n_cnt, ord + n, C, b.height, b.round, b.type, c_h, c_r, c_t,
-                                                        c_rep, c_n);
+        k_tally_emit_counts<<<nblk(n_cnt), 256, 0, s>>>(n_cnt, ord + m, cand, C, b.height, b.round, b.type, c_h, c_r,
+                                                        c_t, c_rep, c_n);
     TCHK(hipGetLastError(), "tally emit");
     if (out->dup) TCHK(hipMemcpyAsync(st + dup_off, d_dup, (size_t)n, hipMemcpyDeviceToDevice, s), "dup stage");
     TCHK(hipMemcpyAsync(tw->host, st, total, hipMemcpyDeviceToHost, s), "tally download");

@@ -96,6 +96,53 @@ def tally_part(v, dbatch, d_bitmap: int, part: int, nparts: int, stream=None, ou
     return pack_tally(a, t.n_counts, t.n_hr)
 
 
+def tally_part_device(v, dbatch, d_bitmap: int, part: int, nparts: int, stream, out, device):
+    """tally_part, with the packed rows left as int64 tensors on `device`
+    ({"counts": [k, 5], "hr": [m, 6]}): the library's outputs (pinned host
+    memory, `out` from tally_out(..., pinned=True)) go back up in one copy
+    per column, so the exchange and the merge stay on the GPU."""
+    import torch
+    from . import _lib
+    lib = _lib.load()
+    t, a = out
+    rc = lib.hd_tally_device_bitmap_part(v.handle, ctypes.byref(dbatch), d_bitmap, part, nparts, ctypes.byref(t),
+                                         stream)
+    if rc != 0:
+        raise _lib.HDError(rc, "hd_tally_device_bitmap_part", lib.hd_ctx_last_error(v.handle).decode())
+
+    def rows(cols, k):
+        if k == 0:
+            return torch.zeros((0, len(cols)), dtype=torch.int64, device=device)
+        return torch.stack([torch.from_numpy(a[c][:k].astype(np.int64, copy=False)).to(device, non_blocking=True)
+                            for c in cols], 1)
+    return {"counts": rows(COUNT_COLS, t.n_counts), "hr": rows(HR_COLS, t.n_hr)}
+
+
+def gather_tally_device(local, world: int, group=None):
+    """gather_tally for RCCL ranks with the rows already on the GPU: sizes
+    all-gathered (the only host read), then the rows padded to the largest,
+    then the merge -- concatenation and a sort by first batch index -- on
+    the device.  Returns the merged int64 tensors on the device."""
+    import torch
+    import torch.distributed as dist
+    dev = local["counts"].device
+    sizes = torch.tensor([local["counts"].shape[0], local["hr"].shape[0]], dtype=torch.int64, device=dev)
+    all_sizes = torch.empty(2 * world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(all_sizes, sizes, group=group)
+    all_sizes = all_sizes.view(world, 2).cpu()
+    merged = {}
+    for j, (key, cols, rep_col) in enumerate((("counts", 5, 3), ("hr", 6, 5))):
+        width = max(1, int(all_sizes[:, j].max()))
+        pad = torch.zeros((width, cols), dtype=torch.int64, device=dev)
+        pad[: local[key].shape[0]] = local[key]
+        out = torch.empty((world * width, cols), dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(out, pad, group=group)
+        keep = (torch.arange(width, device=dev)[None, :] < all_sizes[:, j].to(dev)[:, None]).reshape(-1)
+        rows = out[keep]
+        merged[key] = rows[torch.argsort(rows[:, rep_col], stable=True)]
+    return merged
+
+
 def pack_tally(a, n_counts: int, n_hr: int) -> Dict[str, np.ndarray]:
     return {"counts": np.stack([a[c][:n_counts].astype(np.int64) for c in COUNT_COLS], 1).reshape(n_counts, 5),
             "hr": np.stack([a[c][:n_hr].astype(np.int64) for c in HR_COLS], 1).reshape(n_hr, 6)}

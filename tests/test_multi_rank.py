@@ -136,6 +136,12 @@ def _tally_worker(rank, world, port, out_q):
     verdicts = [0 if i % 7 else 5 for i in range(len(sc.b))]
     local = tally_rows(sc.b, verdicts, rank, world)
     merged = gather_tally(local, world)
+    # the RCCL ranks' form (rows as tensors, exchange and merge in torch),
+    # here on CPU tensors over gloo
+    import torch
+    from hyperdrive_amd.shard import gather_tally_device
+    dev = gather_tally_device({k: torch.from_numpy(v) for k, v in local.items()}, world)
+    assert dev["counts"].tolist() == merged["counts"].tolist() and dev["hr"].tolist() == merged["hr"].tolist()
     out_q.put((rank, merged["counts"].tolist(), merged["hr"].tolist(), len(local["hr"])))
     dist.barrier()
     dist.destroy_process_group()

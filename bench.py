@@ -81,7 +81,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-tally", action="store_true")
     ap.add_argument("--stream-priority", choices=("high", "normal"), default="high",
-                    help="priority of the verify stream over the tally stream")
+                    help="priority of the verify stream")
+    ap.add_argument("--tally-priority", choices=("high", "normal"), default="normal",
+                    help="priority of the tally stream")
     ap.add_argument("--no-aux", action="store_true", help="skip the SURVEY §8(f) side measurements")
     ap.add_argument("--no-sub", action="store_true", help="skip the C3 / C5 sub-benchmarks")
     ap.add_argument("--sub-steps", type=int, default=8)
@@ -267,7 +269,7 @@ def main():
     gen_s = time.perf_counter() - t0
 
     torch.cuda.set_stream(ws)          # torch ops (RCCL all-gather included) share the library's stream
-    ts = torch.cuda.Stream(device=dev)
+    ts = torch.cuda.Stream(device=dev, priority=-1 if args.tally_priority == "high" else 0)
     pipe = Pipeline(v, db, total, B, rank, world, dist, ws, ts, tally=not args.no_tally)
 
     # The first batch on a fresh context is the cold start: every message
@@ -422,7 +424,8 @@ def oracle_sample_check(db, verdict, recovered, sigs, n=512):
 def sub_benchmarks(args, v, sigs, foreign, dev, ws, ts):
     """BASELINE configs beside the headline, on one GPU, steps of verify +
     tally after a key-learning pass: C5 (30 % adversarial, the headline's
-    context and keys) and C3 (1000 signatories, 64 rounds of 1 propose + 1000
+    context and keys), a signatory-set change (100 -> 150 signatories on the
+    same context) and C3 (1000 signatories, 64 rounds of 1 propose + 1000
     prevotes + 1000 precommits = 128,064 messages, a context of its own)."""
     import torch
     import hyperdrive_amd as hd
@@ -440,6 +443,33 @@ def sub_benchmarks(args, v, sigs, foreign, dev, ws, ts):
                                    "verdicts": torch.bincount(vd.long(), minlength=8).cpu().tolist(),
                                    "fallback_msgs": v.fastpath_stats()[1], "tally": p5.tally_info}
     del p5, db5
+    # Signatory-set change (ResetHeight with a new epoch's set): the C2
+    # context switches to 150 signatories, the 100 it knows plus 50 new ones.
+    # The first batch after the change learns the 50 keys and builds their
+    # tables inside the verify call; later batches run at the steady rate.
+    S6 = args.signers + 50
+    k6 = v.gen_keys(S6)
+    t0 = time.perf_counter()
+    v.set_signatories(k6[0])
+    set_s = time.perf_counter() - t0
+    db6, _, _ = generate(v, 0, B, S6, 0, keys=k6, device=str(dev))
+    p6 = Pipeline(v, db6, B, B, 0, 1, None, ws, ts)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    p6.run(1)
+    torch.cuda.synchronize(dev)
+    first6 = time.perf_counter() - t0
+    p6.run(2)
+    el = timed(p6, args.sub_steps, None, dev)
+    vd, _, _ = p6.last(args.sub_steps)
+    out["set_change_100_to_150"] = {
+        "messages": B, "set_signatories_s": set_s, "first_batch_s": first6, "first_batch_msgs_per_s": B / first6,
+        "msgs_per_s": B * args.sub_steps / el, "ms_per_step": el / args.sub_steps * 1e3,
+        "verdicts": torch.bincount(vd.long(), minlength=8).cpu().tolist(),
+        "known_signatories": v.fastpath_stats()[0], "key_windows": v.fastpath_geometry()[1],
+        "note": "hd_set_signatories keeps the 100 known keys; the first batch learns the 50 new ones (full "
+                "recovery of their first messages, tables built in the same call)"}
+    del p6, db6
     # C3: its own context (the 1000 keys' tables need the table budget the
     # C2 context holds: it is released first by the caller's order)
     S3 = 1000

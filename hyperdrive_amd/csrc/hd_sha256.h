@@ -5,7 +5,8 @@
 //   * propose digest   SHA-256(BE64 h || BE64 r || BE64 vr || value) 56 B, 2 blocks
 //     (process/message.go:60-78)
 //   * signatory        SHA-256(pubkey)  SEC1 compressed 33 B (1 block), SEC1
-//     uncompressed 65 B (2 blocks) or raw X || Y 64 B (2 blocks)
+//     uncompressed 65 B (2 blocks), raw X || Y 64 B (2 blocks) or X.Bytes() ||
+//     Y.Bytes() (Go minimal encodings, <= 64 B, 1 or 2 blocks)
 //     [renproject/id v0.4.2 NewSignatory; the encoding is a context setting]
 // plus a small streaming context used only by the synthetic-workload signer
 // (HMAC-SHA256 for RFC6979 nonces).
@@ -129,11 +130,80 @@ HD void sha256_pub64(uint32_t out[8], const uint32_t x_be[8], const uint32_t y_b
     HD_UNROLL for (int i = 0; i < 8; i++) out[i] = st[i];
 }
 
+// Number of leading zero bytes of a big-endian 256-bit value (32 for zero).
+HD uint32_t be_lead_zero_bytes(const uint32_t w[8]) {
+    uint32_t lz = 0;
+    bool found = false;
+    HD_UNROLL for (int i = 0; i < 8; i++) {
+        if (!found) {
+            if (w[i]) {
+                lz += (uint32_t)__builtin_clz(w[i]);
+                found = true;
+            } else {
+                lz += 32;
+            }
+        }
+    }
+    return lz >> 3;
+}
+
+// w <- w shifted towards word 0 by nb bytes (a big-endian byte string loses its
+// first nb bytes), zero fill; nb < 4 N.  A barrel of word selects then one
+// funnel shift per word: every index is a compile-time constant, so the array
+// stays in registers.
+template <int N>
+HD void be_shl_bytes(uint32_t w[N], uint32_t nb) {
+    const uint32_t q = nb >> 2, sh = 8u * (nb & 3u);
+    HD_UNROLL for (int s = 16; s >= 1; s >>= 1) {
+        if (s >= N) continue;
+        const bool take = (q & (uint32_t)s) != 0;
+        HD_UNROLL for (int i = 0; i < N; i++) w[i] = take ? (i + s < N ? w[i + s] : 0u) : w[i];
+    }
+    HD_UNROLL for (int i = 0; i < N; i++) {
+        const uint32_t next = i + 1 < N ? w[i + 1] : 0u;
+        w[i] = (uint32_t)(((((uint64_t)w[i]) << 32) | next) >> (32u - sh));
+    }
+}
+
+// X.Bytes() || Y.Bytes(): Go big.Int minimal big-endian encodings (leading zero
+// bytes of each coordinate dropped), L = 64 - zx - zy bytes; one block when
+// L <= 55 (only when the coordinates have 9+ leading zero bytes between them),
+// else two.
+HD void sha256_pub_xy_stripped(uint32_t out[8], const uint32_t x_be[8], const uint32_t y_be[8]) {
+    const uint32_t zx = be_lead_zero_bytes(x_be), zy = be_lead_zero_bytes(y_be);
+    uint32_t ys[8];
+    HD_UNROLL for (int i = 0; i < 8; i++) ys[i] = y_be[i];
+    be_shl_bytes<8>(ys, zy % 32u);
+    if (zy == 32) HD_UNROLL for (int i = 0; i < 8; i++) ys[i] = 0;
+    uint32_t m[17];
+    HD_UNROLL for (int i = 0; i < 8; i++) { m[i] = x_be[i]; m[8 + i] = ys[i]; }
+    m[16] = 0;
+    be_shl_bytes<17>(m, zx);  // X's zero bytes leave; stripped Y follows X's last byte
+    const uint32_t L = 64u - zx - zy;
+    HD_UNROLL for (int i = 0; i < 17; i++)
+        if ((uint32_t)i == (L >> 2)) m[i] |= 0x80000000u >> (8u * (L & 3u));
+    uint32_t st[8], w[16];
+    sha256_init(st);
+    const bool one = L <= 55;
+    HD_UNROLL for (int i = 0; i < 16; i++) w[i] = m[i];
+    if (one) w[15] = L * 8;
+    sha256_compress(st, w);
+    if (!one) {
+        w[0] = m[16];
+        HD_UNROLL for (int i = 1; i < 15; i++) w[i] = 0;
+        w[15] = L * 8;
+        sha256_compress(st, w);
+    }
+    HD_UNROLL for (int i = 0; i < 8; i++) out[i] = st[i];
+}
+
 // The signatory of an affine key in pubkey format `fmt` (include/hd_verify.h
-// HD_PUBKEY_*: 0 uncompressed, 1 compressed, 2 raw X || Y); y_odd = Y mod 2.
+// HD_PUBKEY_*: 0 uncompressed, 1 compressed, 2 raw X || Y, 3 X.Bytes() ||
+// Y.Bytes()); y_odd = Y mod 2.
 HD void sha256_pubkey(uint32_t out[8], int fmt, const uint32_t x_be[8], const uint32_t y_be[8], uint32_t y_odd) {
     if (fmt == 1) sha256_pub33(out, 2u | (y_odd & 1u), x_be);
     else if (fmt == 2) sha256_pub64(out, x_be, y_be);
+    else if (fmt == 3) sha256_pub_xy_stripped(out, x_be, y_be);
     else sha256_pub65(out, x_be, y_be);
 }
 

@@ -202,7 +202,7 @@ int hd_ctx_destroy(hd_ctx* ctx) {
 }
 
 int hd_ctx_set_pubkey_format(hd_ctx* ctx, int format) {
-    if (!ctx || format < HD_PUBKEY_UNCOMPRESSED || format > HD_PUBKEY_RAW64) return HD_EINVAL;
+    if (!ctx || format < HD_PUBKEY_UNCOMPRESSED || format > HD_PUBKEY_XY_STRIPPED) return HD_EINVAL;
     if (format != ctx->pkfmt) {
         ctx->pkfmt = format;
         // keys were learned under the other signatory derivation
@@ -271,6 +271,8 @@ int hd_launch_slow(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint
         else HD_LAUNCH_VERIFY(1, 3);
     } else if (ctx->pkfmt == HD_PUBKEY_RAW64) {
         HD_LAUNCH_VERIFY(2, 3);
+    } else if (ctx->pkfmt == HD_PUBKEY_XY_STRIPPED) {
+        HD_LAUNCH_VERIFY(3, 3);
     } else {
         HD_LAUNCH_VERIFY(0, 3);
     }

@@ -116,7 +116,8 @@ class Verifier:
     def __init__(self, device: int = 0, compressed=True):
         """compressed: the pubkey encoding of id.NewSignatory -- True / 1 SEC1
         compressed (33 B, default), False / 0 SEC1 uncompressed (65 B),
-        2 raw X || Y (64 B) (include/hd_verify.h HD_PUBKEY_*)."""
+        2 raw X || Y (64 B), 3 X.Bytes() || Y.Bytes() (Go minimal encodings,
+        <= 64 B) (include/hd_verify.h HD_PUBKEY_*)."""
         self._lib = _lib.load()
         h = ctypes.c_void_p()
         rc = self._lib.hd_ctx_create(device, ctypes.byref(h))

@@ -90,10 +90,13 @@ int hd_ctx_destroy(hd_ctx* ctx);
  *   HD_PUBKEY_COMPRESSED   (1, default) SHA-256(02|03 || X), 33 bytes
  *   HD_PUBKEY_UNCOMPRESSED (0)          SHA-256(04 || X || Y), 65 bytes
  *   HD_PUBKEY_RAW64        (2)          SHA-256(X || Y), 64 bytes (X, Y 32-byte big-endian)
+ *   HD_PUBKEY_XY_STRIPPED  (3)          SHA-256(X.Bytes() || Y.Bytes()), Go big.Int minimal
+ *                                       big-endian encodings (leading zero bytes dropped), <= 64 bytes
  * Changing it drops the learned keys of the known-key fast path. */
 #define HD_PUBKEY_UNCOMPRESSED 0
 #define HD_PUBKEY_COMPRESSED 1
 #define HD_PUBKEY_RAW64 2
+#define HD_PUBKEY_XY_STRIPPED 3
 int hd_ctx_set_pubkey_format(hd_ctx* ctx, int format);
 /* Admitted set = procsAllowed.  sigs32: n x 32 bytes, any order, duplicates
  * allowed.  Signer indices reported by the library index this array.

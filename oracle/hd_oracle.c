@@ -14,7 +14,8 @@
  *   - recovery: go-ethereum v1.9.5 crypto/secp256k1 (checkSignature V < 4) ->
  *     libsecp256k1 parse_compact / ecdsa_sig_recover; high-S accepted
  *   - signatory: SHA-256 of the pubkey encoding `compressed` selects:
- *     1 SEC1 compressed (33 B), 0 SEC1 uncompressed (65 B), 2 raw X || Y (64 B)
+ *     1 SEC1 compressed (33 B), 0 SEC1 uncompressed (65 B), 2 raw X || Y (64 B),
+ *     3 X.Bytes() || Y.Bytes() (Go big.Int minimal encodings, <= 64 B)
  *     [renproject/id v0.4.2]
  *   - membership: procsAllowed at mq/mq.go:49-51
  * Parity anchoring: tests/test_oracle.py (KATs + OpenSSL + pyoracle).
@@ -490,6 +491,17 @@ static void* run_job(void* arg) {
             u256_to_be(pk, &qx);
             u256_to_be(pk + 32, &qy);
             pl = 64;
+        } else if (j->compressed == 3) {
+            /* Go big.Int.Bytes(): minimal big-endian, leading zero bytes dropped */
+            uint8_t xb[32], yb[32];
+            size_t zx = 0, zy = 0;
+            u256_to_be(xb, &qx);
+            u256_to_be(yb, &qy);
+            while (zx < 32 && xb[zx] == 0) zx++;
+            while (zy < 32 && yb[zy] == 0) zy++;
+            memcpy(pk, xb + zx, 32 - zx);
+            memcpy(pk + 32 - zx, yb + zy, 32 - zy);
+            pl = 64 - zx - zy;
         } else {
             pk[0] = 4;
             u256_to_be(pk + 1, &qx);

@@ -151,14 +151,22 @@ def lift_x(x: int, odd: int) -> Point:
     return (x, y)
 
 
-PUBKEY_UNCOMPRESSED, PUBKEY_COMPRESSED, PUBKEY_RAW64 = 0, 1, 2   # include/hd_verify.h HD_PUBKEY_*
+PUBKEY_UNCOMPRESSED, PUBKEY_COMPRESSED, PUBKEY_RAW64, PUBKEY_XY_STRIPPED = 0, 1, 2, 3   # include/hd_verify.h
+
+
+def go_big_bytes(v: int) -> bytes:
+    """Go's big.Int.Bytes(): minimal big-endian, no leading zero bytes."""
+    return v.to_bytes((v.bit_length() + 7) // 8, "big")
 
 
 def pubkey_bytes(q: Tuple[int, int], compressed=True) -> bytes:
     """The pubkey encoding id.NewSignatory hashes.  `compressed`: True / 1 =
     SEC1 compressed (33 B), False / 0 = SEC1 uncompressed (65 B), 2 = raw
-    X || Y (64 B)."""
+    X || Y (64 B), 3 = X.Bytes() || Y.Bytes() (`append(pub.X.Bytes(),
+    pub.Y.Bytes()...)`, leading zero bytes of each coordinate dropped)."""
     x, y = q
+    if int(compressed) == PUBKEY_XY_STRIPPED:
+        return go_big_bytes(x) + go_big_bytes(y)
     if int(compressed) == PUBKEY_RAW64:
         return x.to_bytes(32, "big") + y.to_bytes(32, "big")
     if compressed:

@@ -21,7 +21,8 @@ Files (all deterministic; re-running this script reproduces them byte for byte):
   tally_<case>.json       expected first-wins logs/counts (process.go:823-892)
                           and the quorum predicates for a few (h, r).
 
-Usage: python tests/golden/make_golden.py   (about a minute, pure Python)
+Usage: python tests/golden/make_golden.py [case ...]   (about a minute, pure Python;
+       naming cases regenerates only those)
 """
 from __future__ import annotations
 
@@ -42,7 +43,8 @@ sys.path.insert(0, ROOT)
 import hd_pyoracle as O  # noqa: E402
 
 # (name, generator kind, n, signatories, adversarial %, start, pubkey format:
-#  True = SEC1 compressed, False = SEC1 uncompressed, 2 = raw X || Y)
+#  True = SEC1 compressed, False = SEC1 uncompressed, 2 = raw X || Y,
+#  3 = X.Bytes() || Y.Bytes())
 CASES = [
     ("votes_allclasses", O.GEN_VOTES, 260, 10, 100, 0, True),
     ("votes_mix30", O.GEN_VOTES, 200, 10, 30, 0, True),
@@ -53,6 +55,12 @@ CASES = [
 ]
 
 INT64_EDGES = [0, 1, -1, 2 ** 63 - 1, -2 ** 63, 2 ** 32, -(2 ** 31)]
+
+# Signer indices whose public keys have a leading zero byte in Y (58, 504) or
+# X (560, 570), so X.Bytes() || Y.Bytes() is 63 bytes, not 64; 691 (Y) signs
+# from outside the admitted set.
+STRIP_ADMITTED = [58, 504, 560, 570, 0, 1, 2, 3]
+STRIP_FOREIGN = 691
 
 
 def kats():
@@ -109,6 +117,35 @@ def edge_batch(keys, S):
     return b
 
 
+def stripped_batch(keys):
+    """Votes and proposes of the STRIP_ADMITTED signers (honest, double votes,
+    signatures under another signer's From, a corrupted s, a non-admitted
+    signer whose key also has a short coordinate)."""
+    b = O.Batch()
+    rng = random.Random(0x5742)
+    for r in range(3):
+        for t in (O.PROPOSE, O.PREVOTE, O.PRECOMMIT):
+            for j in STRIP_ADMITTED:
+                value = O.canonical_value(5, r) if rng.random() < 0.8 else bytes(rng.randrange(256) for _ in range(32))
+                vr = -1 if t != O.PROPOSE else r - 1
+                d = O.message_digest(t, 5, r, vr, value)
+                b.append(t, 5, r, vr, value, keys.signatory(j), O.sign(keys.sk(j), d))
+    for i, j in enumerate(STRIP_ADMITTED):
+        value = bytes([i + 1]) * 32
+        d = O.message_digest(O.PREVOTE, 5, 1, -1, value)
+        b.append(O.PREVOTE, 5, 1, -1, value, keys.signatory(j), O.sign(keys.sk(j), d))        # double vote
+        other = STRIP_ADMITTED[(i + 1) % len(STRIP_ADMITTED)]
+        b.append(O.PRECOMMIT, 5, 2, -1, value, keys.signatory(other),
+                 O.sign(keys.sk(j), O.message_digest(O.PRECOMMIT, 5, 2, -1, value)))        # From of another
+        d = O.message_digest(O.PRECOMMIT, 5, 0, -1, value)
+        sig = bytearray(O.sign(keys.sk(j), d))
+        sig[40] ^= 0x10
+        b.append(O.PRECOMMIT, 5, 0, -1, value, keys.signatory(j), bytes(sig))                # corrupted s
+        d = O.message_digest(O.PREVOTE, 5, r, -1, value)
+        b.append(O.PREVOTE, 5, r, -1, value, keys.signatory(STRIP_FOREIGN), O.sign(keys.sk(STRIP_FOREIGN), d))
+    return b
+
+
 def batch_arrays(ob):
     n = len(ob)
     return dict(
@@ -151,16 +188,23 @@ def tally_json(ob, verdicts, S):
 
 
 def main():
-    with open(os.path.join(HERE, "kats.json"), "w") as fh:
-        json.dump(kats(), fh, indent=1, sort_keys=True)
-    cases = list(CASES) + [("edges", None, 0, 10, 0, 0, True)]
+    if not sys.argv[1:]:
+        with open(os.path.join(HERE, "kats.json"), "w") as fh:
+            json.dump(kats(), fh, indent=1, sort_keys=True)
+    cases = list(CASES) + [("edges", None, 0, 10, 0, 0, True),
+                           ("votes_xystripped", "strip", 0, len(STRIP_ADMITTED), 0, 0, O.PUBKEY_XY_STRIPPED)]
+    only = sys.argv[1:]
     for name, kind, n, S, adv, start, compressed in cases:
+        if only and name not in only:
+            continue
         keys = O.KeyCache(compressed)
         if kind is None:
             ob, cls = edge_batch(keys, S), []
+        elif kind == "strip":
+            ob, cls = stripped_batch(keys), []
         else:
             ob, cls = O.gen_batch(kind, n, S, adv, start=start, keys=keys)
-        adm = O.admitted_set(S, keys)
+        adm = ([keys.signatory(j) for j in STRIP_ADMITTED] if kind == "strip" else O.admitted_set(S, keys))
         verdicts, recs = O.verify_batch(ob, adm, compressed)
         openssl_check(ob, verdicts)
         arrs = batch_arrays(ob)

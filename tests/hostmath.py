@@ -108,6 +108,11 @@ class HostMath:
                        _p(ty), _p(h), _p(r), _p(vr), _p(val), _p(frm), _p(sg), _p(cl))
         return Batch(ty, h, r, vr, val, frm, sg), cl
 
+    def pubkey_hash(self, fmt: int, x: int, y: int) -> bytes:
+        out = ctypes.create_string_buffer(32)
+        self.L.hdh_pubkey_hash(fmt, b32(x), b32(y), out)
+        return out.raw
+
     def verify(self, batch, admitted_sorted: np.ndarray, compressed: bool = True):
         n = len(batch)
         ver = np.zeros(n, np.uint8)

@@ -324,6 +324,15 @@ extern "C" void hdh_split(const uint8_t* kb, uint8_t* k1b, uint8_t* k2b) {
     le_out(k2b, k2.v);
 }
 
+// signatory hash of hd_sha256.h's sha256_pubkey for arbitrary coordinates
+// (not necessarily on the curve: exercises every encoding length)
+extern "C" void hdh_pubkey_hash(int fmt, const uint8_t* x32, const uint8_t* y32, uint8_t* out32) {
+    uint32_t xb[8], yb[8], d[8];
+    for (int w = 0; w < 8; w++) { xb[w] = load_be32(x32 + 4 * w); yb[w] = load_be32(y32 + 4 * w); }
+    sha256_pubkey(d, fmt, xb, yb, yb[7] & 1u);
+    for (int w = 0; w < 8; w++) store_be32(out32 + 4 * w, d[w]);
+}
+
 // Keccak sponge of hd_keccak.h over a host byte string (pad 0x01 Keccak-256,
 // 0x06 SHA3-256)
 extern "C" void hdh_keccak_bytes(int pad, const uint8_t* data, uint64_t len, uint8_t* out32) {

@@ -185,7 +185,7 @@ def _run(v, db, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("compressed", [True, False, 2])
+@pytest.mark.parametrize("compressed", [True, False, 2, 3])
 @pytest.mark.parametrize("kind,S,n,adv", [(0, 100, 100_003, 30), (1, 1000, 40_000, 30), (0, 7, 5000, 0)])
 def test_fast_path_equals_full_recovery(gpu, kind, S, n, adv, compressed):
     import torch

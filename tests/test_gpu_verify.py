@@ -15,7 +15,7 @@ def verifier(gpu):
     v.close()
 
 
-@pytest.mark.parametrize("compressed", [True, False, 2])
+@pytest.mark.parametrize("compressed", [True, False, 2, 3])
 @pytest.mark.parametrize("kind,S,n,adv", [(0, 10, 300, 60), (1, 7, 150, 40), (0, 100, 257, 30), (1, 1000, 2001 + 5, 10)])
 def test_verify_parity_vs_oracle(gpu, oracle, kind, S, n, adv, compressed):
     v = gpu.Verifier(0, compressed=compressed)

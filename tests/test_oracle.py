@@ -111,7 +111,7 @@ def test_adversarial_classes_produce_intended_verdicts(oracle):
     assert seen >= set(range(13))
 
 
-@pytest.mark.parametrize("compressed", [True, False, 2])
+@pytest.mark.parametrize("compressed", [True, False, 2, 3])
 def test_c_oracle_matches_python_oracle(oracle, coracle, compressed):
     keys = oracle.KeyCache(compressed)
     for kind, n, S, adv in [(oracle.GEN_VOTES, 150, 10, 70), (oracle.GEN_ROUNDS, 60, 7, 40)]:

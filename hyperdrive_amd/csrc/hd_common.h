@@ -55,4 +55,74 @@ HD void store_be32(uint8_t* p, uint32_t x) {
     p[3] = (uint8_t)x;
 }
 
+HD uint32_t bswap32(uint32_t x) {
+    return (x >> 24) | ((x >> 8) & 0xFF00u) | ((x << 8) & 0xFF0000u) | (x << 24);
+}
+
+// Row i of an array of 32-byte records (value32 / from32) as 8 big-endian
+// words.  On the device, when the array base is 16-byte aligned (torch and
+// hipMalloc buffers are), two 16-byte loads replace 32 byte loads -- the
+// base is a kernel argument, so the test is a uniform branch.
+HD void load_row32_be(uint32_t w[8], const uint8_t* base, size_t i) {
+    const uint8_t* p = base + 32 * i;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (((uintptr_t)base & 15u) == 0) {
+        const uint4 a = *(const uint4*)p, b = *(const uint4*)(p + 16);
+        w[0] = bswap32(a.x); w[1] = bswap32(a.y); w[2] = bswap32(a.z); w[3] = bswap32(a.w);
+        w[4] = bswap32(b.x); w[5] = bswap32(b.y); w[6] = bswap32(b.z); w[7] = bswap32(b.w);
+        return;
+    }
+#endif
+    for (int k = 0; k < 8; k++) w[k] = load_be32(p + 4 * k);
+}
+
+// Row i of a 32-byte record array written from 8 big-endian words (16-byte
+// stores when the base is 16-byte aligned, as load_row32_be).
+HD void store_row32_be(uint8_t* base, size_t i, const uint32_t w[8]) {
+    uint8_t* p = base + 32 * i;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (((uintptr_t)base & 15u) == 0) {
+        *(uint4*)p = make_uint4(bswap32(w[0]), bswap32(w[1]), bswap32(w[2]), bswap32(w[3]));
+        *(uint4*)(p + 16) = make_uint4(bswap32(w[4]), bswap32(w[5]), bswap32(w[6]), bswap32(w[7]));
+        return;
+    }
+#endif
+    for (int k = 0; k < 8; k++) store_be32(p + 4 * k, w[k]);
+}
+
+// Signature i of an array of 65-byte R || S || V records: r and s as 8
+// big-endian words each, v the recovery byte.  Record i starts at byte 65 i,
+// i.e. i mod 4 bytes past a 4-byte boundary; on the device (4-byte aligned
+// base) 17 aligned dword loads cover it and a funnel shift per word extracts
+// it, instead of 65 byte loads.  The dword span ends up to 3 bytes past the
+// record, inside record i + 1, so the last record takes the byte path.
+HD void load_sig65(uint32_t r_be[8], uint32_t s_be[8], uint32_t& v, const uint8_t* base, size_t i, size_t n) {
+    const uint8_t* p = base + 65 * i;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (((uintptr_t)base & 3u) == 0 && i + 1 < n) {
+        const uint32_t off = (uint32_t)(i & 3u);
+        const uint32_t* q = (const uint32_t*)(p - off);
+        uint32_t d[17];
+#pragma unroll
+        for (int k = 0; k < 17; k++) d[k] = q[k];
+        const uint32_t sh = 8u * off;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const uint32_t le = (uint32_t)(((((uint64_t)d[k + 1]) << 32) | d[k]) >> sh);
+            if (k < 8) r_be[k] = bswap32(le);
+            else s_be[k - 8] = bswap32(le);
+        }
+        v = (d[16] >> sh) & 0xFFu;
+        return;
+    }
+#else
+    (void)n;
+#endif
+    for (int k = 0; k < 8; k++) {
+        r_be[k] = load_be32(p + 4 * k);
+        s_be[k] = load_be32(p + 32 + 4 * k);
+    }
+    v = p[64];
+}
+
 }  // namespace hd

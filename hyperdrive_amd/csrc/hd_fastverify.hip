@@ -2,7 +2,7 @@
 // the tables it runs on (hd_fixedbase.h).
 //
 // Per batch, stream-ordered, no host synchronisation:
-//   k_fast_prep / k_fast_scalars / k_fast_sums / k_fast_final
+//   k_fast_prep / k_fast_sinv / k_fast_digits / k_fast_sums / k_fast_zinv / k_fast_cmp
 //                   the split known-key check (the default, see "the split
 //                   check" below): a message whose claimed From is an
 //                   admitted signatory with a known key is checked with two
@@ -57,7 +57,7 @@ struct FbWork {
     uint32_t* counts = nullptr;   // [0] slots to build, [1] messages for the slow path
     uint32_t* slow = nullptr;     // message index list
     size_t cap_slow = 0;
-    uint32_t* rows = nullptr;     // the split check's per-message rows (SplitRows, 83 words per message)
+    uint32_t* rows = nullptr;     // the split check's per-message rows (SplitRows, 89 words per message)
     size_t cap_rows = 0;
     uint32_t* zr = nullptr;       // the table builder's z ratios (k_fb_runs: HD_FB_RUN x 9 words per thread)
     // Mapped slots whose key is not READY, in pinned host memory the device
@@ -82,6 +82,7 @@ struct FbWork {
     std::vector<uint32_t> free_slots;
     uint32_t used = 1;            // slots handed out so far (slot 0 = G)
     int wp = HD_FB_W;             // window width of the per-key tables (HD_FB_W or HD_FB_WW)
+    int last_k = 8;               // messages per inversion of the last split check (split_k_for)
     double budget = 0;            // table bytes allowed (HD_FB_MAX_BYTES), shared per device
     size_t bytes = 0;             // table bytes this context holds
 };
@@ -105,6 +106,12 @@ struct FastSrc {
     __device__ __forceinline__ uint32_t sig_r(int w) const { return load_be32(b.sig65 + 65 * (size_t)i + 4 * w); }
     __device__ __forceinline__ uint32_t sig_s(int w) const { return load_be32(b.sig65 + 65 * (size_t)i + 32 + 4 * w); }
     __device__ __forceinline__ uint32_t sig_v() const { return b.sig65[65 * (size_t)i + 64]; }
+    // whole fields with wide loads (hd_common.h)
+    __device__ __forceinline__ void sig(uint32_t r_be[8], uint32_t s_be[8], uint32_t& v) const {
+        load_sig65(r_be, s_be, v, b.sig65, i, b.n);
+    }
+    __device__ __forceinline__ void from_words(uint32_t w[8]) const { load_row32_be(w, b.from32, i); }
+    __device__ __forceinline__ void value_words(uint32_t w[8]) const { load_row32_be(w, b.value32, i); }
 };
 
 // Lane t checks messages 2t and 2t + 1 (verify_fast2: one inversion of each
@@ -199,20 +206,25 @@ __global__ __launch_bounds__(256, WAVES) void k_verify_fast(DevBatch b, const ui
 
 // ---- the split check: K messages per lane share each inversion ----------
 // k_verify_fast inverts s and Z once per two messages.  The split form runs
-// the same check in four kernels so that one inversion of each kind serves
-// K messages of a lane (Montgomery's trick over K), with the per-message
-// state in word-major HBM rows between them (lane t reads word w of message
-// i at w * n + i, coalesced):
-//   k_fast_prep     one per lane: lookup, digest, early checks; m and r
-//   k_fast_scalars  K per lane: prefix products of s, one inversion mod n,
-//                   then u1 = m/s, u2 = r/s as window digits
+// the same check in six kernels: the two inversions (of s mod n, of Z mod p)
+// serve K messages of a lane each (Montgomery's trick over K), and everything
+// else runs one message per lane, so that only the inversion kernels have the
+// low occupancy of n / K lanes.  Per-message state sits in word-major HBM rows
+// between them (lane t reads word w of message i at w * n + i, coalesced):
+//   k_fast_prep     one per lane: lookup, digest, early checks; m, r, s
+//   k_fast_sinv     K per lane: prefix products of s, one inversion mod n,
+//                   s^-1 of each message
+//   k_fast_digits   one per lane: u1 = m / s, u2 = r / s as window digits
 //   k_fast_sums     one per lane: u1 G + u2 P (the first window's point
 //                   loaded, one mixed addition per further window)
-//   k_fast_final    K per lane: prefix products of Z, one inversion mod p,
-//                   the comparison, the outputs and the fallback list
-// Message i of lane t is i = j T + t (j < K, T = ceil(n / K)), so every step
-// j of a wave touches consecutive messages.  The verdicts are the ones
-// verify_fast2 gives: same early checks, same sums, same comparison.
+//   k_fast_zinv     K per lane: prefix products of Z, one inversion mod p,
+//                   Z^-1 of each message
+//   k_fast_cmp      one per lane: the comparison, the outputs, the valid
+//                   bitmap and the fallback list
+// Message i of lane t of an inversion kernel is i = j T + t (j < K,
+// T = ceil(n / K)), so every step j of a wave touches consecutive messages.
+// The verdicts are the ones verify_fast2 gives: same early checks, same sums,
+// same comparison.
 #define HD_FAST_LIVE 0xFDu   // aux code: keep going (the rest are final verdicts or HD_NEEDS_SLOW)
 
 template <int NW>
@@ -227,9 +239,10 @@ HD void soa_store(uint32_t* __restrict__ p, uint32_t n, uint32_t i, const uint32
 struct SplitRows {
     uint32_t* aux;   // n: slot << 8 | code
     int32_t* idx;    // n: admitted (sorted) index
-    uint32_t* u1;    // 8n: m, then m / s
-    uint32_t* u2;    // 8n: r, then r / s
-    uint32_t* pre;   // 9n: prefix products (s: 8 words, then Z: 9 words)
+    uint32_t* u1;    // 8n: m
+    uint32_t* u2;    // 8n: r
+    uint32_t* s;     // 8n: s
+    uint32_t* pre;   // 9n: prefix products of s, then s^-1 R (radix 2^29); later of Z, then Z^-1
     uint32_t* xyz;   // 27n: the Jacobian sum
     uint32_t* dig;   // (NWIN(WG) + NWIN(W)) n: window digits as table references (fb_ref)
 };
@@ -253,7 +266,9 @@ __global__ __launch_bounds__(256) void k_fast_prep(DevBatch b, const uint8_t* __
                                                    const uint32_t* __restrict__ state,
                                                    const int32_t* __restrict__ adm_slot,
                                                    const uint32_t* __restrict__ adm, uint32_t n_adm, int adm_steps,
-                                                   SplitRows rows) {
+                                                   SplitRows rows, int adm_in_lds) {
+    extern __shared__ uint32_t sh_adm[];
+    if (adm_in_lds) adm_stage(sh_adm, adm, n_adm);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = b.n;
     if (i >= n) return;
@@ -265,25 +280,24 @@ __global__ __launch_bounds__(256) void k_fast_prep(DevBatch b, const uint8_t* __
         code = V_BAD_TYPE;
     } else {
         uint32_t from_be[8];
-        HD_UNROLL for (int w = 0; w < 8; w++) from_be[w] = src.from(w);
-        idx = admitted_find(adm, n_adm, adm_steps, from_be);
+        src.from_words(from_be);
+        idx = adm_in_lds ? admitted_find(sh_adm, n_adm, adm_steps, from_be) : admitted_find(adm, n_adm, adm_steps, from_be);
         const int32_t sl = idx >= 0 ? adm_slot[idx] : -1;
         if (sl >= 0 && state[sl] == HD_FB_READY) {
             slot = (uint32_t)sl;
             FastIn in;
             if (digest_in) {
-                HD_UNROLL for (int w = 0; w < 8; w++) in.digest_be[w] = load_be32(digest_in + 32 * (size_t)i + 4 * w);
+                load_row32_be(in.digest_be, digest_in, i);
             } else {
                 uint32_t value_be[8];
-                HD_UNROLL for (int w = 0; w < 8; w++) value_be[w] = src.value(w);
+                src.value_words(value_be);
                 if (type == T_PROPOSE)
                     sha256_propose(in.digest_be, b.height[i], b.round[i], b.valid_round ? b.valid_round[i] : -1,
                                    value_be);
                 else
                     sha256_vote(in.digest_be, b.height[i], b.round[i], value_be);
             }
-            HD_UNROLL for (int w = 0; w < 8; w++) { in.r_be[w] = src.sig_r(w); in.s_be[w] = src.sig_s(w); }
-            in.v = src.sig_v();
+            src.sig(in.r_be, in.s_be, in.v);
             in.ready = true;
             sc r, s, m;
             fe x;
@@ -292,6 +306,7 @@ __global__ __launch_bounds__(256) void k_fast_prep(DevBatch b, const uint8_t* __
                 code = HD_FAST_LIVE;
                 soa_store(rows.u1, n, i, m.v);
                 soa_store(rows.u2, n, i, r.v);
+                soa_store(rows.s, n, i, s.v);
             } else {
                 code = o;
             }
@@ -302,32 +317,31 @@ __global__ __launch_bounds__(256) void k_fast_prep(DevBatch b, const uint8_t* __
 }
 
 // K per lane: prefix products of s over the lane's live messages, one
-// inversion mod n, then u1 = m / s and u2 = r / s as window digits.  The
-// products are Montgomery products in radix 2^29 (hd_scmont.h, R = 2^261):
-// with P_l = prod_{i<=l} s_i R^-l the l-th live prefix, inv = P_last^-1 R
-// gives, walking back, s_l^-1 R = M(inv_l, P_{l-1}) and inv_{l-1} =
-// M(inv_l, s_l), so that u = M(m, s^-1 R) = m / s comes out in plain form.
-template <int K, int WP>
-__global__ __launch_bounds__(256) void k_fast_scalars(DevBatch b, uint32_t T, SplitRows rows) {
+// inversion mod n, then s^-1 of each.  The products are Montgomery products in
+// radix 2^29 (hd_scmont.h, R = 2^261): with P_l = prod_{i<=l} s_i R^-l the l-th
+// live prefix, inv = P_last^-1 R gives, walking back, s_l^-1 R =
+// M(inv_l, P_{l-1}) and inv_{l-1} = M(inv_l, s_l).  s^-1 R leaves in the pre
+// row, over the prefix it replaces (step j reads prefix j - 1 before step
+// j - 1 overwrites it).  Both walks are unrolled, so the loads of every step
+// issue ahead of the products they feed.
+template <int K>
+__global__ __launch_bounds__(256) void k_fast_sinv(uint32_t n, uint32_t T, SplitRows rows) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
-    const uint32_t n = b.n;
     sm acc;
     uint32_t live = 0;   // bit j: message j of this lane goes on
-    HD_NOUNROLL for (int j = 0; j < K; j++) {
+    HD_UNROLL for (int j = 0; j < K; j++) {
         const uint32_t i = (uint32_t)j * T + t;
-        if (i >= n) break;
-        if ((rows.aux[i] & 0xFFu) == HD_FAST_LIVE) {
-            FastSrc src{b, i, nullptr};
+        if (i < n && (rows.aux[i] & 0xFFu) == HD_FAST_LIVE) {
             sc s;
-            HD_UNROLL for (int w = 0; w < 8; w++) s.v[w] = src.sig_s(7 - w);
+            soa_load(s.v, rows.s, n, i);
             sm ss;
             sm_from_sc(ss, s);
             if (live) sm_mul(acc, acc, ss);
             else acc = ss;
             live |= 1u << j;
+            soa_store(rows.pre, n, i, acc.n);
         }
-        if (live) soa_store(rows.pre, n, i, acc.n);
     }
     if (!live) return;
     sm inv;
@@ -340,38 +354,23 @@ __global__ __launch_bounds__(256) void k_fast_scalars(DevBatch b, uint32_t T, Sp
         sm_r2(r2);
         sm_mul(inv, inv, r2);
     }
-    HD_NOUNROLL for (int j = K - 1; j >= 0; j--) {
+    HD_UNROLL for (int j = K - 1; j >= 0; j--) {
         if (!((live >> j) & 1u)) continue;
         const uint32_t i = (uint32_t)j * T + t;
-        sm sinv;
-        if (live & ((1u << j) - 1u)) {   // a live message before this one
-            sm prev, ss;
-            soa_load(prev.n, rows.pre, n, i - T);
-            sm_mul(sinv, inv, prev);
-            FastSrc src{b, i, nullptr};
+        const uint32_t before = live & ((1u << j) - 1u);
+        if (before) {   // a live message before this one: its prefix is the latest of them
+            const int jp = 31 - __builtin_clz(before);
+            sm prev, ss, sinv;
             sc s;
-            HD_UNROLL for (int w = 0; w < 8; w++) s.v[w] = src.sig_s(7 - w);
+            soa_load(prev.n, rows.pre, n, (uint32_t)jp * T + t);
+            soa_load(s.v, rows.s, n, i);
+            sm_mul(sinv, inv, prev);
             sm_from_sc(ss, s);
             sm_mul(inv, inv, ss);
+            soa_store(rows.pre, n, i, sinv.n);
         } else {
-            sinv = inv;
+            soa_store(rows.pre, n, i, inv.n);
         }
-        // u1 = m / s and u2 = r / s leave as their window digits: table
-        // references of the G windows, then of the P windows
-        sc u;
-        sm x;
-        soa_load(u.v, rows.u1, n, i);
-        sm_from_sc(x, u);
-        sm_mul(x, x, sinv);
-        sm_to_sc(u, x);
-        HD_UNROLL for (int w = 0; w < FbL<HD_FB_WG>::NWIN; w++)
-            rows.dig[(size_t)w * n + i] = fb_ref<HD_FB_WG>(fb_digit<HD_FB_WG>(u, w), w);
-        soa_load(u.v, rows.u2, n, i);
-        sm_from_sc(x, u);
-        sm_mul(x, x, sinv);
-        sm_to_sc(u, x);
-        HD_UNROLL for (int w = 0; w < FbL<WP>::NWIN; w++)
-            rows.dig[(size_t)(FbL<HD_FB_WG>::NWIN + w) * n + i] = fb_ref<WP>(fb_digit<WP>(u, w), w);
     }
 }
 
@@ -409,17 +408,53 @@ HD void sum_first(gej& acc, bool& started, const ge& p0, ge cur, uint32_t ec) {
     else sum_step_sel(acc, started, cur, nz);
 }
 
-template <int WAVES, int WP, int PF>
+// the window digits of u1 = m / s and u2 = r / s (Montgomery products with
+// s^-1 R come out plain) as table references: G windows, then P windows;
+// dst[w * stride] for window w
+template <int WP>
+HD void fast_digit_refs(uint32_t* dst, size_t stride, const SplitRows& rows, uint32_t n, uint32_t i) {
+    sm sinv, x;
+    soa_load(sinv.n, rows.pre, n, i);
+    sc u;
+    soa_load(u.v, rows.u1, n, i);
+    sm_from_sc(x, u);
+    sm_mul(x, x, sinv);
+    sm_to_sc(u, x);
+    HD_UNROLL for (int w = 0; w < FbL<HD_FB_WG>::NWIN; w++)
+        dst[(size_t)w * stride] = fb_ref<HD_FB_WG>(fb_digit<HD_FB_WG>(u, w), w);
+    soa_load(u.v, rows.u2, n, i);
+    sm_from_sc(x, u);
+    sm_mul(x, x, sinv);
+    sm_to_sc(u, x);
+    HD_UNROLL for (int w = 0; w < FbL<WP>::NWIN; w++)
+        dst[(size_t)(FbL<HD_FB_WG>::NWIN + w) * stride] = fb_ref<WP>(fb_digit<WP>(u, w), w);
+}
+
+// one message per lane: the digit rows of k_fast_sums<..., DL = false>
+template <int WP>
+__global__ __launch_bounds__(256) void k_fast_digits(uint32_t n, SplitRows rows) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || (rows.aux[i] & 0xFFu) != HD_FAST_LIVE) return;
+    fast_digit_refs<WP>(rows.dig + i, n, rows, n, i);
+}
+
+// DL: the digits are computed here, into this lane's column of an LDS array
+// (no k_fast_digits pass, no digit rows in HBM); else read from the rows.
+template <int WAVES, int WP, int PF, bool DL>
 __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* __restrict__ gtab,
                                                           const gp* __restrict__ tab, SplitRows rows) {
     constexpr int NG = FbL<HD_FB_WG>::NWIN, NT = NG + FbL<WP>::NWIN;
     static_assert(PF == 1 || PF == 2, "prefetch depth");
+    __shared__ uint32_t sdig[DL ? NT * 256 : 1];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t a = rows.aux[i];
     if ((a & 0xFFu) != HD_FAST_LIVE) return;
     const gp* __restrict__ ptab = tab + (size_t)(a >> 8) * FbL<WP>::TAB;
-    const uint32_t* __restrict__ dp = rows.dig + i;
+    // a lane reads back only its own column: no barrier
+    const size_t dstride = DL ? 256 : n;
+    const uint32_t* dp = DL ? sdig + threadIdx.x : rows.dig + i;
+    if (DL) fast_digit_refs<WP>(sdig + threadIdx.x, 256, rows, n, i);
     uint32_t e = dp[0];
     gej acc;
     ge p0;
@@ -432,13 +467,13 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
     // The next PF windows' points, packed (16 words each) until used; the
     // digit of the window after those is read one addition earlier still, so
     // no load waits on another load inside an addition.
-    uint32_t c1 = dp[n], c2 = 0, dn = 0;
+    uint32_t c1 = dp[dstride], c2 = 0, dn = 0;
     gp q1 = gtab[c1 & HD_REF_IDX], q2;
     if (PF == 2) {
-        c2 = dp[2 * (size_t)n];
+        c2 = dp[2 * dstride];
         q2 = (2 < NG ? gtab : ptab)[c2 & HD_REF_IDX];
     }
-    if (PF + 1 < NT) dn = dp[(size_t)(PF + 1) * n];
+    if (PF + 1 < NT) dn = dp[(size_t)(PF + 1) * dstride];
     // window j's point and digit reference, advancing the prefetch queue
     auto advance = [&](int j, gp& cur, uint32_t& ec) {
         cur = q1;
@@ -454,7 +489,7 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
             c1 = dn;
             q1 = (j + 1 < NG ? gtab : ptab)[c1 & HD_REF_IDX];
         }
-        if (j + PF + 1 < NT) dn = dp[(size_t)(j + PF + 1) * n];
+        if (j + PF + 1 < NT) dn = dp[(size_t)(j + PF + 1) * dstride];
     };
     {
         gp cur;
@@ -482,90 +517,116 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
     soa_store(rows.xyz + 18 * (size_t)n, n, i, acc.z.n);
 }
 
-// T is a multiple of 64, so step j of a wavefront covers the 64 messages
-// j T + t0 .. j T + t0 + 63 (t0 = the wave's first lane, a multiple of 64):
-// two whole words of the valid bitmap, written from one ballot.  Messages
-// handed to the full recovery get bit 0 here; k_verify sets theirs.
+// K per lane: prefix products of Z over the lane's live sums, one inversion
+// mod p, then Z^-1 of each into the pre row (over the prefix it replaces, as
+// in k_fast_sinv).  Unrolled like k_fast_sinv.
 template <int K>
-__global__ __launch_bounds__(256) void k_fast_final(DevBatch b, uint32_t T, SplitRows rows,
-                                                    const int32_t* __restrict__ adm_perm,
-                                                    uint8_t* __restrict__ verdict, uint8_t* __restrict__ rec32,
-                                                    int32_t* __restrict__ signer, uint32_t* __restrict__ slow,
-                                                    uint32_t* __restrict__ n_slow, uint32_t* __restrict__ bitmap) {
+__global__ __launch_bounds__(256) void k_fast_zinv(uint32_t n, uint32_t T, SplitRows rows) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
-    const uint32_t n = b.n;
     const uint32_t* zrow = rows.xyz + 18 * (size_t)n;
     fe acc;
-    fe_set_u32(acc, 1);
     uint32_t live = 0;
-    HD_NOUNROLL for (int j = 0; j < K; j++) {
+    HD_UNROLL for (int j = 0; j < K; j++) {
         const uint32_t i = (uint32_t)j * T + t;
-        if (i >= n) break;
-        if ((rows.aux[i] & 0xFFu) == HD_FAST_LIVE) {
+        if (i < n && (rows.aux[i] & 0xFFu) == HD_FAST_LIVE) {
             fe z;
             soa_load(z.n, zrow, n, i);
-            fe_mul(acc, acc, z);
+            if (live) fe_mul(acc, acc, z);
+            else acc = z;
             live |= 1u << j;
+            soa_store(rows.pre, n, i, acc.n);
         }
-        soa_store(rows.pre, n, i, acc.n);
     }
+    if (!live) return;
     fe inv;
-    if (live) fe_inv_divsteps(inv, acc);   // a product of non-zero Z: never 0
-    HD_NOUNROLL for (int j = K - 1; j >= 0; j--) {
+    fe_inv_divsteps(inv, acc);   // a product of non-zero Z: never 0
+    HD_UNROLL for (int j = K - 1; j >= 0; j--) {
+        if (!((live >> j) & 1u)) continue;
         const uint32_t i = (uint32_t)j * T + t;
-        const bool present = i < n;
-        uint8_t v = HD_NEEDS_SLOW;
-        if (present) {
-            v = (uint8_t)(rows.aux[i] & 0xFFu);
-            if ((live >> j) & 1u) {
-                fe prev, zi, z;
-                if (j > 0) soa_load(prev.n, rows.pre, n, i - T);
-                else fe_set_u32(prev, 1);
-                fe_mul(zi, inv, prev);
-                soa_load(z.n, zrow, n, i);
-                fe_mul(inv, inv, z);
-                gej s;
-                soa_load(s.x.n, rows.xyz, n, i);
-                soa_load(s.y.n, rows.xyz + 9 * (size_t)n, n, i);
-                s.z = z;
-                FastSrc src{b, i, nullptr};
-                uint32_t r_be[8], s_be[8];
-                HD_UNROLL for (int w = 0; w < 8; w++) { r_be[w] = src.sig_r(w); s_be[w] = src.sig_s(w); }
-                const uint32_t sv = src.sig_v();
-                sc r_, s_;
-                fe x;
-                (void)sig_prefix(r_, s_, x, r_be, s_be, sv);   // VALID here: k_fast_prep passed it
-                v = fast_final(s, zi, x, sv);
-            }
-            if (v != HD_NEEDS_SLOW) {
-                const bool ok = v == V_VALID;
-                verdict[i] = v;
-                if (rec32) {
-                    uint8_t* o = rec32 + 32 * (size_t)i;
-                    const uint8_t* f = b.from32 + 32 * (size_t)i;
-                    HD_UNROLL for (int w = 0; w < 8; w++) store_be32(o + 4 * w, ok ? load_be32(f + 4 * w) : 0u);
-                }
-                if (signer) signer[i] = ok ? adm_perm[rows.idx[i]] : -1;
-            }
+        const uint32_t before = live & ((1u << j) - 1u);
+        if (before) {
+            const int jp = 31 - __builtin_clz(before);
+            fe prev, z, zi;
+            soa_load(prev.n, rows.pre, n, (uint32_t)jp * T + t);
+            soa_load(z.n, zrow, n, i);
+            fe_mul(zi, inv, prev);
+            fe_mul(inv, inv, z);
+            soa_store(rows.pre, n, i, zi.n);
+        } else {
+            soa_store(rows.pre, n, i, inv.n);
         }
-        const bool to_slow = present && v == HD_NEEDS_SLOW;
-        const unsigned long long bal = __ballot(to_slow);
-        const uint32_t lane = threadIdx.x & 63u;
-        if (bal) {
-            const uint32_t leader = (uint32_t)__ffsll((long long)bal) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(n_slow, (uint32_t)__popcll(bal));
-            base = __shfl(base, (int)leader);
-            if (to_slow) slow[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1))] = i;
+    }
+}
+
+// x = r (+ n when v & 2) as a field element: the x coordinate of R (the range
+// checks of sig_prefix passed in k_fast_prep)
+HD void fast_rx(fe& x, const sc& r, uint32_t v) {
+    uint32_t xw[8];
+    HD_UNROLL for (int k = 0; k < 8; k++) xw[k] = r.v[k];
+    if (v & 2) {
+        const uint32_t N[8] = {HD_N0, HD_N1, HD_N2, HD_N3, HD_N4, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        uint64_t c = 0;
+        HD_UNROLL for (int k = 0; k < 8; k++) { c += (uint64_t)xw[k] + N[k]; xw[k] = (uint32_t)c; c >>= 32; }
+    }
+    fe_from_le(x, xw);
+}
+
+// One message per lane over a grid of whole wavefronts: the comparison of a
+// live message, the outputs of every message that has its final verdict, the
+// fallback list, and the valid bitmap -- a wavefront covers 64 consecutive
+// messages, two bitmap words written from one ballot.  Messages handed to the
+// full recovery get bit 0 here; k_verify sets theirs.
+__global__ __launch_bounds__(256) void k_fast_cmp(DevBatch b, SplitRows rows, const int32_t* __restrict__ adm_perm,
+                                                  uint8_t* __restrict__ verdict, uint8_t* __restrict__ rec32,
+                                                  int32_t* __restrict__ signer, uint32_t* __restrict__ slow,
+                                                  uint32_t* __restrict__ n_slow, uint32_t* __restrict__ bitmap) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = b.n;
+    const bool present = i < n;
+    uint8_t v = HD_NEEDS_SLOW;
+    if (present) {
+        v = (uint8_t)(rows.aux[i] & 0xFFu);
+        if (v == HD_FAST_LIVE) {
+            gej s;
+            fe zi, x;
+            soa_load(s.x.n, rows.xyz, n, i);
+            soa_load(s.y.n, rows.xyz + 9 * (size_t)n, n, i);
+            fe_clear(s.z);   // fast_final reads x, y and Z^-1 only
+            soa_load(zi.n, rows.pre, n, i);
+            sc r;
+            soa_load(r.v, rows.u2, n, i);
+            const uint32_t sv = b.sig65[65 * (size_t)i + 64];
+            fast_rx(x, r, sv);
+            v = fast_final(s, zi, x, sv);
         }
-        if (bitmap) {
-            const unsigned long long ok = __ballot(present && v == V_VALID);
-            const uint32_t i0 = i - lane;   // multiple of 64
-            if (lane == 0 && i0 < n) {
-                bitmap[i0 >> 5] = (uint32_t)ok;
-                if (i0 + 32 < n) bitmap[(i0 >> 5) + 1] = (uint32_t)(ok >> 32);
+        if (v != HD_NEEDS_SLOW) {
+            const bool ok = v == V_VALID;
+            verdict[i] = v;
+            if (rec32) {
+                uint32_t f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                if (ok) load_row32_be(f, b.from32, i);
+                store_row32_be(rec32, i, f);
             }
+            if (signer) signer[i] = ok ? adm_perm[rows.idx[i]] : -1;
+        }
+    }
+    const bool to_slow = present && v == HD_NEEDS_SLOW;
+    const unsigned long long bal = __ballot(to_slow);
+    const uint32_t lane = threadIdx.x & 63u;
+    if (bal) {
+        const uint32_t leader = (uint32_t)__ffsll((long long)bal) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(n_slow, (uint32_t)__popcll(bal));
+        base = __shfl(base, (int)leader);
+        if (to_slow) slow[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1))] = i;
+    }
+    if (bitmap) {
+        const unsigned long long ok = __ballot(present && v == V_VALID);
+        const uint32_t i0 = i - lane;   // multiple of 64
+        if (lane == 0 && i0 < n) {
+            bitmap[i0 >> 5] = (uint32_t)ok;
+            if (i0 + 32 < n) bitmap[(i0 >> 5) + 1] = (uint32_t)(ok >> 32);
         }
     }
 }
@@ -871,13 +932,25 @@ void hd_fb_release(hd_ctx* ctx) {
 
 // messages per lane of the split check (HD_FAST_K: 4, 8, the default, or 16;
 // 0 = the paired single-kernel check k_verify_fast)
+// Messages per inversion of the split check: HD_FAST_K = 0 (the paired
+// kernel), 4, 8 or 16; unset = by batch size (split_k_for).
 static int fast_split_k() {
     static const int k = [] {
         const char* e = getenv("HD_FAST_K");
-        const int v = e ? atoi(e) : 8;
+        if (!e) return -1;
+        const int v = atoi(e);
         return v <= 0 ? 0 : v <= 4 ? 4 : v <= 8 ? 8 : 16;
     }();
     return k;
+}
+// 16 messages per inversion from 2^20 messages up (65,536 lanes, one wave per
+// SIMD), else 8: the inversion kernels are bound by their work, not by their
+// occupancy, down to one wave per SIMD (1M C2 messages, one box: k_fast_sinv
+// 111 -> 90 us, k_fast_zinv 102 -> 85 us from K = 8 to 16; K = 4: 177 / 166 us)
+static int split_k_for(uint32_t n) {
+    const int k = fast_split_k();
+    if (k >= 0) return k;
+    return n >= (1u << 20) - (1u << 16) ? 16 : 8;
 }
 
 // Per-key window width for an admitted set of m: the wide tables
@@ -993,18 +1066,27 @@ static hipEvent_t* fb_prof_pair(std::vector<hipEvent_t>& ev, size_t& used, bool 
 
 // k_fast_sums occupancy (HD_SUM_WAVES: 2 or 3, the default) and prefetch
 // depth (HD_SUM_PF: 1, the default, or 2 windows ahead)
-template <int WP>
+// k_fast_sums occupancy (HD_SUM_WAVES: 2 or 3, the default), prefetch depth
+// (HD_SUM_PF: 1, the default, or 2 windows ahead) and where the window digits
+// come from (sums_digits_lds)
+template <int WP, bool DL>
 static void launch_sums(uint32_t blocks, hipStream_t s, uint32_t n, const gp* gtab, const gp* tab,
                         const SplitRows& rows) {
     static const int w = getenv("HD_SUM_WAVES") ? atoi(getenv("HD_SUM_WAVES")) : 3;
     static const int pf = getenv("HD_SUM_PF") ? atoi(getenv("HD_SUM_PF")) : 1;
     if (pf == 2) {
-        if (w == 3) k_fast_sums<3, WP, 2><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
-        else k_fast_sums<2, WP, 2><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
+        if (w == 3) k_fast_sums<3, WP, 2, DL><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
+        else k_fast_sums<2, WP, 2, DL><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
     } else {
-        if (w == 2) k_fast_sums<2, WP, 1><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
-        else k_fast_sums<3, WP, 1><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
+        if (w == 2) k_fast_sums<2, WP, 1, DL><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
+        else k_fast_sums<3, WP, 1, DL><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
     }
+}
+// HD_SUM_DIGITS=rows: a k_fast_digits pass writes the digit rows; default:
+// k_fast_sums computes them into LDS
+static bool sums_digits_lds() {
+    static const bool lds = !(getenv("HD_SUM_DIGITS") && strcmp(getenv("HD_SUM_DIGITS"), "rows") == 0);
+    return lds;
 }
 
 template <int K, int WP>
@@ -1015,16 +1097,22 @@ static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest
     const uint32_t n = b.n;
     // lanes of the K-per-lane kernels, a multiple of 64 (k_fast_final's bitmap words)
     const uint32_t T = ((n + (uint32_t)K - 1) / (uint32_t)K + 63u) & ~63u;
-    const uint32_t tb = (T + 255) / 256;
-    k_fast_prep<<<(n + 255) / 256, 256, 0, s>>>(b, d_digest, f->state, f->adm_slot, ctx->d_adm, ctx->n_adm,
-                                                ctx->adm_steps, rows);
-    k_fast_scalars<K, WP><<<tb, 256, 0, s>>>(b, T, rows);
+    const uint32_t tb = (T + 255) / 256, nb = (n + 255) / 256;
+    const size_t adm_lds = adm_lds_bytes(ctx->n_adm);
+    k_fast_prep<<<nb, 256, adm_lds, s>>>(b, d_digest, f->state, f->adm_slot, ctx->d_adm, ctx->n_adm, ctx->adm_steps,
+                                         rows, adm_lds > 0);
+    k_fast_sinv<K><<<tb, 256, 0, s>>>(n, T, rows);
+    const bool dl = sums_digits_lds();
+    if (!dl) k_fast_digits<WP><<<nb, 256, 0, s>>>(n, rows);
     hipEvent_t* pe = fb_prof_pair(f->ev_sums, f->n_sums, f->prof);
     if (pe) (void)hipEventRecord(pe[0], s);
-    launch_sums<WP>((n + 255) / 256, s, n, f->gtab, f->tab, rows);
+    if (dl) launch_sums<WP, true>(nb, s, n, f->gtab, f->tab, rows);
+    else launch_sums<WP, false>(nb, s, n, f->gtab, f->tab, rows);
     if (pe) (void)hipEventRecord(pe[1], s);
-    k_fast_final<K><<<tb, 256, 0, s>>>(b, T, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer, f->slow,
-                                       f->counts + 1, d_bitmap);
+    k_fast_zinv<K><<<tb, 256, 0, s>>>(n, T, rows);
+    // whole blocks of 256: every wavefront's 64 messages are one bitmap word pair
+    k_fast_cmp<<<nb, 256, 0, s>>>(b, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer, f->slow, f->counts + 1,
+                                  d_bitmap);
 }
 
 static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict,
@@ -1053,8 +1141,8 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
     const uint32_t blocks = (b.n + 255) / 256;
     const uint32_t fast_blocks = ((b.n + 1) / 2 + 255) / 256;   // two messages per lane
     FBCHK(hipMemsetAsync(f->counts + 1, 0, 4, s), "fb count reset");
-    if (ctx->n_adm > 0 && f->adm_slot && fast_split_k() > 0) {
-        constexpr size_t ROW_WORDS = 54 + FbL<HD_FB_WG>::NWIN + FbL<HD_FB_W>::NWIN;   // the narrow width has more windows
+    if (ctx->n_adm > 0 && f->adm_slot && split_k_for(b.n) > 0) {
+        constexpr size_t ROW_WORDS = 62 + FbL<HD_FB_WG>::NWIN + FbL<HD_FB_W>::NWIN;   // the narrow width has more windows
         rc = hd_dev_grow(ctx, (void**)&f->rows, &f->cap_rows, 4 * ROW_WORDS * (size_t)b.n);
         if (rc) return rc;
         const uint32_t n = b.n;
@@ -1063,10 +1151,12 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         rows.idx = (int32_t*)(f->rows + (size_t)n);
         rows.u1 = f->rows + 2 * (size_t)n;
         rows.u2 = f->rows + 10 * (size_t)n;
-        rows.pre = f->rows + 18 * (size_t)n;
-        rows.xyz = f->rows + 27 * (size_t)n;
-        rows.dig = f->rows + 54 * (size_t)n;
-        const int k = fast_split_k();
+        rows.s = f->rows + 18 * (size_t)n;
+        rows.pre = f->rows + 26 * (size_t)n;
+        rows.xyz = f->rows + 35 * (size_t)n;
+        rows.dig = f->rows + 62 * (size_t)n;
+        const int k = split_k_for(n);
+        f->last_k = k;
         if (f->wp == HD_FB_WW) {
             if (k == 16) launch_split<16, HD_FB_WW>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, s);
             else if (k == 4) launch_split<4, HD_FB_WW>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, s);
@@ -1140,7 +1230,7 @@ int hd_ctx_set_fastpath(hd_ctx* ctx, int enable) {
 
 int hd_ctx_fastpath_geometry(hd_ctx* ctx, int* g_windows, int* key_windows, int* msgs_per_inversion) {
     if (!ctx) return HD_EINVAL;
-    const int k = fast_split_k();
+    const int k = ctx->fb ? ctx->fb->last_k : 8;
     if (g_windows) *g_windows = FbL<HD_FB_WG>::NWIN;
     if (key_windows) *key_windows = fb_nwin(ctx->fb ? ctx->fb->wp : HD_FB_W);
     if (msgs_per_inversion) *msgs_per_inversion = k > 0 ? k : 2;

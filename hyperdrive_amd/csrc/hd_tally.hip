@@ -234,7 +234,9 @@ __global__ void k_tally_rounds(DevBatch b, const uint32_t* __restrict__ cand, ui
 __global__ void k_tally_logs(DevBatch b, const uint32_t* __restrict__ cand, uint32_t m,
                              const uint32_t* __restrict__ gslot, const uint32_t* __restrict__ rank_of,
                              const uint32_t* __restrict__ adm, uint32_t S, int adm_steps, uint32_t* __restrict__ Dd,
-                             uint32_t* __restrict__ D, uint32_t mask, uint32_t* __restrict__ ref) {
+                             uint32_t* __restrict__ D, uint32_t mask, uint32_t* __restrict__ ref, int adm_in_lds) {
+    extern __shared__ uint32_t sh_adm[];
+    if (adm_in_lds) adm_stage(sh_adm, adm, S);
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < m; q += stride) {
         const uint32_t g = gslot[q];
@@ -245,8 +247,8 @@ __global__ void k_tally_logs(DevBatch b, const uint32_t* __restrict__ cand, uint
         int32_t signer = -1;
         if (Dd) {
             uint32_t from_be[8];
-            HD_UNROLL for (int w = 0; w < 8; w++) from_be[w] = load_be32(from + 4 * w);
-            signer = admitted_find(adm, S, adm_steps, from_be);
+            load_row32_be(from_be, b.from32, i);
+            signer = adm_in_lds ? admitted_find(sh_adm, S, adm_steps, from_be) : admitted_find(adm, S, adm_steps, from_be);
         }
         if (signer >= 0) {
             const uint32_t cell = (rank_of[g] * 2u + (t == T_PRECOMMIT ? 1u : 0u)) * S + (uint32_t)signer;
@@ -281,6 +283,7 @@ __device__ __forceinline__ void count_value(CTab C, uint32_t mask, const DevBatc
     const uint4 v0 = vw[0], v1 = vw[1];
     const int lane = threadIdx.x & 63;
     unsigned long long pending = __ballot(true);
+    uint32_t mine = 0;   // on a key's lowest lane: the number of lanes with the key
     while (pending) {
         const int lead = __ffsll((long long)pending) - 1;
         uint32_t diff = (uint32_t)__shfl((int)g, lead, 64) ^ g;
@@ -294,20 +297,21 @@ __device__ __forceinline__ void count_value(CTab C, uint32_t mask, const DevBatc
         diff |= (uint32_t)__shfl((int)v1.z, lead, 64) ^ v1.z;
         diff |= (uint32_t)__shfl((int)v1.w, lead, 64) ^ v1.w;
         const unsigned long long same = __ballot(diff == 0 && ((pending >> lane) & 1ull));
-        if (lane == lead) {
-            const uint64_t hv = *reinterpret_cast<const uint64_t*>(value) ^
-                                *reinterpret_cast<const uint64_t*>(value + 8);
-            bool created;
-            const uint32_t c = probe(C.claim, mask, mix64(hv ^ ((uint64_t)g << 1 | (t & 1u))), q,
-                                     [&](uint32_t o) {
-                                         const uint32_t io = msg_of(cand, o);
-                                         return gslot[o] == g && b.type[io] == t &&
-                                                eq32(b.value32 + 32 * (size_t)io, value);
-                                     },
-                                     created);
-            atomicAdd(&C.n[c], (uint32_t)__popcll(same));
-        }
+        if (lane == lead) mine = (uint32_t)__popcll(same);
         pending &= ~same;
+    }
+    // the keys' lowest lanes probe C together (their keys differ), instead of
+    // one after another inside the loop above
+    if (mine) {
+        const uint64_t hv = *reinterpret_cast<const uint64_t*>(value) ^ *reinterpret_cast<const uint64_t*>(value + 8);
+        bool created;
+        const uint32_t c = probe(C.claim, mask, mix64(hv ^ ((uint64_t)g << 1 | (t & 1u))), q,
+                                 [&](uint32_t o) {
+                                     const uint32_t io = msg_of(cand, o);
+                                     return gslot[o] == g && b.type[io] == t && eq32(b.value32 + 32 * (size_t)io, value);
+                                 },
+                                 created);
+        atomicAdd(&C.n[c], mine);
     }
 }
 
@@ -573,7 +577,9 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
         if (rc) return rc;
         TCHK(hipMemsetAsync(Dd, 0xFF, 4 * cells, s), "clear dense logs");
     }
-    k_tally_logs<<<grid, 256, 0, s>>>(b, cand, m, gslot, rank_of, ctx->d_adm, S, ctx->adm_steps, Dd, d, mask, ref);
+    const size_t adm_lds = Dd ? adm_lds_bytes(S) : 0;
+    k_tally_logs<<<grid, 256, adm_lds, s>>>(b, cand, m, gslot, rank_of, ctx->d_adm, S, ctx->adm_steps, Dd, d, mask, ref,
+                                            adm_lds > 0);
     k_tally_values<<<grid, 256, 0, s>>>(b, cand, m, Dd, S, d, G, C, mask, gslot, ref, d_dup);
     TCHK(hipGetLastError(), "tally kernels");
     rc = table_order(ctx, m, cap, C.claim, at + m, ccnt, ord + m, nullptr, tot + 1, s);

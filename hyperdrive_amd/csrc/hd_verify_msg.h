@@ -56,6 +56,19 @@ HD int32_t admitted_find(AdmTab adm, uint32_t n, int steps, const uint32_t key[8
     return cmp_be256(e, key) == 0 ? (int32_t)lo : -1;
 }
 
+// The admitted table is searched by every message of a batch.  Kernels stage
+// it in LDS (dynamic shared memory, one copy per block) when it holds at most
+// HD_ADM_LDS_MAX entries, so the binary search's dependent loads are LDS reads
+// instead of L2 round trips.
+#define HD_ADM_LDS_MAX 1024u
+#if defined(__HIPCC__)
+__device__ __forceinline__ void adm_stage(uint32_t* sh, const uint32_t* __restrict__ adm, uint32_t n) {
+    for (uint32_t k = threadIdx.x; k < 8 * n; k += blockDim.x) sh[k] = adm[k];
+    __syncthreads();
+}
+#endif
+HD_HOSTONLY size_t adm_lds_bytes(uint32_t n) { return n <= HD_ADM_LDS_MAX ? 32 * (size_t)n : 0; }
+
 // Full verdict for one message.  Src supplies the message fields on demand
 // (type(), h(), r(), vr(), value(w), from(w), sig_r(w), sig_s(w), sig_v(),
 // and has_digest() / digest(w) when the digest is given rather than computed),

@@ -122,7 +122,8 @@ int hd_ctx_fastpath_stats(hd_ctx* ctx, uint32_t* known_keys, uint32_t* last_fall
  * g_windows / key_windows: fixed-base windows of the G table and of the
  * per-key tables (one table point each; the first is loaded, the rest are
  * mixed additions); msgs_per_inversion: messages that share one inversion of
- * each kind (8 or 16 for the split check, 2 for the paired kernel).
+ * each kind in the last verify call (the split check takes 16 from 2^20 - 2^16
+ * messages up, else 8; 2 for the paired kernel).
  * Host-only (no device access); any pointer may be NULL. */
 int hd_ctx_fastpath_geometry(hd_ctx* ctx, int* g_windows, int* key_windows, int* msgs_per_inversion);
 /* Device-time profile for roofline reports.  While enabled, every verify

@@ -57,8 +57,9 @@ def fast_ops_per_msg(g_windows, key_windows, per_inv):
 
 
 def sums_ops_per_msg(g_windows, key_windows):
-    """k_fast_sums alone: the mixed additions, 11 M each."""
-    return (g_windows + key_windows - 1) * 11 * M_OPS
+    """k_fast_sums alone: the mixed additions, 11 M each, and (from round 2b)
+    its prologue's u1 = m / s and u2 = r / s, 2 M."""
+    return ((g_windows + key_windows - 1) * 11 + 2) * M_OPS
 
 
 BYTES_PER_MSG = 146 + 33        # SURVEY §8(d): HBM in + out per message
@@ -353,7 +354,7 @@ def main():
                 "kernel_ms": sums_avg,
                 "launches_timed": sums_launches,
                 "algorithmic_ops_per_msg": w_sums,
-                "ops_model": "(g_windows + key_windows - 1) mixed additions x 11 M x 160 int32 ops "
+                "ops_model": "((g_windows + key_windows - 1) mixed additions x 11 M + u1, u2 2 M) x 160 int32 ops "
                              "(SURVEY §8(d) M); messages per launch = batch - fallback",
                 "verify_call": {
                     "ms": call_avg,

@@ -7,6 +7,9 @@
 #pragma once
 #include <stdint.h>
 
+#include <type_traits>
+#include <utility>
+
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define HD __host__ __device__ __forceinline__
@@ -29,6 +32,18 @@
 #endif
 
 namespace hd {
+
+// Compile-time loop: f(std::integral_constant<int, j>) for j = 0 .. N-1, each
+// call a separate copy (arrays indexed by j stay in registers, whatever the
+// unroller's size limits).
+template <typename F, int... J>
+HD void static_for_impl(F&& f, std::integer_sequence<int, J...>) {
+    (f(std::integral_constant<int, J>{}), ...);
+}
+template <int N, typename F>
+HD void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 // Verdict enum -- mirrors include/hd_verify.h (HD_VERDICT_*).
 enum Verdict : uint8_t {

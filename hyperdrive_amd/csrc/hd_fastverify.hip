@@ -321,29 +321,36 @@ __global__ __launch_bounds__(256) void k_fast_prep(DevBatch b, const uint8_t* __
 // radix 2^29 (hd_scmont.h, R = 2^261): with P_l = prod_{i<=l} s_i R^-l the l-th
 // live prefix, inv = P_last^-1 R gives, walking back, s_l^-1 R =
 // M(inv_l, P_{l-1}) and inv_{l-1} = M(inv_l, s_l).  s^-1 R leaves in the pre
-// row, over the prefix it replaces (step j reads prefix j - 1 before step
-// j - 1 overwrites it).  Both walks are unrolled, so the loads of every step
-// issue ahead of the products they feed.
+// row.  The lane's K scalars and prefixes stay in registers (both walks are
+// unrolled), and the loads of all K messages issue together up front: with
+// n / K lanes there are too few waves to hide a load per step.
 template <int K>
 __global__ __launch_bounds__(256) void k_fast_sinv(uint32_t n, uint32_t T, SplitRows rows) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
-    sm acc;
+    sc sv[K];
     uint32_t live = 0;   // bit j: message j of this lane goes on
-    HD_UNROLL for (int j = 0; j < K; j++) {
+    static_for<K>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
         const uint32_t i = (uint32_t)j * T + t;
-        if (i < n && (rows.aux[i] & 0xFFu) == HD_FAST_LIVE) {
-            sc s;
-            soa_load(s.v, rows.s, n, i);
-            sm ss;
-            sm_from_sc(ss, s);
-            if (live) sm_mul(acc, acc, ss);
-            else acc = ss;
-            live |= 1u << j;
-            soa_store(rows.pre, n, i, acc.n);
-        }
-    }
+        const uint32_t ic = i < n ? i : n - 1;   // rows exist up to n - 1
+        const uint32_t a = rows.aux[ic];
+        soa_load(sv[j].v, rows.s, n, ic);
+        live |= (i < n && (a & 0xFFu) == HD_FAST_LIVE) ? 1u << j : 0u;
+    });
     if (!live) return;
+    sm pre[K], acc;
+    HD_UNROLL for (int k = 0; k < 9; k++) acc.n[k] = 0;
+    static_for<K>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if ((live >> j) & 1u) {
+            sm ss;
+            sm_from_sc(ss, sv[j]);
+            if (live & ((1u << j) - 1u)) sm_mul(acc, acc, ss);
+            else acc = ss;
+        }
+        pre[j] = acc;   // the product of the live messages up to j
+    });
     sm inv;
     {
         sc p, pinv;
@@ -354,24 +361,20 @@ __global__ __launch_bounds__(256) void k_fast_sinv(uint32_t n, uint32_t T, Split
         sm_r2(r2);
         sm_mul(inv, inv, r2);
     }
-    HD_UNROLL for (int j = K - 1; j >= 0; j--) {
-        if (!((live >> j) & 1u)) continue;
+    static_for<K>([&](auto jc) {
+        constexpr int j = K - 1 - decltype(jc)::value;
+        if (!((live >> j) & 1u)) return;
         const uint32_t i = (uint32_t)j * T + t;
-        const uint32_t before = live & ((1u << j) - 1u);
-        if (before) {   // a live message before this one: its prefix is the latest of them
-            const int jp = 31 - __builtin_clz(before);
-            sm prev, ss, sinv;
-            sc s;
-            soa_load(prev.n, rows.pre, n, (uint32_t)jp * T + t);
-            soa_load(s.v, rows.s, n, i);
-            sm_mul(sinv, inv, prev);
-            sm_from_sc(ss, s);
+        if (j > 0 && (live & ((1u << j) - 1u))) {   // a live message before this one
+            sm sinv, ss;
+            sm_mul(sinv, inv, pre[j > 0 ? j - 1 : 0]);
+            sm_from_sc(ss, sv[j]);
             sm_mul(inv, inv, ss);
             soa_store(rows.pre, n, i, sinv.n);
         } else {
             soa_store(rows.pre, n, i, inv.n);
         }
-    }
+    });
 }
 
 // u1 G + u2 P from the digit rows: the first G window's point starts the
@@ -518,45 +521,49 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
 }
 
 // K per lane: prefix products of Z over the lane's live sums, one inversion
-// mod p, then Z^-1 of each into the pre row (over the prefix it replaces, as
-// in k_fast_sinv).  Unrolled like k_fast_sinv.
+// mod p, then Z^-1 of each into the pre row.  Registers and up-front loads as
+// in k_fast_sinv.
 template <int K>
 __global__ __launch_bounds__(256) void k_fast_zinv(uint32_t n, uint32_t T, SplitRows rows) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
     const uint32_t* zrow = rows.xyz + 18 * (size_t)n;
-    fe acc;
+    fe zv[K];
     uint32_t live = 0;
-    HD_UNROLL for (int j = 0; j < K; j++) {
+    static_for<K>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
         const uint32_t i = (uint32_t)j * T + t;
-        if (i < n && (rows.aux[i] & 0xFFu) == HD_FAST_LIVE) {
-            fe z;
-            soa_load(z.n, zrow, n, i);
-            if (live) fe_mul(acc, acc, z);
-            else acc = z;
-            live |= 1u << j;
-            soa_store(rows.pre, n, i, acc.n);
-        }
-    }
+        const uint32_t ic = i < n ? i : n - 1;
+        const uint32_t a = rows.aux[ic];
+        soa_load(zv[j].n, zrow, n, ic);
+        live |= (i < n && (a & 0xFFu) == HD_FAST_LIVE) ? 1u << j : 0u;
+    });
     if (!live) return;
+    fe pre[K], acc;
+    fe_clear(acc);
+    static_for<K>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if ((live >> j) & 1u) {
+            if (live & ((1u << j) - 1u)) fe_mul(acc, acc, zv[j]);
+            else acc = zv[j];
+        }
+        pre[j] = acc;
+    });
     fe inv;
     fe_inv_divsteps(inv, acc);   // a product of non-zero Z: never 0
-    HD_UNROLL for (int j = K - 1; j >= 0; j--) {
-        if (!((live >> j) & 1u)) continue;
+    static_for<K>([&](auto jc) {
+        constexpr int j = K - 1 - decltype(jc)::value;
+        if (!((live >> j) & 1u)) return;
         const uint32_t i = (uint32_t)j * T + t;
-        const uint32_t before = live & ((1u << j) - 1u);
-        if (before) {
-            const int jp = 31 - __builtin_clz(before);
-            fe prev, z, zi;
-            soa_load(prev.n, rows.pre, n, (uint32_t)jp * T + t);
-            soa_load(z.n, zrow, n, i);
-            fe_mul(zi, inv, prev);
-            fe_mul(inv, inv, z);
+        if (j > 0 && (live & ((1u << j) - 1u))) {
+            fe zi;
+            fe_mul(zi, inv, pre[j > 0 ? j - 1 : 0]);
+            fe_mul(inv, inv, zv[j]);
             soa_store(rows.pre, n, i, zi.n);
         } else {
             soa_store(rows.pre, n, i, inv.n);
         }
-    }
+    });
 }
 
 // x = r (+ n when v & 2) as a field element: the x coordinate of R (the range
@@ -932,6 +939,9 @@ void hd_fb_release(hd_ctx* ctx) {
 
 // messages per lane of the split check (HD_FAST_K: 4, 8, the default, or 16;
 // 0 = the paired single-kernel check k_verify_fast)
+#ifndef HD_SPLIT_K_BIG
+#define HD_SPLIT_K_BIG 16   // messages per inversion from 2^20 - 2^16 messages up (0: always 8)
+#endif
 // Messages per inversion of the split check: HD_FAST_K = 0 (the paired
 // kernel), 4, 8 or 16; unset = by batch size (split_k_for).
 static int fast_split_k() {
@@ -944,13 +954,15 @@ static int fast_split_k() {
     return k;
 }
 // 16 messages per inversion from 2^20 messages up (65,536 lanes, one wave per
-// SIMD), else 8: the inversion kernels are bound by their work, not by their
-// occupancy, down to one wave per SIMD (1M C2 messages, one box: k_fast_sinv
-// 111 -> 90 us, k_fast_zinv 102 -> 85 us from K = 8 to 16; K = 4: 177 / 166 us)
+// SIMD), else 8: the inversion kernels are bound by their dependent ALU
+// chains; halving the inversions outweighs the lost second wave per SIMD
+// (1M C2 messages, one box, scalars and prefixes in registers: k_fast_sinv
+// 102 -> 91 us, k_fast_zinv 91 -> 76 us from K = 8 to 16; with the rows in
+// HBM between steps K = 4 / 8 / 16 gave 177 / 111 / 90 and 166 / 102 / 85 us)
 static int split_k_for(uint32_t n) {
     const int k = fast_split_k();
     if (k >= 0) return k;
-    return n >= (1u << 20) - (1u << 16) ? 16 : 8;
+    return HD_SPLIT_K_BIG > 0 && n >= (1u << 20) - (1u << 16) ? HD_SPLIT_K_BIG : 8;
 }
 
 // Per-key window width for an admitted set of m: the wide tables

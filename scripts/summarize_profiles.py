@@ -1,7 +1,7 @@
 """Condense rocprofv3 outputs under gpurun_out/ into profiles/<round>/.
 
 profiles/<round>/kernel_stats.csv   rocprofv3 --kernel-trace --stats summary
-profiles/<round>/pmc_k_fast_{scalars,sums,final}.json, pmc_known_key_check.json, pmc_k_verify.json
+profiles/<round>/pmc_k_fast_*.json, pmc_known_key_check.json, pmc_k_verify.json
                                     per-launch PMC averages of the known-key check and of
                                     the full recovery, and the
                                     HBM traffic derived per MI355X_MICROARCH.md
@@ -66,10 +66,14 @@ def kernel_pmc(match, outname, skip_first=False):
     return out
 
 
-# the known-key check: its three kernels, and their sum per verify call
-parts = [kernel_pmc(k, "pmc_%s.json" % k, skip_first=True) for k in ("k_fast_prep", "k_fast_scalars", "k_fast_sums", "k_fast_final")]
+# the known-key check: its kernels (round 1-2a: prep / scalars / sums / final;
+# from round 2b: prep / sinv / sums / zinv / cmp), and their sum per verify call
+KK = [k for k in ("k_fast_prep", "k_fast_scalars", "k_fast_sinv", "k_fast_sums", "k_fast_final", "k_fast_zinv",
+                  "k_fast_cmp") if any(k in r["Kernel_Name"] for r in csv.DictReader(
+                      open(os.path.join(src, "prof", "run_kernel_trace.csv"))))]
+parts = [kernel_pmc(k, "pmc_%s.json" % k, skip_first=True) for k in KK]
 if all(parts) and all("hbm_bytes_raw" in p for p in parts):
-    tot = {"kernels": ["k_fast_prep", "k_fast_scalars", "k_fast_sums", "k_fast_final"],
+    tot = {"kernels": KK,
            "hbm_bytes_raw": sum(p["hbm_bytes_raw"] for p in parts),
            "hbm_bytes_corrected": sum(p["hbm_bytes_corrected"] for p in parts)}
     if all("kernel_stats" in p for p in parts):

@@ -141,22 +141,26 @@ class Pipeline:
             self.t_part = tally_out(v, total, pinned=True)
         self.tally_info = {}
         self.last_tally = None
+        self.tally_group = None   # set by main() for RCCL ranks
         self.host_trace = [] if os.environ.get("HD_BENCH_HOSTTRACE") else None
 
     def verify(self, k):
         import torch
-        from hyperdrive_amd.shard import gather_bitmaps
+        from hyperdrive_amd.shard import gather_bitmaps_async
         buf = k % self.NBUF
         self.v.verify_batch_device(self.shard, self.verdicts[buf].data_ptr(), self.recovered[buf].data_ptr(), None,
                                    self.bitmaps[buf].data_ptr(), self.ws.cuda_stream)
+        work = None
         if self.dist is not None:
             with torch.cuda.stream(self.ws):
-                gathered = gather_bitmaps(self.bitmaps[buf], self.total, self.world)   # RCCL all-gather over xGMI
+                # RCCL all-gather over xGMI; the tally stream waits for it, the
+                # next verification does not
+                gathered, work = gather_bitmaps_async(self.bitmaps[buf], self.total, self.world)
         else:
             gathered = self.bitmaps[buf]
         done = torch.cuda.Event()
         done.record(self.ws)
-        return gathered, done
+        return gathered, done, work
 
     def tally(self, pending):
         import torch
@@ -164,8 +168,12 @@ class Pipeline:
         from hyperdrive_amd.shard import gather_tally, pack_tally, tally_part
         if pending is None or not self.do_tally:
             return
-        gathered, done = pending
+        gathered, done, work = pending
         self.ts.wait_event(done)
+        if work is not None:
+            with torch.cuda.stream(self.ts):
+                work.wait()
+            gathered.record_stream(self.ts)
         if self.dist is None:
             lib = _lib.load()
             rc = lib.hd_tally_device_bitmap(self.v.handle, ctypes.byref(self.full), gathered.data_ptr(),
@@ -183,7 +191,9 @@ class Pipeline:
                 with torch.cuda.stream(self.ts):
                     local = tally_part_device(self.v, self.full, gathered.data_ptr(), self.rank, self.world,
                                               self.ts.cuda_stream, self.t_part, gathered.device)
-                    merged = gather_tally_device(local, self.world)
+                    # its own communicator: the count exchange of step k does
+                    # not queue behind the bitmap all-gathers of steps k+1..
+                    merged = gather_tally_device(local, self.world, group=self.tally_group)
             else:
                 local = tally_part(self.v, self.full, gathered.data_ptr(), self.rank, self.world, self.ts.cuda_stream,
                                    out=self.t_part)
@@ -272,6 +282,8 @@ def main():
     torch.cuda.set_stream(ws)          # torch ops (RCCL all-gather included) share the library's stream
     ts = torch.cuda.Stream(device=dev, priority=-1 if args.tally_priority == "high" else 0)
     pipe = Pipeline(v, db, total, B, rank, world, dist, ws, ts, tally=not args.no_tally)
+    if dist is not None and args.dist_backend == "nccl":
+        pipe.tally_group = dist.new_group(backend="nccl")
 
     # The first batch on a fresh context is the cold start: every message
     # takes the full recovery, the first VALID message of each signatory

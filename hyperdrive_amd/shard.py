@@ -65,6 +65,22 @@ def gather_bitmaps(local_bits, n: int, world: int, group=None):
     return torch.cat(parts)[: (n + 31) // 32]
 
 
+def gather_bitmaps_async(local_bits, n: int, world: int, group=None):
+    """gather_bitmaps without making the calling stream wait: returns
+    (bitmap, work).  With RCCL and equal shards the all-gather is issued with
+    async_op=True; the consumer calls work.wait() on ITS stream (so the next
+    verification on the caller's stream does not wait for the exchange).  Any
+    other case gathers synchronously and returns work = None."""
+    import torch.distributed as dist
+    per_words = {(shard_range(n, r, world)[1] - shard_range(n, r, world)[0] + 31) // 32 for r in range(world)}
+    if not local_bits.is_cuda or dist.get_backend(group) != "nccl" or len(per_words) != 1:
+        return gather_bitmaps(local_bits, n, world, group), None
+    import torch
+    out = torch.empty(per_words.pop() * world, dtype=local_bits.dtype, device=local_bits.device)
+    work = dist.all_gather_into_tensor(out, local_bits.contiguous(), group=group, async_op=True)
+    return out[: (n + 31) // 32], work
+
+
 def partition_of(height: int, round_: int, nparts: int) -> int:
     """The rank that tallies (height, round) among nparts
     (include/hd_verify.h hd_tally_partition_of; a host function of the

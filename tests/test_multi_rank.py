@@ -13,7 +13,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from hyperdrive_amd.shard import gather_bitmaps, gather_tally, partition_of, shard_range
+from hyperdrive_amd.shard import gather_bitmaps, gather_bitmaps_async, gather_tally, partition_of, shard_range
 
 
 def _free_port():
@@ -50,6 +50,13 @@ def _worker(rank, world, port, verdicts, out_q):
     lo, hi = shard_range(n, rank, world)
     local = torch.from_numpy(_bits_of(verdicts[lo:hi]).view(np.int32).copy())
     full = gather_bitmaps(local, n, world)
+    # the bench's asynchronous form: over gloo it gathers at once (work None)
+    full2, work = gather_bitmaps_async(local, n, world)
+    assert work is None and torch.equal(full, full2)
+    # a second communicator (the bench's tally exchange group) works beside the default one
+    g2 = dist.new_group(backend="gloo")
+    full3 = gather_bitmaps(local, n, world, group=g2)
+    assert torch.equal(full, full3)
     out_q.put((rank, full.numpy().view(np.uint32).tolist()))
     dist.barrier()
     dist.destroy_process_group()

@@ -36,7 +36,7 @@ __device__ __forceinline__ void st_be64(uint8_t* p, uint64_t v) {
     }
 }
 
-// decode: 128 records per workgroup (37 KB of LDS -> 4 workgroups per CU)
+// decode: 128 records per workgroup (20 KB of LDS -> 8 workgroups per CU)
 #define HD_DEC_BLOCK 128
 template <bool PROPOSE, bool SIG>
 __global__ __launch_bounds__(HD_DEC_BLOCK) void k_unmarshal(const uint8_t* __restrict__ buf, uint64_t len, uint32_t n,
@@ -63,27 +63,38 @@ __global__ __launch_bounds__(HD_DEC_BLOCK) void k_unmarshal(const uint8_t* __res
     __syncthreads();
     const uint32_t t = threadIdx.x;
     if (SIG && out.sig65) {
-        // the block's signatures form one contiguous 65 * nrec byte range of
-        // sig65: gather them in LDS order, then store with 16-byte vectors
-        // (the two boundary words shared with neighbouring blocks bytewise)
-        __shared__ uint4 sg[(HD_DEC_BLOCK * 65 + 32) / 16];
-        uint8_t* sb = reinterpret_cast<uint8_t*>(sg);
-        const uint64_t s0 = 65ull * rec0, s1 = s0 + 65ull * nrec, g0 = s0 & ~15ull;
+        // The block's signatures form one contiguous 65 * nrec byte range of
+        // sig65 starting at s0 = 65 * rec0, a multiple of 16 (rec0 is a
+        // multiple of 128).  Each lane builds whole 16-byte output words from
+        // LDS dwords: an output dword lies inside one signature, or straddles
+        // two (the last 1..3 bytes of one and the first of the next) and is
+        // merged from two reads.  Only a partial last word goes bytewise.
+        const uint64_t s0 = 65ull * rec0;
+        const uint32_t sbytes = 65u * nrec;
         const uint8_t* Lb = reinterpret_cast<const uint8_t*>(lds);
-        for (uint32_t k = t; k < 65 * nrec; k += HD_DEC_BLOCK) {
-            const uint32_t rec = k / 65, kb = k - 65 * rec;
-            const uint64_t rs = byte0 + (uint64_t)rec * S;
-            sb[(s0 - g0) + k] = rs + S <= len ? Lb[(rs - a0) + (S - 65) + kb] : 0;
-        }
-        __syncthreads();
-        for (uint64_t w = t; g0 + 16 * w < s1; w += HD_DEC_BLOCK) {
-            const uint64_t addr = g0 + 16 * w;
-            if (addr >= s0 && addr + 16 <= s1) {
-                *reinterpret_cast<uint4*>(out.sig65 + addr) = sg[w];
+        const uint32_t base = (uint32_t)(byte0 - a0) + (S - 65u);   // LDS offset of signature 0
+        auto sig_ok = [&](uint32_t r) { return byte0 + (uint64_t)(r + 1) * S <= len; };
+        auto out_dword = [&](uint32_t rel) -> uint32_t {   // bytes [rel, rel + 4) of the signature stream
+            const uint32_t r = rel / 65u, kb = rel - 65u * r;
+            const uint32_t src = base + r * S + kb;
+            const uint32_t lo = sig_ok(r) ? lds_word(Lb, src) : 0u;
+            if (kb <= 61u) return lo;
+            const uint32_t nlo = 65u - kb;   // 1..3 bytes of signature r, the rest from r + 1
+            const uint32_t m = (1u << (8u * nlo)) - 1u;
+            const uint32_t hi = (r + 1 < nrec && sig_ok(r + 1)) ? lds_word(Lb, base + (r + 1) * S - nlo) : 0u;
+            return (lo & m) | (hi & ~m);
+        };
+        for (uint32_t w = t; 16 * w < sbytes; w += HD_DEC_BLOCK) {
+            const uint32_t rel = 16 * w;
+            const uint4 v = make_uint4(out_dword(rel), rel + 4 < sbytes ? out_dword(rel + 4) : 0u,
+                                       rel + 8 < sbytes ? out_dword(rel + 8) : 0u,
+                                       rel + 12 < sbytes ? out_dword(rel + 12) : 0u);
+            uint8_t* dst = out.sig65 + s0 + rel;
+            if (rel + 16 <= sbytes) {
+                *reinterpret_cast<uint4*>(dst) = v;
             } else {
-                const uint8_t* s = reinterpret_cast<const uint8_t*>(&sg[w]);
-                for (int k = 0; k < 16; k++)
-                    if (addr + k >= s0 && addr + k < s1) out.sig65[addr + k] = s[k];
+                const uint8_t* b = reinterpret_cast<const uint8_t*>(&v);
+                for (uint32_t k = 0; rel + k < sbytes; k++) dst[k] = b[k];
             }
         }
     }

@@ -456,6 +456,7 @@ def sub_benchmarks(args, v, sigs, foreign, dev, ws, ts):
                                    "verdicts": torch.bincount(vd.long(), minlength=8).cpu().tolist(),
                                    "fallback_msgs": v.fastpath_stats()[1], "tally": p5.tally_info}
     del p5, db5
+    out["C5_ingress_out_of_order"] = ingress_c5(v, (sigs, foreign), args.signers, B, ws, str(dev))
     # Signatory-set change (ResetHeight with a new epoch's set): the C2
     # context switches to 150 signatories, the 100 it knows plus 50 new ones.
     # The first batch after the change learns the 50 keys and builds their
@@ -511,6 +512,59 @@ def sub_benchmarks(args, v, sigs, foreign, dev, ws, ts):
     del p3, db3
     v3.close()
     return out
+
+
+def ingress_c5(v, keys, S, n, ws, dev, heights=64):
+    """BASELINE config 5 through the replica ingress (hyperdrive_amd/ingress.py):
+    the C2 stream with 30 % of the messages corrupted, shuffled so that heights
+    arrive out of order, marshalled per message type to wire bytes.  Timed:
+    the pushes (unmarshal -> verify -> filterHeight -> mq insert with a
+    per-sender capacity of 1000, every authenticated message buffered), then
+    `heights` flushes with ResetHeight between (mq.Consume of the current
+    height against procsAllowed -> vote logs).  Checked: the messages
+    delivered are exactly the VALID ones of heights 1..`heights` (the queues
+    keep each sender's lowest heights, mq.go:125-142)."""
+    import torch
+    from hyperdrive_amd.codec import marshal_device
+    from hyperdrive_amd.device import DeviceBatch, generate
+    from hyperdrive_amd.ingress import Ingress
+    db, _, _ = generate(v, 0, n, S, 30, keys=keys, device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    perm = torch.randperm(n, device=dev, generator=g)
+    parts = []
+    for t in (2, 3):
+        idx = perm[(db.type == t)[perm]]
+        sub = DeviceBatch(int(idx.numel()), *(getattr(db, f)[idx].contiguous()
+                                               for f in ("type", "height", "round", "valid_round", "value", "frm",
+                                                         "sig")))
+        parts.append((t, sub, marshal_device(v, t, sub, with_sig=True, stream=ws)))
+    ing = Ingress(v, height=1, max_capacity=1000)
+    for t, sub, wire in parts:                        # warm (allocations)
+        ing.push_wire(t, wire, sub.n, stream=ws)
+    ing.reset_height(1)
+    ing.mq.drop_below(2 ** 62)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    verdicts = [ing.push_wire(t, wire, sub.n, stream=ws) for t, sub, wire in parts]
+    t1 = time.perf_counter()
+    delivered = 0
+    for h in range(1, heights + 1):
+        if h > 1:
+            ing.reset_height(h)
+        delivered += len(ing.flush().consumed)
+    t2 = time.perf_counter()
+    want = sum(int(((vd == 0) & (sub.height >= 1) & (sub.height <= heights)).sum())
+               for vd, (_, sub, _) in zip(verdicts, parts))
+    vh = torch.bincount(torch.cat(verdicts).long(), minlength=8).cpu().tolist()
+    buffered = len(ing.mq)
+    ing.close()
+    return {"messages": n, "push_ms": (t1 - t0) * 1e3, "push_msgs_per_s": n / (t1 - t0),
+            "flushes": heights, "flush_ms": (t2 - t1) * 1e3, "total_msgs_per_s": n / (t2 - t0),
+            "verdicts": vh, "delivered": delivered, "delivered_equals_valid_at_flushed_heights": delivered == want,
+            "buffered_after": buffered,
+            "note": "30 % adversarial C2 batch in random order (heights out of order), prevote and precommit wire "
+                    "buffers; wall time of the synchronous ingress calls"}
 
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured float4 copy)

@@ -1100,6 +1100,7 @@ static void launch_sums(uint32_t blocks, hipStream_t s, uint32_t n, const gp* gt
         else k_fast_sums<2, WP, 2, DL><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
     } else {
         if (w == 2) k_fast_sums<2, WP, 1, DL><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
+        else if (w == 4) k_fast_sums<4, WP, 1, DL><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
         else k_fast_sums<3, WP, 1, DL><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
     }
 }

@@ -298,3 +298,46 @@ def test_key_table_widths_equal_full_recovery(gpu, monkeypatch, width):
     assert fast.known_keys() > 0
     fast.close()
     slow.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("off", [1, 4, 8])
+def test_misaligned_records_equal_aligned(gpu, off):
+    """The record loads (hd_common.h) take 16-byte / dword vector paths only
+    for aligned bases: signatures, values, Froms and the recovered-signatory
+    output at byte offsets 1, 4 and 8 must give what aligned buffers give, on
+    the known-key check and the full recovery alike."""
+    import torch
+    from hyperdrive_amd._lib import HdBatch
+    from hyperdrive_amd.device import generate, work_stream
+    from hyperdrive_amd.verify import Verifier
+    n, S = 5003, 100
+    v = Verifier(0)
+    ks = v.gen_keys(S)
+    v.set_signatories(ks[0])
+    db, _, _ = generate(v, 0, n, S, 30, keys=ks, start=77)
+    first = _run(v, db, n)                       # full recovery, learns the keys
+    ref = _run(v, db, n)                         # known-key check
+    for a, b in zip(first, ref):
+        assert torch.equal(a, b)
+
+    def shifted(t):
+        flat = torch.zeros(t.numel() + off, dtype=torch.uint8, device="cuda")
+        view = flat[off:off + t.numel()]
+        view.copy_(t.reshape(-1))
+        return flat, view
+    keep = [shifted(db.value), shifted(db.frm), shifted(db.sig)]
+    mb = HdBatch(n, db.type.data_ptr(), db.height.data_ptr(), db.round.data_ptr(), db.valid_round.data_ptr(),
+                 keep[0][1].data_ptr(), keep[1][1].data_ptr(), keep[2][1].data_ptr())
+    rec_flat = torch.zeros(32 * n + off, dtype=torch.uint8, device="cuda")
+    verdict = torch.empty(n, dtype=torch.uint8, device="cuda")
+    signer = torch.empty(n, dtype=torch.int32, device="cuda")
+    bitmap = torch.zeros((n + 31) // 32, dtype=torch.int32, device="cuda")
+    ws = work_stream()
+    v.verify_batch_device(mb, verdict.data_ptr(), rec_flat[off:].data_ptr(), signer.data_ptr(), bitmap.data_ptr(),
+                          ws.cuda_stream)
+    ws.synchronize()
+    assert torch.equal(verdict, ref[0]) and torch.equal(signer, ref[1]) and torch.equal(bitmap, ref[3])
+    assert torch.equal(rec_flat[off:off + 32 * n].view(n, 32), ref[2])
+    assert int((ref[0] == 0).sum()) > 0 and v.fastpath_stats()[1] <= int((ref[0] != 0).sum())
+    v.close()

@@ -1100,7 +1100,6 @@ static void launch_sums(uint32_t blocks, hipStream_t s, uint32_t n, const gp* gt
         else k_fast_sums<2, WP, 2, DL><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
     } else {
         if (w == 2) k_fast_sums<2, WP, 1, DL><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
-        else if (w == 4) k_fast_sums<4, WP, 1, DL><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
         else k_fast_sums<3, WP, 1, DL><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
     }
 }
@@ -1204,9 +1203,7 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
                                             ctx->n_adm, ctx->adm_steps, d_verdict, d_rec32, d_signer, f->slow,       \
                                             f->counts + 1)
         if (fw == 2) HD_LAUNCH_FAST(2);
-        else if (fw == 4) HD_LAUNCH_FAST(4);
-        else if (fw == 5) HD_LAUNCH_FAST(5);
-        else HD_LAUNCH_FAST(3);
+        else HD_LAUNCH_FAST(3);   // (4 and 5 waves spill heavily; not offered)
 #undef HD_LAUNCH_FAST
         FBCHK(hipGetLastError(), "k_verify_fast launch");
         // the fallback list is usually short (its length is only known on the

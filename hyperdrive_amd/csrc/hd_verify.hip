@@ -158,7 +158,9 @@ int hd_ctx_create(int device, hd_ctx** out) {
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->n_cu = prop.multiProcessorCount;
     if (const char* w = getenv("HD_VERIFY_WAVES")) {
         int v = atoi(w);
-        if (v >= 2 && v <= 4) ctx->verify_waves = v;
+        // 2 or 3: the 4-wave build (128 VGPRs) miscompiles the recovery
+        // (every signatory mismatched, round 2b), so it is not offered
+        if (v == 2 || v == 3) ctx->verify_waves = v;
     }
     if (const char* f = getenv("HD_VERIFY_FASTPATH")) ctx->fastpath = atoi(f) != 0;
     // G tables (1G..2048G and lambda*(1G..2048G), affine), built once on the
@@ -263,11 +265,10 @@ int hd_launch_slow(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint
 #define HD_LAUNCH_VERIFY(C, W)                                                                                    \
     k_verify<C, W><<<blocks, 256, 0, s>>>(b, ctx->d_gtab, ctx->d_adm, ctx->d_adm_perm, ctx->n_adm, ctx->adm_steps, \
                                           d_verdict, d_rec32, d_signer, d_bitmap, d_digest, ctl)
-    // waves/SIMD the kernel is register-allocated for (HD_VERIFY_WAVES = 2/3/4, default 3)
+    // waves/SIMD the kernel is register-allocated for (HD_VERIFY_WAVES = 2/3, default 3)
     const int w = ctx->verify_waves;
     if (ctx->pkfmt == HD_PUBKEY_COMPRESSED) {
         if (w == 2) HD_LAUNCH_VERIFY(1, 2);
-        else if (w == 4) HD_LAUNCH_VERIFY(1, 4);
         else HD_LAUNCH_VERIFY(1, 3);
     } else if (ctx->pkfmt == HD_PUBKEY_RAW64) {
         HD_LAUNCH_VERIFY(2, 3);

@@ -7,7 +7,7 @@ from hyperdrive_amd.device import generate, work_stream
 
 N, S = 1 << 20, 100
 ctxs = {}
-for w in (2, 3, 4):
+for w in (2, 3):   # (4: the build miscompiles the recovery, removed in round 2b)
     os.environ["HD_VERIFY_WAVES"] = str(w)
     ctxs[w] = hd.Verifier(0)
 sigs, foreign = ctxs[2].gen_keys(S)

@@ -931,6 +931,11 @@ int hd_fb_init(hd_ctx* ctx) {
     return fb_g_table(ctx, &f->gtab);
 }
 
+const gp* hd_fb_gtab(const hd_ctx* ctx) {
+    if (getenv("HD_RECOVER_GLV_G")) return nullptr;   // A/B: the GLV ladder's own G table
+    return ctx && ctx->fb ? ctx->fb->gtab : nullptr;
+}
+
 void hd_fb_release(hd_ctx* ctx) {
     if (!ctx || !ctx->fb) return;
     FbWork* f = ctx->fb;

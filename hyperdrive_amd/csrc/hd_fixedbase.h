@@ -386,6 +386,79 @@ HD void verify_fast2(uint8_t out[2], const FastIn in[2], GT gtab, PT ptab0, PT p
     out[1] = ok1 ? fast_final(acc1, zib, x1, in[1].v) : o1;
 }
 
+// ---- the full recovery's multiplication over the fixed-base G table --------
+// Q = u1 G + u2 R as ecmult_glv computes it, with u1 G taken out of the
+// ladder: the ladder keeps u2 R (GLV halves, 4-bit windows, 128 doublings on
+// the isomorphic curve of the R table) and u1 G runs as fixed-base additions
+// from the W-bit G table of the known-key check (FbL<W>: one table point per
+// window, no doublings) in an accumulator of its own.  Its additions are
+// interleaved with the ladder (one per third ladder window, the rest after it)
+// but never on the ladder's dependency chain, and there are NWIN of them
+// instead of the 2 x 11 G additions of the GLV ladder.  Every addition is the
+// exact gej_add_ge / gej_add (infinity and P = +-Q handled), so the result is
+// the same point; the caller's checks on it are unchanged.
+template <int W, typename FbTab>
+HD void ecmult_glv_fbg(gej& out, const ge& R, const sc& u1, const sc& u2, FbTab fbg) {
+    ge rt[HD_RTAB_N], lt[HD_RTAB_N];
+    fe zg;
+    build_rtab_iso(rt, lt, zg, R);
+    int16_t dra[HD_GLV_NWIN_R], drb[HD_GLV_NWIN_R];
+    {
+        sc k1, k2;
+        uint32_t a[5];
+        sc_split_lambda(k1, k2, u2);
+        bool neg = sc_signed_abs(a, k1);
+        HD_UNROLL for (int j = 0; j < HD_GLV_NWIN_R; j++) dra[j] = (int16_t)booth_digit160<HD_WR>(a, j, neg);
+        neg = sc_signed_abs(a, k2);
+        HD_UNROLL for (int j = 0; j < HD_GLV_NWIN_R; j++) drb[j] = (int16_t)booth_digit160<HD_WR>(a, j, neg);
+    }
+    gej acc, accg;
+    gej_set_inf(acc);
+    gej_set_inf(accg);
+    int gw = 0;   // next G window
+    auto g_step = [&]() {
+        const int d = fb_digit<W>(u1, gw);
+        if (d != 0) {
+            const int ad = d < 0 ? -d : d;
+            ge t = fbg[(size_t)gw * FbL<W>::N + (uint32_t)(ad - 1)];
+            if (d < 0) fe_neg(t.y, t.y);
+            gej_add_ge(accg, accg, t);
+        }
+        gw++;
+    };
+    HD_NOUNROLL for (int j = HD_GLV_NWIN_R - 1; j >= 0; j--) {
+        if (j != HD_GLV_NWIN_R - 1) {
+            HD_NOUNROLL for (int k = 0; k < HD_WR; k++) gej_dbl(acc, acc);
+        }
+        if (j % 3 == 0 && gw < FbL<W>::NWIN) g_step();
+        HD_NOUNROLL for (int half = 0; half < 2; half++) {
+            const int d = half ? drb[j] : dra[j];
+            const int ad = d < 0 ? -d : d;
+            ge t = half ? lt[ad == 0 ? 0 : ad - 1] : rt[ad == 0 ? 0 : ad - 1];
+            if (d < 0) fe_neg(t.y, t.y);
+            gej s;
+            gej_add_ge(s, acc, t);
+            gej_cmov(acc, s, d != 0);
+        }
+    }
+    HD_NOUNROLL while (gw < FbL<W>::NWIN) g_step();
+    fe_mul(acc.z, acc.z, zg);  // back from E' to E
+    if (gej_is_inf(accg)) {
+        out = acc;
+    } else {
+        gej q;
+        gej_add(q, acc, accg);
+        out = q;
+    }
+}
+template <int W, typename FbTab>
+struct GlvFbgMult {
+    FbTab fbg;
+    HD_MEMBER void operator()(gej& out, const ge& R, const sc& u1, const sc& u2) const {
+        ecmult_glv_fbg<W>(out, R, u1, u2, fbg);
+    }
+};
+
 // ---- table construction (one entry per lane) --------------------------
 // 2^(W j) B, affine canonical
 HD void fb_window_base(ge& out, const ge& B, int W, int j) {

@@ -618,9 +618,19 @@ HD void gej_to_ge(fe& x, fe& y, const gej& a) {
 //   Q = inf -> INFINITY.  High-S accepted.  m = digest mod n.
 // On VALID writes the affine Q (x, y), canonical.
 // gtab: 2 * HD_GLV_GTAB_N entries (build_gtab_glv).
+// the multiplication Q = u1 G + u2 R of the recovery (ecmult_glv over the
+// small GLV G table; hd_fixedbase.h has a form over the fixed-base G table)
 template <typename GTab>
-HD uint8_t recover(fe& qx, fe& qy, const uint32_t digest_be[8], const uint32_t r_be[8],
-                   const uint32_t s_be[8], uint32_t v, GTab gtab) {
+struct GlvMult {
+    GTab gtab;
+    HD_MEMBER void operator()(gej& out, const ge& R, const sc& u1, const sc& u2) const {
+        ecmult_glv(out, R, u1, u2, gtab);
+    }
+};
+
+template <typename Mult>
+HD uint8_t recover_m(fe& qx, fe& qy, const uint32_t digest_be[8], const uint32_t r_be[8],
+                     const uint32_t s_be[8], uint32_t v, Mult mult) {
     if (v >= 4) return V_BAD_RECID;
     sc r, s;
     HD_UNROLL for (int i = 0; i < 8; i++) { r.v[i] = r_be[7 - i]; s.v[i] = s_be[7 - i]; }
@@ -670,7 +680,7 @@ HD uint8_t recover(fe& qx, fe& qy, const uint32_t digest_be[8], const uint32_t r
     sc_mul(u2, s, rinv);
 
     gej Q;
-    ecmult_glv(Q, R, u1, u2, gtab);
+    mult(Q, R, u1, u2);
     if (gej_is_inf(Q)) return V_INFINITY;
     fe zi, zi2;
     fe_inv_divsteps(zi, Q.z);
@@ -681,6 +691,11 @@ HD uint8_t recover(fe& qx, fe& qy, const uint32_t digest_be[8], const uint32_t r
     fe_normalize(qx);
     fe_normalize(qy);
     return V_VALID;
+}
+template <typename GTab>
+HD uint8_t recover(fe& qx, fe& qy, const uint32_t digest_be[8], const uint32_t r_be[8],
+                   const uint32_t s_be[8], uint32_t v, GTab gtab) {
+    return recover_m(qx, qy, digest_be, r_be, s_be, v, GlvMult<GTab>{gtab});
 }
 
 }  // namespace hd

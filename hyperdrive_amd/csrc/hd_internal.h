@@ -5,7 +5,7 @@
 #include <string>
 
 #include "../../include/hd_verify.h"
-#include "hd_group.h"
+#include "hd_fixedbase.h"
 
 struct DevBatch {
     uint32_t n;
@@ -59,6 +59,7 @@ void hd_tally_release(hd_ctx* ctx);
 // known-key fast path (hd_fastverify.hip)
 int hd_fb_init(hd_ctx* ctx);                    // tables of G (slot 0); at context creation
 void hd_fb_release(hd_ctx* ctx);
+const hd::gp* hd_fb_gtab(const hd_ctx* ctx);    // the shared fixed-base G table (NULL: none)
 int hd_fb_map_signatories(hd_ctx* ctx, const uint8_t* sorted_sigs32, uint32_t m);  // after hd_set_signatories
 int hd_fb_clear_keys(hd_ctx* ctx);               // pubkey format changed: learned keys no longer apply
 // fast kernel + slow recovery of the rest + learning; the whole verify of a device batch

@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256, WAVES) void k_verify(DevBatch b, const ge* __r
                                                 uint32_t n_adm, int adm_steps, uint8_t* __restrict__ verdict,
                                                 uint8_t* __restrict__ rec32, int32_t* __restrict__ signer,
                                                 uint32_t* __restrict__ bitmap, const uint8_t* __restrict__ digest_in,
-                                                SlowCtl ctl) {
+                                                SlowCtl ctl, const gp* __restrict__ fbg) {
     const uint32_t stride = gridDim.x * blockDim.x;
     const uint32_t total = ctl.list ? *ctl.count : b.n;
     for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += stride) {
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256, WAVES) void k_verify(DevBatch b, const ge* __r
             uint32_t rec[8];
             int32_t s;
             ge q;
-            v = verify_msg_src(src, gtab_g, adm, n_adm, adm_steps, PKFMT, rec, s, ctl.adm_slot ? &q : nullptr);
+            v = verify_msg_src(src, gtab_g, adm, n_adm, adm_steps, PKFMT, rec, s, ctl.adm_slot ? &q : nullptr, fbg);
             verdict[i] = v;
             if (rec32) {
                 uint8_t* o = rec32 + 32 * (size_t)i;
@@ -264,9 +264,10 @@ int hd_launch_slow(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint
                    int32_t* d_signer, uint32_t* d_bitmap, const SlowCtl& ctl, uint32_t blocks, hipStream_t s) {
 #define HD_LAUNCH_VERIFY(C, W)                                                                                    \
     k_verify<C, W><<<blocks, 256, 0, s>>>(b, ctx->d_gtab, ctx->d_adm, ctx->d_adm_perm, ctx->n_adm, ctx->adm_steps, \
-                                          d_verdict, d_rec32, d_signer, d_bitmap, d_digest, ctl)
+                                          d_verdict, d_rec32, d_signer, d_bitmap, d_digest, ctl, fbg)
     // waves/SIMD the kernel is register-allocated for (HD_VERIFY_WAVES = 2/3, default 3)
     const int w = ctx->verify_waves;
+    const gp* fbg = hd_fb_gtab(ctx);   // the fixed-base G table, when the context has one
     if (ctx->pkfmt == HD_PUBKEY_COMPRESSED) {
         if (w == 2) HD_LAUNCH_VERIFY(1, 2);
         else HD_LAUNCH_VERIFY(1, 3);

@@ -6,6 +6,7 @@
 // process/message_test.go:147-154 (sign -> Signatory(&hash) -> Equal);
 // mq/mq.go:49-51 + replica/replica.go:69-72 (procsAllowed membership).
 #pragma once
+#include "hd_fixedbase.h"
 #include "hd_group.h"
 #include "hd_sha256.h"
 
@@ -76,9 +77,11 @@ HD_HOSTONLY size_t adm_lds_bytes(uint32_t n) { return n <= HD_ADM_LDS_MAX ? 32 *
 // nothing but the accumulator stays live across the ladder.  rec_be receives
 // the recovered signatory (zeros when recovery failed); signer the
 // admitted-table index; qout (optional) the recovered key of a VALID message.
+// fbg (optional, device): the known-key check's fixed-base G table; the
+// recovery then takes u1 G from it (ecmult_glv_fbg) instead of the GLV ladder.
 template <typename Src, typename GTab, typename AdmTab>
 HD uint8_t verify_msg_src(const Src& src, GTab gtab, AdmTab adm, uint32_t n_adm, int adm_steps, int pkfmt,
-                          uint32_t rec_be[8], int32_t& signer, ge* qout = nullptr) {
+                          uint32_t rec_be[8], int32_t& signer, ge* qout = nullptr, const gp* fbg = nullptr) {
     signer = -1;
     HD_UNROLL for (int i = 0; i < 8; i++) rec_be[i] = 0;
     const uint32_t type = src.type();
@@ -98,7 +101,8 @@ HD uint8_t verify_msg_src(const Src& src, GTab gtab, AdmTab adm, uint32_t n_adm,
     {
         uint32_t r_be[8], s_be[8];
         HD_UNROLL for (int w = 0; w < 8; w++) { r_be[w] = src.sig_r(w); s_be[w] = src.sig_s(w); }
-        verdict = recover(qx, qy, d, r_be, s_be, src.sig_v(), gtab);
+        if (fbg) verdict = recover_m(qx, qy, d, r_be, s_be, src.sig_v(), GlvFbgMult<HD_FB_WG, GpTab>{GpTab{fbg}});
+        else verdict = recover(qx, qy, d, r_be, s_be, src.sig_v(), gtab);
     }
     if (verdict != V_VALID) return verdict;
     {

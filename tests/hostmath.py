@@ -54,6 +54,14 @@ class HostMath:
             return None
         return int.from_bytes(out.raw[:32], "big"), int.from_bytes(out.raw[32:], "big")
 
+    def ecmult_glv_fbg8(self, R, u1: int, u2: int):
+        """ecmult_glv_fbg over an 8-bit-window fixed-base G table (hd_fixedbase.h)"""
+        out = ctypes.create_string_buffer(64)
+        inf = self.L.hdh_ecmult_glv_fbg8(b32(R[0]), b32(R[1]), b32(u1), b32(u2), out)
+        if inf:
+            return None
+        return int.from_bytes(out.raw[:32], "big"), int.from_bytes(out.raw[32:], "big")
+
     def split(self, k: int):
         a = ctypes.create_string_buffer(32)
         b = ctypes.create_string_buffer(32)

@@ -488,3 +488,38 @@ extern "C" void hdh_fb_verify2(const uint8_t* pub64, const uint8_t* digests, con
     FastPark park;
     verify_fast2(out, in, hdh_fb_cache(0)->data(), hdh_fb_cache(1)->data(), hdh_fb_cache(1)->data(), &park);
 }
+
+// ecmult_glv_fbg (hd_fixedbase.h: the full recovery's u1 G from a fixed-base
+// G table) over an 8-bit-window host table of G (32 windows: 11 interleaved
+// with the ladder, 21 after it), against ecmult_glv; returns 1 for infinity.
+static const ge* fbg8_table() {
+    static std::vector<ge> tab;
+    if (tab.empty()) {
+        tab.resize(FbL<8>::TAB);
+        const ge& G = gtab()[0];
+        for (int j = 0; j < FbL<8>::NWIN; j++) {
+            ge bj;
+            fb_window_base(bj, G, 8, j);
+            const uint32_t nd = j == FbL<8>::NWIN - 1 ? FbL<8>::NTOP : FbL<8>::N;
+            for (uint32_t d = 1; d <= nd; d++) fb_entry(tab[(size_t)j * FbL<8>::N + d - 1], bj, d);
+        }
+    }
+    return tab.data();
+}
+extern "C" int hdh_ecmult_glv_fbg8(const uint8_t* rx, const uint8_t* ry, const uint8_t* u1b, const uint8_t* u2b,
+                                   uint8_t* out) {
+    ge R;
+    sc u1, u2;
+    fe_in(R.x, rx);
+    fe_in(R.y, ry);
+    le_in(u1.v, u1b);
+    le_in(u2.v, u2b);
+    gej Q;
+    ecmult_glv_fbg<8>(Q, R, u1, u2, fbg8_table());
+    if (gej_is_inf(Q)) return 1;
+    fe x, y;
+    gej_to_ge(x, y, Q);
+    fe_out(out, x);
+    fe_out(out + 32, y);
+    return 0;
+}

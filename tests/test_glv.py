@@ -52,3 +52,27 @@ def test_ecmult_glv(oracle, hostmath):
                       (LG, 0, 7), (G, 0, 0), (G, 7, 0), (LG, oracle.N - LAM, 1)]:
         want = oracle.point_add(oracle.point_mul(u1, G), oracle.point_mul(u2, R))
         assert hostmath.ecmult_glv(R, u1, u2) == want, (u1, u2)
+
+
+def test_ecmult_glv_fixed_base_g(oracle, hostmath):
+    """ecmult_glv_fbg: u2 R by the GLV ladder, u1 G by fixed-base additions
+    from a G table in an accumulator of its own, joined by one exact Jacobian
+    addition -- the same point as ecmult_glv / the oracle, including zero
+    scalars, the join cancelling (u1 G = -u2 R: infinity) and the join
+    doubling (u1 G = u2 R)."""
+    N, G = oracle.N, oracle.G
+    rng = random.Random(43)
+    cases = []
+    for _ in range(10):
+        k = rng.randrange(1, N)
+        cases.append((k, rng.randrange(N), rng.randrange(N)))
+    for k in (1, 2, 7, N - 1, LAM):
+        u2 = rng.randrange(1, N)
+        cases += [(k, (-u2 * k) % N, u2), (k, u2 * k % N, u2), (k, 0, u2), (k, rng.randrange(N), 0), (k, 0, 0),
+                  (k, 1, 0), (k, N - 1, 1), (k, 2 ** 255 % N, 3)]
+    for k, u1, u2 in cases:
+        R = oracle.point_mul(k, G)
+        want = oracle.point_add(oracle.point_mul(u1, G), oracle.point_mul(u2, R))
+        got = hostmath.ecmult_glv_fbg8(R, u1, u2)
+        assert got == want, (hex(k), hex(u1), hex(u2))
+        assert got == hostmath.ecmult_glv(R, u1, u2)

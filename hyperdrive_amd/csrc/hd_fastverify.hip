@@ -1168,8 +1168,10 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
     const uint32_t fast_blocks = ((b.n + 1) / 2 + 255) / 256;   // two messages per lane
     FBCHK(hipMemsetAsync(f->counts + 1, 0, 4, s), "fb count reset");
     if (ctx->n_adm > 0 && f->adm_slot && split_k_for(b.n) > 0) {
-        constexpr size_t ROW_WORDS = 62 + FbL<HD_FB_WG>::NWIN + FbL<HD_FB_W>::NWIN;   // the narrow width has more windows
-        rc = hd_dev_grow(ctx, (void**)&f->rows, &f->cap_rows, 4 * ROW_WORDS * (size_t)b.n);
+        // 62 words per message; the digit rows (the narrow width has more
+        // windows) only for the HD_SUM_DIGITS=rows A/B form
+        const size_t row_words = 62 + (sums_digits_lds() ? 0 : FbL<HD_FB_WG>::NWIN + FbL<HD_FB_W>::NWIN);
+        rc = hd_dev_grow(ctx, (void**)&f->rows, &f->cap_rows, 4 * row_words * (size_t)b.n);
         if (rc) return rc;
         const uint32_t n = b.n;
         SplitRows rows;
@@ -1180,7 +1182,7 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         rows.s = f->rows + 18 * (size_t)n;
         rows.pre = f->rows + 26 * (size_t)n;
         rows.xyz = f->rows + 35 * (size_t)n;
-        rows.dig = f->rows + 62 * (size_t)n;
+        rows.dig = sums_digits_lds() ? nullptr : f->rows + 62 * (size_t)n;
         const int k = split_k_for(n);
         f->last_k = k;
         if (f->wp == HD_FB_WW) {

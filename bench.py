@@ -547,6 +547,7 @@ def ingress_c5(v, keys, S, n, ws, dev, heights=64):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     verdicts = [ing.push_wire(t, wire, sub.n, stream=ws) for t, sub, wire in parts]
+    torch.cuda.synchronize()                          # push_ms includes the device work it queued
     t1 = time.perf_counter()
     delivered = 0
     for h in range(1, heights + 1):

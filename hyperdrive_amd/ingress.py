@@ -59,6 +59,10 @@ class Ingress:
         self.f = None              # set by reset_height(signatories=...): len(signatories) // 3 (replica.go:138)
         self.mq = MessageQueue(v, max_capacity)
         self.votes = VoteLog(self.height)
+        # (height, insert count) of the last consume: while the queue has had
+        # no insert since, every message in it is above that height, so a
+        # ResetHeight to at most height + 1 has nothing to drop
+        self._clean = None
 
     def close(self):
         self.mq.close()
@@ -95,6 +99,7 @@ class Ingress:
         """mq.Consume(CurrentHeight, ..., procsAllowed) with procsAllowed = the
         verifier's admitted set now, then the vote-log inserts."""
         b, senders = self.mq.consume(self.height, allowed=None)
+        self._clean = (self.height, self.mq.inserts)
         status, double_of = self.votes.insert_batch(b)
         return FlushResult(b, senders, status, double_of, np.flatnonzero(b.type == PROPOSE), self.mq.last_removed)
 
@@ -104,7 +109,9 @@ class Ingress:
         set replaces procsAllowed (and the verifier's admitted set)."""
         self.height = int(height)
         self.votes.reset(self.height)
-        self.mq.drop_below(self.height)
+        clean = self._clean is not None and self._clean[1] == self.mq.inserts and self.height <= self._clean[0] + 1
+        if not clean:
+            self.mq.drop_below(self.height)
         if signatories is not None and len(signatories):
             self.v.set_signatories(signatories)
             self.f = len(signatories) // 3

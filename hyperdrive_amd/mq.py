@@ -42,6 +42,7 @@ class MessageQueue:
         self._q = h
         self.max_capacity = max_capacity
         self.last_removed = 0        # Consume's n (delivered + dropped by procsAllowed) of the last consume
+        self.inserts = 0             # insert calls so far (lets a caller know the pool is unchanged)
         _lib.track(self)
 
     def close(self):
@@ -71,6 +72,7 @@ class MessageQueue:
             if insert.dtype == torch.bool:
                 insert = insert.to(torch.uint8)
             ptr = insert.data_ptr()
+        self.inserts += 1
         self._check(self._lib.hd_mq_insert_device(self._q, ctypes.byref(cs), ptr, ws.cuda_stream),
                     "hd_mq_insert_device")
 
@@ -82,6 +84,7 @@ class MessageQueue:
         ws = stream or work_stream(batch.height.device)
         ws.wait_stream(torch.cuda.current_stream(ws.device))
         cs = batch.c_struct()
+        self.inserts += 1
         self._check(self._lib.hd_mq_insert_verified_device(self._q, ctypes.byref(cs), verdict.data_ptr(),
                                                            int(min_height), ws.cuda_stream),
                     "hd_mq_insert_verified_device")
@@ -106,10 +109,12 @@ class MessageQueue:
         number removed, delivered or not."""
         cap = len(self)
         n = max(cap, 1)
-        a = dict(type=np.zeros(n, np.uint8), height=np.zeros(n, np.int64), round=np.zeros(n, np.int64),
-                 valid_round=np.zeros(n, np.int64), value=np.zeros((n, 32), np.uint8),
-                 frm=np.zeros((n, 32), np.uint8), sig=np.zeros((n, 65), np.uint8))
-        snd = np.zeros(n, np.int32)
+        # np.empty: only the first `got` rows are written and returned, and the
+        # untouched pages of a large buffer are never faulted in
+        a = dict(type=np.empty(n, np.uint8), height=np.empty(n, np.int64), round=np.empty(n, np.int64),
+                 valid_round=np.empty(n, np.int64), value=np.empty((n, 32), np.uint8),
+                 frm=np.empty((n, 32), np.uint8), sig=np.empty((n, 65), np.uint8))
+        snd = np.empty(n, np.int32)
         p = lambda x: x.ctypes.data
         out = HdBatchOut(p(a["type"]), p(a["height"]), p(a["round"]), p(a["valid_round"]), p(a["value"]),
                          p(a["frm"]), p(a["sig"]), None)

@@ -406,18 +406,24 @@ static int dev_minmax(hd_mq* q, const T* d, uint32_t n, T* mn, T* mx, hipStream_
 }
 
 // select-flagged over [0, n) -> out indices, returns count (synchronises)
-static int select_idx(hd_mq* q, const uint8_t* flag, uint32_t n, uint32_t* out, uint32_t* count, hipStream_t s) {
+// Indices of the set flags, in order.  The count lands in *count after a
+// stream sync when wait is set; with wait unset it is only queued (the caller
+// syncs before reading it), and with count == nullptr it is not downloaded
+// (a caller that knows it).  Counts queued together use different slots.
+static int select_idx(hd_mq* q, const uint8_t* flag, uint32_t n, uint32_t* out, uint32_t* count, hipStream_t s,
+                      int slot = 0, bool wait = true) {
     int rc = 0;
     uint32_t* nsel = (uint32_t*)qbuf(q, MQ_NSEL, 64, &rc);
     if (rc) return rc;
+    nsel += slot;
     hipcub::CountingInputIterator<uint32_t> iota(0);
     size_t need = 0;
     QCHK(hipcub::DeviceSelect::Flagged(nullptr, need, iota, flag, out, nsel, n, s), "select size");
     void* tmp = qbuf(q, MQ_TMP, need, &rc);
     if (rc) return rc;
     QCHK(hipcub::DeviceSelect::Flagged(tmp, need, iota, flag, out, nsel, n, s), "select");
-    QCHK(hipMemcpyAsync(count, nsel, 4, hipMemcpyDeviceToHost, s), "select count");
-    QCHK(hipStreamSynchronize(s), "select sync");
+    if (count) QCHK(hipMemcpyAsync(count, nsel, 4, hipMemcpyDeviceToHost, s), "select count");
+    if (count && wait) QCHK(hipStreamSynchronize(s), "select sync");
     return HD_OK;
 }
 
@@ -462,13 +468,15 @@ static int sort_pass32(hd_mq* q, hipcub::DoubleBuffer<uint32_t>& perm, const uin
 }
 
 // keep the pool elements whose flag is set, in order
-static int pool_filter(hd_mq* q, const uint8_t* keep, hipStream_t s) {
+// Keep the pool entries whose keep flag is set; `kept` = their number when
+// the caller knows it (saves the count download), else -1.
+static int pool_filter(hd_mq* q, const uint8_t* keep, hipStream_t s, int64_t kept = -1) {
     int rc = 0;
     const uint32_t M = q->pool.n;
     uint32_t* sel = (uint32_t*)qbuf(q, MQ_SEL, 4 * (size_t)M, &rc);
     if (rc) return rc;
-    uint32_t n = 0;
-    rc = select_idx(q, keep, M, sel, &n, s);
+    uint32_t n = kept >= 0 ? (uint32_t)kept : 0;
+    rc = select_idx(q, keep, M, sel, kept >= 0 ? nullptr : &n, s, 2);
     if (rc) return rc;
     rc = pool_reserve(q->ctx, q->spare, std::max(n, 1u));
     if (rc) return rc;
@@ -726,9 +734,9 @@ int hd_mq_consume(hd_mq* q, int64_t h, const uint8_t* allowed32, uint32_t n_allo
     k_mq_pred<<<nblk(M), 256, 0, s>>>(M, q->pool.h, q->pool.sender, h, 0, allow, removed, deliver, inv);
     QCHK(hipGetLastError(), "k_mq_pred");
     uint32_t nr = 0, c = 0;
-    rc = select_idx(q, removed, M, sel2, &nr, s);
+    rc = select_idx(q, removed, M, sel2, &nr, s, 0, false);   // counted by the next select's sync
     if (rc) return rc;
-    rc = select_idx(q, deliver, M, sel, &c, s);
+    rc = select_idx(q, deliver, M, sel, &c, s, 1);
     if (rc) return rc;
     *n_out = c;
     if (c > cap) return HD_ECAP;
@@ -750,7 +758,7 @@ int hd_mq_consume(hd_mq* q, int64_t h, const uint8_t* allowed32, uint32_t n_allo
         if (out->adv_class) memset(out->adv_class, 0, c);
         QCHK(hipStreamSynchronize(s), "consume sync");
     }
-    return nr ? pool_filter(q, inv, s) : HD_OK;
+    return nr ? pool_filter(q, inv, s, (int64_t)M - nr) : HD_OK;
 }
 
 int hd_mq_drop_below(hd_mq* q, int64_t h) {

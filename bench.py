@@ -106,12 +106,17 @@ def cpu_baseline(args, S):
 
 
 class Pipeline:
-    """verify (library stream `ws`) -> bitmap all-gather -> tally (stream
-    `ts`) for one batch shape, with NBUF output buffers: the tally of step k
-    runs on its own stream while the verifications of steps k+1 .. k+NBUF-1
-    are queued, so the tally's host syncs never drain the verify queue; every
-    step's verification and tally complete inside the timed region."""
+    """verify (library streams `ws`, alternating) -> bitmap all-gather ->
+    tally (stream `ts`) for one batch shape, with NBUF output buffers: the
+    tally of step k runs on its own stream while the verifications of steps
+    k+1 .. k+NBUF-1 are queued, so the tally's host syncs never drain the
+    verify queue; consecutive verifications go to different streams, so the
+    device runs step k+1's kernels in the SIMD slots step k's inversion
+    kernels, last k_fast_sums round and fallback recovery leave idle (the
+    library's per-call scratch sets, hd_fastverify.hip FbWork); every step's
+    verification and tally complete inside the timed region."""
     NBUF = int(os.environ.get("HD_BENCH_NBUF", 3))
+    VSTREAMS = int(os.environ.get("HD_BENCH_VSTREAMS", 2))
 
     def __init__(self, v, db, total, B, rank, world, dist, ws, ts, tally=True):
         import torch
@@ -121,6 +126,7 @@ class Pipeline:
         self.rank, self.world, self.dist, self.ws, self.ts = rank, world, dist, ws, ts
         self.do_tally = tally
         dev = db.height.device
+        self.wss = [ws] + [torch.cuda.Stream(device=dev, priority=ws.priority) for _ in range(self.VSTREAMS - 1)]
         lo, hi = shard_range(total, rank, world)
         assert hi - lo == B and B % 32 == 0
         self.lo = lo
@@ -148,18 +154,19 @@ class Pipeline:
         import torch
         from hyperdrive_amd.shard import gather_bitmaps_async
         buf = k % self.NBUF
+        ws = self.wss[k % len(self.wss)]
         self.v.verify_batch_device(self.shard, self.verdicts[buf].data_ptr(), self.recovered[buf].data_ptr(), None,
-                                   self.bitmaps[buf].data_ptr(), self.ws.cuda_stream)
+                                   self.bitmaps[buf].data_ptr(), ws.cuda_stream)
         work = None
         if self.dist is not None:
-            with torch.cuda.stream(self.ws):
+            with torch.cuda.stream(ws):
                 # RCCL all-gather over xGMI; the tally stream waits for it, the
                 # next verification does not
                 gathered, work = gather_bitmaps_async(self.bitmaps[buf], self.total, self.world)
         else:
             gathered = self.bitmaps[buf]
         done = torch.cuda.Event()
-        done.record(self.ws)
+        done.record(ws)
         return gathered, done, work
 
     def tally(self, pending):
@@ -297,16 +304,25 @@ def main():
     torch.cuda.synchronize(dev)
     cold_s = time.perf_counter() - t0
     pipe.run(args.warmup)
-    v.profile(True)
-    v.profile_read()                    # clear
     if pipe.host_trace is not None:
         pipe.host_trace.clear()
     elapsed = timed(pipe, args.steps, dist, dev)
     if pipe.host_trace:
         t0h = pipe.host_trace[0][2]
         print("host trace:", [(a, k, round((t - t0h) * 1e3, 3)) for a, k, t in pipe.host_trace], file=sys.stderr)
+    # Roofline pass (untimed for `value`): the same steps with one verify
+    # stream, so that every k_fast_sums launch and verify call runs alone and
+    # its HIP-event duration is its own (in the timed region consecutive calls
+    # overlap and share the CUs)
+    all_streams = pipe.wss
+    pipe.wss = pipe.wss[:1]
+    torch.cuda.synchronize(dev)
+    v.profile(True)
+    v.profile_read()                    # clear
+    prof_s = timed(pipe, args.steps, dist, dev)
     calls, verify_ms, sums_launches, sums_ms = v.profile_read()
     v.profile(False)
+    pipe.wss = all_streams
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -391,6 +407,8 @@ def main():
                      "note": "first batch on a fresh context: full recovery of every message, key learning and "
                              "the per-key table build; ctx_create_s builds the shared G table"},
             "gen_s": gen_s,
+            "one_stream_msgs_per_s": total * args.steps / prof_s,
+            "verify_streams": len(all_streams),
         }
         if world == 1:
             out["oracle_sample_check"] = oracle_sample_check(db, verdict, recovered, sigs)
@@ -542,7 +560,7 @@ def ingress_c5(v, keys, S, n, ws, dev, heights=64):
     ing = Ingress(v, height=1, max_capacity=1000)
     for t, sub, wire in parts:                        # warm (allocations)
         ing.push_wire(t, wire, sub.n, stream=ws)
-    ing.reset_height(1)
+    ing.votes.reset(1)
     ing.mq.drop_below(2 ** 62)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -659,7 +677,7 @@ def aux_benchmarks(v, db, ws):
     wire = marshal_device(v, 2, db, with_sig=True, stream=ws)
     ing = Ingress(v, height=1, max_capacity=1000)
     ing.push_wire(2, wire, n, stream=ws)                  # warm (allocations)
-    ing.reset_height(1)
+    ing.votes.reset(1)
     ing.mq.drop_below(2 ** 62)
     torch.cuda.synchronize()
     t0 = time.perf_counter()

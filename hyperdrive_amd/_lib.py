@@ -112,6 +112,13 @@ SIGNATURES = {
     "hd_multi_set_pubkey_format": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "hd_multi_verify_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "hd_route_candidates_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
+                                                  ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                                  ctypes.POINTER(ctypes.c_uint32), ctypes.c_void_p]),
+    "hd_unroute_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                         ctypes.POINTER(HdBatchOut), ctypes.c_void_p, ctypes.c_void_p]),
+    "hd_tally_routed_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
+                                              ctypes.POINTER(HdTallyOut), ctypes.c_void_p]),
     "hd_gen_keys": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
     "hd_gen_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
                                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,

@@ -200,7 +200,10 @@ int hd_unmarshal_batch_device(hd_ctx* ctx, int type, int with_sig, const uint8_t
         return HD_EINVAL;
     if (type == T_PROPOSE && !d_out->valid_round) return HD_EINVAL;
     if (with_sig && !d_out->sig65) return HD_EINVAL;
-    if (((uintptr_t)d_buf & 15) || ((uintptr_t)d_out->value32 & 15) || ((uintptr_t)d_out->from32 & 15))
+    // k_unmarshal writes 16-byte words into value32, from32 and a block's
+    // contiguous sig65 range
+    if (((uintptr_t)d_buf & 15) || ((uintptr_t)d_out->value32 & 15) || ((uintptr_t)d_out->from32 & 15) ||
+        (with_sig && ((uintptr_t)d_out->sig65 & 15)))
         return HD_EINVAL;
     (void)hipSetDevice(ctx->device);
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;

@@ -45,21 +45,41 @@ using namespace hd;
 
 struct FbWork {
     const gp* gtab = nullptr;   // the shared G table of the device (fb_g_table)
-    uint32_t nslots = 0;        // allocated slots; slot 0 is unused
+    uint32_t nslots = 0;        // slots with a table (whole chunks); slot 0 is unused
     uint32_t max_slots = 0;     // from HD_FB_MAX_BYTES (slot 0 included)
-    gp* tab = nullptr;          // nslots x fb_tab_entries(wp) packed points
-    ge* base = nullptr;         // nslots x HD_FB_NWIN window bases
-    ge* pub = nullptr;          // nslots keys
-    uint32_t* state = nullptr;  // nslots HD_FB_* states
+    // Per-key tables live in chunks of HD_FB_CHUNK slots that are allocated
+    // when the admitted set first needs them and never moved: a set change
+    // that adds keys allocates only new chunks (no regrow, no copy of the
+    // tables already built).  tabs[slot] points at the slot's table.
+    gp** tabs = nullptr;        // device: max_slots table pointers
+    std::vector<gp*> chunks;    // host: the chunk allocations
+    ge* base = nullptr;         // max_slots x HD_FB_NWIN window bases
+    ge* pub = nullptr;          // max_slots keys
+    uint32_t* state = nullptr;  // max_slots HD_FB_* states
     int32_t* adm_slot = nullptr;  // admitted sorted index -> slot
     size_t cap_adm_slot = 0;
-    uint32_t* list = nullptr;     // slot work list (nslots)
-    uint32_t* counts = nullptr;   // [0] slots to build, [1] messages for the slow path
-    uint32_t* slow = nullptr;     // message index list
-    size_t cap_slow = 0;
-    uint32_t* rows = nullptr;     // the split check's per-message rows (SplitRows, 89 words per message)
-    size_t cap_rows = 0;
+    uint32_t* list = nullptr;     // slot work list (max_slots)
+    uint32_t* counts = nullptr;   // [0] slots to build (the table builder's)
     uint32_t* zr = nullptr;       // the table builder's z ratios (k_fb_runs: HD_FB_RUN x 9 words per thread)
+    // Per-call scratch, HD_FB_NSCRATCH sets used round robin, so that verify
+    // calls issued on different streams can run concurrently on the device:
+    // the next call's one-message-per-lane kernels fill the SIMDs that this
+    // call's inversion kernels (n / K lanes), the last partial round of its
+    // k_fast_sums and its fallback recovery leave idle.
+    struct Scratch {
+        uint32_t* rows = nullptr;     // the split check's per-message rows (SplitRows, 62 words per message)
+        size_t cap_rows = 0;
+        uint32_t* slow = nullptr;     // message index list for the full recovery
+        size_t cap_slow = 0;
+        uint32_t* count = nullptr;    // its length (device word)
+        hipEvent_t done = nullptr;    // recorded after the last call that used this set
+        hipStream_t stream = nullptr; // that call's stream
+        bool used = false;
+    };
+    static constexpr int NSCRATCH = 3;
+    Scratch sc[NSCRATCH];
+    int next = 0;                 // the set the next call takes
+    int last_set = -1;            // the set of the last call (hd_ctx_fastpath_stats)
     // Mapped slots whose key is not READY, in pinned host memory the device
     // also writes (k_fb_ready subtracts what it finished): 0 means nothing
     // can be learned any more, so a verify call launches no table-build
@@ -67,13 +87,17 @@ struct FbWork {
     // or the key format changes; UINT32_MAX = unknown.
     uint32_t* nr_host = nullptr;
     uint32_t* nr_dev = nullptr;
-    // The scratch above (rows, slow, counts) is per context: a verify call
-    // on another stream than the previous one first waits for that call's
-    // end, so calls of one context never overlap on the device whatever
-    // streams the caller uses (hd_verify_batch_device is asynchronous).
-    hipEvent_t done = nullptr;
+    // Ordering between calls (hd_fb_verify): a call waits (on the device) for
+    // the last call that used its scratch set.  While keys can still be
+    // learned (nr_host != 0), or on the first call after the last key became
+    // READY, a call also waits for the previous call, whatever its stream:
+    // learning writes the shared tables, states and builder scratch.  In the
+    // steady state (every mapped key READY, nothing written but per-call
+    // scratch and the caller's outputs) calls on different streams overlap.
+    hipEvent_t done = nullptr;    // recorded after every call
     hipStream_t last = nullptr;
     bool any = false;
+    bool steady = false;          // the previous call ran with nothing to learn
     // hd_ctx_profile: event pairs around whole calls and around k_fast_sums
     bool prof = false;
     std::vector<hipEvent_t> ev_call, ev_sums;
@@ -118,7 +142,7 @@ struct FastSrc {
 // kind for the pair).
 template <int WAVES>
 __global__ __launch_bounds__(256, WAVES) void k_verify_fast(DevBatch b, const uint8_t* __restrict__ digest_in,
-                                                     const gp* __restrict__ gtab, const gp* __restrict__ tab, const uint32_t* __restrict__ state,
+                                                     const gp* __restrict__ gtab, const gp* const* __restrict__ tabs, const uint32_t* __restrict__ state,
                                                      const int32_t* __restrict__ adm_slot,
                                                      const uint32_t* __restrict__ adm, const int32_t* __restrict__ adm_perm,
                                                      uint32_t n_adm, int adm_steps, uint8_t* __restrict__ verdict,
@@ -166,8 +190,8 @@ __global__ __launch_bounds__(256, WAVES) void k_verify_fast(DevBatch b, const ui
     }
     uint8_t v[2];
     __shared__ FastPark park[256];
-    verify_fast2(v, in, GpTab{gtab}, GpTab{tab + (size_t)(slot[0] > 0 ? slot[0] : 0) * HD_FB_TAB},
-                 GpTab{tab + (size_t)(slot[1] > 0 ? slot[1] : 0) * HD_FB_TAB}, &park[threadIdx.x]);
+    verify_fast2(v, in, GpTab{gtab}, GpTab{slot[0] > 0 ? tabs[slot[0]] : gtab},
+                 GpTab{slot[1] > 0 ? tabs[slot[1]] : gtab}, &park[threadIdx.x]);
     bool to_slow[2];
     HD_UNROLL for (int k = 0; k < 2; k++) {
         const uint32_t i = 2 * t + k;
@@ -445,7 +469,7 @@ __global__ __launch_bounds__(256) void k_fast_digits(uint32_t n, SplitRows rows)
 // (no k_fast_digits pass, no digit rows in HBM); else read from the rows.
 template <int WAVES, int WP, int PF, bool DL>
 __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* __restrict__ gtab,
-                                                          const gp* __restrict__ tab, SplitRows rows) {
+                                                          const gp* const* __restrict__ tabs, SplitRows rows) {
     constexpr int NG = FbL<HD_FB_WG>::NWIN, NT = NG + FbL<WP>::NWIN;
     static_assert(PF == 1 || PF == 2, "prefetch depth");
     __shared__ uint32_t sdig[DL ? NT * 256 : 1];
@@ -453,7 +477,7 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
     if (i >= n) return;
     const uint32_t a = rows.aux[i];
     if ((a & 0xFFu) != HD_FAST_LIVE) return;
-    const gp* __restrict__ ptab = tab + (size_t)(a >> 8) * FbL<WP>::TAB;
+    const gp* __restrict__ ptab = tabs[a >> 8];
     // a lane reads back only its own column: no barrier
     const size_t dstride = DL ? 256 : n;
     const uint32_t* dp = DL ? sdig + threadIdx.x : rows.dig + i;
@@ -693,11 +717,12 @@ __global__ __launch_bounds__(256) void k_fb_bases(const uint32_t* __restrict__ l
 // is B itself, written directly), so (d0 + k) B = +-B cannot occur.
 #define HD_FB_RUN 32
 #define HD_FB_SEG 512
+#define HD_FB_CHUNK 8   // slots per table allocation (fb_grow_slots)
 template <int W>
 __global__ __launch_bounds__(256) void k_fb_runs(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
-                                                 const ge* __restrict__ base, gp* __restrict__ tab,
+                                                 const ge* __restrict__ base, gp* const* __restrict__ tabs,
                                                  uint32_t* __restrict__ zr_scratch) {
-    constexpr uint32_t N = FbL<W>::N, NW = FbL<W>::NWIN, TAB = FbL<W>::TAB;
+    constexpr uint32_t N = FbL<W>::N, NW = FbL<W>::NWIN;
     constexpr uint32_t SW = N / HD_FB_SEG;                                  // segments per full window
     constexpr uint32_t SB = (NW - 1) * SW + FbL<W>::NTOP / HD_FB_SEG;      // segments per base
     static_assert(N % HD_FB_SEG == 0 && FbL<W>::NTOP % HD_FB_SEG == 0 && HD_FB_SEG % HD_FB_RUN == 0, "segments");
@@ -710,7 +735,7 @@ __global__ __launch_bounds__(256) void k_fb_runs(const uint32_t* __restrict__ li
         const uint32_t j = min(rem / SW, NW - 1);
         const uint32_t d0 = 1 + (rem - j * SW) * HD_FB_SEG;
         const ge B = base[(size_t)slot * NW + j];
-        gp* out = tab + (size_t)slot * TAB + (size_t)j * N + (d0 - 1);
+        gp* out = tabs[slot] + (size_t)j * N + (d0 - 1);
         gej a;
         uint32_t k0 = 0;   // first entry of the segment the walk produces
         if (d0 == 1) {
@@ -805,45 +830,54 @@ size_t fb_device_bytes(int device) {
 
 void fb_free_tables(hd_ctx* ctx) {
     FbWork* f = ctx->fb;
-    void* ptrs[] = {f->tab, f->base, f->pub, f->state, f->list};
+    for (gp* c : f->chunks) (void)hipFree(c);
+    f->chunks.clear();
+    void* ptrs[] = {f->tabs, f->base, f->pub, f->state, f->list};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
-    f->tab = nullptr;
+    f->tabs = nullptr;
     f->base = f->pub = nullptr;
     f->state = f->list = nullptr;
     f->nslots = 0;
     fb_account(ctx, 0, f->bytes);
 }
 
+// The per-slot arrays for max_slots slots (small: bases, keys, states, table
+// pointers), once per table width; no table memory yet.
+int fb_alloc_slots(hd_ctx* ctx) {
+    FbWork* f = ctx->fb;
+    const size_t m = f->max_slots, NWIN = (size_t)fb_nwin(f->wp);
+    FBCHK(hipMalloc(&f->tabs, sizeof(gp*) * m), "fb table pointers");
+    FBCHK(hipMalloc(&f->base, sizeof(ge) * NWIN * m), "fb bases");
+    FBCHK(hipMalloc(&f->pub, sizeof(ge) * m), "fb keys");
+    FBCHK(hipMalloc(&f->state, 4 * m), "fb state");
+    FBCHK(hipMalloc(&f->list, 4 * m), "fb list");
+    FBCHK(hipMemsetAsync(f->state, 0, 4 * m, ctx->stream), "fb state clear");
+    FBCHK(hipMemsetAsync(f->tabs, 0, sizeof(gp*) * m, ctx->stream), "fb table pointers clear");
+    FBCHK(hipStreamSynchronize(ctx->stream), "fb slot arrays");
+    fb_account(ctx, (sizeof(gp*) + sizeof(ge) * (NWIN + 1) + 8) * m, 0);
+    return HD_OK;
+}
+
+// Table chunks until `want` slots have tables (chunks never move: the slots
+// already built keep their tables).
 int fb_grow_slots(hd_ctx* ctx, uint32_t want) {
     FbWork* f = ctx->fb;
-    if (want <= f->nslots) return HD_OK;
-    const uint32_t n = std::min(f->max_slots, std::max(want, 2 * f->nslots));
-    const size_t TAB = fb_tab_entries(f->wp), NWIN = (size_t)fb_nwin(f->wp);
-    gp* tab = nullptr;
-    ge *base = nullptr, *pub = nullptr;
-    uint32_t *state = nullptr, *list = nullptr;
-    FBCHK(hipMalloc(&tab, sizeof(gp) * TAB * (size_t)n), "fb tables");
-    FBCHK(hipMalloc(&base, sizeof(ge) * NWIN * (size_t)n), "fb bases");
-    FBCHK(hipMalloc(&pub, sizeof(ge) * (size_t)n), "fb keys");
-    FBCHK(hipMalloc(&state, 4 * (size_t)n), "fb state");
-    FBCHK(hipMalloc(&list, 4 * (size_t)n), "fb list");
-    FBCHK(hipMemset(state, 0, 4 * (size_t)n), "fb state clear");
-    if (f->nslots) {
-        const size_t k = f->nslots;
-        FBCHK(hipMemcpy(tab, f->tab, sizeof(gp) * TAB * k, hipMemcpyDeviceToDevice), "fb copy");
-        FBCHK(hipMemcpy(base, f->base, sizeof(ge) * NWIN * k, hipMemcpyDeviceToDevice), "fb copy");
-        FBCHK(hipMemcpy(pub, f->pub, sizeof(ge) * k, hipMemcpyDeviceToDevice), "fb copy");
-        FBCHK(hipMemcpy(state, f->state, 4 * k, hipMemcpyDeviceToDevice), "fb copy");
+    want = std::min(want, f->max_slots);
+    const size_t TAB = fb_tab_entries(f->wp);
+    while (f->nslots < want) {
+        const uint32_t k = std::min<uint32_t>(HD_FB_CHUNK, f->max_slots - f->nslots);
+        gp* c = nullptr;
+        FBCHK(hipMalloc(&c, sizeof(gp) * TAB * k), "fb table chunk");
+        f->chunks.push_back(c);
+        std::vector<gp*> ptr(k);
+        for (uint32_t j = 0; j < k; j++) ptr[j] = c + TAB * j;
+        FBCHK(hipMemcpyAsync(f->tabs + f->nslots, ptr.data(), sizeof(gp*) * k, hipMemcpyHostToDevice, ctx->stream),
+              "fb table pointers");
+        FBCHK(hipStreamSynchronize(ctx->stream), "fb table pointers");
+        f->nslots += k;
+        fb_account(ctx, sizeof(gp) * TAB * k, 0);
     }
-    fb_free_tables(ctx);
-    f->tab = tab;
-    f->base = base;
-    f->pub = pub;
-    f->state = state;
-    f->list = list;
-    f->nslots = n;
-    fb_account(ctx, (size_t)(fb_slot_bytes(f->wp) * n), 0);
     return HD_OK;
 }
 
@@ -860,10 +894,10 @@ int fb_learn(hd_ctx* ctx, hipStream_t s) {
     k_fb_list<<<1, 256, 0, s>>>(f->nslots, f->state, f->list, f->counts);
     if (f->wp == HD_FB_WW) {
         k_fb_bases<HD_FB_WW><<<g, 256, 0, s>>>(f->list, f->counts, f->pub, f->base);
-        k_fb_runs<HD_FB_WW><<<fb_run_blocks(ctx), 256, 0, s>>>(f->list, f->counts, f->base, f->tab, f->zr);
+        k_fb_runs<HD_FB_WW><<<fb_run_blocks(ctx), 256, 0, s>>>(f->list, f->counts, f->base, f->tabs, f->zr);
     } else {
         k_fb_bases<HD_FB_W><<<g, 256, 0, s>>>(f->list, f->counts, f->pub, f->base);
-        k_fb_runs<HD_FB_W><<<fb_run_blocks(ctx), 256, 0, s>>>(f->list, f->counts, f->base, f->tab, f->zr);
+        k_fb_runs<HD_FB_W><<<fb_run_blocks(ctx), 256, 0, s>>>(f->list, f->counts, f->base, f->tabs, f->zr);
     }
     k_fb_ready<<<1, 256, 0, s>>>(f->list, f->counts, f->state, f->nr_dev);
     FBCHK(hipGetLastError(), "fb table kernels");
@@ -892,22 +926,27 @@ static int fb_g_table(hd_ctx* ctx, const gp** out) {
     fe_from_be(g.x, GX);
     fe_from_be(g.y, GY);
     gp* tab = nullptr;
+    gp** tp = nullptr;       // the builder's table pointer array: {tab}
     ge *base = nullptr, *pub = nullptr;
     uint32_t* cl = nullptr;  // [0] = list {0}, [1] = count 1
     FBCHK(hipMalloc(&tab, sizeof(gp) * (size_t)FbL<HD_FB_WG>::TAB), "G table");
+    FBCHK(hipMalloc(&tp, sizeof(gp*)), "G table pointer");
     FBCHK(hipMalloc(&base, sizeof(ge) * FbL<HD_FB_WG>::NWIN), "G bases");
     FBCHK(hipMalloc(&pub, sizeof(ge)), "G point");
     FBCHK(hipMalloc(&cl, 8), "G list");
     const uint32_t hl[2] = {0u, 1u};
-    FBCHK(hipMemcpy(pub, &g, sizeof(ge), hipMemcpyHostToDevice), "G point");
-    FBCHK(hipMemcpy(cl, hl, 8, hipMemcpyHostToDevice), "G list");
-    k_fb_bases<HD_FB_WG><<<1, 64, 0, ctx->stream>>>(cl, cl + 1, pub, base);
-    k_fb_runs<HD_FB_WG><<<fb_run_blocks(ctx), 256, 0, ctx->stream>>>(cl, cl + 1, base, tab, ctx->fb->zr);
+    hipStream_t s = ctx->stream;
+    FBCHK(hipMemcpyAsync(pub, &g, sizeof(ge), hipMemcpyHostToDevice, s), "G point");
+    FBCHK(hipMemcpyAsync(cl, hl, 8, hipMemcpyHostToDevice, s), "G list");
+    FBCHK(hipMemcpyAsync(tp, &tab, sizeof(gp*), hipMemcpyHostToDevice, s), "G table pointer");
+    k_fb_bases<HD_FB_WG><<<1, 64, 0, s>>>(cl, cl + 1, pub, base);
+    k_fb_runs<HD_FB_WG><<<fb_run_blocks(ctx), 256, 0, s>>>(cl, cl + 1, base, tp, ctx->fb->zr);
     FBCHK(hipGetLastError(), "G table kernels");
-    FBCHK(hipStreamSynchronize(ctx->stream), "G table build");
+    FBCHK(hipStreamSynchronize(s), "G table build");
     (void)hipFree(base);
     (void)hipFree(pub);
     (void)hipFree(cl);
+    (void)hipFree(tp);
     g_fb_g_tables[ctx->device] = tab;
     *out = tab;
     return HD_OK;
@@ -926,7 +965,7 @@ int hd_fb_init(hd_ctx* ctx) {
     FBCHK(hipHostMalloc((void**)&f->nr_host, 4, hipHostMallocMapped | hipHostMallocCoherent), "fb ready count");
     *f->nr_host = 0xFFFFFFFFu;
     FBCHK(hipHostGetDevicePointer((void**)&f->nr_dev, f->nr_host, 0), "fb ready count map");
-    int rc = fb_grow_slots(ctx, 1);
+    int rc = fb_alloc_slots(ctx);
     if (rc) return rc;
     return fb_g_table(ctx, &f->gtab);
 }
@@ -943,7 +982,13 @@ void hd_fb_release(hd_ctx* ctx) {
     if (f->done) (void)hipEventDestroy(f->done);
     for (hipEvent_t e : f->ev_call) (void)hipEventDestroy(e);
     for (hipEvent_t e : f->ev_sums) (void)hipEventDestroy(e);
-    void* ptrs[] = {f->counts, f->slow, f->adm_slot, f->rows, f->zr};
+    for (auto& sc : f->sc) {
+        if (sc.done) (void)hipEventDestroy(sc.done);
+        void* sp[] = {sc.rows, sc.slow, sc.count};
+        for (void* p : sp)
+            if (p) (void)hipFree(p);
+    }
+    void* ptrs[] = {f->counts, f->adm_slot, f->zr};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (f->nr_host) (void)hipHostFree(f->nr_host);
@@ -999,7 +1044,9 @@ static int fb_count_not_ready(hd_ctx* ctx) {
     uint32_t nr = 0;
     if (!f->slot_of.empty()) {
         std::vector<uint32_t> st(f->nslots);
-        FBCHK(hipMemcpy(st.data(), f->state, 4 * (size_t)f->nslots, hipMemcpyDeviceToHost), "fb state read");
+        FBCHK(hipMemcpyAsync(st.data(), f->state, 4 * (size_t)f->nslots, hipMemcpyDeviceToHost, ctx->stream),
+              "fb state read");
+        FBCHK(hipStreamSynchronize(ctx->stream), "fb state read");
         for (const auto& kv : f->slot_of) nr += st[kv.second] != HD_FB_READY ? 1u : 0u;
     }
     *(volatile uint32_t*)f->nr_host = nr;
@@ -1008,19 +1055,22 @@ static int fb_count_not_ready(hd_ctx* ctx) {
 
 int hd_fb_map_signatories(hd_ctx* ctx, const uint8_t* sorted, uint32_t m) {
     FbWork* f = ctx->fb;
-    // no verify call of this context may still learn into a slot reassigned here
-    FBCHK(hipDeviceSynchronize(), "fb map sync");
+    // no verify call of this context may still learn into a slot reassigned
+    // here (hd_set_signatories quiesced the context already)
+    int rq = hd_ctx_quiesce(ctx);
+    if (rq) return rq;
     *(volatile uint32_t*)f->nr_host = 0xFFFFFFFFu;
     const int wp = fb_pick_width(ctx, m);
     if (wp != f->wp) {
         // another table width: every key is learned again (full recovery)
-        FBCHK(hipDeviceSynchronize(), "fb width change sync");
         fb_free_tables(ctx);
         f->slot_of.clear();
         f->free_slots.clear();
         f->used = 1;
         f->wp = wp;
         f->max_slots = (uint32_t)std::max(1.0, std::min(1e6, f->budget / fb_slot_bytes(wp)));
+        int ra = fb_alloc_slots(ctx);
+        if (ra) return ra;
     }
     std::unordered_map<std::string, uint32_t> keep;
     std::vector<int32_t> adm_slot(std::max(m, 1u), -1);
@@ -1057,19 +1107,21 @@ int hd_fb_map_signatories(hd_ctx* ctx, const uint8_t* sorted, uint32_t m) {
     }
     int rc = fb_grow_slots(ctx, f->used);
     if (rc) return rc;
-    for (uint32_t slot : fresh) FBCHK(hipMemset(f->state + slot, 0, 4), "fb slot reset");
+    hipStream_t s = ctx->stream;
+    for (uint32_t slot : fresh) FBCHK(hipMemsetAsync(f->state + slot, 0, 4, s), "fb slot reset");
     rc = hd_dev_grow(ctx, (void**)&f->adm_slot, &f->cap_adm_slot, 4 * adm_slot.size());
     if (rc) return rc;
-    FBCHK(hipMemcpy(f->adm_slot, adm_slot.data(), 4 * adm_slot.size(), hipMemcpyHostToDevice), "fb adm_slot");
-    FBCHK(hipDeviceSynchronize(), "fb map done");
+    FBCHK(hipMemcpyAsync(f->adm_slot, adm_slot.data(), 4 * adm_slot.size(), hipMemcpyHostToDevice, s), "fb adm_slot");
+    FBCHK(hipStreamSynchronize(s), "fb map");
     return fb_count_not_ready(ctx);
 }
 
 int hd_fb_clear_keys(hd_ctx* ctx) {
     FbWork* f = ctx->fb;
-    FBCHK(hipDeviceSynchronize(), "fb clear sync");
-    if (f->nslots > 1) FBCHK(hipMemset(f->state + 1, 0, 4 * (size_t)(f->nslots - 1)), "fb clear");
-    FBCHK(hipDeviceSynchronize(), "fb clear done");
+    int rq = hd_ctx_quiesce(ctx);
+    if (rq) return rq;
+    if (f->nslots > 1) FBCHK(hipMemsetAsync(f->state + 1, 0, 4 * (size_t)(f->nslots - 1), ctx->stream), "fb clear");
+    FBCHK(hipStreamSynchronize(ctx->stream), "fb clear");
     return fb_count_not_ready(ctx);
 }
 
@@ -1096,7 +1148,7 @@ static hipEvent_t* fb_prof_pair(std::vector<hipEvent_t>& ev, size_t& used, bool 
 // (HD_SUM_PF: 1, the default, or 2 windows ahead) and where the window digits
 // come from (sums_digits_lds)
 template <int WP, bool DL>
-static void launch_sums(uint32_t blocks, hipStream_t s, uint32_t n, const gp* gtab, const gp* tab,
+static void launch_sums(uint32_t blocks, hipStream_t s, uint32_t n, const gp* gtab, const gp* const* tab,
                         const SplitRows& rows) {
     static const int w = getenv("HD_SUM_WAVES") ? atoi(getenv("HD_SUM_WAVES")) : 3;
     static const int pf = getenv("HD_SUM_PF") ? atoi(getenv("HD_SUM_PF")) : 1;
@@ -1118,7 +1170,7 @@ static bool sums_digits_lds() {
 template <int K, int WP>
 static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict,
                          uint8_t* d_rec32, int32_t* d_signer, uint32_t* d_bitmap, const SplitRows& rows,
-                         hipStream_t s) {
+                         const FbWork::Scratch& sc, hipStream_t s) {
     FbWork* f = ctx->fb;
     const uint32_t n = b.n;
     // lanes of the K-per-lane kernels, a multiple of 64 (k_fast_final's bitmap words)
@@ -1132,72 +1184,101 @@ static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest
     if (!dl) k_fast_digits<WP><<<nb, 256, 0, s>>>(n, rows);
     hipEvent_t* pe = fb_prof_pair(f->ev_sums, f->n_sums, f->prof);
     if (pe) (void)hipEventRecord(pe[0], s);
-    if (dl) launch_sums<WP, true>(nb, s, n, f->gtab, f->tab, rows);
-    else launch_sums<WP, false>(nb, s, n, f->gtab, f->tab, rows);
+    if (dl) launch_sums<WP, true>(nb, s, n, f->gtab, f->tabs, rows);
+    else launch_sums<WP, false>(nb, s, n, f->gtab, f->tabs, rows);
     if (pe) (void)hipEventRecord(pe[1], s);
     k_fast_zinv<K><<<tb, 256, 0, s>>>(n, T, rows);
     // whole blocks of 256: every wavefront's 64 messages are one bitmap word pair
-    k_fast_cmp<<<nb, 256, 0, s>>>(b, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer, f->slow, f->counts + 1,
+    k_fast_cmp<<<nb, 256, 0, s>>>(b, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer, sc.slow, sc.count,
                                   d_bitmap);
 }
 
 static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict,
-                          uint8_t* d_rec32, int32_t* d_signer, uint32_t* d_bitmap, hipStream_t s);
+                          uint8_t* d_rec32, int32_t* d_signer, uint32_t* d_bitmap, FbWork::Scratch& sc,
+                          hipStream_t s);
 
 int hd_fb_verify(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict, uint8_t* d_rec32,
                  int32_t* d_signer, uint32_t* d_bitmap, hipStream_t s) {
     FbWork* f = ctx->fb;
     if (!f->done) FBCHK(hipEventCreateWithFlags(&f->done, hipEventDisableTiming), "fb event");
-    if (f->any && f->last != s) FBCHK(hipStreamWaitEvent(s, f->done, 0), "fb stream order");
+    const int j = f->next;
+    f->next = (j + 1) % FbWork::NSCRATCH;
+    FbWork::Scratch& sc = f->sc[j];
+    if (!sc.done) FBCHK(hipEventCreateWithFlags(&sc.done, hipEventDisableTiming), "fb scratch event");
+    if (!sc.count) FBCHK(hipMalloc(&sc.count, 4), "fb scratch count");
+    // see FbWork: in the steady state only this set's previous user orders
+    // this call; otherwise the previous call does, on whatever stream
+    const bool steady = f->nr_host && *(volatile uint32_t*)f->nr_host == 0;
+    if (sc.used && sc.stream != s) FBCHK(hipStreamWaitEvent(s, sc.done, 0), "fb scratch order");
+    if (f->any && f->last != s && !(steady && f->steady)) FBCHK(hipStreamWaitEvent(s, f->done, 0), "fb stream order");
     hipEvent_t* pe = fb_prof_pair(f->ev_call, f->n_call, f->prof);
     if (pe) (void)hipEventRecord(pe[0], s);
-    const int rc = fb_verify_impl(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, s);
+    const int rc = fb_verify_impl(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, sc, s);
     if (pe) (void)hipEventRecord(pe[1], s);
+    FBCHK(hipEventRecord(sc.done, s), "fb scratch record");
     FBCHK(hipEventRecord(f->done, s), "fb event record");
+    sc.used = true;
+    sc.stream = s;
+    f->last_set = j;
     f->last = s;
     f->any = true;
+    f->steady = steady;
     return rc;
 }
 
-static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict,
-                          uint8_t* d_rec32, int32_t* d_signer, uint32_t* d_bitmap, hipStream_t s) {
+// Every verify call of this context has finished (the host waits on the
+// call events; other contexts and streams are not waited for).
+int hd_fb_quiesce(hd_ctx* ctx) {
     FbWork* f = ctx->fb;
-    int rc = hd_dev_grow(ctx, (void**)&f->slow, &f->cap_slow, 4 * (size_t)b.n);
+    if (!f) return HD_OK;
+    for (auto& sc : f->sc)
+        if (sc.used) FBCHK(hipEventSynchronize(sc.done), "fb quiesce");
+    if (f->any) FBCHK(hipEventSynchronize(f->done), "fb quiesce");
+    return HD_OK;
+}
+
+static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict,
+                          uint8_t* d_rec32, int32_t* d_signer, uint32_t* d_bitmap, FbWork::Scratch& sc,
+                          hipStream_t s) {
+    FbWork* f = ctx->fb;
+    int rc = hd_dev_grow(ctx, (void**)&sc.slow, &sc.cap_slow, 4 * (size_t)b.n);
     if (rc) return rc;
     const uint32_t blocks = (b.n + 255) / 256;
     const uint32_t fast_blocks = ((b.n + 1) / 2 + 255) / 256;   // two messages per lane
-    FBCHK(hipMemsetAsync(f->counts + 1, 0, 4, s), "fb count reset");
+    FBCHK(hipMemsetAsync(sc.count, 0, 4, s), "fb count reset");
     if (ctx->n_adm > 0 && f->adm_slot && split_k_for(b.n) > 0) {
         // 62 words per message; the digit rows (the narrow width has more
         // windows) only for the HD_SUM_DIGITS=rows A/B form
         const size_t row_words = 62 + (sums_digits_lds() ? 0 : FbL<HD_FB_WG>::NWIN + FbL<HD_FB_W>::NWIN);
-        rc = hd_dev_grow(ctx, (void**)&f->rows, &f->cap_rows, 4 * row_words * (size_t)b.n);
+        rc = hd_dev_grow(ctx, (void**)&sc.rows, &sc.cap_rows, 4 * row_words * (size_t)b.n);
         if (rc) return rc;
         const uint32_t n = b.n;
         SplitRows rows;
-        rows.aux = f->rows;
-        rows.idx = (int32_t*)(f->rows + (size_t)n);
-        rows.u1 = f->rows + 2 * (size_t)n;
-        rows.u2 = f->rows + 10 * (size_t)n;
-        rows.s = f->rows + 18 * (size_t)n;
-        rows.pre = f->rows + 26 * (size_t)n;
-        rows.xyz = f->rows + 35 * (size_t)n;
-        rows.dig = sums_digits_lds() ? nullptr : f->rows + 62 * (size_t)n;
+        rows.aux = sc.rows;
+        rows.idx = (int32_t*)(sc.rows + (size_t)n);
+        rows.u1 = sc.rows + 2 * (size_t)n;
+        rows.u2 = sc.rows + 10 * (size_t)n;
+        rows.s = sc.rows + 18 * (size_t)n;
+        rows.pre = sc.rows + 26 * (size_t)n;
+        rows.xyz = sc.rows + 35 * (size_t)n;
+        rows.dig = sums_digits_lds() ? nullptr : sc.rows + 62 * (size_t)n;
         const int k = split_k_for(n);
         f->last_k = k;
+#define HD_SPLIT(K, WP) launch_split<K, WP>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, sc, s)
         if (f->wp == HD_FB_WW) {
-            if (k == 16) launch_split<16, HD_FB_WW>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, s);
-            else if (k == 4) launch_split<4, HD_FB_WW>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, s);
-            else launch_split<8, HD_FB_WW>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, s);
+            if (k == 16) HD_SPLIT(16, HD_FB_WW);
+            else if (k == 4) HD_SPLIT(4, HD_FB_WW);
+            else HD_SPLIT(8, HD_FB_WW);
         } else {
-            if (k == 16) launch_split<16, HD_FB_W>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, s);
-            else if (k == 4) launch_split<4, HD_FB_W>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, s);
-            else launch_split<8, HD_FB_W>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, s);
+            if (k == 16) HD_SPLIT(16, HD_FB_W);
+            else if (k == 4) HD_SPLIT(4, HD_FB_W);
+            else HD_SPLIT(8, HD_FB_W);
         }
+#undef HD_SPLIT
         FBCHK(hipGetLastError(), "split check launch");
-        // k_fast_final wrote the valid bitmap; the slow path sets the bits of
+        // k_fast_cmp wrote the valid bitmap; the slow path sets the bits of
         // its VALID messages
-        const SlowCtl ctl{f->slow, f->counts + 1, f->adm_slot, f->state, f->pub, d_bitmap};
+        const SlowCtl ctl{sc.slow, sc.count, f->adm_slot, f->state, f->pub, d_bitmap};
         const uint32_t slow_blocks = std::min(blocks, (uint32_t)std::max(ctx->n_cu, 1) * 4u);
         rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl, slow_blocks, s);
         if (rc) return rc;
@@ -1206,9 +1287,9 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
     if (ctx->n_adm > 0 && f->adm_slot) {
         static const int fw = getenv("HD_FAST_WAVES") ? atoi(getenv("HD_FAST_WAVES")) : 2;
 #define HD_LAUNCH_FAST(W)                                                                                        \
-    k_verify_fast<W><<<fast_blocks, 256, 0, s>>>(b, d_digest, f->gtab, f->tab, f->state, f->adm_slot, ctx->d_adm, ctx->d_adm_perm, \
-                                            ctx->n_adm, ctx->adm_steps, d_verdict, d_rec32, d_signer, f->slow,       \
-                                            f->counts + 1)
+    k_verify_fast<W><<<fast_blocks, 256, 0, s>>>(b, d_digest, f->gtab, f->tabs, f->state, f->adm_slot, ctx->d_adm, ctx->d_adm_perm, \
+                                            ctx->n_adm, ctx->adm_steps, d_verdict, d_rec32, d_signer, sc.slow,       \
+                                            sc.count)
         if (fw == 2) HD_LAUNCH_FAST(2);
         else HD_LAUNCH_FAST(3);   // (4 and 5 waves spill heavily; not offered)
 #undef HD_LAUNCH_FAST
@@ -1216,7 +1297,7 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         // the fallback list is usually short (its length is only known on the
         // device): a grid of 4 blocks per CU walks it, instead of one block
         // per 256 messages that would mostly start and exit
-        const SlowCtl ctl{f->slow, f->counts + 1, f->adm_slot, f->state, f->pub, nullptr};
+        const SlowCtl ctl{sc.slow, sc.count, f->adm_slot, f->state, f->pub, nullptr};
         const uint32_t slow_blocks = std::min(blocks, (uint32_t)std::max(ctx->n_cu, 1) * 4u);
         rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl, slow_blocks, s);
         if (rc) return rc;
@@ -1307,13 +1388,15 @@ int hd_ctx_fastpath_stats(hd_ctx* ctx, uint32_t* known_keys, uint32_t* last_fall
     if (!ctx->fb) return HD_OK;
     (void)hipSetDevice(ctx->device);
     FbWork* f = ctx->fb;
-    FBCHK(hipDeviceSynchronize(), "fastpath stats sync");
+    int rq = hd_ctx_quiesce(ctx);
+    if (rq) return rq;
     if (known_keys && f->nslots > 1) {
         std::vector<uint32_t> st(f->nslots);
         FBCHK(hipMemcpy(st.data(), f->state, 4 * (size_t)f->nslots, hipMemcpyDeviceToHost), "state read");
         for (uint32_t k = 1; k < f->nslots; k++) *known_keys += st[k] == HD_FB_READY;
     }
-    if (last_fallback) FBCHK(hipMemcpy(last_fallback, f->counts + 1, 4, hipMemcpyDeviceToHost), "fallback read");
+    if (last_fallback && f->last_set >= 0)
+        FBCHK(hipMemcpy(last_fallback, f->sc[f->last_set].count, 4, hipMemcpyDeviceToHost), "fallback read");
     return HD_OK;
 }
 

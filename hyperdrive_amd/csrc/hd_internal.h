@@ -47,8 +47,15 @@ struct hd_ctx {
     TallyWork* tally = nullptr;
     FbWork* fb = nullptr;
     bool fastpath = true;   // known-key fast path (HD_VERIFY_FASTPATH=0 disables)
+    hipEvent_t ev_slow = nullptr;   // after the last full-recovery-only verify call (fast path off)
     std::string last_error;
 };
+
+// Wait (host) for every kernel this context queued: its own stream and the
+// verify calls on caller streams.  Replaces device-wide synchronisation, so a
+// set change does not stall other contexts or streams of the device.
+int hd_ctx_quiesce(hd_ctx* ctx);
+int hd_fb_quiesce(hd_ctx* ctx);   // the known-key path's calls (hd_fastverify.hip)
 
 int hd_ctx_fail(hd_ctx* ctx, hipError_t e, const char* what);
 int hd_dev_grow(hd_ctx* ctx, void** p, size_t* cap, size_t need);

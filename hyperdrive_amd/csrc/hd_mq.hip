@@ -737,7 +737,11 @@ int hd_mq_consume(hd_mq* q, int64_t h, const uint8_t* allowed32, uint32_t n_allo
     rc = select_idx(q, removed, M, sel2, &nr, s, 0, false);   // counted by the next select's sync
     if (rc) return rc;
     rc = select_idx(q, deliver, M, sel, &c, s, 1);
-    if (rc) return rc;
+    if (rc) {
+        // the first select's count download into nr may still be in flight
+        (void)hipStreamSynchronize(s);
+        return rc;
+    }
     *n_out = c;
     if (c > cap) return HD_ECAP;
     if (n_removed) *n_removed = nr;

@@ -45,14 +45,14 @@ using namespace hd;
 static const uint32_t kEmpty = 0xFFFFFFFFu;
 
 struct TallyWork {
-    DevBuf b[12];
+    DevBuf b[13];
     void* host = nullptr;   // pinned download stage (hipHostMalloc)
     size_t host_cap = 0;
 };
 // T_G: the hash tables; T_C: the dense log cells; T_D: a partition's candidates;
 // T_SEL: the output stage;
 // T_SORTK / T_SORTV: order marks / compacted order
-enum TSlot { T_G, T_D, T_C, T_GSLOT, T_DSLOT, T_NSEL, T_SEL, T_SORTK, T_SORTV, T_TMP, T_DUP };
+enum TSlot { T_G, T_D, T_C, T_GSLOT, T_DSLOT, T_NSEL, T_SEL, T_SORTK, T_SORTV, T_TMP, T_DUP, T_ROUTE };
 
 // table layouts (structure of arrays inside one allocation, capacity cap)
 struct GTab {   // (h, r)
@@ -86,11 +86,14 @@ struct Part {
     uint32_t part, nparts;
 };
 
+// verdict and bitmap both NULL: every Prevote / Precommit is a candidate (a
+// batch of routed candidates, hd_unroute_device)
 __device__ __forceinline__ bool candidate(const DevBatch& b, const uint8_t* verdict, const uint32_t* bitmap,
                                           uint32_t i, Part p) {
     const uint8_t t = b.type[i];
     if (t != T_PREVOTE && t != T_PRECOMMIT) return false;
-    if (!(verdict ? verdict[i] == V_VALID : ((bitmap[i >> 5] >> (i & 31)) & 1u))) return false;
+    if (verdict && verdict[i] != V_VALID) return false;
+    if (bitmap && !((bitmap[i >> 5] >> (i & 31)) & 1u)) return false;
     return p.nparts <= 1 || part_of(hash_hr(b.height[i], b.round[i]), p.nparts) == p.part;
 }
 
@@ -427,14 +430,14 @@ __global__ __launch_bounds__(256) void k_tally_chunk_write(uint32_t n, const uin
 }
 
 __global__ void k_tally_emit_hr(uint32_t n_hr, const uint32_t* __restrict__ slot, const uint32_t* __restrict__ cand,
-                                GTab G, const int64_t* __restrict__ h,
+                                const uint32_t* __restrict__ gidx, GTab G, const int64_t* __restrict__ h,
                                 const int64_t* __restrict__ r, int64_t* __restrict__ oh, int64_t* __restrict__ orr,
                                 uint32_t* __restrict__ oprev, uint32_t* __restrict__ oprec, uint32_t* __restrict__ oany,
                                 uint32_t* __restrict__ orep) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_hr) return;
     const uint32_t s = slot[k], i = msg_of(cand, G.claim[s]);
-    orep[k] = i;
+    orep[k] = gidx ? gidx[i] : i;
     oh[k] = h[i];
     orr[k] = r[i];
     oprev[k] = G.nprev[s];
@@ -443,7 +446,7 @@ __global__ void k_tally_emit_hr(uint32_t n_hr, const uint32_t* __restrict__ slot
 }
 
 __global__ void k_tally_emit_counts(uint32_t n_c, const uint32_t* __restrict__ slot, const uint32_t* __restrict__ cand,
-                                    CTab C, const int64_t* __restrict__ h,
+                                    const uint32_t* __restrict__ gidx, CTab C, const int64_t* __restrict__ h,
                                     const int64_t* __restrict__ r, const uint8_t* __restrict__ type,
                                     int64_t* __restrict__ oh, int64_t* __restrict__ orr, uint8_t* __restrict__ ot,
                                     uint32_t* __restrict__ orep, uint32_t* __restrict__ on) {
@@ -453,8 +456,116 @@ __global__ void k_tally_emit_counts(uint32_t n_c, const uint32_t* __restrict__ s
     oh[k] = h[i];
     orr[k] = r[i];
     ot[k] = type[i];
-    orep[k] = i;
+    orep[k] = gidx ? gidx[i] : i;
     on[k] = C.n[s];
+}
+
+// ---------------------------------------------------------- routing (C4)
+// The multi-GPU tally without a replicated batch: each device turns the
+// candidates of ITS shard (VALID Prevotes / Precommits) into 64-byte route
+// rows, grouped by the rank that owns the candidate's round
+// (hd_tally_partition_of) and in index order inside a group; the groups
+// cross xGMI (one grouped send/recv or all-to-all); the owner rebuilds a
+// batch from the rows it received -- concatenated in source-rank order,
+// which is global index order, since shards are contiguous index ranges --
+// and tallies it (every row a candidate) with the reps mapped back to global
+// indices.  First-wins is per (height, round, type, signer), so the owner of
+// a round sees every candidate of its keys, in the order of the whole batch.
+struct RouteRow {          // 64 B
+    int64_t h, r;
+    uint4 value[2];        // the 32 value bytes as stored
+    uint32_t gidx;         // global batch index
+    uint32_t signer_type;  // admitted (sorted) index << 8 | type
+    uint32_t pad[2];
+};
+static_assert(sizeof(RouteRow) == 64, "route row");
+#define HD_ROUTE_MAX_PARTS 64u
+
+// per block and owner: the number of candidates (o-major: cnt[o * nb + blk])
+__global__ __launch_bounds__(256) void k_route_count(DevBatch b, const uint32_t* __restrict__ bitmap, uint32_t nparts,
+                                                     uint32_t* __restrict__ cnt) {
+    __shared__ uint32_t c[HD_ROUTE_MAX_PARTS];
+    if (threadIdx.x < nparts) c[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < b.n && candidate(b, nullptr, bitmap, i, Part{0, 1}))
+        atomicAdd(&c[part_of(hash_hr(b.height[i], b.round[i]), nparts)], 1u);
+    __syncthreads();
+    if (threadIdx.x < nparts) cnt[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = c[threadIdx.x];
+}
+
+// the rows: block blk's candidates of owner o start at off[o * nb + blk]
+// (the exclusive scan of k_route_count's counts), ranked inside the block by
+// wavefront ballots, so each owner's rows keep the batch order
+__global__ __launch_bounds__(256) void k_route_write(DevBatch b, const uint32_t* __restrict__ bitmap, uint32_t nparts,
+                                                     uint32_t base, const uint32_t* __restrict__ off,
+                                                     const uint32_t* __restrict__ adm, uint32_t n_adm, int adm_steps,
+                                                     int adm_in_lds, RouteRow* __restrict__ rows) {
+    extern __shared__ uint32_t sh_adm[];
+    __shared__ uint32_t wcnt[4][HD_ROUTE_MAX_PARTS];
+    if (adm_in_lds) adm_stage(sh_adm, adm, n_adm);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const bool c = i < b.n && candidate(b, nullptr, bitmap, i, Part{0, 1});
+    const uint32_t o = c ? part_of(hash_hr(b.height[i], b.round[i]), nparts) : 0xFFFFFFFFu;
+    uint32_t rank = 0;
+    for (uint32_t k = 0; k < nparts; k++) {
+        const unsigned long long bal = __ballot(o == k);
+        if (o == k) rank = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) wcnt[w][k] = (uint32_t)__popcll(bal);
+    }
+    __syncthreads();
+    if (!c) return;
+    uint32_t pos = off[(size_t)o * gridDim.x + blockIdx.x] + rank;
+    for (uint32_t v = 0; v < w; v++) pos += wcnt[v][o];
+    uint32_t from_be[8];
+    load_row32_be(from_be, b.from32, i);
+    const int32_t sg = adm_in_lds ? admitted_find(sh_adm, n_adm, adm_steps, from_be)
+                                  : admitted_find(adm, n_adm, adm_steps, from_be);
+    RouteRow row;
+    row.h = b.height[i];
+    row.r = b.round[i];
+    const uint4* vp = reinterpret_cast<const uint4*>(b.value32 + 32 * (size_t)i);
+    row.value[0] = vp[0];
+    row.value[1] = vp[1];
+    row.gidx = base + i;
+    // a VALID message's From is admitted (NOT_ADMITTED otherwise); a caller
+    // set changed since verification routes it as "not admitted" (0xFFFFFF)
+    row.signer_type = ((uint32_t)(sg >= 0 ? sg : 0xFFFFFF) << 8) | b.type[i];
+    row.pad[0] = row.pad[1] = 0;
+    rows[pos] = row;
+}
+
+// the owners' starts: starts[o] = off[o * nb], starts[nparts] = the total
+__global__ void k_route_starts(const uint32_t* __restrict__ off, const uint32_t* __restrict__ cnt, uint32_t nparts,
+                               uint32_t nb, uint32_t* __restrict__ starts) {
+    const uint32_t o = threadIdx.x;
+    if (o < nparts) starts[o] = off[(size_t)o * nb];
+    if (o == 0) {
+        const size_t last = (size_t)nparts * nb - 1;
+        starts[nparts] = off[last] + cnt[last];
+    }
+}
+
+// received rows -> a batch (From rebuilt from the admitted set) + gidx
+__global__ __launch_bounds__(256) void k_unroute(const RouteRow* __restrict__ rows, uint32_t n,
+                                                 const uint32_t* __restrict__ adm, uint32_t n_adm, hd_batch_out o,
+                                                 uint32_t* __restrict__ gidx) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const RouteRow row = rows[j];
+    const uint32_t sg = row.signer_type >> 8;
+    o.type[j] = (uint8_t)(row.signer_type & 0xFFu);
+    ((int64_t*)o.height)[j] = row.h;
+    ((int64_t*)o.round)[j] = row.r;
+    if (o.valid_round) ((int64_t*)o.valid_round)[j] = -1;
+    uint4* vp = reinterpret_cast<uint4*>(o.value32 + 32 * (size_t)j);
+    vp[0] = row.value[0];
+    vp[1] = row.value[1];
+    uint32_t f[8];
+    HD_UNROLL for (int k = 0; k < 8; k++) f[k] = sg < n_adm ? adm[8 * (size_t)sg + k] : 0xFFFFFFFFu;
+    store_row32_be(o.from32, j, f);
+    gidx[j] = row.gidx;
 }
 
 // ---------------------------------------------------------------- host side
@@ -502,8 +613,10 @@ static int table_order(hd_ctx* ctx, uint32_t n, uint32_t cap, const uint32_t* cl
 // candidate (e.g. a batch of a million single-message rounds)
 #define HD_TALLY_DENSE_MAX (64ull << 20)
 
+// gidx (optional): the batch's messages' global indices -- the rep outputs
+// are mapped through it (a routed batch, hd_tally_routed_device)
 static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdict, const uint32_t* d_bitmap,
-                        Part part, hd_tally_out* out, hipStream_t s) {
+                        Part part, hd_tally_out* out, hipStream_t s, const uint32_t* gidx = nullptr) {
     const uint32_t n = hb->n;
     if (!ctx->tally) ctx->tally = new TallyWork();
     DevBatch b{n, hb->type, hb->height, hb->round, hb->valid_round, hb->value32, hb->from32, hb->sig65};
@@ -619,11 +732,11 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     uint32_t* c_n = c_rep + n_cnt;
     uint8_t* c_t = reinterpret_cast<uint8_t*>(c_n + n_cnt);
     if (n_hr)
-        k_tally_emit_hr<<<nblk(n_hr), 256, 0, s>>>(n_hr, ord, cand, G, b.height, b.round, o_h, o_r, o_prev, o_prec,
-                                                   o_any, o_rep);
+        k_tally_emit_hr<<<nblk(n_hr), 256, 0, s>>>(n_hr, ord, cand, gidx, G, b.height, b.round, o_h, o_r, o_prev,
+                                                   o_prec, o_any, o_rep);
     if (n_cnt)
-        k_tally_emit_counts<<<nblk(n_cnt), 256, 0, s>>>(n_cnt, ord + m, cand, C, b.height, b.round, b.type, c_h, c_r,
-                                                        c_t, c_rep, c_n);
+        k_tally_emit_counts<<<nblk(n_cnt), 256, 0, s>>>(n_cnt, ord + m, cand, gidx, C, b.height, b.round, b.type, c_h,
+                                                        c_r, c_t, c_rep, c_n);
     TCHK(hipGetLastError(), "tally emit");
     if (out->dup) TCHK(hipMemcpyAsync(st + dup_off, d_dup, (size_t)n, hipMemcpyDeviceToDevice, s), "dup stage");
     TCHK(hipMemcpyAsync(tw->host, st, total, hipMemcpyDeviceToHost, s), "tally download");
@@ -700,6 +813,78 @@ int hd_tally_device_bitmap_part(hd_ctx* ctx, const hd_batch* dbatch, const uint3
 
 uint32_t hd_tally_partition_of(int64_t height, int64_t round, uint32_t nparts) {
     return part_of(hash_hr(height, round), nparts);
+}
+
+int hd_route_candidates_device(hd_ctx* ctx, const hd_batch* dshard, const uint32_t* d_valid_bitmap,
+                               uint32_t base_index, uint32_t nparts, uint8_t* d_rows, uint32_t cap_rows,
+                               uint32_t* counts, void* stream) {
+    if (!ctx || !dshard || !counts || nparts == 0 || nparts > HD_ROUTE_MAX_PARTS) return HD_EINVAL;
+    for (uint32_t o = 0; o < nparts; o++) counts[o] = 0;
+    const uint32_t n = dshard->n;
+    if (n == 0) return HD_OK;
+    if (!d_valid_bitmap || !d_rows || !dshard->type || !dshard->height || !dshard->round || !dshard->value32 ||
+        !dshard->from32 || ((uintptr_t)d_rows & 15) || ((uintptr_t)dshard->value32 & 15))
+        return HD_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    if (!ctx->tally) ctx->tally = new TallyWork();
+    DevBatch b{n, dshard->type, dshard->height, dshard->round, nullptr, dshard->value32, dshard->from32, nullptr};
+    const uint32_t nb = nblk(n);
+    const size_t cells = (size_t)nparts * nb;
+    int rc = 0;
+    uint32_t* cnt = (uint32_t*)tbuf(ctx, T_ROUTE, 4 * (2 * cells + nparts + 1) + 4096, &rc);
+    if (rc) return rc;
+    uint32_t* off = cnt + cells;
+    uint32_t* starts = off + cells;
+    void* tmp = (void*)(starts + nparts + 1);
+    size_t tmp_bytes = 0;
+    TCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, off, (int)cells, s), "route scan size");
+    // the scan's temporary storage after the counts (grown with them)
+    cnt = (uint32_t*)tbuf(ctx, T_ROUTE, 4 * (2 * cells + nparts + 1) + 64 + tmp_bytes, &rc);
+    if (rc) return rc;
+    off = cnt + cells;
+    starts = off + cells;
+    tmp = (void*)(((uintptr_t)(starts + nparts + 1) + 63) & ~(uintptr_t)63);
+    k_route_count<<<nb, 256, 0, s>>>(b, d_valid_bitmap, nparts, cnt);
+    TCHK(hipGetLastError(), "k_route_count");
+    TCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, (int)cells, s), "route scan");
+    k_route_starts<<<1, 64, 0, s>>>(off, cnt, nparts, nb, starts);
+    std::vector<uint32_t> st(nparts + 1);
+    TCHK(hipMemcpyAsync(st.data(), starts, 4 * (nparts + 1), hipMemcpyDeviceToHost, s), "route counts");
+    TCHK(hipStreamSynchronize(s), "route counts");
+    for (uint32_t o = 0; o < nparts; o++) counts[o] = st[o + 1] - st[o];
+    if (st[nparts] > cap_rows) return HD_ECAP;
+    const size_t adm_lds = adm_lds_bytes(ctx->n_adm);
+    k_route_write<<<nb, 256, adm_lds, s>>>(b, d_valid_bitmap, nparts, base_index, off, ctx->d_adm, ctx->n_adm,
+                                           ctx->adm_steps, adm_lds > 0, reinterpret_cast<RouteRow*>(d_rows));
+    TCHK(hipGetLastError(), "k_route_write");
+    return HD_OK;
+}
+
+int hd_unroute_device(hd_ctx* ctx, const uint8_t* d_rows, uint32_t n, const hd_batch_out* d_out, uint32_t* d_gidx,
+                      void* stream) {
+    if (!ctx || !d_out) return HD_EINVAL;
+    if (n == 0) return HD_OK;
+    if (!d_rows || !d_gidx || !d_out->type || !d_out->height || !d_out->round || !d_out->value32 || !d_out->from32 ||
+        ((uintptr_t)d_rows & 15) || ((uintptr_t)d_out->value32 & 15) || ((uintptr_t)d_out->from32 & 15))
+        return HD_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    k_unroute<<<nblk(n), 256, 0, s>>>(reinterpret_cast<const RouteRow*>(d_rows), n, ctx->d_adm, ctx->n_adm, *d_out,
+                                      d_gidx);
+    TCHK(hipGetLastError(), "k_unroute");
+    return HD_OK;
+}
+
+int hd_tally_routed_device(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* d_gidx, hd_tally_out* out,
+                           void* stream) {
+    if (!ctx || !dbatch || !tally_out_ok(out)) return HD_EINVAL;
+    out->n_counts = out->n_hr = 0;
+    if (dbatch->n == 0) return HD_OK;
+    if (!d_gidx) return HD_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    return tally_device(ctx, dbatch, nullptr, nullptr, Part{0, 1}, out, stream ? (hipStream_t)stream : ctx->stream,
+                        d_gidx);
 }
 
 int hd_process_batch(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8_t* recovered32,

@@ -190,7 +190,8 @@ int hd_ctx_create(int device, hd_ctx** out) {
 int hd_ctx_destroy(hd_ctx* ctx) {
     if (!ctx) return HD_EINVAL;
     (void)hipSetDevice(ctx->device);
-    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    (void)hd_ctx_quiesce(ctx);
+    if (ctx->ev_slow) (void)hipEventDestroy(ctx->ev_slow);
     void* ptrs[] = {ctx->d_gtab, ctx->d_adm, ctx->d_adm_perm};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -216,8 +217,10 @@ int hd_ctx_set_pubkey_format(hd_ctx* ctx, int format) {
 int hd_set_signatories(hd_ctx* ctx, const uint8_t* sigs32, uint32_t n) {
     if (!ctx || (n && !sigs32)) return HD_EINVAL;
     (void)hipSetDevice(ctx->device);
-    // kernels of earlier calls (any stream) may still read the admitted tables
-    if (hipDeviceSynchronize() != hipSuccess) return hd_ctx_fail(ctx, hipGetLastError(), "set_signatories sync");
+    // kernels of earlier calls of this context (any stream) may still read
+    // the admitted tables
+    int rq = hd_ctx_quiesce(ctx);
+    if (rq) return rq;
     // sort (stable on the original index so duplicates map to the first)
     std::vector<uint32_t> order(n);
     for (uint32_t i = 0; i < n; i++) order[i] = i;
@@ -242,8 +245,10 @@ int hd_set_signatories(hd_ctx* ctx, const uint8_t* sigs32, uint32_t n) {
     ctx->cap_adm_perm = cap_p;
     hipError_t e = hipSuccess;
     if (m) {
-        e = hipMemcpy(ctx->d_adm, words.data(), 32 * (size_t)m, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(ctx->d_adm_perm, perm.data(), 4 * (size_t)m, hipMemcpyHostToDevice);
+        e = hipMemcpyAsync(ctx->d_adm, words.data(), 32 * (size_t)m, hipMemcpyHostToDevice, ctx->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(ctx->d_adm_perm, perm.data(), 4 * (size_t)m, hipMemcpyHostToDevice, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     }
     if (e != hipSuccess) return hd_ctx_fail(ctx, e, "set_signatories upload");
     ctx->n_adm = m;
@@ -298,9 +303,20 @@ int launch_verify(hd_ctx* ctx, const hd_batch* db, const uint8_t* d_digest, uint
     // 13.2 ms vs 13.5 ms at 2x resident blocks, 14.3 ms at 1x)
     const uint32_t blocks = (db->n + 255) / 256;
     const SlowCtl none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    return hd_launch_slow(ctx, b, d_digest, d_verdict, d_recovered32, d_signer, d_valid_bitmap, none, blocks, s);
+    const int rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_recovered32, d_signer, d_valid_bitmap, none, blocks, s);
+    if (rc) return rc;
+    hipError_t e = ctx->ev_slow ? hipSuccess : hipEventCreateWithFlags(&ctx->ev_slow, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(ctx->ev_slow, s);
+    return e == hipSuccess ? HD_OK : hd_ctx_fail(ctx, e, "verify event");
 }
 }  // namespace
+
+int hd_ctx_quiesce(hd_ctx* ctx) {
+    hipError_t e = ctx->stream ? hipStreamSynchronize(ctx->stream) : hipSuccess;
+    if (e == hipSuccess && ctx->ev_slow) e = hipEventSynchronize(ctx->ev_slow);
+    if (e != hipSuccess) return hd_ctx_fail(ctx, e, "quiesce");
+    return ctx->fb ? hd_fb_quiesce(ctx) : HD_OK;
+}
 
 extern "C" {
 

@@ -13,8 +13,11 @@ for a whole batch:
     ing.push_wire(PREVOTE, buf, n)          # unmarshal + verify + filterHeight + mq insert (GPU)
     res = ing.flush()                       # mq.Consume(h, procsAllowed) + vote-log inserts (host table)
     res.proposes                            # handed to the CPU's insertPropose (scheduler/validator)
-    ing.reset_height(h + 1, signatories)    # ResetHeight: logs emptied, mq.DropMessagesBelowHeight,
-                                            # a new signatory set rebuilds procsAllowed (replica.go:132-145)
+    res.events                              # HD_VOTE_EV_* quorum crossings per delivered vote (f known)
+    ing.advance_height(h + 1)               # the Process committed: CurrentHeight++, logs emptied (process.go:710-725)
+    ing.reset_height(h + 5, signatories)    # ResetHeight: ignored unless above the current height
+                                            # (replica.go:222-225); logs emptied, mq.DropMessagesBelowHeight,
+                                            # a new signatory set rebuilds procsAllowed and f (replica.go:132-145)
 
 Membership follows the reference: every *authenticated* message
 (recovered signatory == From: verdict VALID or NOT_ADMITTED) with height >=
@@ -50,19 +53,29 @@ class FlushResult:
     double_of: np.ndarray      # batch index of the logged vote for DOUBLE, else votes.NO_INDEX
     proposes: np.ndarray       # indices (into consumed) of the proposes, for the CPU
     removed: int = 0           # messages consumed, delivered or dropped by procsAllowed (Consume's n)
+    events: Optional[np.ndarray] = None   # uint8 HD_VOTE_EV_* per consumed message (votes.EV_*), f known
 
 
 class Ingress:
     def __init__(self, v: Verifier, height: int = 1, max_capacity: int = 1000):
         self.v = v
         self.height = int(height)
-        self.f = None              # set by reset_height(signatories=...): len(signatories) // 3 (replica.go:138)
         self.mq = MessageQueue(v, max_capacity)
         self.votes = VoteLog(self.height)
+        # f = len(signatories) / 3 (replica.go:54, 138): from the verifier's
+        # admitted set now, and again on every ResetHeight with a new set; the
+        # vote logs report the 2f+1 / f+1 crossings with it
+        self.f = None
+        if getattr(v, "n_signatories", 0):
+            self._set_f(v.n_signatories // 3)
         # (height, insert count) of the last consume: while the queue has had
         # no insert since, every message in it is above that height, so a
         # ResetHeight to at most height + 1 has nothing to drop
         self._clean = None
+
+    def _set_f(self, f: int) -> None:
+        self.f = int(f)
+        self.votes.set_f(self.f)
 
     def close(self):
         self.mq.close()
@@ -101,12 +114,28 @@ class Ingress:
         b, senders = self.mq.consume(self.height, allowed=None)
         self._clean = (self.height, self.mq.inserts)
         status, double_of = self.votes.insert_batch(b)
-        return FlushResult(b, senders, status, double_of, np.flatnonzero(b.type == PROPOSE), self.mq.last_removed)
+        events = np.asarray(self.votes.last_events, np.uint8) if len(b) else np.zeros(0, np.uint8)
+        return FlushResult(b, senders, status, double_of, np.flatnonzero(b.type == PROPOSE), self.mq.last_removed,
+                           events)
 
-    def reset_height(self, height: int, signatories=None) -> None:
-        """ResetHeightMessage (replica.go:132-145): the logs restart at
-        `height`, lower heights leave the queue, and a non-empty signatory
-        set replaces procsAllowed (and the verifier's admitted set)."""
+    def advance_height(self, height: int) -> None:
+        """The Process's own height change after a commit (process.go:710-725:
+        CurrentHeight = height, vote logs emptied); the queue keeps its
+        messages (Consume removes every message at or below the height it
+        consumes, mq.go:36-66)."""
+        if int(height) <= self.height:
+            raise ValueError(f"advance_height({height}) at height {self.height}")
+        self.height = int(height)
+        self.votes.reset(self.height)
+
+    def reset_height(self, height: int, signatories=None) -> bool:
+        """Replica.ResetHeight (replica.go:216-235): ignored (returns False)
+        unless `height` is above the current height (:223-225).  Otherwise the
+        ResetHeightMessage (:132-145): the logs restart at `height`, lower
+        heights leave the queue, and a non-empty signatory set replaces
+        procsAllowed (the verifier's admitted set) and f."""
+        if int(height) <= self.height:
+            return False
         self.height = int(height)
         self.votes.reset(self.height)
         clean = self._clean is not None and self._clean[1] == self.mq.inserts and self.height <= self._clean[0] + 1
@@ -114,7 +143,8 @@ class Ingress:
             self.mq.drop_below(self.height)
         if signatories is not None and len(signatories):
             self.v.set_signatories(signatories)
-            self.f = len(signatories) // 3
+            self._set_f(len(signatories) // 3)
+        return True
 
 
 __all__ = ["Ingress", "FlushResult"]

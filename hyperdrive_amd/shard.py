@@ -159,6 +159,82 @@ def gather_tally_device(local, world: int, group=None):
     return merged
 
 
+# ---- routed tally (the C4 data path: no replicated batch) -----------------
+ROUTE_ROW_BYTES = 64       # include/hd_verify.h HD_ROUTE_ROW_BYTES
+
+
+def route_candidates(v, dshard, d_bitmap: int, base_index: int, world: int, stream, rows=None):
+    """This rank's candidates (VALID Prevotes / Precommits of its shard, global
+    index base_index + i) as route rows grouped by the owner of their round
+    (hd_route_candidates_device).  Returns (rows uint8 tensor [cap, 64], counts
+    list of `world` ints); rows may be passed in for reuse."""
+    import torch
+    from . import _lib
+    lib = _lib.load()
+    n = dshard.n
+    dev = torch.device("cuda", v.device)
+    if rows is None or rows.shape[0] < max(n, 1):
+        rows = torch.empty((max(n, 1), ROUTE_ROW_BYTES), dtype=torch.uint8, device=dev)
+    counts = (ctypes.c_uint32 * world)()
+    rc = lib.hd_route_candidates_device(v.handle, ctypes.byref(dshard), d_bitmap, int(base_index), int(world),
+                                        rows.data_ptr(), rows.shape[0], counts, stream)
+    if rc != 0:
+        raise _lib.HDError(rc, "hd_route_candidates_device", lib.hd_ctx_last_error(v.handle).decode())
+    return rows, [int(c) for c in counts]
+
+
+def exchange_routed(rows, counts, world: int, group=None):
+    """All-to-all of the route rows: rank o receives every rank's group o, in
+    source-rank order (= global index order).  rows: [>= sum(counts), 64] uint8
+    tensor (CUDA for RCCL, CPU for gloo).  Returns the received rows tensor.
+    One host read per call: the receive sizes (an all-to-all of the counts)."""
+    import torch
+    import torch.distributed as dist
+    send = torch.tensor(counts, dtype=torch.int64, device=rows.device)
+    recv = torch.empty(world, dtype=torch.int64, device=rows.device)
+    dist.all_to_all_single(recv, send, group=group)
+    rc = recv.cpu().tolist()
+    out = torch.empty((max(sum(rc), 1), ROUTE_ROW_BYTES), dtype=torch.uint8, device=rows.device)
+    total = sum(counts)
+    dist.all_to_all_single(out[: sum(rc)], rows[:total], output_split_sizes=rc, input_split_sizes=list(counts),
+                           group=group)
+    return out[: sum(rc)]
+
+
+def unroute(v, rows, stream):
+    """Received route rows -> (DeviceBatch, gidx int32 tensor) (hd_unroute_device)."""
+    import torch
+    from . import _lib
+    from .device import DeviceBatch
+    lib = _lib.load()
+    m = rows.shape[0]
+    db = DeviceBatch.empty(m, str(rows.device))
+    gidx = torch.empty(max(m, 1), dtype=torch.int32, device=rows.device)
+    if m:
+        rc = lib.hd_unroute_device(v.handle, rows.data_ptr(), m, ctypes.byref(db.c_out()), gidx.data_ptr(), stream)
+        if rc != 0:
+            raise _lib.HDError(rc, "hd_unroute_device", lib.hd_ctx_last_error(v.handle).decode())
+    return db, gidx[:m]
+
+
+def tally_routed_device(v, db, gidx, stream, out, device):
+    """The owner's tally of its received candidates (hd_tally_routed_device):
+    packed rows {"counts": [k, 5], "hr": [m, 6]} as int64 tensors on `device`,
+    reps already global indices.  out: a pinned struct from tally_out."""
+    import torch
+    from . import _lib
+    lib = _lib.load()
+    t, a = out
+    if db.n == 0:
+        return {"counts": torch.zeros((0, 5), dtype=torch.int64, device=device),
+                "hr": torch.zeros((0, 6), dtype=torch.int64, device=device)}
+    rc = lib.hd_tally_routed_device(v.handle, ctypes.byref(db.c_struct()), gidx.data_ptr(), ctypes.byref(t), stream)
+    if rc != 0:
+        raise _lib.HDError(rc, "hd_tally_routed_device", lib.hd_ctx_last_error(v.handle).decode())
+    packed = pack_tally(a, t.n_counts, t.n_hr)     # host copies of the pinned stage: the next call may reuse it
+    return {"counts": torch.from_numpy(packed["counts"]).to(device), "hr": torch.from_numpy(packed["hr"]).to(device)}
+
+
 def pack_tally(a, n_counts: int, n_hr: int) -> Dict[str, np.ndarray]:
     return {"counts": np.stack([a[c][:n_counts].astype(np.int64) for c in COUNT_COLS], 1).reshape(n_counts, 5),
             "hr": np.stack([a[c][:n_hr].astype(np.int64) for c in HR_COLS], 1).reshape(n_hr, 6)}

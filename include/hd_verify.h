@@ -264,6 +264,32 @@ int hd_gen_batch_device(hd_ctx* ctx, uint32_t kind, uint64_t start, uint32_t n, 
                         const uint8_t* d_signatories32, const uint8_t* d_foreign32, const hd_batch_out* d_out,
                         void* stream);
 
+/* ---- multi-GPU tally routing (the C4 data path) -----------
+ * The tally of a batch sharded over G GPUs without replicating the batch:
+ * hd_route_candidates_device turns the candidates of one device's shard --
+ * VALID Prevotes / Precommits per d_valid_bitmap, global index base_index + i
+ * -- into HD_ROUTE_ROW_BYTES rows in d_rows (16-byte aligned, cap_rows rows),
+ * grouped by the owner rank of their round (hd_tally_partition_of(h, r,
+ * nparts), nparts <= 64) and in index order inside each group; counts[nparts]
+ * (host) gets the group sizes (group o starts at row sum(counts[0..o))).
+ * Synchronous (one small download); HD_ECAP when cap_rows is too small.
+ * The rows cross xGMI (grouped ncclSend/Recv or an all-to-all); the owner
+ * concatenates what it received in source-rank order (= global index order)
+ * and calls hd_unroute_device: a device batch (type, height, round, value32,
+ * From rebuilt from the admitted set; valid_round -1 if given) and each
+ * row's global index; hd_tally_routed_device then tallies it (every row is a
+ * candidate; count_rep / hr_rep are global indices; dup is per received row).
+ * The owners' tables are disjoint and their union ordered by count_rep /
+ * hr_rep is the single-GPU tally.  All contexts need the same admitted set. */
+#define HD_ROUTE_ROW_BYTES 64
+int hd_route_candidates_device(hd_ctx* ctx, const hd_batch* dshard, const uint32_t* d_valid_bitmap,
+                               uint32_t base_index, uint32_t nparts, uint8_t* d_rows, uint32_t cap_rows,
+                               uint32_t* counts, void* stream);
+int hd_unroute_device(hd_ctx* ctx, const uint8_t* d_rows, uint32_t n, const hd_batch_out* d_out, uint32_t* d_gidx,
+                      void* stream);
+int hd_tally_routed_device(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* d_gidx, hd_tally_out* out,
+                           void* stream);
+
 /* ---- misc ------------------------------------------------------------- */
 const char* hd_strerror(int code);
 /* last HIP error text recorded by the ctx (empty if none) */

@@ -16,6 +16,10 @@ run() {  # name seconds cmd...
 for step in "$@"; do
   case $step in
     light) run first_light 600 python scripts/first_light.py ;;
+    probe) run w4_probe 240 python -u scripts/w4_probe.py base ;;
+    gtest1) run pytest_gpu1 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "golden or c1 or fast_path_equals or set_change" ;;
+    bench_vs1) HD_BENCH_VSTREAMS=1 run bench_vs1 300 python bench.py --no-cpu --no-aux ;;
+    bench_fast) run bench_fast 300 python bench.py --no-cpu --no-aux ;;
     fieldbench) run fieldbench 120 scripts/fieldbench 3 ;;
     gtest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     gputest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;

@@ -1,0 +1,186 @@
+// w4_probe.hip -- debug aid (not product code): bisects the full recovery of
+// hd_verify_msg.h by phase, compiled for 3 and 4 waves per SIMD, so that the
+// first phase whose output differs between register budgets (and from the
+// host build of the same headers) can be named.
+//
+// Stage s of k_stage<W, S> runs the recovery from (digest, sig) up to phase S
+// and writes that phase's output (16 words per message):
+//   0  lift: R.y canonical (x = r[+n] is the input)
+//   1  u1 = -m / r, u2 = s / r
+//   2  the ladder's Jacobian Q = u1 G + u2 R, made affine (x, y)
+//   3  the recovered signatory SHA-256(pubkey) and the verdict
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared
+//        -I../include scripts/w4_probe.hip -o scripts/w4_probe.so
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <vector>
+
+#include "../hyperdrive_amd/csrc/hd_verify_msg.h"
+
+using namespace hd;
+
+struct PSrc {
+    const uint32_t* dg;
+    const uint8_t* sig;
+    const uint8_t* frm;
+    uint32_t i;
+    HD_MEMBER uint32_t type() const { return 2; }
+    HD_MEMBER int64_t h() const { return 0; }
+    HD_MEMBER int64_t r() const { return 0; }
+    HD_MEMBER int64_t vr() const { return -1; }
+    HD_MEMBER uint32_t value(int) const { return 0; }
+    HD_MEMBER uint32_t from(int w) const { return load_be32(frm + 32 * (size_t)i + 4 * w); }
+    HD_MEMBER uint32_t sig_r(int w) const { return load_be32(sig + 65 * (size_t)i + 4 * w); }
+    HD_MEMBER uint32_t sig_s(int w) const { return load_be32(sig + 65 * (size_t)i + 32 + 4 * w); }
+    HD_MEMBER uint32_t sig_v() const { return sig[65 * (size_t)i + 64]; }
+    HD_MEMBER bool has_digest() const { return true; }
+    HD_MEMBER uint32_t digest(int w) const { return dg[8 * (size_t)i + w]; }
+};
+
+template <int S>
+__host__ __device__ uint8_t stage_run(const PSrc& src, const ge* gtab, uint32_t out[16]) {
+    HD_UNROLL for (int k = 0; k < 16; k++) out[k] = 0;
+    if (S == 3) {
+        uint32_t rec[8];
+        int32_t signer;
+        const uint8_t v = verify_msg_src(src, gtab, (const uint32_t*)nullptr, 0u, 0, 1, rec, signer);
+        HD_UNROLL for (int k = 0; k < 8; k++) out[k] = rec[k];
+        return v;
+    }
+    uint32_t d[8], r_be[8], s_be[8];
+    HD_UNROLL for (int w = 0; w < 8; w++) {
+        d[w] = src.digest(w);
+        r_be[w] = src.sig_r(w);
+        s_be[w] = src.sig_s(w);
+    }
+    const uint32_t v = src.sig_v();
+    sc r, s;
+    HD_UNROLL for (int i = 0; i < 8; i++) { r.v[i] = r_be[7 - i]; s.v[i] = s_be[7 - i]; }
+    uint32_t xw[8];
+    HD_UNROLL for (int i = 0; i < 8; i++) xw[i] = r.v[i];
+    if (v & 2) {
+        const uint32_t N[8] = {HD_N0, HD_N1, HD_N2, HD_N3, HD_N4, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        uint64_t c = 0;
+        HD_UNROLL for (int i = 0; i < 8; i++) { c += (uint64_t)xw[i] + N[i]; xw[i] = (uint32_t)c; c >>= 32; }
+    }
+    fe x;
+    fe_from_le(x, xw);
+    fe y2, y;
+    fe_sqr(y2, x);
+    fe_mul(y2, y2, x);
+    fe seven;
+    fe_set_u32(seven, 7);
+    fe_add(y2, y2, seven);
+    if (!fe_sqrt(y, y2)) return 3;
+    fe_normalize(y);
+    if ((uint32_t)(y.n[0] & 1u) != (v & 1u)) {
+        fe_neg(y, y);
+        fe_normalize(y);
+    }
+    if (S == 0) {
+        fe_to_le(out, y);
+        return 0;
+    }
+    ge R;
+    R.x = x;
+    R.y = y;
+    sc m, rinv, u1, u2;
+    sc_from_be_reduce(m, d);
+    sc_inv_divsteps(rinv, r);
+    sc_mul(u1, m, rinv);
+    sc_neg(u1, u1);
+    sc_mul(u2, s, rinv);
+    if (S == 1) {
+        HD_UNROLL for (int k = 0; k < 8; k++) { out[k] = u1.v[k]; out[8 + k] = u2.v[k]; }
+        return 0;
+    }
+    gej Q;
+    ecmult_glv(Q, R, u1, u2, gtab);
+    if (gej_is_inf(Q)) return 4;
+    fe qx, qy;
+    gej_to_ge(qx, qy, Q);
+    fe_to_le(out, qx);
+    fe_to_le(out + 8, qy);
+    return 0;
+}
+
+template <int W, int S>
+__global__ __launch_bounds__(256, W) void k_stage(uint32_t n, const uint32_t* __restrict__ dg,
+                                                  const uint8_t* __restrict__ sig, const uint8_t* __restrict__ from,
+                                                  const ge* __restrict__ gtab, uint32_t* __restrict__ out,
+                                                  uint8_t* __restrict__ verdict) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    PSrc src{dg, sig, from, i};
+    uint32_t o[16];
+    const uint8_t v = stage_run<S>(src, gtab, o);
+    HD_UNROLL for (int k = 0; k < 16; k++) out[16 * (size_t)i + k] = o[k];
+    verdict[i] = v;
+}
+
+template <int W>
+static void launch(int stage, uint32_t n, const uint32_t* dg, const uint8_t* sig, const uint8_t* from,
+                   const ge* gtab, uint32_t* out, uint8_t* verdict) {
+    const uint32_t b = (n + 255) / 256;
+    if (stage == 0) k_stage<W, 0><<<b, 256>>>(n, dg, sig, from, gtab, out, verdict);
+    else if (stage == 1) k_stage<W, 1><<<b, 256>>>(n, dg, sig, from, gtab, out, verdict);
+    else if (stage == 2) k_stage<W, 2><<<b, 256>>>(n, dg, sig, from, gtab, out, verdict);
+    else k_stage<W, 3><<<b, 256>>>(n, dg, sig, from, gtab, out, verdict);
+}
+
+// host: digests (8 BE words per message), sigs (65 B), froms (32 B) -> out
+// (16 words per message) and verdicts, for waves W (3 or 4) and stage 0..3
+extern "C" int probe_run(int waves, int stage, uint32_t n, const uint32_t* dg, const uint8_t* sig,
+                         const uint8_t* from, uint32_t* out, uint8_t* verdict) {
+    static std::vector<ge> tab;
+    if (tab.empty()) {
+        tab.resize(2 * HD_GLV_GTAB_N);
+        build_gtab_glv(tab.data());
+    }
+    ge* d_tab;
+    uint32_t *d_dg, *d_out;
+    uint8_t *d_sig, *d_from, *d_v;
+    if (hipMalloc(&d_tab, sizeof(ge) * tab.size()) || hipMalloc(&d_dg, 32 * (size_t)n) ||
+        hipMalloc(&d_out, 64 * (size_t)n) || hipMalloc(&d_sig, 65 * (size_t)n) ||
+        hipMalloc(&d_from, 32 * (size_t)n) || hipMalloc(&d_v, n))
+        return -2;
+    hipMemcpy(d_tab, tab.data(), sizeof(ge) * tab.size(), hipMemcpyHostToDevice);
+    hipMemcpy(d_dg, dg, 32 * (size_t)n, hipMemcpyHostToDevice);
+    hipMemcpy(d_sig, sig, 65 * (size_t)n, hipMemcpyHostToDevice);
+    hipMemcpy(d_from, from, 32 * (size_t)n, hipMemcpyHostToDevice);
+    if (waves == 4) launch<4>(stage, n, d_dg, d_sig, d_from, d_tab, d_out, d_v);
+    else launch<3>(stage, n, d_dg, d_sig, d_from, d_tab, d_out, d_v);
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(out, d_out, 64 * (size_t)n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(verdict, d_v, n, hipMemcpyDeviceToHost);
+    hipFree(d_tab);
+    hipFree(d_dg);
+    hipFree(d_out);
+    hipFree(d_sig);
+    hipFree(d_from);
+    hipFree(d_v);
+    return e == hipSuccess ? 0 : -3;
+}
+
+// the same stages on the host (g++-equivalent host build of the headers)
+extern "C" int probe_host(int stage, uint32_t n, const uint32_t* dg, const uint8_t* sig, const uint8_t* from,
+                          uint32_t* out, uint8_t* verdict) {
+    static std::vector<ge> tab;
+    if (tab.empty()) {
+        tab.resize(2 * HD_GLV_GTAB_N);
+        build_gtab_glv(tab.data());
+    }
+    for (uint32_t i = 0; i < n; i++) {
+        PSrc src{dg, sig, from, i};
+        uint32_t o[16];
+        uint8_t v;
+        if (stage == 0) v = stage_run<0>(src, tab.data(), o);
+        else if (stage == 1) v = stage_run<1>(src, tab.data(), o);
+        else if (stage == 2) v = stage_run<2>(src, tab.data(), o);
+        else v = stage_run<3>(src, tab.data(), o);
+        for (int k = 0; k < 16; k++) out[16 * (size_t)i + k] = o[k];
+        verdict[i] = v;
+    }
+    return 0;
+}

@@ -73,7 +73,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=1 << 20, help="messages per GPU")
+    ap.add_argument("--batch", type=int, default=1 << 20, help="messages per GPU (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="messages over all GPUs (strong scaling; C4 = 16777216), split into contiguous shards")
     ap.add_argument("--signers", type=int, default=100)
     ap.add_argument("--adv", type=int, default=0, help="adversarial percentage (C5)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20,
@@ -106,44 +108,47 @@ def cpu_baseline(args, S):
 
 
 class Pipeline:
-    """verify (library streams `ws`, alternating) -> bitmap all-gather ->
-    tally (stream `ts`) for one batch shape, with NBUF output buffers: the
-    tally of step k runs on its own stream while the verifications of steps
-    k+1 .. k+NBUF-1 are queued, so the tally's host syncs never drain the
-    verify queue; consecutive verifications go to different streams, so the
-    device runs step k+1's kernels in the SIMD slots step k's inversion
-    kernels, last k_fast_sums round and fallback recovery leave idle (the
-    library's per-call scratch sets, hd_fastverify.hip FbWork); every step's
-    verification and tally complete inside the timed region."""
+    """verify (library streams `ws`, alternating) -> tally (stream `ts`) for
+    one batch shape, with NBUF output buffers: the tally of step k runs on its
+    own stream while the verifications of steps k+1 .. k+NBUF-1 are queued,
+    so the tally's host syncs never drain the verify queue; consecutive
+    verifications go to different streams, so the device runs step k+1's
+    kernels in the SIMD slots step k's inversion kernels, last k_fast_sums
+    round and fallback recovery leave idle (the library's per-call scratch
+    sets, hd_fastverify.hip FbWork); every step's verification and tally
+    complete inside the timed region.
+
+    N > 1 (one process per GPU): `db` is this rank's shard only (global
+    indices lo .. lo + B - 1); the tally routes the shard's candidates to the
+    owners of their rounds over RCCL (shard.route_candidates /
+    exchange_routed: one all-to-all of the counts, one of the 64-byte rows),
+    each owner tallies what it received (hd_tally_routed_device) and the
+    owners' small tables are all-gathered and merged (gather_tally_device)."""
     NBUF = int(os.environ.get("HD_BENCH_NBUF", 3))
     VSTREAMS = int(os.environ.get("HD_BENCH_VSTREAMS", 2))
 
-    def __init__(self, v, db, total, B, rank, world, dist, ws, ts, tally=True):
+    def __init__(self, v, db, total, lo, rank, world, dist, ws, ts, tally=True):
         import torch
-        from hyperdrive_amd._lib import HdBatch
-        from hyperdrive_amd.shard import shard_range
-        self.v, self.db, self.total, self.B = v, db, total, B
+        self.v, self.db, self.total, self.B, self.lo = v, db, total, db.n, lo
         self.rank, self.world, self.dist, self.ws, self.ts = rank, world, dist, ws, ts
         self.do_tally = tally
         dev = db.height.device
+        self.dev = dev
+        B = db.n
+        assert B % 32 == 0
         self.wss = [ws] + [torch.cuda.Stream(device=dev, priority=ws.priority) for _ in range(self.VSTREAMS - 1)]
-        lo, hi = shard_range(total, rank, world)
-        assert hi - lo == B and B % 32 == 0
-        self.lo = lo
-        # shard view: device pointers offset into the replicated batch
-        self.shard = HdBatch(B, db.type.data_ptr() + lo, db.height.data_ptr() + 8 * lo,
-                             db.round.data_ptr() + 8 * lo, db.valid_round.data_ptr() + 8 * lo,
-                             db.value.data_ptr() + 32 * lo, db.frm.data_ptr() + 32 * lo, db.sig.data_ptr() + 65 * lo)
-        self.full = db.c_struct()
+        self.shard = db.c_struct()
         self.verdicts = [torch.empty(B, dtype=torch.uint8, device=dev) for _ in range(self.NBUF)]
         self.recovered = [torch.empty((B, 32), dtype=torch.uint8, device=dev) for _ in range(self.NBUF)]
         self.bitmaps = [torch.zeros(B // 32, dtype=torch.int32, device=dev) for _ in range(self.NBUF)]
-        self.t_out, self.t_arr = v._tally_struct(total, pinned=True)
+        self.t_out, self.t_arr = v._tally_struct(B, pinned=True)
         if os.environ.get("HD_BENCH_NO_DUP"):      # A/B probe: skip the per-message classification download
             self.t_out.dup = None
         self.t_part = None
+        self.route_rows = None
         if world > 1:
             from hyperdrive_amd.shard import tally_out
+            # an owner receives about B candidates; sized for all of a skewed batch
             self.t_part = tally_out(v, total, pinned=True)
         self.tally_info = {}
         self.last_tally = None
@@ -152,63 +157,45 @@ class Pipeline:
 
     def verify(self, k):
         import torch
-        from hyperdrive_amd.shard import gather_bitmaps_async
         buf = k % self.NBUF
         ws = self.wss[k % len(self.wss)]
         self.v.verify_batch_device(self.shard, self.verdicts[buf].data_ptr(), self.recovered[buf].data_ptr(), None,
                                    self.bitmaps[buf].data_ptr(), ws.cuda_stream)
-        work = None
-        if self.dist is not None:
-            with torch.cuda.stream(ws):
-                # RCCL all-gather over xGMI; the tally stream waits for it, the
-                # next verification does not
-                gathered, work = gather_bitmaps_async(self.bitmaps[buf], self.total, self.world)
-        else:
-            gathered = self.bitmaps[buf]
         done = torch.cuda.Event()
         done.record(ws)
-        return gathered, done, work
+        return self.bitmaps[buf], done
 
     def tally(self, pending):
         import torch
         from hyperdrive_amd import _lib
-        from hyperdrive_amd.shard import gather_tally, pack_tally, tally_part
         if pending is None or not self.do_tally:
             return
-        gathered, done, work = pending
+        bitmap, done = pending
         self.ts.wait_event(done)
-        if work is not None:
-            with torch.cuda.stream(self.ts):
-                work.wait()
-            gathered.record_stream(self.ts)
         if self.dist is None:
             lib = _lib.load()
-            rc = lib.hd_tally_device_bitmap(self.v.handle, ctypes.byref(self.full), gathered.data_ptr(),
+            rc = lib.hd_tally_device_bitmap(self.v.handle, ctypes.byref(self.shard), bitmap.data_ptr(),
                                             ctypes.byref(self.t_out), self.ts.cuda_stream)
             if rc != 0:
                 raise _lib.HDError(rc, "hd_tally_device_bitmap", lib.hd_ctx_last_error(self.v.handle).decode())
             self.tally_info = {"n_hr": self.t_out.n_hr, "n_counts": self.t_out.n_counts}
             self.last_tally = (self.t_out, self.t_arr)
-        else:
-            # this rank's rounds, then the merged count tables of all ranks:
-            # on the GPU over RCCL (exchange and merge stay on the device),
-            # through host arrays over gloo
-            if self.dist.get_backend() == "nccl":
-                from hyperdrive_amd.shard import gather_tally_device, tally_part_device
-                with torch.cuda.stream(self.ts):
-                    local = tally_part_device(self.v, self.full, gathered.data_ptr(), self.rank, self.world,
-                                              self.ts.cuda_stream, self.t_part, gathered.device)
-                    # its own communicator: the count exchange of step k does
-                    # not queue behind the bitmap all-gathers of steps k+1..
-                    merged = gather_tally_device(local, self.world, group=self.tally_group)
-            else:
-                local = tally_part(self.v, self.full, gathered.data_ptr(), self.rank, self.world, self.ts.cuda_stream,
-                                   out=self.t_part)
-                with torch.cuda.stream(self.ts):
-                    merged = gather_tally(local, self.world, device=gathered.device)
-            self.tally_info = {"n_hr": len(merged["hr"]), "n_counts": len(merged["counts"]),
-                               "n_hr_this_rank": len(local["hr"])}
-            self.last_tally = merged
+            return
+        from hyperdrive_amd.shard import (exchange_routed, gather_tally_device, route_candidates,
+                                          tally_routed_device, unroute)
+        s = self.ts.cuda_stream
+        with torch.cuda.stream(self.ts):
+            rows, counts = route_candidates(self.v, self.shard, bitmap.data_ptr(), self.lo, self.world, s,
+                                            rows=self.route_rows)
+            self.route_rows = rows
+            recv = exchange_routed(rows, counts, self.world, group=self.tally_group)
+            db, gidx = unroute(self.v, recv, s)
+            local = tally_routed_device(self.v, db, gidx, s, self.t_part, self.dev)
+            merged = gather_tally_device(local, self.world, group=self.tally_group)
+        self.tally_info = {"n_hr": len(merged["hr"]), "n_counts": len(merged["counts"]),
+                           "n_hr_this_rank": len(local["hr"]), "routed_in": int(recv.shape[0]),
+                           "routed_out": int(sum(counts))}
+        self.last_tally = merged
 
     def run(self, steps):
         """steps verifications + tallies; buffer k % NBUF is rewritten by
@@ -272,8 +259,13 @@ def main():
     import hyperdrive_amd as hd
     from hyperdrive_amd.device import generate, work_stream
 
-    B, S = args.batch, args.signers
-    total = B * world
+    S = args.signers
+    from hyperdrive_amd.shard import shard_range
+    total = args.global_batch or args.batch * world
+    lo, hi = shard_range(total, rank, world)
+    B = hi - lo
+    if B % 32 or B == 0:
+        raise SystemExit(f"shard of {B} messages: use a global batch that splits into whole bitmap words")
     t0 = time.perf_counter()
     v = hd.Verifier(dev.index)                  # builds the device's shared G table (5.4 GB, once per process)
     ctx_s = time.perf_counter() - t0
@@ -282,13 +274,14 @@ def main():
     sigs, foreign = v.gen_keys(S)
     v.set_signatories(sigs)
     t0 = time.perf_counter()
-    # replicated batch metadata (whole stream), generated on this GPU
-    db, _, _ = generate(v, 0, total, S, args.adv, keys=(sigs, foreign), device=str(dev))
+    # this rank's shard only (messages lo .. hi - 1 of the seeded stream),
+    # generated on its GPU: no rank holds another's messages
+    db, _, _ = generate(v, 0, B, S, args.adv, keys=(sigs, foreign), start=lo, device=str(dev))
     gen_s = time.perf_counter() - t0
 
     torch.cuda.set_stream(ws)          # torch ops (RCCL all-gather included) share the library's stream
     ts = torch.cuda.Stream(device=dev, priority=-1 if args.tally_priority == "high" else 0)
-    pipe = Pipeline(v, db, total, B, rank, world, dist, ws, ts, tally=not args.no_tally)
+    pipe = Pipeline(v, db, total, lo, rank, world, dist, ws, ts, tally=not args.no_tally)
     if dist is not None and args.dist_backend == "nccl":
         pipe.tally_group = dist.new_group(backend="nccl")
 
@@ -337,7 +330,7 @@ def main():
     hist = torch.bincount(verdict.long(), minlength=8).cpu().tolist()
     if args.adv == 0:
         full_bits = int(bitmap.view(torch.uint8).cpu().numpy().astype("uint8").sum())
-        same_from = bool((recovered == db.frm[pipe.lo: pipe.lo + B]).all())
+        same_from = bool((recovered == db.frm).all())
         if hist[0] != B or full_bits != 255 * (B // 8) or not same_from:
             print(json.dumps({"error": "verification produced wrong outputs", "verdicts": hist}), flush=True)
             sys.exit(1)
@@ -362,15 +355,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.global_batch else "weak",
             "vs_baseline": None,
             "dtype": "u32 (256-bit modular integer arithmetic)",
             "data": "synthetic (seeded RFC6979-signed votes generated on the GPU)",
-            "config": {"workload": "C2: batch-verify 1M Prevote/Precommit from 100 signatories + 2f+1 tally",
+            "config": {"workload": (f"C4: {total}-message batch sharded over {world} GPU(s) + 2f+1 tally"
+                                    if args.global_batch else
+                                    "C2: batch-verify 1M Prevote/Precommit from 100 signatories + 2f+1 tally"),
                        "messages_per_gpu": B, "global_batch": total, "signatories": S, "adversarial_pct": args.adv,
                        "outputs_per_step": "verdict, recovered signatory, valid bitmap, tally",
-                       "parallelism": f"shard-by-index x{world}, RCCL all-gather of valid bitmaps, "
-                                      f"tally partitioned by round x{world}"},
+                       "parallelism": (f"shard-by-index x{world} (each rank holds only its shard); candidates routed "
+                                       f"to their round's owner by an RCCL all-to-all; owners' tables all-gathered"
+                                       if world > 1 else "one GPU")},
             "roofline": {
                 "bound": "valu",
                 "kernel": "k_fast_sums (the known-key check's mixed additions; dominant kernel of the verify call)",
@@ -465,7 +461,7 @@ def sub_benchmarks(args, v, sigs, foreign, dev, ws, ts):
     # C5: the C2 stream with 30 % of the messages corrupted across the classes
     B = args.batch
     db5, _, _ = generate(v, 0, B, args.signers, 30, keys=(sigs, foreign), device=str(dev))
-    p5 = Pipeline(v, db5, B, B, 0, 1, None, ws, ts)
+    p5 = Pipeline(v, db5, B, 0, 0, 1, None, ws, ts)
     p5.run(2)
     el = timed(p5, args.sub_steps, None, dev)
     vd, _, _ = p5.last(args.sub_steps)
@@ -485,7 +481,7 @@ def sub_benchmarks(args, v, sigs, foreign, dev, ws, ts):
     v.set_signatories(k6[0])
     set_s = time.perf_counter() - t0
     db6, _, _ = generate(v, 0, B, S6, 0, keys=k6, device=str(dev))
-    p6 = Pipeline(v, db6, B, B, 0, 1, None, ws, ts)
+    p6 = Pipeline(v, db6, B, 0, 0, 1, None, ws, ts)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     p6.run(1)
@@ -513,7 +509,7 @@ def sub_benchmarks(args, v, sigs, foreign, dev, ws, ts):
     n3p = (n3 + 31) // 32 * 32
     if n3p != n3:
         db3, _, _ = generate(v3, 1, n3p, S3, 0, keys=k3, device=str(dev))   # whole bitmap words
-    p3 = Pipeline(v3, db3, n3p, n3p, 0, 1, None, ws, ts)
+    p3 = Pipeline(v3, db3, n3p, 0, 0, 1, None, ws, ts)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     p3.run(1)

@@ -92,6 +92,11 @@ SIGNATURES = {
                                        ctypes.c_void_p, ctypes.c_void_p]),
     "hd_verify_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "hd_verify_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
+    "hd_verify_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
+    "hd_host_alloc": (ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
+    "hd_host_free": (ctypes.c_int, [ctypes.c_void_p]),
     "hd_tally": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                 ctypes.POINTER(HdTallyOut)]),
     "hd_tally_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,

@@ -1,0 +1,249 @@
+// hd_host.hip -- asynchronous host-buffer verification (include/hd_verify.h
+// hd_verify_submit / hd_verify_wait / hd_host_alloc).
+//
+// The cgo caller hands over host messages (replica/replica.go:156-181);
+// hd_verify_batch uploads, verifies and downloads in series, so its PCIe time
+// adds to the kernels'.  Here a context keeps HD_HOST_SLOTS pipelines, each
+// with its own stream, device buffers and pinned staging: a submit queues
+// H2D copies -> hd_verify_batch_device -> D2H copies on its pipeline's stream
+// and returns, so batch k+1's upload runs under batch k's kernels (and the
+// two pipelines' verify calls overlap on the device, hd_fastverify.hip's
+// scratch sets).  Inputs and outputs in pinned memory move by DMA straight
+// from / to the caller's buffers; pageable ones pass through pinned staging,
+// copied by host threads (one memcpy thread cannot keep up with PCIe).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../../include/hd_verify.h"
+#include "hd_internal.h"
+
+namespace {
+
+enum { HC_TYPE, HC_H, HC_R, HC_VR, HC_VALUE, HC_FROM, HC_SIG, HC_N };
+
+struct HostSlot {
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    uint64_t ticket = 0;     // in flight or awaiting delivery (0: idle)
+    DevBuf col[HC_N], verdict, rec, bitmap;
+    void* hin = nullptr;     // pinned input staging (pageable inputs)
+    size_t hin_cap = 0;
+    void* hout = nullptr;    // pinned output staging (pageable outputs)
+    size_t hout_cap = 0;
+    // delivery of staged outputs at completion: (dst, staged src, bytes)
+    struct Copy { void* dst; const void* src; size_t n; };
+    std::vector<Copy> deliver;
+};
+
+}  // namespace
+
+struct HostPipe {
+    HostSlot slot[HD_HOST_SLOTS];
+    uint64_t next = 1;
+};
+
+namespace {
+
+#define HCHK(expr, what)                                          \
+    do {                                                          \
+        hipError_t e_ = (expr);                                   \
+        if (e_ != hipSuccess) return hd_ctx_fail(ctx, e_, what);  \
+    } while (0)
+
+bool is_pinned(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();   // pageable memory is reported as an error on some runtimes
+        return false;
+    }
+    return a.type == hipMemoryTypeHost || a.type == hipMemoryTypeManaged;
+}
+
+// memcpy with host threads for large copies
+void par_copy(void* dst, const void* src, size_t n) {
+    const size_t kMin = 4u << 20;
+    unsigned t = std::min<unsigned>(8u, std::max(1u, std::thread::hardware_concurrency()));
+    if (n < kMin || t <= 1) {
+        memcpy(dst, src, n);
+        return;
+    }
+    t = (unsigned)std::min<size_t>(t, n / kMin + 1);
+    const size_t per = (n + t - 1) / t;
+    std::vector<std::thread> th;
+    for (unsigned k = 0; k < t; k++) {
+        const size_t lo = k * per, hi = std::min(n, lo + per);
+        if (lo >= hi) break;
+        th.emplace_back([=] { memcpy((char*)dst + lo, (const char*)src + lo, hi - lo); });
+    }
+    for (auto& x : th) x.join();
+}
+
+int grow_pinned(hd_ctx* ctx, void** p, size_t* cap, size_t need) {
+    if (need <= *cap) return HD_OK;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    const size_t want = need + need / 4;
+    HCHK(hipHostMalloc(p, want, hipHostMallocDefault), "pinned staging");
+    *cap = want;
+    return HD_OK;
+}
+
+// wait for the slot's ticket and deliver its staged outputs
+int complete(hd_ctx* ctx, HostSlot& s) {
+    if (!s.ticket) return HD_OK;
+    HCHK(hipEventSynchronize(s.done), "host pipeline wait");
+    for (const auto& c : s.deliver) par_copy(c.dst, c.src, c.n);
+    s.deliver.clear();
+    s.ticket = 0;
+    return HD_OK;
+}
+
+int slot_init(hd_ctx* ctx, HostSlot& s) {
+    if (s.stream) return HD_OK;
+    HCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "host pipeline stream");
+    HCHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "host pipeline event");
+    return HD_OK;
+}
+
+}  // namespace
+
+void hd_host_release(hd_ctx* ctx) {
+    HostPipe* p = ctx ? ctx->host : nullptr;
+    if (!p) return;
+    for (HostSlot& s : p->slot) {
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
+        for (DevBuf& b : s.col)
+            if (b.p) (void)hipFree(b.p);
+        for (DevBuf* b : {&s.verdict, &s.rec, &s.bitmap})
+            if (b->p) (void)hipFree(b->p);
+        if (s.hin) (void)hipHostFree(s.hin);
+        if (s.hout) (void)hipHostFree(s.hout);
+        if (s.done) (void)hipEventDestroy(s.done);
+        if (s.stream) (void)hipStreamDestroy(s.stream);
+    }
+    delete p;
+    ctx->host = nullptr;
+}
+
+extern "C" {
+
+int hd_verify_submit(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8_t* recovered32,
+                     uint32_t* valid_bitmap, uint64_t* ticket) {
+    if (!ctx || !batch || !verdict || !ticket) return HD_EINVAL;
+    if (batch->n && (!batch->type || !batch->height || !batch->round || !batch->value32 || !batch->from32 ||
+                     !batch->sig65))
+        return HD_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    if (!ctx->host) ctx->host = new (std::nothrow) HostPipe();
+    if (!ctx->host) return HD_ENOMEM;
+    HostPipe* p = ctx->host;
+    const uint64_t t = p->next++;
+    HostSlot& s = p->slot[(t - 1) % HD_HOST_SLOTS];
+    int rc = complete(ctx, s);
+    if (rc) return rc;
+    if ((rc = slot_init(ctx, s))) return rc;
+    *ticket = t;
+    const uint32_t n = batch->n;
+    if (n == 0) return HD_OK;
+    // inputs: pinned columns by DMA, pageable ones through the staging
+    struct Col { const void* src; size_t sz; };
+    const Col cols[HC_N] = {{batch->type, n},
+                            {batch->height, 8 * (size_t)n},
+                            {batch->round, 8 * (size_t)n},
+                            {batch->valid_round, 8 * (size_t)n},
+                            {batch->value32, 32 * (size_t)n},
+                            {batch->from32, 32 * (size_t)n},
+                            {batch->sig65, 65 * (size_t)n}};
+    size_t stage = 0;
+    bool pinned[HC_N];
+    for (int k = 0; k < HC_N; k++) {
+        pinned[k] = cols[k].src && is_pinned(cols[k].src);
+        if (cols[k].src && !pinned[k]) stage += (cols[k].sz + 255) & ~(size_t)255;
+    }
+    if (stage && (rc = grow_pinned(ctx, &s.hin, &s.hin_cap, stage))) return rc;
+    const void* dst[HC_N];
+    size_t off = 0;
+    for (int k = 0; k < HC_N; k++) {
+        dst[k] = nullptr;
+        if (!cols[k].src) continue;
+        if ((rc = hd_dev_grow(ctx, &s.col[k].p, &s.col[k].cap, cols[k].sz))) return rc;
+        const void* src = cols[k].src;
+        if (!pinned[k]) {
+            void* st = (char*)s.hin + off;
+            par_copy(st, src, cols[k].sz);
+            off += (cols[k].sz + 255) & ~(size_t)255;
+            src = st;
+        }
+        HCHK(hipMemcpyAsync(s.col[k].p, src, cols[k].sz, hipMemcpyHostToDevice, s.stream), "submit upload");
+        dst[k] = s.col[k].p;
+    }
+    hd_batch db{n,
+                (const uint8_t*)dst[HC_TYPE],
+                (const int64_t*)dst[HC_H],
+                (const int64_t*)dst[HC_R],
+                (const int64_t*)dst[HC_VR],
+                (const uint8_t*)dst[HC_VALUE],
+                (const uint8_t*)dst[HC_FROM],
+                (const uint8_t*)dst[HC_SIG]};
+    const size_t nwords = (n + 31) / 32;
+    if ((rc = hd_dev_grow(ctx, &s.verdict.p, &s.verdict.cap, n))) return rc;
+    if (recovered32 && (rc = hd_dev_grow(ctx, &s.rec.p, &s.rec.cap, 32 * (size_t)n))) return rc;
+    if (valid_bitmap && (rc = hd_dev_grow(ctx, &s.bitmap.p, &s.bitmap.cap, 4 * nwords))) return rc;
+    rc = hd_verify_batch_device(ctx, &db, (uint8_t*)s.verdict.p, recovered32 ? (uint8_t*)s.rec.p : nullptr, nullptr,
+                                valid_bitmap ? (uint32_t*)s.bitmap.p : nullptr, s.stream);
+    if (rc) return rc;
+    // outputs: straight into pinned caller buffers, else into staging and
+    // copied at completion
+    struct Out { void* dst; const void* dev; size_t sz; };
+    const Out outs[3] = {{verdict, s.verdict.p, n},
+                         {recovered32, s.rec.p, 32 * (size_t)n},
+                         {valid_bitmap, s.bitmap.p, 4 * nwords}};
+    size_t ostage = 0;
+    for (const Out& o : outs)
+        if (o.dst && !is_pinned(o.dst)) ostage += (o.sz + 255) & ~(size_t)255;
+    if (ostage && (rc = grow_pinned(ctx, &s.hout, &s.hout_cap, ostage))) return rc;
+    off = 0;
+    s.deliver.clear();
+    for (const Out& o : outs) {
+        if (!o.dst) continue;
+        if (is_pinned(o.dst)) {
+            HCHK(hipMemcpyAsync(o.dst, o.dev, o.sz, hipMemcpyDeviceToHost, s.stream), "submit download");
+        } else {
+            void* st = (char*)s.hout + off;
+            off += (o.sz + 255) & ~(size_t)255;
+            HCHK(hipMemcpyAsync(st, o.dev, o.sz, hipMemcpyDeviceToHost, s.stream), "submit download");
+            s.deliver.push_back({o.dst, st, o.sz});
+        }
+    }
+    HCHK(hipEventRecord(s.done, s.stream), "submit record");
+    s.ticket = t;
+    return HD_OK;
+}
+
+int hd_verify_wait(hd_ctx* ctx, uint64_t ticket) {
+    if (!ctx || ticket == 0) return HD_EINVAL;
+    if (!ctx->host) return ticket == 0 ? HD_EINVAL : HD_OK;
+    (void)hipSetDevice(ctx->device);
+    for (HostSlot& s : ctx->host->slot)
+        if (s.ticket == ticket) return complete(ctx, s);
+    return ticket < ctx->host->next ? HD_OK : HD_EINVAL;
+}
+
+int hd_host_alloc(size_t bytes, void** out) {
+    if (!out) return HD_EINVAL;
+    *out = nullptr;
+    if (hipHostMalloc(out, std::max<size_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) return HD_ENOMEM;
+    return HD_OK;
+}
+
+int hd_host_free(void* p) {
+    if (!p) return HD_OK;
+    return hipHostFree(p) == hipSuccess ? HD_OK : HD_EINVAL;
+}
+
+}  // extern "C"

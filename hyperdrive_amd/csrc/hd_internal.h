@@ -29,6 +29,7 @@ struct DevBuf {
 };
 
 struct TallyWork;  // hd_tally.hip
+struct HostPipe;   // hd_host.hip: hd_verify_submit pipelines
 struct FbWork;     // hd_fastverify.hip: known-key tables and fast-path scratch
 
 struct hd_ctx {
@@ -48,6 +49,7 @@ struct hd_ctx {
     FbWork* fb = nullptr;
     bool fastpath = true;   // known-key fast path (HD_VERIFY_FASTPATH=0 disables)
     hipEvent_t ev_slow = nullptr;   // after the last full-recovery-only verify call (fast path off)
+    HostPipe* host = nullptr;
     std::string last_error;
 };
 
@@ -62,6 +64,7 @@ int hd_dev_grow(hd_ctx* ctx, void** p, size_t* cap, size_t need);
 int hd_upload_batch(hd_ctx* ctx, const hd_batch* hb, hd_batch* db);
 int hd_verify_uploaded(hd_ctx* ctx, const hd_batch* db, uint8_t* verdict, uint8_t* recovered32, uint32_t* valid_bitmap);
 void hd_tally_release(hd_ctx* ctx);
+void hd_host_release(hd_ctx* ctx);
 
 // known-key fast path (hd_fastverify.hip)
 int hd_fb_init(hd_ctx* ctx);                    // tables of G (slot 0); at context creation

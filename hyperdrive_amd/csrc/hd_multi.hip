@@ -5,19 +5,21 @@
 // and one RCCL communicator over the devices (ncclCommInitAll: the
 // single-process, multi-device form a cgo caller -- one Go Replica -- needs).
 // Per hd_multi_verify_batch:
-//   1. device k uploads the batch metadata (type, height, round, valid round,
-//      value, From: 81 B/message, replicated -- the tally needs every round's
-//      messages) and the signatures of its shard only;
-//   2. device k verifies its contiguous, 32-aligned shard (the known-key
-//      check / full recovery of hd_verify_batch_device), writing its bitmap
-//      words in place into a whole-batch bitmap;
-//   3. one in-place ncclAllGather of those words over xGMI (the only
-//      collective on the data path) gives every device the whole bitmap;
-//   4. device k tallies only the rounds hd_tally_partition_of gives it
-//      (hd_tally_device_bitmap_part); the host merges the small per-device
-//      tables in first-batch-index order -- the single-device output.
+//   1. device k uploads its contiguous, 32-aligned shard only (every column:
+//      146 B per message, 1/G of the batch per device over PCIe);
+//   2. device k verifies it (the known-key check / full recovery of
+//      hd_verify_batch_device): verdicts, signatories, its bitmap words;
+//   3. with a tally: device k routes its shard's candidates (VALID Prevotes /
+//      Precommits) to the owners of their rounds (hd_route_candidates_device,
+//      64-byte rows); one grouped ncclSend / ncclRecv moves every group over
+//      xGMI (the only collective on the data path); device o rebuilds a batch
+//      from what it received, in global index order, and tallies it
+//      (hd_unroute_device + hd_tally_routed_device);
+//   4. the host merges the owners' disjoint tables in first-batch-index order
+//      -- the single-device output -- and scatters their per-row dup
+//      classification to the global indices (3 for non-candidates).
 // RCCL takes one rank per device; when a device is listed twice (e.g. two
-// contexts on one GPU in a test) step 3 is done with device-to-device copies.
+// contexts on one GPU in a test) step 3 moves the groups with device copies.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -38,12 +40,15 @@ struct Dev {
     hd_ctx* ctx = nullptr;
     int device = 0;
     hipStream_t stream = nullptr;   // the ctx's stream
-    DevBuf sig, verdict, rec, bitmap;
+    DevBuf verdict, rec, bitmap;
+    DevBuf rows, recv, gidx, rb[5];  // route rows out / in, global indices, the rebuilt batch (type h r value from)
     uint32_t lo = 0, hi = 0;        // shard
-    // this device's tally partition (host)
+    std::vector<uint32_t> counts;   // route rows per owner
+    uint32_t m = 0;                 // rows received
+    // this device's tally of the rounds it owns (host)
     std::vector<int64_t> ch, cr, hh, hr;
     std::vector<uint8_t> ct, dup;
-    std::vector<uint32_t> crep, cn, hprev, hprec, hany, hrep;
+    std::vector<uint32_t> crep, cn, hprev, hprec, hany, hrep, gidx_h;
     uint32_t n_counts = 0, n_hr = 0;
     int rc = HD_OK;
 };
@@ -75,60 +80,83 @@ void shard(uint32_t n, int G, int k, uint32_t* lo, uint32_t* hi, uint32_t* per) 
     *hi = std::min<uint64_t>(n, (uint64_t)*lo + p);
 }
 
-// steps 1-2 on device d
-int verify_shard(Dev& d, const hd_batch* hb, uint32_t words_per_shard, int G, int k, bool want_rec, hd_batch* dfull) {
+// steps 1-2 on device d: its shard only
+int verify_shard(Dev& d, const hd_batch* hb, bool want_rec, hd_batch* dshard) {
     (void)hipSetDevice(d.device);
-    hd_batch meta = *hb;
-    meta.sig65 = nullptr;
-    int rc = hd_upload_batch(d.ctx, &meta, dfull);
-    if (rc) return rc;
     const uint32_t m = d.hi - d.lo;
-    const size_t words = (size_t)words_per_shard * G;
-    if ((rc = hd_dev_grow(d.ctx, &d.bitmap.p, &d.bitmap.cap, 4 * words))) return rc;
-    MCHK(hipMemsetAsync(d.bitmap.p, 0, 4 * words, d.stream), "clear bitmap");
+    dshard->n = 0;
     if (m == 0) return HD_OK;
-    if ((rc = hd_dev_grow(d.ctx, &d.sig.p, &d.sig.cap, 65 * (size_t)m))) return rc;
-    if ((rc = hd_dev_grow(d.ctx, &d.verdict.p, &d.verdict.cap, m))) return rc;
-    if (want_rec && (rc = hd_dev_grow(d.ctx, &d.rec.p, &d.rec.cap, 32 * (size_t)m))) return rc;
-    MCHK(hipMemcpyAsync(d.sig.p, hb->sig65 + 65 * (size_t)d.lo, 65 * (size_t)m, hipMemcpyHostToDevice, d.stream),
-         "signature upload");
     const size_t lo = d.lo;
     hd_batch sh{m,
-                dfull->type + lo,
-                dfull->height + lo,
-                dfull->round + lo,
-                dfull->valid_round ? dfull->valid_round + lo : nullptr,
-                dfull->value32 + 32 * lo,
-                dfull->from32 + 32 * lo,
-                (const uint8_t*)d.sig.p};
-    uint32_t* bits = (uint32_t*)d.bitmap.p + (size_t)words_per_shard * k;
-    rc = hd_verify_batch_device(d.ctx, &sh, (uint8_t*)d.verdict.p, want_rec ? (uint8_t*)d.rec.p : nullptr, nullptr,
-                                bits, d.stream);
+                hb->type + lo,
+                hb->height + lo,
+                hb->round + lo,
+                hb->valid_round ? hb->valid_round + lo : nullptr,
+                hb->value32 + 32 * lo,
+                hb->from32 + 32 * lo,
+                hb->sig65 + 65 * lo};
+    int rc = hd_upload_batch(d.ctx, &sh, dshard);
+    if (rc) return rc;
+    if ((rc = hd_dev_grow(d.ctx, &d.bitmap.p, &d.bitmap.cap, 4 * (size_t)((m + 31) / 32)))) return rc;
+    if ((rc = hd_dev_grow(d.ctx, &d.verdict.p, &d.verdict.cap, m))) return rc;
+    if (want_rec && (rc = hd_dev_grow(d.ctx, &d.rec.p, &d.rec.cap, 32 * (size_t)m))) return rc;
+    rc = hd_verify_batch_device(d.ctx, dshard, (uint8_t*)d.verdict.p, want_rec ? (uint8_t*)d.rec.p : nullptr, nullptr,
+                                (uint32_t*)d.bitmap.p, d.stream);
     if (rc) return rc;
     MCHK(hipStreamSynchronize(d.stream), "verify sync");
     return HD_OK;
 }
 
-// step 4 on device d: its partition of the rounds, into host vectors
-int tally_part(Dev& d, const hd_batch* dfull, int G, int k) {
+// step 3a on device d: its candidates as route rows, grouped by owner
+int route_shard(Dev& d, const hd_batch* dshard, int G) {
     (void)hipSetDevice(d.device);
-    const uint32_t n = dfull->n;
-    d.ch.resize(n); d.cr.resize(n); d.ct.resize(n); d.crep.resize(n); d.cn.resize(n);
-    d.hh.resize(n); d.hr.resize(n); d.hprev.resize(n); d.hprec.resize(n); d.hany.resize(n); d.hrep.resize(n);
-    d.dup.resize(n);
-    hd_tally_out o{};
-    o.cap_counts = n;
-    o.count_height = d.ch.data(); o.count_round = d.cr.data(); o.count_type = d.ct.data();
-    o.count_rep = d.crep.data(); o.count_n = d.cn.data();
-    o.cap_hr = n;
-    o.hr_height = d.hh.data(); o.hr_round = d.hr.data(); o.hr_prevotes = d.hprev.data();
-    o.hr_precommits = d.hprec.data(); o.hr_any = d.hany.data(); o.hr_rep = d.hrep.data();
-    o.dup = d.dup.data();
-    const int rc = hd_tally_device_bitmap_part(d.ctx, dfull, (const uint32_t*)d.bitmap.p, (uint32_t)k, (uint32_t)G, &o,
-                                               d.stream);
-    d.n_counts = o.n_counts;
-    d.n_hr = o.n_hr;
-    return rc;
+    d.counts.assign(G, 0);
+    const uint32_t m = d.hi - d.lo;
+    if (m == 0) return HD_OK;
+    int rc = hd_dev_grow(d.ctx, &d.rows.p, &d.rows.cap, (size_t)HD_ROUTE_ROW_BYTES * m);
+    if (rc) return rc;
+    return hd_route_candidates_device(d.ctx, dshard, (const uint32_t*)d.bitmap.p, d.lo, (uint32_t)G,
+                                      (uint8_t*)d.rows.p, m, d.counts.data(), d.stream);
+}
+
+// step 3c on device d: the received rows -> a batch -> the tally of its
+// rounds (host vectors sized by what it received)
+int tally_owned(Dev& d, bool want_dup) {
+    (void)hipSetDevice(d.device);
+    const uint32_t m = d.m;
+    d.n_counts = d.n_hr = 0;
+    if (m == 0) return HD_OK;
+    const size_t sz[5] = {m, 8 * (size_t)m, 8 * (size_t)m, 32 * (size_t)m, 32 * (size_t)m};
+    for (int k = 0; k < 5; k++) {
+        const int rc = hd_dev_grow(d.ctx, &d.rb[k].p, &d.rb[k].cap, sz[k]);
+        if (rc) return rc;
+    }
+    int rc = hd_dev_grow(d.ctx, &d.gidx.p, &d.gidx.cap, 4 * (size_t)m);
+    if (rc) return rc;
+    hd_batch_out o{(uint8_t*)d.rb[0].p, (int64_t*)d.rb[1].p, (int64_t*)d.rb[2].p, nullptr, (uint8_t*)d.rb[3].p,
+                   (uint8_t*)d.rb[4].p, nullptr, nullptr};
+    rc = hd_unroute_device(d.ctx, (const uint8_t*)d.recv.p, m, &o, (uint32_t*)d.gidx.p, d.stream);
+    if (rc) return rc;
+    hd_batch b{m, o.type, o.height, o.round, nullptr, o.value32, o.from32, nullptr};
+    d.ch.resize(m); d.cr.resize(m); d.ct.resize(m); d.crep.resize(m); d.cn.resize(m);
+    d.hh.resize(m); d.hr.resize(m); d.hprev.resize(m); d.hprec.resize(m); d.hany.resize(m); d.hrep.resize(m);
+    d.dup.resize(want_dup ? m : 0);
+    hd_tally_out t{};
+    t.cap_counts = m;
+    t.count_height = d.ch.data(); t.count_round = d.cr.data(); t.count_type = d.ct.data();
+    t.count_rep = d.crep.data(); t.count_n = d.cn.data();
+    t.cap_hr = m;
+    t.hr_height = d.hh.data(); t.hr_round = d.hr.data(); t.hr_prevotes = d.hprev.data();
+    t.hr_precommits = d.hprec.data(); t.hr_any = d.hany.data(); t.hr_rep = d.hrep.data();
+    t.dup = want_dup ? d.dup.data() : nullptr;
+    rc = hd_tally_routed_device(d.ctx, &b, (const uint32_t*)d.gidx.p, &t, d.stream);
+    d.n_counts = t.n_counts;
+    d.n_hr = t.n_hr;
+    if (rc || !want_dup) return rc;
+    d.gidx_h.resize(m);
+    MCHK(hipMemcpyAsync(d.gidx_h.data(), d.gidx.p, 4 * (size_t)m, hipMemcpyDeviceToHost, d.stream), "gidx download");
+    MCHK(hipStreamSynchronize(d.stream), "gidx download");
+    return HD_OK;
 }
 
 template <typename F>
@@ -177,10 +205,10 @@ int merge_tally(hd_multi* m, uint32_t n, hd_tally_out* out) {
         if (out->hr_rep) out->hr_rep[j] = d.hrep[r];
     }
     if (out->dup) {
-        // a partition that does not own a message's round reports 3
+        // non-candidates 3; each owner's rows at their global indices
         memset(out->dup, 3, n);
         for (const Dev& d : m->dev)
-            for (uint32_t i = 0; i < n; i++) out->dup[i] = std::min(out->dup[i], d.dup[i]);
+            for (size_t j = 0; j < d.dup.size(); j++) out->dup[d.gidx_h[j]] = d.dup[j];
     }
     return HD_OK;
 }
@@ -231,8 +259,10 @@ int hd_multi_destroy(hd_multi* m) {
         if (!d.ctx) continue;
         (void)hipSetDevice(d.device);
         (void)hipStreamSynchronize(d.stream);
-        for (DevBuf* b : {&d.sig, &d.verdict, &d.rec, &d.bitmap})
+        for (DevBuf* b : {&d.verdict, &d.rec, &d.bitmap, &d.rows, &d.recv, &d.gidx})
             if (b->p) (void)hipFree(b->p);
+        for (DevBuf& b : d.rb)
+            if (b.p) (void)hipFree(b.p);
         hd_ctx_destroy(d.ctx);
     }
     delete m;
@@ -280,63 +310,88 @@ int hd_multi_verify_batch(hd_multi* m, const hd_batch* batch, uint8_t* verdict, 
     const int G = (int)m->dev.size();
     uint32_t per = 0;
     for (int k = 0; k < G; k++) shard(n, G, k, &m->dev[k].lo, &m->dev[k].hi, &per);
-    const uint32_t wps = per / 32;   // bitmap words per shard
-    std::vector<hd_batch> dfull(G);
-    // 1-2: upload and verify every shard, one host thread per device
-    int rc = on_all_devices(m, [&](Dev& d, int k) {
-        return verify_shard(d, batch, wps, G, k, recovered32 != nullptr, &dfull[k]);
-    });
+    std::vector<hd_batch> dshard(G);
+    // 1-2: every shard uploaded to and verified on its device
+    int rc = on_all_devices(m, [&](Dev& d, int k) { return verify_shard(d, batch, recovered32 != nullptr, &dshard[k]); });
     if (rc) return rc;
-    // 3: every device gets the whole bitmap
-    if (G > 1) {
-        if (!m->comm.empty()) {
-            if (ncclGroupStart() != ncclSuccess) return HD_EDEVICE;
-            for (int k = 0; k < G; k++) {
-                Dev& d = m->dev[k];
-                uint32_t* bm = (uint32_t*)d.bitmap.p;
-                if (ncclAllGather(bm + (size_t)wps * k, bm, wps, ncclUint32, m->comm[k], d.stream) != ncclSuccess) {
-                    (void)ncclGroupEnd();
-                    return HD_EDEVICE;
-                }
-            }
-            if (ncclGroupEnd() != ncclSuccess) return HD_EDEVICE;
-        } else {
-            for (int k = 0; k < G; k++)
-                for (int j = 0; j < G; j++) {
-                    if (j == k) continue;
-                    Dev& d = m->dev[k];
-                    const size_t off = (size_t)wps * j;
-                    MCHK(hipMemcpyPeerAsync((uint32_t*)d.bitmap.p + off, d.device,
-                                            (const uint32_t*)m->dev[j].bitmap.p + off, m->dev[j].device, 4 * (size_t)wps,
-                                            d.stream),
-                         "bitmap exchange");
-                }
-        }
-        for (Dev& d : m->dev) {
-            (void)hipSetDevice(d.device);
-            MCHK(hipStreamSynchronize(d.stream), "bitmap exchange sync");
-        }
-    }
-    // outputs of the shards
+    // outputs of the shards (the bitmap words of a shard are its own: shards
+    // are whole words except the last)
     for (int k = 0; k < G; k++) {
         Dev& d = m->dev[k];
         const uint32_t len = d.hi - d.lo;
         if (!len) continue;
         (void)hipSetDevice(d.device);
-        MCHK(hipMemcpy(verdict + d.lo, d.verdict.p, len, hipMemcpyDeviceToHost), "verdict download");
+        MCHK(hipMemcpyAsync(verdict + d.lo, d.verdict.p, len, hipMemcpyDeviceToHost, d.stream), "verdict download");
         if (recovered32)
-            MCHK(hipMemcpy(recovered32 + 32 * (size_t)d.lo, d.rec.p, 32 * (size_t)len, hipMemcpyDeviceToHost),
+            MCHK(hipMemcpyAsync(recovered32 + 32 * (size_t)d.lo, d.rec.p, 32 * (size_t)len, hipMemcpyDeviceToHost,
+                                d.stream),
                  "recovered download");
+        if (valid_bitmap)
+            MCHK(hipMemcpyAsync(valid_bitmap + d.lo / 32, d.bitmap.p, 4 * (size_t)((len + 31) / 32),
+                                hipMemcpyDeviceToHost, d.stream),
+                 "bitmap download");
     }
-    if (valid_bitmap) {
-        Dev& d = m->dev[0];
+    for (Dev& d : m->dev) {
         (void)hipSetDevice(d.device);
-        MCHK(hipMemcpy(valid_bitmap, d.bitmap.p, 4 * (size_t)((n + 31) / 32), hipMemcpyDeviceToHost),
-             "bitmap download");
+        MCHK(hipStreamSynchronize(d.stream), "output download");
     }
     if (!tally) return HD_OK;
-    // 4: each device its rounds; merged on the host
-    rc = on_all_devices(m, [&](Dev& d, int k) { return tally_part(d, &dfull[k], G, k); });
+    // 3a: candidates -> route rows grouped by owner
+    rc = on_all_devices(m, [&](Dev& d, int k) { return route_shard(d, &dshard[k], G); });
+    if (rc) return rc;
+    // 3b: the groups to their owners, source-rank order (= global index order)
+    std::vector<std::vector<size_t>> soff(G, std::vector<size_t>(G + 1, 0)), roff(G, std::vector<size_t>(G + 1, 0));
+    for (int k = 0; k < G; k++)
+        for (int o = 0; o < G; o++) {
+            soff[k][o + 1] = soff[k][o] + m->dev[k].counts[o];
+            roff[o][k + 1] = roff[o][k] + m->dev[k].counts[o];
+        }
+    const size_t RB = HD_ROUTE_ROW_BYTES;
+    for (int o = 0; o < G; o++) {
+        Dev& d = m->dev[o];
+        d.m = (uint32_t)roff[o][G];
+        (void)hipSetDevice(d.device);
+        if ((rc = hd_dev_grow(d.ctx, &d.recv.p, &d.recv.cap, RB * std::max<size_t>(d.m, 1)))) return rc;
+    }
+    if (!m->comm.empty()) {
+        if (ncclGroupStart() != ncclSuccess) return HD_EDEVICE;
+        for (int k = 0; k < G; k++) {
+            Dev& d = m->dev[k];
+            for (int o = 0; o < G; o++) {
+                const size_t c = m->dev[k].counts[o];   // k -> o
+                const size_t r = m->dev[o].counts[k];   // o -> k
+                if (c && ncclSend((const char*)d.rows.p + RB * soff[k][o], RB * c, ncclUint8, o, m->comm[k], d.stream) !=
+                             ncclSuccess) {
+                    (void)ncclGroupEnd();
+                    return HD_EDEVICE;
+                }
+                if (r && ncclRecv((char*)d.recv.p + RB * roff[k][o], RB * r, ncclUint8, o, m->comm[k], d.stream) !=
+                             ncclSuccess) {
+                    (void)ncclGroupEnd();
+                    return HD_EDEVICE;
+                }
+            }
+        }
+        if (ncclGroupEnd() != ncclSuccess) return HD_EDEVICE;
+    } else {
+        for (int k = 0; k < G; k++)
+            for (int o = 0; o < G; o++) {
+                const size_t c = m->dev[k].counts[o];
+                if (!c) continue;
+                Dev& d = m->dev[o];
+                (void)hipSetDevice(d.device);
+                MCHK(hipMemcpyPeerAsync((char*)d.recv.p + RB * roff[o][k], d.device,
+                                        (const char*)m->dev[k].rows.p + RB * soff[k][o], m->dev[k].device, RB * c,
+                                        d.stream),
+                     "route exchange");
+            }
+    }
+    for (Dev& d : m->dev) {
+        (void)hipSetDevice(d.device);
+        MCHK(hipStreamSynchronize(d.stream), "route exchange sync");
+    }
+    // 3c-4: each owner tallies its rounds; merged on the host
+    rc = on_all_devices(m, [&](Dev& d, int) { return tally_owned(d, tally->dup != nullptr); });
     if (rc) return rc;
     return merge_tally(m, n, tally);
 }

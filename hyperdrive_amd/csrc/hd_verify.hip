@@ -197,6 +197,7 @@ int hd_ctx_destroy(hd_ctx* ctx) {
         if (p) (void)hipFree(p);
     for (auto& b : ctx->bufs)
         if (b.p) (void)hipFree(b.p);
+    hd_host_release(ctx);
     hd_tally_release(ctx);
     hd_fb_release(ctx);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

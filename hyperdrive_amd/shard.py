@@ -142,6 +142,9 @@ def gather_tally_device(local, world: int, group=None):
     import torch
     import torch.distributed as dist
     dev = local["counts"].device
+    if local["counts"].is_cuda and dist.get_backend(group) == "gloo":
+        out = gather_tally_device({k: t.cpu() for k, t in local.items()}, world, group)
+        return {k: t.to(dev) for k, t in out.items()}
     sizes = torch.tensor([local["counts"].shape[0], local["hr"].shape[0]], dtype=torch.int64, device=dev)
     all_sizes = torch.empty(2 * world, dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(all_sizes, sizes, group=group)
@@ -190,6 +193,9 @@ def exchange_routed(rows, counts, world: int, group=None):
     One host read per call: the receive sizes (an all-to-all of the counts)."""
     import torch
     import torch.distributed as dist
+    if rows.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo moves host tensors only (CPU rehearsal of the multi-GPU path)
+        return exchange_routed(rows.cpu(), counts, world, group).to(rows.device)
     send = torch.tensor(counts, dtype=torch.int64, device=rows.device)
     recv = torch.empty(world, dtype=torch.int64, device=rows.device)
     dist.all_to_all_single(recv, send, group=group)

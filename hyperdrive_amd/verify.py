@@ -208,6 +208,22 @@ class Verifier:
                                               _ptr(rec) if recovered else None, _ptr(bitmap)), "hd_verify_batch")
         return VerifyResult(verdict, rec, bitmap)
 
+    def submit(self, batch: Batch, verdict: np.ndarray, recovered: Optional[np.ndarray] = None,
+               bitmap: Optional[np.ndarray] = None) -> int:
+        """Asynchronous host-buffer verification (hd_verify_submit): returns a
+        ticket; the outputs land in the given arrays by wait(ticket).  The
+        batch arrays and the outputs must stay alive (and the inputs
+        unchanged) until then; pinned arrays (torch pin_memory / pinned_empty)
+        move by DMA without a staging copy."""
+        cb = batch.c_struct()
+        t = ctypes.c_uint64()
+        self._check(self._lib.hd_verify_submit(self._ctx, ctypes.byref(cb), _ptr(verdict), _ptr(recovered),
+                                               _ptr(bitmap), ctypes.byref(t)), "hd_verify_submit")
+        return t.value
+
+    def wait(self, ticket: int) -> None:
+        self._check(self._lib.hd_verify_wait(self._ctx, int(ticket)), "hd_verify_wait")
+
     def verify_batch_device(self, dbatch: HdBatch, d_verdict: int, d_recovered: Optional[int] = None,
                             d_signer: Optional[int] = None, d_bitmap: Optional[int] = None,
                             stream: Optional[int] = None) -> None:

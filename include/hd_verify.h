@@ -148,11 +148,36 @@ int hd_verify_batch(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8_
 /* Same, with every pointer (batch fields and outputs) in device memory of the
  * ctx's device; signer (n x int32 or NULL) receives the index of From in the
  * hd_set_signatories array for VALID messages, -1 otherwise.  Enqueued on
- * `stream` (a hipStream_t, NULL = the ctx's stream); asynchronous.  Calls on
- * one context share its scratch: a call on another stream than the previous
- * call's first waits (on the device) for that call to finish. */
+ * `stream` (a hipStream_t, NULL = the ctx's stream); asynchronous.  The
+ * context keeps three scratch sets used round robin.  Once every admitted
+ * signatory's key tables are built, calls issued on different streams run
+ * concurrently on the device (a call waits only for the last call that used
+ * its scratch set), so a caller that alternates two streams fills the SIMDs
+ * one call's low-occupancy kernels leave idle; while keys are still being
+ * learned, a call on another stream first waits for the previous call. */
 int hd_verify_batch_device(hd_ctx* ctx, const hd_batch* dbatch, uint8_t* d_verdict, uint8_t* d_recovered32,
                            int32_t* d_signer, uint32_t* d_valid_bitmap, void* stream);
+
+/* Asynchronous host-buffer verification (the cgo caller's path,
+ * replica/replica.go:156-181, without its synchronous upload -> verify ->
+ * download): hd_verify_submit queues the upload of `batch`, the verification
+ * and the download of the outputs on one of the context's HD_HOST_SLOTS
+ * pipelines and returns a ticket; hd_verify_wait(ticket) blocks until the
+ * outputs are in the caller's buffers.  Consecutive submits overlap: batch
+ * k+1's upload runs under batch k's kernels, and the two pipelines' verify
+ * calls under each other.  Inputs in pinned memory (hd_host_alloc) are
+ * uploaded by DMA straight from the caller's buffers; pageable inputs are
+ * first copied into pinned staging by host threads.  The input buffers must
+ * stay unchanged, and the output buffers valid, until the ticket's wait
+ * returns.  A submit that reuses a pipeline first completes its previous
+ * ticket.  Tickets start at 1; waiting on a completed ticket returns at once. */
+#define HD_HOST_SLOTS 2
+int hd_verify_submit(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8_t* recovered32,
+                     uint32_t* valid_bitmap, uint64_t* ticket);
+int hd_verify_wait(hd_ctx* ctx, uint64_t ticket);
+/* pinned (page-locked) host memory for inputs the caller fills directly */
+int hd_host_alloc(size_t bytes, void** out);
+int hd_host_free(void* p);
 
 /* ---- tally --------------------------------------------------------------
  * Input: a batch and its verdicts.  Candidates are VALID Prevotes and
@@ -223,15 +248,17 @@ int hd_process_batch(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8
  * A context per device plus an RCCL communicator over the devices
  * (ncclCommInitAll); for one caller (a Replica) that owns several GPUs.
  * hd_multi_verify_batch = hd_process_batch over the devices: message i is
- * verified on the device whose contiguous 32-aligned shard holds i; the
- * per-device valid bitmaps are all-gathered in place over RCCL (xGMI), so
- * every device holds the whole bitmap; with `tally` non-NULL every device
- * tallies the rounds hd_tally_partition_of gives it and the host merges the
- * tables into the single-device output (same rows, same order).  Host
- * buffers, synchronous; outputs as hd_verify_batch / hd_tally.  devices:
- * ngpus ordinals (NULL: 0 .. ngpus-1); a device listed twice gets two
- * contexts and the bitmap exchange uses device copies (RCCL takes one rank
- * per device).  Not thread-safe (one hd_multi per caller thread). */
+ * uploaded to and verified on the device whose contiguous 32-aligned shard
+ * holds i (each device receives 1/G of the batch over PCIe); with `tally`
+ * non-NULL each device routes its shard's candidates to the owners of their
+ * rounds (hd_route_candidates_device) with one grouped ncclSend / ncclRecv
+ * over xGMI, every owner tallies what it received (hd_tally_routed_device)
+ * and the host merges the disjoint tables into the single-device output
+ * (same rows, same order).  Host buffers, synchronous; outputs as
+ * hd_verify_batch / hd_tally.  devices: ngpus ordinals (NULL: 0 ..
+ * ngpus-1); a device listed twice gets two contexts and the exchange uses
+ * device copies (RCCL takes one rank per device).  Not thread-safe (one
+ * hd_multi per caller thread). */
 typedef struct hd_multi hd_multi;
 int hd_multi_create(int ngpus, const int* devices, hd_multi** out);
 int hd_multi_destroy(hd_multi* m);

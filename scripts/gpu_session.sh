@@ -20,6 +20,7 @@ for step in "$@"; do
     gtest1) run pytest_gpu1 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "golden or c1 or fast_path_equals or set_change" ;;
     bench_vs1) HD_BENCH_VSTREAMS=1 run bench_vs1 300 python bench.py --no-cpu --no-aux ;;
     bench_fast) run bench_fast 300 python bench.py --no-cpu --no-aux ;;
+    trace2) run trace2 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace2 -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub ;;
     fieldbench) run fieldbench 120 scripts/fieldbench 3 ;;
     gtest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     gputest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;

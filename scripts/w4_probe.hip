@@ -39,8 +39,8 @@ struct PSrc {
 };
 
 template <int S>
-__host__ __device__ uint8_t stage_run(const PSrc& src, const ge* gtab, uint32_t out[16]) {
-    HD_UNROLL for (int k = 0; k < 16; k++) out[k] = 0;
+__host__ __device__ uint8_t stage_run(const PSrc& src, const ge* gtab, uint32_t out[48]) {
+    HD_UNROLL for (int k = 0; k < 48; k++) out[k] = 0;
     if (S == 3) {
         uint32_t rec[8];
         int32_t signer;
@@ -95,8 +95,70 @@ __host__ __device__ uint8_t stage_run(const PSrc& src, const ge* gtab, uint32_t 
         HD_UNROLL for (int k = 0; k < 8; k++) { out[k] = u1.v[k]; out[8 + k] = u2.v[k]; }
         return 0;
     }
+    if (S == 10) {   // build_rtab_iso
+        ge rt[HD_RTAB_N], lt[HD_RTAB_N];
+        fe zg;
+        build_rtab_iso(rt, lt, zg, R);
+        fe a = zg, b = rt[7].x, c = lt[3].x, d = rt[2].y, e = rt[0].x, f = lt[7].y;
+        fe_normalize(a); fe_normalize(b); fe_normalize(c); fe_normalize(d); fe_normalize(e); fe_normalize(f);
+        fe_to_le(out, a); fe_to_le(out + 8, b); fe_to_le(out + 16, c); fe_to_le(out + 24, d);
+        fe_to_le(out + 32, e); fe_to_le(out + 40, f);
+        return 0;
+    }
+    if (S == 11) {   // GLV splits
+        sc k1, k2, k3, k4;
+        sc_split_lambda(k1, k2, u1);
+        sc_split_lambda(k3, k4, u2);
+        HD_UNROLL for (int k = 0; k < 8; k++) {
+            out[k] = k1.v[k]; out[8 + k] = k2.v[k]; out[16 + k] = k3.v[k]; out[24 + k] = k4.v[k];
+        }
+        return 0;
+    }
+    if (S == 12) {   // Booth digits of the four halves
+        sc k1, k2;
+        uint32_t a5[5];
+        bool neg;
+        int16_t dg[88];
+        sc_split_lambda(k1, k2, u2);
+        neg = sc_signed_abs(a5, k1);
+        HD_UNROLL for (int j = 0; j < HD_GLV_NWIN_R; j++) dg[j] = (int16_t)booth_digit160<HD_WR>(a5, j, neg);
+        neg = sc_signed_abs(a5, k2);
+        HD_UNROLL for (int j = 0; j < HD_GLV_NWIN_R; j++) dg[33 + j] = (int16_t)booth_digit160<HD_WR>(a5, j, neg);
+        sc_split_lambda(k1, k2, u1);
+        neg = sc_signed_abs(a5, k1);
+        HD_UNROLL for (int j = 0; j < HD_GLV_NWIN_G; j++) dg[66 + j] = (int16_t)booth_digit160<HD_WG_GLV>(a5, j, neg);
+        neg = sc_signed_abs(a5, k2);
+        HD_UNROLL for (int j = 0; j < HD_GLV_NWIN_G; j++) dg[77 + j] = (int16_t)booth_digit160<HD_WG_GLV>(a5, j, neg);
+        HD_UNROLL for (int k = 0; k < 44; k++) out[k] = (uint32_t)(uint16_t)dg[2 * k] | ((uint32_t)(uint16_t)dg[2 * k + 1] << 16);
+        return 0;
+    }
+    if (S == 13) {   // one G addition on E' (gej_add_ge_zinv) from a doubled R
+        ge rt[HD_RTAB_N], lt[HD_RTAB_N];
+        fe zg;
+        build_rtab_iso(rt, lt, zg, R);
+        gej a, o;
+        gej_set_ge(a, rt[2]);
+        gej_dbl(a, a);
+        const ge t = gtab[5 + (d[0] & 1023u)];
+        gej_add_ge_zinv(o, a, t, zg);
+        fe x = o.x, y = o.y, z = o.z;
+        fe_normalize(x); fe_normalize(y); fe_normalize(z);
+        fe_to_le(out, x); fe_to_le(out + 8, y); fe_to_le(out + 16, z);
+        gej_add_ge(o, a, rt[5]);
+        x = o.x; y = o.y; z = o.z;
+        fe_normalize(x); fe_normalize(y); fe_normalize(z);
+        fe_to_le(out + 24, x); fe_to_le(out + 32, y); fe_to_le(out + 40, z);
+        return 0;
+    }
     gej Q;
-    ecmult_glv(Q, R, u1, u2, gtab);
+    if (S == 14 || S == 15) {   // the ladder with one side only
+        sc zero;
+        HD_UNROLL for (int k = 0; k < 8; k++) zero.v[k] = 0;
+        if (S == 14) ecmult_glv(Q, R, zero, u2, gtab);
+        else ecmult_glv(Q, R, u1, zero, gtab);
+    } else {
+        ecmult_glv(Q, R, u1, u2, gtab);
+    }
     if (gej_is_inf(Q)) return 4;
     fe qx, qy;
     gej_to_ge(qx, qy, Q);
@@ -113,9 +175,9 @@ __global__ __launch_bounds__(256, W) void k_stage(uint32_t n, const uint32_t* __
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     PSrc src{dg, sig, from, i};
-    uint32_t o[16];
+    uint32_t o[48];
     const uint8_t v = stage_run<S>(src, gtab, o);
-    HD_UNROLL for (int k = 0; k < 16; k++) out[16 * (size_t)i + k] = o[k];
+    HD_UNROLL for (int k = 0; k < 48; k++) out[48 * (size_t)i + k] = o[k];
     verdict[i] = v;
 }
 
@@ -123,10 +185,10 @@ template <int W>
 static void launch(int stage, uint32_t n, const uint32_t* dg, const uint8_t* sig, const uint8_t* from,
                    const ge* gtab, uint32_t* out, uint8_t* verdict) {
     const uint32_t b = (n + 255) / 256;
-    if (stage == 0) k_stage<W, 0><<<b, 256>>>(n, dg, sig, from, gtab, out, verdict);
-    else if (stage == 1) k_stage<W, 1><<<b, 256>>>(n, dg, sig, from, gtab, out, verdict);
-    else if (stage == 2) k_stage<W, 2><<<b, 256>>>(n, dg, sig, from, gtab, out, verdict);
-    else k_stage<W, 3><<<b, 256>>>(n, dg, sig, from, gtab, out, verdict);
+#define HD_ST(S) else if (stage == S) k_stage<W, S><<<b, 256>>>(n, dg, sig, from, gtab, out, verdict)
+    if (0) {}
+    HD_ST(0); HD_ST(1); HD_ST(2); HD_ST(3); HD_ST(10); HD_ST(11); HD_ST(12); HD_ST(13); HD_ST(14); HD_ST(15);
+#undef HD_ST
 }
 
 // host: digests (8 BE words per message), sigs (65 B), froms (32 B) -> out
@@ -142,7 +204,7 @@ extern "C" int probe_run(int waves, int stage, uint32_t n, const uint32_t* dg, c
     uint32_t *d_dg, *d_out;
     uint8_t *d_sig, *d_from, *d_v;
     if (hipMalloc(&d_tab, sizeof(ge) * tab.size()) || hipMalloc(&d_dg, 32 * (size_t)n) ||
-        hipMalloc(&d_out, 64 * (size_t)n) || hipMalloc(&d_sig, 65 * (size_t)n) ||
+        hipMalloc(&d_out, 192 * (size_t)n) || hipMalloc(&d_sig, 65 * (size_t)n) ||
         hipMalloc(&d_from, 32 * (size_t)n) || hipMalloc(&d_v, n))
         return -2;
     hipMemcpy(d_tab, tab.data(), sizeof(ge) * tab.size(), hipMemcpyHostToDevice);
@@ -152,7 +214,7 @@ extern "C" int probe_run(int waves, int stage, uint32_t n, const uint32_t* dg, c
     if (waves == 4) launch<4>(stage, n, d_dg, d_sig, d_from, d_tab, d_out, d_v);
     else launch<3>(stage, n, d_dg, d_sig, d_from, d_tab, d_out, d_v);
     hipError_t e = hipDeviceSynchronize();
-    if (e == hipSuccess) e = hipMemcpy(out, d_out, 64 * (size_t)n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(out, d_out, 192 * (size_t)n, hipMemcpyDeviceToHost);
     if (e == hipSuccess) e = hipMemcpy(verdict, d_v, n, hipMemcpyDeviceToHost);
     hipFree(d_tab);
     hipFree(d_dg);
@@ -173,13 +235,13 @@ extern "C" int probe_host(int stage, uint32_t n, const uint32_t* dg, const uint8
     }
     for (uint32_t i = 0; i < n; i++) {
         PSrc src{dg, sig, from, i};
-        uint32_t o[16];
-        uint8_t v;
-        if (stage == 0) v = stage_run<0>(src, tab.data(), o);
-        else if (stage == 1) v = stage_run<1>(src, tab.data(), o);
-        else if (stage == 2) v = stage_run<2>(src, tab.data(), o);
-        else v = stage_run<3>(src, tab.data(), o);
-        for (int k = 0; k < 16; k++) out[16 * (size_t)i + k] = o[k];
+        uint32_t o[48];
+        uint8_t v = 0;
+#define HD_ST(S) else if (stage == S) v = stage_run<S>(src, tab.data(), o)
+        if (0) {}
+        HD_ST(0); HD_ST(1); HD_ST(2); HD_ST(3); HD_ST(10); HD_ST(11); HD_ST(12); HD_ST(13); HD_ST(14); HD_ST(15);
+#undef HD_ST
+        for (int k = 0; k < 48; k++) out[48 * (size_t)i + k] = o[k];
         verdict[i] = v;
     }
     return 0;

@@ -43,16 +43,16 @@ def main():
         lib.probe_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint32] + [ctypes.c_void_p] * 5
         lib.probe_host.argtypes = [ctypes.c_int, ctypes.c_uint32] + [ctypes.c_void_p] * 5
         res = {}
-        for stage in range(4):
+        for stage in (0, 1, 2, 3, 10, 11, 12, 13, 14, 15):
             outs = {}
             for w in (3, 4):
-                out = np.zeros((n, 16), np.uint32)
+                out = np.zeros((n, 48), np.uint32)
                 ver = np.zeros(n, np.uint8)
                 rc = lib.probe_run(w, stage, n, dg.ctypes.data, sig.ctypes.data, frm.ctypes.data,
                                    out.ctypes.data, ver.ctypes.data)
                 assert rc == 0, rc
                 outs[w] = (out, ver)
-            out = np.zeros((n, 16), np.uint32)
+            out = np.zeros((n, 48), np.uint32)
             ver = np.zeros(n, np.uint8)
             lib.probe_host(stage, n, dg.ctypes.data, sig.ctypes.data, frm.ctypes.data, out.ctypes.data,
                            ver.ctypes.data)

@@ -173,3 +173,112 @@ def test_gloo_partitioned_tally_equals_single_rank(world):
     for rank, counts, hrs, n_local in res:
         assert counts == want["counts"].tolist() and hrs == want["hr"].tolist()
         assert 0 < n_local < len(want["hr"])             # every rank tallied a strict share of the rounds
+
+
+# ---- routed tally (the C4 data path: every rank holds only its shard) -------
+ROW = 64
+
+
+def route_rows_np(b, verdicts, lo, hi, nparts, adm_sorted):
+    """Restatement of hd_route_candidates_device (include/hd_verify.h) for the
+    shard [lo, hi) of an oracle batch: 64-byte rows (h, r: int64 LE; value:
+    32 B; global index: u32 LE; admitted sorted index << 8 | type: u32 LE;
+    8 zero bytes), grouped by owner, index order inside a group."""
+    groups = [[] for _ in range(nparts)]
+    index = {a: k for k, a in enumerate(adm_sorted)}
+    for i in range(lo, hi):
+        t = b.mtype[i]
+        if verdicts[i] != 0 or t not in (2, 3):
+            continue
+        o = partition_of(b.height[i], b.round[i], nparts)
+        row = (int(b.height[i]).to_bytes(8, "little", signed=True) + int(b.round[i]).to_bytes(8, "little", signed=True)
+               + b.value[i] + int(i).to_bytes(4, "little") + ((index[b.frm[i]] << 8) | t).to_bytes(4, "little")
+               + bytes(8))
+        groups[o].append(row)
+    counts = [len(g) for g in groups]
+    rows = np.frombuffer(b"".join(b"".join(g) for g in groups), np.uint8).reshape(-1, ROW).copy()
+    return rows, counts
+
+
+def unroute_np(rows, adm_sorted):
+    """Restatement of hd_unroute_device: rows -> (type, h, r, value, from, gidx) lists."""
+    out = []
+    for row in rows:
+        r = bytes(row)
+        st = int.from_bytes(r[52:56], "little")
+        out.append((st & 0xFF, int.from_bytes(r[0:8], "little", signed=True), int.from_bytes(r[8:16], "little",
+                                                                                             signed=True),
+                    r[16:48], adm_sorted[st >> 8], int.from_bytes(r[48:52], "little")))
+    return out
+
+
+class _RB:
+    """The oracle-batch face tally_rows reads."""
+
+    def __init__(self, rows):
+        self.mtype = [x[0] for x in rows]
+        self.height = [x[1] for x in rows]
+        self.round = [x[2] for x in rows]
+        self.value = [x[3] for x in rows]
+        self.frm = [x[4] for x in rows]
+
+    def __len__(self):
+        return len(self.mtype)
+
+
+def routed_tally_rows(rows, adm_sorted):
+    """The owner's tally of its received rows, reps mapped to global indices."""
+    got = unroute_np(rows, adm_sorted)
+    t = tally_rows(_RB(got), [0] * len(got))
+    g = np.array([x[5] for x in got], np.int64)
+    for key, col in (("counts", 3), ("hr", 5)):
+        if len(t[key]):
+            t[key][:, col] = g[t[key][:, col]]
+    return t
+
+
+def _routed_worker(rank, world, port, out_q):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__))))
+    from tally_cases import scenarios
+    from hyperdrive_amd.shard import exchange_routed, gather_tally_device
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sc = [s for s in scenarios() if s.name == "random_mix"][0]
+    verdicts = [0 if i % 7 else 5 for i in range(len(sc.b))]
+    adm = sorted(set(sc.b.frm))
+    lo, hi = shard_range(len(sc.b), rank, world)
+    rows, counts = route_rows_np(sc.b, verdicts, lo, hi, world, adm)
+    recv = exchange_routed(torch.from_numpy(rows), counts, world)
+    local = routed_tally_rows(recv.numpy(), adm)
+    merged = gather_tally_device({k: torch.from_numpy(v) for k, v in local.items()}, world)
+    out_q.put((rank, merged["counts"].tolist(), merged["hr"].tolist(), int(recv.shape[0]), sum(counts)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_routed_tally_equals_single_rank(world):
+    """Each rank routes only its shard's candidates to the owners of their
+    rounds (one all-to-all of the counts, one of the rows: shard.
+    exchange_routed), every owner tallies what it received, the owners'
+    tables are all-gathered and merged: the single-rank tally, row for row."""
+    from tally_cases import scenarios
+    sc = [s for s in scenarios() if s.name == "random_mix"][0]
+    verdicts = [0 if i % 7 else 5 for i in range(len(sc.b))]
+    want = tally_rows(sc.b, verdicts)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_routed_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n_cand = sum(1 for i in range(len(sc.b)) if verdicts[i] == 0 and sc.b.mtype[i] in (2, 3))
+    assert sum(r[3] for r in res) == n_cand == sum(r[4] for r in res)   # every candidate reached one owner
+    for rank, counts, hrs, n_in, n_out in res:
+        assert counts == want["counts"].tolist() and hrs == want["hr"].tolist()

@@ -85,6 +85,8 @@ SIGNATURES = {
     "hd_ctx_fastpath_geometry": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
                                                 ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "hd_ctx_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "hd_ctx_set_variant": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "hd_ctx_get_variant": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "hd_ctx_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32),
                                            ctypes.POINTER(ctypes.c_double)]),

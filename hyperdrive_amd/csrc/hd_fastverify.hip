@@ -970,10 +970,7 @@ int hd_fb_init(hd_ctx* ctx) {
     return fb_g_table(ctx, &f->gtab);
 }
 
-const gp* hd_fb_gtab(const hd_ctx* ctx) {
-    if (getenv("HD_RECOVER_GLV_G")) return nullptr;   // A/B: the GLV ladder's own G table
-    return ctx && ctx->fb ? ctx->fb->gtab : nullptr;
-}
+const gp* hd_fb_gtab(const hd_ctx* ctx) { return ctx && ctx->fb ? ctx->fb->gtab : nullptr; }
 
 void hd_fb_release(hd_ctx* ctx) {
     if (!ctx || !ctx->fb) return;
@@ -996,32 +993,18 @@ void hd_fb_release(hd_ctx* ctx) {
     ctx->fb = nullptr;
 }
 
-// messages per lane of the split check (HD_FAST_K: 4, 8, the default, or 16;
-// 0 = the paired single-kernel check k_verify_fast)
-#ifndef HD_SPLIT_K_BIG
-#define HD_SPLIT_K_BIG 16   // messages per inversion from 2^20 - 2^16 messages up (0: always 8)
-#endif
-// Messages per inversion of the split check: HD_FAST_K = 0 (the paired
-// kernel), 4, 8 or 16; unset = by batch size (split_k_for).
-static int fast_split_k() {
-    static const int k = [] {
-        const char* e = getenv("HD_FAST_K");
-        if (!e) return -1;
-        const int v = atoi(e);
-        return v <= 0 ? 0 : v <= 4 ? 4 : v <= 8 ? 8 : 16;
-    }();
-    return k;
-}
-// 16 messages per inversion from 2^20 messages up (65,536 lanes, one wave per
-// SIMD), else 8: the inversion kernels are bound by their dependent ALU
-// chains; halving the inversions outweighs the lost second wave per SIMD
-// (1M C2 messages, one box, scalars and prefixes in registers: k_fast_sinv
-// 102 -> 91 us, k_fast_zinv 91 -> 76 us from K = 8 to 16; with the rows in
-// HBM between steps K = 4 / 8 / 16 gave 177 / 111 / 90 and 166 / 102 / 85 us)
-static int split_k_for(uint32_t n) {
-    const int k = fast_split_k();
+// Messages per inversion of the split check (HD_VAR_SPLIT_K): 0 = the paired
+// kernel k_verify_fast, 4, 8 or 16; -1 (default) by batch size: 16 from
+// 2^20 - 2^16 messages up (65,536 lanes, one wave per SIMD), else 8.  The
+// inversion kernels are bound by their dependent ALU chains; halving the
+// inversions outweighs the lost second wave per SIMD (1M C2 messages, one
+// box, scalars and prefixes in registers: k_fast_sinv 102 -> 91 us,
+// k_fast_zinv 91 -> 76 us from K = 8 to 16; with the rows in HBM between
+// steps K = 4 / 8 / 16 gave 177 / 111 / 90 and 166 / 102 / 85 us)
+static int split_k_for(const hd_ctx* ctx, uint32_t n) {
+    const int k = ctx->var[HD_VAR_SPLIT_K];
     if (k >= 0) return k;
-    return HD_SPLIT_K_BIG > 0 && n >= (1u << 20) - (1u << 16) ? HD_SPLIT_K_BIG : 8;
+    return n >= (1u << 20) - (1u << 16) ? 16 : 8;
 }
 
 // Per-key window width for an admitted set of m: the wide tables
@@ -1030,8 +1013,8 @@ static int split_k_for(uint32_t n) {
 // narrow ones.  HD_FB_PW=16|20 forces one; the paired check (HD_FAST_K=0)
 // only has the narrow form.
 static int fb_pick_width(hd_ctx* ctx, uint32_t m) {
-    if (fast_split_k() == 0) return HD_FB_W;
-    if (const char* e = getenv("HD_FB_PW")) return atoi(e) == HD_FB_WW ? HD_FB_WW : HD_FB_W;
+    if (ctx->var[HD_VAR_SPLIT_K] == 0) return HD_FB_W;
+    if (ctx->var[HD_VAR_KEY_WIDTH]) return ctx->var[HD_VAR_KEY_WIDTH];
     FbWork* f = ctx->fb;
     const double others = (double)(fb_device_bytes(ctx->device) - std::min(fb_device_bytes(ctx->device), f->bytes));
     const double need = fb_slot_bytes(HD_FB_WW) * ((double)m + 1);
@@ -1142,16 +1125,13 @@ static hipEvent_t* fb_prof_pair(std::vector<hipEvent_t>& ev, size_t& used, bool 
     return &ev[2 * used++];
 }
 
-// k_fast_sums occupancy (HD_SUM_WAVES: 2 or 3, the default) and prefetch
-// depth (HD_SUM_PF: 1, the default, or 2 windows ahead)
-// k_fast_sums occupancy (HD_SUM_WAVES: 2 or 3, the default), prefetch depth
-// (HD_SUM_PF: 1, the default, or 2 windows ahead) and where the window digits
-// come from (sums_digits_lds)
+// k_fast_sums occupancy (HD_VAR_SUM_WAVES), prefetch depth
+// (HD_VAR_SUM_PREFETCH) and where the window digits come from (DL:
+// HD_VAR_SUM_DIGITS 0 = computed into LDS, 1 = a k_fast_digits pass)
 template <int WP, bool DL>
-static void launch_sums(uint32_t blocks, hipStream_t s, uint32_t n, const gp* gtab, const gp* const* tab,
-                        const SplitRows& rows) {
-    static const int w = getenv("HD_SUM_WAVES") ? atoi(getenv("HD_SUM_WAVES")) : 3;
-    static const int pf = getenv("HD_SUM_PF") ? atoi(getenv("HD_SUM_PF")) : 1;
+static void launch_sums(const hd_ctx* ctx, uint32_t blocks, hipStream_t s, uint32_t n, const gp* gtab,
+                        const gp* const* tab, const SplitRows& rows) {
+    const int w = ctx->var[HD_VAR_SUM_WAVES], pf = ctx->var[HD_VAR_SUM_PREFETCH];
     if (pf == 2) {
         if (w == 3) k_fast_sums<3, WP, 2, DL><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
         else k_fast_sums<2, WP, 2, DL><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
@@ -1160,12 +1140,7 @@ static void launch_sums(uint32_t blocks, hipStream_t s, uint32_t n, const gp* gt
         else k_fast_sums<3, WP, 1, DL><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
     }
 }
-// HD_SUM_DIGITS=rows: a k_fast_digits pass writes the digit rows; default:
-// k_fast_sums computes them into LDS
-static bool sums_digits_lds() {
-    static const bool lds = !(getenv("HD_SUM_DIGITS") && strcmp(getenv("HD_SUM_DIGITS"), "rows") == 0);
-    return lds;
-}
+static bool sums_digits_lds(const hd_ctx* ctx) { return ctx->var[HD_VAR_SUM_DIGITS] == 0; }
 
 template <int K, int WP>
 static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict,
@@ -1180,12 +1155,12 @@ static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest
     k_fast_prep<<<nb, 256, adm_lds, s>>>(b, d_digest, f->state, f->adm_slot, ctx->d_adm, ctx->n_adm, ctx->adm_steps,
                                          rows, adm_lds > 0);
     k_fast_sinv<K><<<tb, 256, 0, s>>>(n, T, rows);
-    const bool dl = sums_digits_lds();
+    const bool dl = sums_digits_lds(ctx);
     if (!dl) k_fast_digits<WP><<<nb, 256, 0, s>>>(n, rows);
     hipEvent_t* pe = fb_prof_pair(f->ev_sums, f->n_sums, f->prof);
     if (pe) (void)hipEventRecord(pe[0], s);
-    if (dl) launch_sums<WP, true>(nb, s, n, f->gtab, f->tabs, rows);
-    else launch_sums<WP, false>(nb, s, n, f->gtab, f->tabs, rows);
+    if (dl) launch_sums<WP, true>(ctx, nb, s, n, f->gtab, f->tabs, rows);
+    else launch_sums<WP, false>(ctx, nb, s, n, f->gtab, f->tabs, rows);
     if (pe) (void)hipEventRecord(pe[1], s);
     k_fast_zinv<K><<<tb, 256, 0, s>>>(n, T, rows);
     // whole blocks of 256: every wavefront's 64 messages are one bitmap word pair
@@ -1246,10 +1221,10 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
     const uint32_t blocks = (b.n + 255) / 256;
     const uint32_t fast_blocks = ((b.n + 1) / 2 + 255) / 256;   // two messages per lane
     FBCHK(hipMemsetAsync(sc.count, 0, 4, s), "fb count reset");
-    if (ctx->n_adm > 0 && f->adm_slot && split_k_for(b.n) > 0) {
+    if (ctx->n_adm > 0 && f->adm_slot && split_k_for(ctx, b.n) > 0) {
         // 62 words per message; the digit rows (the narrow width has more
         // windows) only for the HD_SUM_DIGITS=rows A/B form
-        const size_t row_words = 62 + (sums_digits_lds() ? 0 : FbL<HD_FB_WG>::NWIN + FbL<HD_FB_W>::NWIN);
+        const size_t row_words = 62 + (sums_digits_lds(ctx) ? 0 : FbL<HD_FB_WG>::NWIN + FbL<HD_FB_W>::NWIN);
         rc = hd_dev_grow(ctx, (void**)&sc.rows, &sc.cap_rows, 4 * row_words * (size_t)b.n);
         if (rc) return rc;
         const uint32_t n = b.n;
@@ -1261,8 +1236,8 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         rows.s = sc.rows + 18 * (size_t)n;
         rows.pre = sc.rows + 26 * (size_t)n;
         rows.xyz = sc.rows + 35 * (size_t)n;
-        rows.dig = sums_digits_lds() ? nullptr : sc.rows + 62 * (size_t)n;
-        const int k = split_k_for(n);
+        rows.dig = sums_digits_lds(ctx) ? nullptr : sc.rows + 62 * (size_t)n;
+        const int k = split_k_for(ctx, n);
         f->last_k = k;
 #define HD_SPLIT(K, WP) launch_split<K, WP>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, sc, s)
         if (f->wp == HD_FB_WW) {
@@ -1285,7 +1260,7 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         return fb_learn(ctx, s);
     }
     if (ctx->n_adm > 0 && f->adm_slot) {
-        static const int fw = getenv("HD_FAST_WAVES") ? atoi(getenv("HD_FAST_WAVES")) : 2;
+        const int fw = ctx->var[HD_VAR_FAST_WAVES];
 #define HD_LAUNCH_FAST(W)                                                                                        \
     k_verify_fast<W><<<fast_blocks, 256, 0, s>>>(b, d_digest, f->gtab, f->tabs, f->state, f->adm_slot, ctx->d_adm, ctx->d_adm_perm, \
                                             ctx->n_adm, ctx->adm_steps, d_verdict, d_rec32, d_signer, sc.slow,       \

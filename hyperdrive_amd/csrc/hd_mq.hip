@@ -18,10 +18,15 @@
 // batch's min and cut to their significant bits, so a typical insert costs a
 // handful of 8-bit digit passes -- and keeps each sender's first max_capacity
 // elements: exactly the result of inserting one message at a time with
-// mq.go:133-142's truncation.  Consume(h) and DropMessagesBelowHeight(h) are
-// order-preserving partitions (each sender's consumed messages are a prefix of
-// its run, mq.go:38-41); Consume delivers only senders in procsAllowed
-// (mq.go:49-51), evaluated against the set given at that call.
+// mq.go:133-142's truncation.  Consume(h) and DropMessagesBelowHeight(h)
+// remove a prefix of every sender's run (mq.go:38-41, 70-83), so they only
+// move per-sender head offsets: one single-block kernel binary-searches each
+// run for the cut and scans the delivered counts, one kernel gathers the
+// delivered prefixes (of senders in procsAllowed, mq.go:49-51, evaluated
+// against the set given at that call) into a packed stage that comes back in
+// ONE copy.  The consumed prefixes are compacted away lazily, by the next
+// insert, which rebuilds the pool anyway -- a consume costs two host syncs
+// and no pass over the pool.
 #include <hip/hip_runtime.h>
 
 #include <hipcub/hipcub.hpp>
@@ -75,6 +80,26 @@ int pool_reserve(hd_ctx* ctx, Pool& p, uint32_t need) {
     p.base = base;
     p.cap = cap;
     return HD_OK;
+}
+
+// the Pool field layout inside a region of pool_bytes(cap) bytes at base
+size_t pool_bytes(uint32_t cap) { return (size_t)cap * (8 + 8 + 8 + 32 + 32 + 65 + 4 + 1) + 64; }
+Pool pool_view(void* base, uint32_t cap) {
+    Pool p;
+    const size_t c = cap;
+    char* b = (char*)base;
+    p.h = (int64_t*)b;
+    p.r = p.h + c;
+    p.vr = p.r + c;
+    p.value = (uint8_t*)(p.vr + c);
+    p.from = p.value + 32 * c;
+    p.sig = p.from + 32 * c;
+    p.sender = (int32_t*)(((uintptr_t)(p.sig + 65 * c) + 15) & ~(uintptr_t)15);
+    p.type = (uint8_t*)(p.sender + c);
+    p.base = base;
+    p.cap = cap;
+    p.n = 0;
+    return p;
 }
 
 // ---------------------------------------------------------------- senders
@@ -339,6 +364,97 @@ __global__ void k_mq_pred(uint32_t n, const int64_t* __restrict__ ph, const int3
     inv[e] = !f;
 }
 
+// per sender run of a freshly sorted pool: head = its first index, send = one
+// past its last (senders without messages keep 0, 0)
+__global__ void k_mq_runs(uint32_t M, const int32_t* __restrict__ snd, uint32_t* __restrict__ head,
+                          uint32_t* __restrict__ send) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= M) return;
+    const int32_t s = snd[k];
+    if (k == 0 || snd[k - 1] != s) head[s] = k;
+    if (k == M - 1 || snd[k + 1] != s) send[s] = k + 1;
+}
+
+// Consume / DropMessagesBelowHeight plan, one block: for each sender the cut
+// of its live run [head, send) -- the first message with height > h (consume)
+// or >= h (drop, strict) -- by binary search (a run is sorted by height);
+// removed = cut - head; delivered = removed for allowed senders (allow NULL:
+// none delivered); off = exclusive scan of delivered; totals = {delivered,
+// removed}; newhead = cut (committed by the caller once the outputs fit).
+__global__ __launch_bounds__(1024) void k_mq_plan(uint32_t nsend, const int64_t* __restrict__ ph,
+                                                  const uint32_t* __restrict__ head, const uint32_t* __restrict__ send,
+                                                  int64_t h, int strict, const uint8_t* __restrict__ allow,
+                                                  uint32_t* __restrict__ newhead, uint32_t* __restrict__ off,
+                                                  uint32_t* __restrict__ totals) {
+    typedef hipcub::BlockScan<uint32_t, 1024> Scan;
+    typedef hipcub::BlockReduce<uint32_t, 1024> Red;
+    __shared__ typename Scan::TempStorage ts;
+    __shared__ typename Red::TempStorage rs;
+    __shared__ uint32_t carry_d, carry_r;
+    if (threadIdx.x == 0) carry_d = carry_r = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < nsend; base += 1024) {
+        const uint32_t s = base + threadIdx.x;
+        uint32_t rem = 0, del = 0;
+        if (s < nsend) {
+            uint32_t lo = head[s], hi = send[s];
+            const uint32_t h0 = lo;
+            while (lo < hi) {   // first index with the height past the cut
+                const uint32_t mid = lo + (hi - lo) / 2;
+                const bool in = strict ? ph[mid] < h : ph[mid] <= h;
+                if (in) lo = mid + 1;
+                else hi = mid;
+            }
+            rem = lo - h0;
+            del = allow && allow[s] ? rem : 0u;
+            newhead[s] = lo;
+        }
+        uint32_t o = 0, agg = 0;
+        Scan(ts).ExclusiveSum(del, o, agg);
+        const uint32_t rsum = Red(rs).Sum(rem);
+        if (s < nsend) off[s] = carry_d + o;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            carry_d += agg;
+            carry_r += rsum;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        totals[0] = carry_d;
+        totals[1] = carry_r;
+    }
+}
+
+// the delivered prefixes into the packed stage: block s copies sender s's
+__global__ __launch_bounds__(256) void k_mq_take(Pool p, const uint32_t* __restrict__ head,
+                                                 const uint32_t* __restrict__ newhead, const uint32_t* __restrict__ off,
+                                                 const uint8_t* __restrict__ allow, Pool d) {
+    const uint32_t s = blockIdx.x;
+    if (!allow[s]) return;
+    const uint32_t lo = head[s], n = newhead[s] - lo, o = off[s];
+    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
+        const uint32_t e = lo + j, k = o + j;
+        d.sender[k] = p.sender[e];
+        d.type[k] = p.type[e];
+        d.h[k] = p.h[e];
+        d.r[k] = p.r[e];
+        d.vr[k] = p.vr[e];
+        for (int w = 0; w < 2; w++) {
+            reinterpret_cast<uint4*>(d.value + 32 * (size_t)k)[w] = reinterpret_cast<const uint4*>(p.value + 32 * (size_t)e)[w];
+            reinterpret_cast<uint4*>(d.from + 32 * (size_t)k)[w] = reinterpret_cast<const uint4*>(p.from + 32 * (size_t)e)[w];
+        }
+        for (int w = 0; w < 65; w++) d.sig[65 * (size_t)k + w] = p.sig[65 * (size_t)e + w];
+    }
+}
+
+// live pool entries (not in a consumed / dropped prefix)
+__global__ void k_mq_live(uint32_t M, const int32_t* __restrict__ snd, const uint32_t* __restrict__ head,
+                          uint8_t* __restrict__ keep) {
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < M) keep[e] = e >= head[snd[e]];
+}
+
 inline uint32_t nblk(uint32_t n) { return (n + 255) / 256; }
 
 int bits_of(uint64_t range) {
@@ -351,7 +467,7 @@ int bits_of(uint64_t range) {
 
 enum MqSlot { MQ_FLAG, MQ_NEWIDX, MQ_NSEL, MQ_HK, MQ_RK, MQ_SK, MQ_PERM0, MQ_PERM1, MQ_K64A, MQ_K64B, MQ_K32A, MQ_K32B,
               MQ_HEAD, MQ_KEEP, MQ_SEL, MQ_RED, MQ_TMP, MQ_SID, MQ_LSLOT, MQ_LCLAIM, MQ_LID, MQ_REPS, MQ_ALLOW,
-              MQ_LIST, MQ_DELIV, MQ_SEL2, MQ__N };
+              MQ_LIST, MQ_DELIV, MQ_SEL2, MQ_HEADS, MQ_SEND, MQ_NEWHEAD, MQ_OFF, MQ_TOT, MQ_STAGE, MQ__N };
 
 struct hd_mq {
     hd_ctx* ctx = nullptr;
@@ -365,6 +481,13 @@ struct hd_mq {
     uint32_t* slots = nullptr;  // tcap ids
     uint32_t tcap = 0;
     uint64_t seed = 0;
+    // live messages; consumed / dropped prefixes not yet compacted away
+    uint64_t live = 0;
+    bool dead = false;
+    uint32_t runs_for = 0;      // senders the head / send arrays hold
+    // pinned host stage of consume (the packed outputs + the plan totals)
+    void* hstage = nullptr;
+    size_t hstage_cap = 0;
 };
 
 #define QCHK(expr, what)                                           \
@@ -557,9 +680,42 @@ static int intern_senders(hd_mq* q, const hd_batch* b, const uint32_t* newidx, u
     return HD_OK;
 }
 
+// drop the consumed prefixes from the pool (the live count is known)
+static int mq_compact(hd_mq* q, hipStream_t s) {
+    if (!q->dead) return HD_OK;
+    const uint32_t M = q->pool.n;
+    int rc = 0;
+    uint8_t* keep = (uint8_t*)qbuf(q, MQ_KEEP, M, &rc);
+    if (rc) return rc;
+    k_mq_live<<<nblk(M), 256, 0, s>>>(M, q->pool.sender, (const uint32_t*)q->buf[MQ_HEADS].p, keep);
+    QCHK(hipGetLastError(), "k_mq_live");
+    rc = pool_filter(q, keep, s, (int64_t)q->live);
+    if (rc) return rc;
+    q->dead = false;
+    return HD_OK;
+}
+
+// per-sender runs of the (freshly sorted, compact) pool
+static int mq_runs(hd_mq* q, hipStream_t s) {
+    int rc = 0;
+    const uint32_t ns = std::max(q->nsend, 1u);
+    uint32_t* head = (uint32_t*)qbuf(q, MQ_HEADS, 4 * (size_t)ns, &rc);
+    uint32_t* send = (uint32_t*)qbuf(q, MQ_SEND, 4 * (size_t)ns, &rc);
+    if (rc) return rc;
+    QCHK(hipMemsetAsync(head, 0, 4 * (size_t)ns, s), "clear runs");
+    QCHK(hipMemsetAsync(send, 0, 4 * (size_t)ns, s), "clear runs");
+    if (q->pool.n) k_mq_runs<<<nblk(q->pool.n), 256, 0, s>>>(q->pool.n, q->pool.sender, head, send);
+    QCHK(hipGetLastError(), "k_mq_runs");
+    q->runs_for = q->nsend;
+    q->live = q->pool.n;
+    q->dead = false;
+    return HD_OK;
+}
+
 static int mq_insert_flagged(hd_mq* q, const hd_batch* d_batch, const uint8_t* flag, hipStream_t s) {
     const uint32_t nb = d_batch->n;
-    int rc = 0;
+    int rc = mq_compact(q, s);
+    if (rc) return rc;
     // 1. the batch's insertable messages, in batch order
     uint32_t* newidx = (uint32_t*)qbuf(q, MQ_NEWIDX, 4 * (size_t)nb, &rc);
     if (rc) return rc;
@@ -614,6 +770,8 @@ static int mq_insert_flagged(hd_mq* q, const hd_batch* d_batch, const uint8_t* f
     QCHK(hipGetLastError(), "mq insert kernels");
     std::swap(q->pool, q->spare);
     q->pool.n = kept;
+    rc = mq_runs(q, s);
+    if (rc) return rc;
     QCHK(hipStreamSynchronize(s), "mq insert sync");
     return HD_OK;
 }
@@ -642,13 +800,14 @@ int hd_mq_destroy(hd_mq* q) {
     if (q->slots) (void)hipFree(q->slots);
     for (auto& b : q->buf)
         if (b.p) (void)hipFree(b.p);
+    if (q->hstage) (void)hipHostFree(q->hstage);
     delete q;
     return HD_OK;
 }
 
 int hd_mq_size(hd_mq* q, uint64_t* n) {
     if (!q || !n) return HD_EINVAL;
-    *n = q->pool.n;
+    *n = q->live;
     return HD_OK;
 }
 
@@ -692,6 +851,37 @@ int hd_mq_insert_verified_device(hd_mq* q, const hd_batch* d_batch, const uint8_
     return mq_insert_flagged(q, d_batch, flag, s);
 }
 
+// the plan of a consume / drop (k_mq_plan) and its totals on the host
+static int mq_plan(hd_mq* q, int64_t h, int strict, const uint8_t* allow, uint32_t totals[2], hipStream_t s) {
+    int rc = 0;
+    const uint32_t ns = q->nsend;
+    uint32_t* newhead = (uint32_t*)qbuf(q, MQ_NEWHEAD, 4 * (size_t)ns, &rc);
+    uint32_t* off = (uint32_t*)qbuf(q, MQ_OFF, 4 * (size_t)ns, &rc);
+    uint32_t* tot = (uint32_t*)qbuf(q, MQ_TOT, 8, &rc);
+    if (rc) return rc;
+    if (q->hstage_cap < 64) {
+        QCHK(hipHostMalloc(&q->hstage, 1u << 16, hipHostMallocDefault), "mq host stage");
+        q->hstage_cap = 1u << 16;
+    }
+    k_mq_plan<<<1, 1024, 0, s>>>(ns, q->pool.h, (const uint32_t*)q->buf[MQ_HEADS].p,
+                                 (const uint32_t*)q->buf[MQ_SEND].p, h, strict, allow, newhead, off, tot);
+    QCHK(hipGetLastError(), "k_mq_plan");
+    QCHK(hipMemcpyAsync(q->hstage, tot, 8, hipMemcpyDeviceToHost, s), "plan totals");
+    QCHK(hipStreamSynchronize(s), "plan sync");
+    memcpy(totals, q->hstage, 8);
+    return HD_OK;
+}
+
+// the plan's new heads become the queue's
+static int mq_commit(hd_mq* q, uint32_t removed, hipStream_t s) {
+    if (!removed) return HD_OK;
+    QCHK(hipMemcpyAsync(q->buf[MQ_HEADS].p, q->buf[MQ_NEWHEAD].p, 4 * (size_t)q->nsend, hipMemcpyDeviceToDevice, s),
+         "commit heads");
+    q->live -= removed;
+    q->dead = true;
+    return HD_OK;
+}
+
 int hd_mq_consume(hd_mq* q, int64_t h, const uint8_t* allowed32, uint32_t n_allowed, const hd_batch_out* out,
                   int32_t* out_sender, uint32_t cap, uint32_t* n_out, uint32_t* n_removed) {
     if (!q || !out || !n_out) return HD_EINVAL;
@@ -699,8 +889,7 @@ int hd_mq_consume(hd_mq* q, int64_t h, const uint8_t* allowed32, uint32_t n_allo
     if (allowed32 == nullptr && n_allowed != 0) return HD_EINVAL;
     *n_out = 0;
     if (n_removed) *n_removed = 0;
-    const uint32_t M = q->pool.n;
-    if (M == 0) return HD_OK;
+    if (q->live == 0) return HD_OK;
     (void)hipSetDevice(q->ctx->device);
     hipStream_t s = q->ctx->stream;
     int rc = 0;
@@ -725,59 +914,58 @@ int hd_mq_consume(hd_mq* q, int64_t h, const uint8_t* allowed32, uint32_t n_allo
         be = 1;
     }
     if (na) k_mq_allow<<<nblk(na), 256, 0, s>>>(na, list, be, dict_of(q), allow);
-    uint8_t* removed = (uint8_t*)qbuf(q, MQ_FLAG, M, &rc);
-    uint8_t* deliver = (uint8_t*)qbuf(q, MQ_DELIV, M, &rc);
-    uint8_t* inv = (uint8_t*)qbuf(q, MQ_KEEP, M, &rc);
-    uint32_t* sel = (uint32_t*)qbuf(q, MQ_SEL, 4 * (size_t)M, &rc);
-    uint32_t* sel2 = (uint32_t*)qbuf(q, MQ_SEL2, 4 * (size_t)M, &rc);
-    if (rc) return rc;
-    k_mq_pred<<<nblk(M), 256, 0, s>>>(M, q->pool.h, q->pool.sender, h, 0, allow, removed, deliver, inv);
-    QCHK(hipGetLastError(), "k_mq_pred");
-    uint32_t nr = 0, c = 0;
-    rc = select_idx(q, removed, M, sel2, &nr, s, 0, false);   // counted by the next select's sync
-    if (rc) return rc;
-    rc = select_idx(q, deliver, M, sel, &c, s, 1);
-    if (rc) {
-        // the first select's count download into nr may still be in flight
-        (void)hipStreamSynchronize(s);
-        return rc;
-    }
+    uint32_t tot[2];
+    if ((rc = mq_plan(q, h, 0, allow, tot, s))) return rc;
+    const uint32_t c = tot[0], nr = tot[1];
     *n_out = c;
-    if (c > cap) return HD_ECAP;
+    if (c > cap) return HD_ECAP;   // nothing committed
     if (n_removed) *n_removed = nr;
     if (c) {
-        rc = pool_reserve(q->ctx, q->spare, c);
+        // gather into a packed stage (the Pool layout at capacity c16) and
+        // bring it back in one copy
+        const uint32_t c16 = (c + 15u) & ~15u;
+        const size_t bytes = pool_bytes(c16);
+        void* dst = qbuf(q, MQ_STAGE, bytes, &rc);
         if (rc) return rc;
-        MqSrc src{q->pool, DevBatch{}, nullptr, nullptr, M};
-        k_mq_gather<<<nblk(c), 256, 0, s>>>(src, c, sel, q->spare);
-        const Pool& d = q->spare;
+        if (q->hstage_cap < bytes) {
+            (void)hipHostFree(q->hstage);
+            q->hstage = nullptr;
+            q->hstage_cap = 0;
+            QCHK(hipHostMalloc(&q->hstage, bytes + bytes / 2, hipHostMallocDefault), "mq host stage");
+            q->hstage_cap = bytes + bytes / 2;
+        }
+        const Pool d = pool_view(dst, c16);
+        k_mq_take<<<q->nsend, 256, 0, s>>>(q->pool, (const uint32_t*)q->buf[MQ_HEADS].p,
+                                           (const uint32_t*)q->buf[MQ_NEWHEAD].p, (const uint32_t*)q->buf[MQ_OFF].p,
+                                           allow, d);
+        QCHK(hipGetLastError(), "k_mq_take");
+        QCHK(hipMemcpyAsync(q->hstage, dst, bytes, hipMemcpyDeviceToHost, s), "consume download");
+        if ((rc = mq_commit(q, nr, s))) return rc;
+        QCHK(hipStreamSynchronize(s), "consume sync");
+        const Pool hp = pool_view(q->hstage, c16);
         struct Cp { void* dst; const void* src; size_t sz; } cp[] = {
-            {out->type, d.type, (size_t)c},          {out->height, d.h, 8 * (size_t)c},
-            {out->round, d.r, 8 * (size_t)c},        {out->valid_round, d.vr, 8 * (size_t)c},
-            {out->value32, d.value, 32 * (size_t)c}, {out->from32, d.from, 32 * (size_t)c},
-            {out->sig65, d.sig, 65 * (size_t)c},     {out_sender, d.sender, 4 * (size_t)c},
+            {out->type, hp.type, (size_t)c},          {out->height, hp.h, 8 * (size_t)c},
+            {out->round, hp.r, 8 * (size_t)c},        {out->valid_round, hp.vr, 8 * (size_t)c},
+            {out->value32, hp.value, 32 * (size_t)c}, {out->from32, hp.from, 32 * (size_t)c},
+            {out->sig65, hp.sig, 65 * (size_t)c},     {out_sender, hp.sender, 4 * (size_t)c},
         };
         for (auto& x : cp)
-            if (x.dst) QCHK(hipMemcpyAsync(x.dst, x.src, x.sz, hipMemcpyDeviceToHost, s), "consume download");
+            if (x.dst) memcpy(x.dst, x.src, x.sz);
         if (out->adv_class) memset(out->adv_class, 0, c);
-        QCHK(hipStreamSynchronize(s), "consume sync");
+        return HD_OK;
     }
-    return nr ? pool_filter(q, inv, s, (int64_t)M - nr) : HD_OK;
+    return mq_commit(q, nr, s);
 }
 
 int hd_mq_drop_below(hd_mq* q, int64_t h) {
     if (!q) return HD_EINVAL;
-    const uint32_t M = q->pool.n;
-    if (M == 0) return HD_OK;
+    if (q->live == 0) return HD_OK;
     (void)hipSetDevice(q->ctx->device);
     hipStream_t s = q->ctx->stream;
-    int rc = 0;
-    uint8_t* flag = (uint8_t*)qbuf(q, MQ_FLAG, M, &rc);
-    uint8_t* inv = (uint8_t*)qbuf(q, MQ_KEEP, M, &rc);
+    uint32_t tot[2];
+    int rc = mq_plan(q, h, 1, nullptr, tot, s);
     if (rc) return rc;
-    k_mq_pred<<<nblk(M), 256, 0, s>>>(M, q->pool.h, q->pool.sender, h, 1, nullptr, flag, nullptr, inv);
-    QCHK(hipGetLastError(), "k_mq_pred");
-    return pool_filter(q, inv, s);
+    return mq_commit(q, tot[1], s);
 }
 
 }  // extern "C"

@@ -156,12 +156,16 @@ int hd_ctx_create(int device, hd_ctx** out) {
     }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->n_cu = prop.multiProcessorCount;
-    if (const char* w = getenv("HD_VERIFY_WAVES")) {
-        int v = atoi(w);
-        // 2 or 3: the 4-wave build (128 VGPRs) miscompiles the recovery
-        // (every signatory mismatched, round 2b), so it is not offered
-        if (v == 2 || v == 3) ctx->verify_waves = v;
-    }
+    // variant defaults from the environment (hd_ctx_set_variant)
+    struct { int key; const char* env; } envs[] = {
+        {HD_VAR_VERIFY_WAVES, "HD_VERIFY_WAVES"}, {HD_VAR_SUM_WAVES, "HD_SUM_WAVES"},
+        {HD_VAR_SUM_PREFETCH, "HD_SUM_PF"},       {HD_VAR_SPLIT_K, "HD_FAST_K"},
+        {HD_VAR_FAST_WAVES, "HD_FAST_WAVES"},     {HD_VAR_KEY_WIDTH, "HD_FB_PW"},
+    };
+    for (auto& ev : envs)
+        if (const char* e = getenv(ev.env)) (void)hd_ctx_set_variant(ctx, ev.key, atoi(e));
+    if (const char* e = getenv("HD_SUM_DIGITS")) (void)hd_ctx_set_variant(ctx, HD_VAR_SUM_DIGITS, strcmp(e, "rows") == 0);
+    if (getenv("HD_RECOVER_GLV_G")) (void)hd_ctx_set_variant(ctx, HD_VAR_RECOVER_G, 1);
     if (const char* f = getenv("HD_VERIFY_FASTPATH")) ctx->fastpath = atoi(f) != 0;
     // G tables (1G..2048G and lambda*(1G..2048G), affine), built once on the
     // host with the same code the device runs, then uploaded.
@@ -202,6 +206,28 @@ int hd_ctx_destroy(hd_ctx* ctx) {
     hd_fb_release(ctx);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
+    return HD_OK;
+}
+
+int hd_ctx_set_variant(hd_ctx* ctx, int which, int value) {
+    if (!ctx || which < 0 || which >= HD_VAR__COUNT) return HD_EINVAL;
+    bool ok = false;
+    switch (which) {
+        case HD_VAR_VERIFY_WAVES: case HD_VAR_SUM_WAVES: case HD_VAR_FAST_WAVES: ok = value == 2 || value == 3; break;
+        case HD_VAR_SUM_PREFETCH: ok = value == 1 || value == 2; break;
+        case HD_VAR_SUM_DIGITS: case HD_VAR_RECOVER_G: ok = value == 0 || value == 1; break;
+        case HD_VAR_SPLIT_K: ok = value == -1 || value == 0 || value == 4 || value == 8 || value == 16; break;
+        case HD_VAR_KEY_WIDTH: ok = value == 0 || value == HD_FB_W || value == HD_FB_WW; break;
+    }
+    if (!ok) return HD_EINVAL;
+    ctx->var[which] = value;
+    if (which == HD_VAR_VERIFY_WAVES) ctx->verify_waves = value;
+    return HD_OK;
+}
+
+int hd_ctx_get_variant(hd_ctx* ctx, int which, int* value) {
+    if (!ctx || !value || which < 0 || which >= HD_VAR__COUNT) return HD_EINVAL;
+    *value = ctx->var[which];
     return HD_OK;
 }
 
@@ -273,7 +299,8 @@ int hd_launch_slow(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint
                                           d_verdict, d_rec32, d_signer, d_bitmap, d_digest, ctl, fbg)
     // waves/SIMD the kernel is register-allocated for (HD_VERIFY_WAVES = 2/3, default 3)
     const int w = ctx->verify_waves;
-    const gp* fbg = hd_fb_gtab(ctx);   // the fixed-base G table, when the context has one
+    // the fixed-base G table, when the context has one (HD_VAR_RECOVER_G 0)
+    const gp* fbg = ctx->var[HD_VAR_RECOVER_G] ? nullptr : hd_fb_gtab(ctx);
     if (ctx->pkfmt == HD_PUBKEY_COMPRESSED) {
         if (w == 2) HD_LAUNCH_VERIFY(1, 2);
         else HD_LAUNCH_VERIFY(1, 3);

@@ -101,35 +101,48 @@ class MessageQueue:
         self._check(self._lib.hd_mq_senders(self._q, ctypes.byref(n)), "hd_mq_senders")
         return int(n.value)
 
+    def _out_arrays(self, n: int):
+        """Host arrays for up to n delivered messages, reused across consumes
+        (grown on demand): a flush delivers a few messages per sender, the
+        queue may hold a million."""
+        if getattr(self, "_cap", 0) < n:
+            n = max(n, 2 * getattr(self, "_cap", 0), 1024)
+            self._a = dict(type=np.empty(n, np.uint8), height=np.empty(n, np.int64), round=np.empty(n, np.int64),
+                           valid_round=np.empty(n, np.int64), value=np.empty((n, 32), np.uint8),
+                           frm=np.empty((n, 32), np.uint8), sig=np.empty((n, 65), np.uint8))
+            self._snd = np.empty(n, np.int32)
+            p = lambda x: x.ctypes.data
+            a = self._a
+            self._out = HdBatchOut(p(a["type"]), p(a["height"]), p(a["round"]), p(a["valid_round"]), p(a["value"]),
+                                   p(a["frm"]), p(a["sig"]), None)
+            self._cap = n
+        return self._a, self._snd, self._out
+
     def consume(self, height: int, allowed=None) -> Tuple[Batch, np.ndarray]:
         """Remove every message with height <= `height`; return those of
         senders in `allowed` (procsAllowed; None = the verifier's admitted set
         now), sender queues in creation order, each by (height, round,
         arrival), with their sender-queue ids.  ``last_removed`` is set to the
         number removed, delivered or not."""
-        cap = len(self)
-        n = max(cap, 1)
-        # np.empty: only the first `got` rows are written and returned, and the
-        # untouched pages of a large buffer are never faulted in
-        a = dict(type=np.empty(n, np.uint8), height=np.empty(n, np.int64), round=np.empty(n, np.int64),
-                 valid_round=np.empty(n, np.int64), value=np.empty((n, 32), np.uint8),
-                 frm=np.empty((n, 32), np.uint8), sig=np.empty((n, 65), np.uint8))
-        snd = np.empty(n, np.int32)
         p = lambda x: x.ctypes.data
-        out = HdBatchOut(p(a["type"]), p(a["height"]), p(a["round"]), p(a["valid_round"]), p(a["value"]),
-                         p(a["frm"]), p(a["sig"]), None)
         got, removed = ctypes.c_uint32(), ctypes.c_uint32()
         if allowed is None:
             al, na = None, 0
         else:
             arr = _sig_array(allowed)
             al, na = (p(arr) if len(arr) else p(np.zeros((1, 32), np.uint8))), len(arr)
-        self._check(self._lib.hd_mq_consume(self._q, int(height), al, na, ctypes.byref(out), p(snd), cap,
-                                            ctypes.byref(got), ctypes.byref(removed)), "hd_mq_consume")
+        a, snd, out = self._out_arrays(1024)
+        while True:
+            rc = self._lib.hd_mq_consume(self._q, int(height), al, na, ctypes.byref(out), p(snd), self._cap,
+                                         ctypes.byref(got), ctypes.byref(removed))
+            if rc != _lib.HD_ECAP:
+                break
+            a, snd, out = self._out_arrays(int(got.value))     # nothing was removed: retry with room
+        self._check(rc, "hd_mq_consume")
         k = int(got.value)
         self.last_removed = int(removed.value)
-        b = Batch(a["type"][:k], a["height"][:k], a["round"][:k], a["valid_round"][:k], a["value"][:k], a["frm"][:k],
-                  a["sig"][:k])
+        b = Batch(a["type"][:k].copy(), a["height"][:k].copy(), a["round"][:k].copy(), a["valid_round"][:k].copy(),
+                  a["value"][:k].copy(), a["frm"][:k].copy(), a["sig"][:k].copy())
         return b, snd[:k].copy()
 
     def drop_below(self, height: int) -> None:

@@ -161,6 +161,20 @@ class Verifier:
         self._check(self._lib.hd_set_signatories(self._ctx, _ptr(arr), len(arr)), "hd_set_signatories")
         self.n_signatories = len(arr)
 
+    # include/hd_verify.h HD_VAR_*: kernel variants of this context
+    VARIANTS = {"verify_waves": 0, "sum_waves": 1, "sum_prefetch": 2, "sum_digits": 3, "split_k": 4,
+                "recover_g": 5, "fast_waves": 6, "key_width": 7}
+
+    def set_variant(self, name: str, value: int) -> None:
+        """Select a compiled kernel variant (A/B, variant tests); see
+        include/hd_verify.h HD_VAR_* for the keys and values."""
+        self._check(self._lib.hd_ctx_set_variant(self._ctx, self.VARIANTS[name], int(value)), "hd_ctx_set_variant")
+
+    def variant(self, name: str) -> int:
+        v = ctypes.c_int()
+        self._check(self._lib.hd_ctx_get_variant(self._ctx, self.VARIANTS[name], ctypes.byref(v)), "hd_ctx_get_variant")
+        return v.value
+
     def set_fastpath(self, enable: bool) -> None:
         """Known-key fast path on/off (include/hd_verify.h hd_ctx_set_fastpath)."""
         self._check(self._lib.hd_ctx_set_fastpath(self._ctx, 1 if enable else 0), "hd_ctx_set_fastpath")

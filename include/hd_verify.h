@@ -134,6 +134,25 @@ int hd_ctx_fastpath_geometry(hd_ctx* ctx, int* g_windows, int* key_windows, int*
  * pointer may be NULL; sums_ms covers the calls that ran the kernel, counted
  * in *sums_launches) and clears the record. */
 int hd_ctx_profile(hd_ctx* ctx, int enable);
+/* Kernel variants of a context, for A/B measurements and for the tests that
+ * run every compiled instantiation against the golden fixtures.  Defaults
+ * come from the environment at context creation (the variable in brackets);
+ * HD_EINVAL for an unknown key or value. */
+#define HD_VAR_VERIFY_WAVES 0   /* k_verify register budget, waves per SIMD: 2 or 3 (default) [HD_VERIFY_WAVES] */
+#define HD_VAR_SUM_WAVES 1      /* k_fast_sums: 2 or 3 (default) [HD_SUM_WAVES] */
+#define HD_VAR_SUM_PREFETCH 2   /* k_fast_sums table-point prefetch depth: 1 (default) or 2 [HD_SUM_PF] */
+#define HD_VAR_SUM_DIGITS 3     /* window digits: 0 in k_fast_sums' LDS (default), 1 a k_fast_digits pass
+                                   [HD_SUM_DIGITS=rows] */
+#define HD_VAR_SPLIT_K 4        /* messages per inversion of the known-key check: -1 by batch size (default),
+                                   0 the paired kernel k_verify_fast, 4, 8 or 16 [HD_FAST_K] */
+#define HD_VAR_RECOVER_G 5      /* the full recovery's u1 G: 0 from the fixed-base G table (default), 1 from the
+                                   GLV ladder's own 12-bit table [HD_RECOVER_GLV_G] */
+#define HD_VAR_FAST_WAVES 6     /* k_verify_fast (split K = 0): 2 (default) or 3 [HD_FAST_WAVES] */
+#define HD_VAR_KEY_WIDTH 7      /* per-key table windows: 0 by the table budget (default), 16 or 20; applies from
+                                   the next hd_set_signatories [HD_FB_PW] */
+#define HD_VAR__COUNT 8
+int hd_ctx_set_variant(hd_ctx* ctx, int which, int value);
+int hd_ctx_get_variant(hd_ctx* ctx, int which, int* value);
 int hd_ctx_profile_read(hd_ctx* ctx, uint32_t* calls, double* verify_ms, uint32_t* sums_launches, double* sums_ms);
 
 /* ---- verification ------------------------------------------------------

@@ -547,3 +547,151 @@ int oracle_verify_batch(uint32_t n, const uint8_t* type, const int64_t* height, 
     free(adm);
     return 0;
 }
+
+/* ---- tally + quorum decisions (process/process.go) ---------------------
+ * TEST INFRASTRUCTURE / CPU baseline: the first-wins vote logs of
+ * insertPrevote / insertPrecommit (process.go:823-892) over the VALID
+ * Prevotes / Precommits in batch order, and the counts the 2f+1 / f+1 rules
+ * read (process.go:486-494, 534, 574-582, 626-632, 658, 696-702, 751):
+ *   counts  (h, r, type, value) -> number of first-wins votes, rows in order of
+ *           the group's first logged vote (rep)
+ *   hr      (h, r) -> len(PrevoteLogs[r]), len(PrecommitLogs[r]), distinct vote
+ *           signers, rep = the first candidate of the round
+ *   decide  per hr row, with f and the propose value `pv` (32 B per hr row,
+ *           NULL: none): bit 0 L34 timeout_prevote, 1 L44 precommit_nil, 2
+ *           L47 reached (>=), 3 L47 exact (==), 4 L55 skip (no propose signer),
+ *           5 L36 precommit_value, 6 L49 commit -- hyperdrive_amd.quorum.decide
+ * Open-addressing tables keyed by batch index (keys compared in the batch). */
+typedef struct {
+    uint32_t* slot;
+    uint32_t mask;
+} otab_t;
+
+static uint64_t omix(uint64_t x) {
+    x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull; x ^= x >> 27; x *= 0x94D049BB133111EBull; x ^= x >> 31;
+    return x;
+}
+static uint64_t ohash_bytes(const uint8_t* p, size_t n, uint64_t h) {
+    for (size_t k = 0; k + 8 <= n; k += 8) {
+        uint64_t w;
+        memcpy(&w, p + k, 8);
+        h = omix(h ^ w);
+    }
+    return h;
+}
+
+typedef struct {
+    const uint8_t* type; const int64_t* h; const int64_t* r; const uint8_t* value; const uint8_t* from;
+} obatch_t;
+
+/* mode 0: (h, r); 1: (h, r, type, from); 2: (h, r, from); 3: (h, r, type, value) */
+static uint64_t okey_hash(const obatch_t* b, uint32_t i, int mode) {
+    uint64_t x = omix((uint64_t)b->h[i] * 0x9E3779B97F4A7C15ull ^ omix((uint64_t)b->r[i]) ^ (uint64_t)mode << 60);
+    if (mode == 1 || mode == 3) x = omix(x ^ b->type[i]);
+    if (mode == 1 || mode == 2) x = ohash_bytes(b->from + 32 * (size_t)i, 32, x);
+    if (mode == 3) x = ohash_bytes(b->value + 32 * (size_t)i, 32, x);
+    return x;
+}
+static int okey_eq(const obatch_t* b, uint32_t i, uint32_t j, int mode) {
+    if (b->h[i] != b->h[j] || b->r[i] != b->r[j]) return 0;
+    if ((mode == 1 || mode == 3) && b->type[i] != b->type[j]) return 0;
+    if ((mode == 1 || mode == 2) && memcmp(b->from + 32 * (size_t)i, b->from + 32 * (size_t)j, 32)) return 0;
+    if (mode == 3 && memcmp(b->value + 32 * (size_t)i, b->value + 32 * (size_t)j, 32)) return 0;
+    return 1;
+}
+/* the slot of i's key: its first index there, *fresh = 1 when i created it */
+static uint32_t ofind(otab_t* t, const obatch_t* b, uint32_t i, int mode, int* fresh) {
+    uint32_t s = (uint32_t)okey_hash(b, i, mode) & t->mask;
+    for (;;) {
+        uint32_t c = t->slot[s];
+        if (c == 0xFFFFFFFFu) { t->slot[s] = i; *fresh = 1; return s; }
+        if (okey_eq(b, i, c, mode)) { *fresh = 0; return s; }
+        s = (s + 1) & t->mask;
+    }
+}
+
+int oracle_tally(uint32_t n, const uint8_t* type, const int64_t* height, const int64_t* round, const uint8_t* value32,
+                 const uint8_t* from32, const uint8_t* verdict, uint32_t f, const uint8_t* pv_by_hr,
+                 int64_t* counts /* 5 x n: h r type rep n (row-major) */, uint32_t* n_counts,
+                 int64_t* hr /* 6 x n: h r prevotes precommits any rep */, uint32_t* n_hr, uint8_t* decide) {
+    obatch_t b = {type, height, round, value32, from32};
+    uint32_t cap = 1024;
+    while (cap < 2 * (uint64_t)n + 2) cap <<= 1;
+    otab_t T[4];
+    uint32_t* row_of[4];
+    for (int k = 0; k < 4; k++) {
+        T[k].slot = (uint32_t*)malloc(4 * (size_t)cap);
+        row_of[k] = (uint32_t*)malloc(4 * (size_t)cap);
+        if (!T[k].slot || !row_of[k]) return -1;
+        memset(T[k].slot, 0xFF, 4 * (size_t)cap);
+        T[k].mask = cap - 1;
+    }
+    uint32_t nh = 0, nc = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (verdict[i] != 0 || (type[i] != 2 && type[i] != 3)) continue;
+        int fresh;
+        uint32_t s = ofind(&T[0], &b, i, 0, &fresh);
+        if (fresh) {
+            int64_t* o = hr + 6 * (size_t)nh;
+            o[0] = height[i]; o[1] = round[i]; o[2] = o[3] = o[4] = 0; o[5] = i;
+            row_of[0][s] = nh++;
+        }
+        int64_t* g = hr + 6 * (size_t)row_of[0][s];
+        ofind(&T[1], &b, i, 1, &fresh);          /* first wins per (h, r, type, From) */
+        if (!fresh) continue;
+        g[type[i] == 2 ? 2 : 3]++;
+        ofind(&T[2], &b, i, 2, &fresh);          /* distinct signers of the round */
+        if (fresh) g[4]++;
+        s = ofind(&T[3], &b, i, 3, &fresh);
+        if (fresh) {
+            int64_t* o = counts + 5 * (size_t)nc;
+            o[0] = height[i]; o[1] = round[i]; o[2] = type[i]; o[3] = i; o[4] = 0;
+            row_of[3][s] = nc++;
+        }
+        counts[5 * (size_t)row_of[3][s] + 4]++;
+    }
+    *n_counts = nc;
+    *n_hr = nh;
+    if (decide) {
+        /* count of (h, r, type, value v) by probing T[3] with a scratch key */
+        const int64_t q = 2 * (int64_t)f + 1;
+        static const uint8_t nil[32] = {0};
+        for (uint32_t k = 0; k < nh; k++) {
+            const int64_t* g = hr + 6 * (size_t)k;
+            int64_t cnt[3] = {0, 0, 0};   /* prevotes nil, prevotes pv, precommits pv */
+            const uint8_t* pv = pv_by_hr ? pv_by_hr + 32 * (size_t)k : NULL;
+            for (int c = 0; c < 3; c++) {
+                const uint8_t* val = c == 0 ? nil : pv;
+                const uint8_t ty = c == 2 ? 3 : 2;
+                if (!val) continue;
+                /* a one-message batch view holding the probe key */
+                int64_t hh = g[0], rr = g[1];
+                uint8_t tt = ty;
+                obatch_t kb = {&tt, &hh, &rr, val, from32};
+                uint32_t s = (uint32_t)okey_hash(&kb, 0, 3) & T[3].mask;
+                for (;;) {
+                    uint32_t e = T[3].slot[s];
+                    if (e == 0xFFFFFFFFu) break;
+                    if (height[e] == hh && round[e] == rr && type[e] == ty && !memcmp(value32 + 32 * (size_t)e, val, 32)) {
+                        cnt[c] = counts[5 * (size_t)row_of[3][s] + 4];
+                        break;
+                    }
+                    s = (s + 1) & T[3].mask;
+                }
+            }
+            uint8_t d = 0;
+            d |= (g[2] >= q) << 0;
+            d |= (cnt[0] >= q) << 1;
+            d |= (g[3] >= q) << 2;
+            d |= (g[3] == q) << 3;
+            d |= (g[4] >= (int64_t)f + 1) << 4;
+            if (pv) {
+                d |= (cnt[1] >= q) << 5;
+                d |= (cnt[2] >= q) << 6;
+            }
+            decide[k] = d;
+        }
+    }
+    for (int k = 0; k < 4; k++) { free(T[k].slot); free(row_of[k]); }
+    return 0;
+}

@@ -17,7 +17,7 @@ for step in "$@"; do
   case $step in
     light) run first_light 600 python scripts/first_light.py ;;
     probe) run w4_probe 240 python -u scripts/w4_probe.py base ;;
-    gtest1) run pytest_gpu1 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "golden or c1 or fast_path_equals or set_change" ;;
+    gtest1) run pytest_gpu1 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "golden or c1 or host_pipeline or routed or multi" ;;
     bench_vs1) HD_BENCH_VSTREAMS=1 run bench_vs1 300 python bench.py --no-cpu --no-aux ;;
     bench_fast) run bench_fast 300 python bench.py --no-cpu --no-aux ;;
     trace2) run trace2 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace2 -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub ;;

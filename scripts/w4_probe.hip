@@ -38,8 +38,61 @@ struct PSrc {
     HD_MEMBER uint32_t digest(int w) const { return dg[8 * (size_t)i + w]; }
 };
 
+// ecmult_glv (hd_group.h) stopped after window jstop: the Jacobian
+// accumulator (normalised x, y, z) -- to find the first window whose result
+// differs between the device and the host build
+template <typename GTab>
+HD void ladder_until(gej& acc, const ge& R, const sc& u1, const sc& u2, GTab gtab, int jstop) {
+    ge rt[HD_RTAB_N], lt[HD_RTAB_N];
+    fe zg;
+    build_rtab_iso(rt, lt, zg, R);
+    int16_t dra[HD_GLV_NWIN_R], drb[HD_GLV_NWIN_R], dga[HD_GLV_NWIN_G], dgb[HD_GLV_NWIN_G];
+    {
+        sc k1, k2;
+        uint32_t a[5];
+        bool neg;
+        sc_split_lambda(k1, k2, u2);
+        neg = sc_signed_abs(a, k1);
+        HD_UNROLL for (int j = 0; j < HD_GLV_NWIN_R; j++) dra[j] = (int16_t)booth_digit160<HD_WR>(a, j, neg);
+        neg = sc_signed_abs(a, k2);
+        HD_UNROLL for (int j = 0; j < HD_GLV_NWIN_R; j++) drb[j] = (int16_t)booth_digit160<HD_WR>(a, j, neg);
+        sc_split_lambda(k1, k2, u1);
+        neg = sc_signed_abs(a, k1);
+        HD_UNROLL for (int j = 0; j < HD_GLV_NWIN_G; j++) dga[j] = (int16_t)booth_digit160<HD_WG_GLV>(a, j, neg);
+        neg = sc_signed_abs(a, k2);
+        HD_UNROLL for (int j = 0; j < HD_GLV_NWIN_G; j++) dgb[j] = (int16_t)booth_digit160<HD_WG_GLV>(a, j, neg);
+    }
+    gej_set_inf(acc);
+    HD_NOUNROLL for (int j = HD_GLV_NWIN_R - 1; j >= jstop; j--) {
+        if (j != HD_GLV_NWIN_R - 1) {
+            HD_NOUNROLL for (int k = 0; k < HD_WR; k++) gej_dbl(acc, acc);
+        }
+        if (j % 3 == 0) {
+            HD_NOUNROLL for (int half = 0; half < 2; half++) {
+                const int d = half ? dgb[j / 3] : dga[j / 3];
+                const int ad = d < 0 ? -d : d;
+                ge t = gtab[half * HD_GLV_GTAB_N + (ad == 0 ? 0 : ad - 1)];
+                if (d < 0) fe_neg(t.y, t.y);
+                gej s;
+                gej_add_ge_zinv(s, acc, t, zg);
+                gej_cmov(acc, s, d != 0);
+            }
+        }
+        HD_NOUNROLL for (int half = 0; half < 2; half++) {
+            const int d = half ? drb[j] : dra[j];
+            const int ad = d < 0 ? -d : d;
+            ge t = half ? lt[ad == 0 ? 0 : ad - 1] : rt[ad == 0 ? 0 : ad - 1];
+            if (d < 0) fe_neg(t.y, t.y);
+            gej s;
+            gej_add_ge(s, acc, t);
+            gej_cmov(acc, s, d != 0);
+        }
+    }
+}
+
 template <int S>
-__host__ __device__ uint8_t stage_run(const PSrc& src, const ge* gtab, uint32_t out[48]) {
+__host__ __device__ __forceinline__ uint8_t stage_run(const PSrc& src, const ge* gtab, uint32_t out[48],
+                                                     int arg = 0) {
     HD_UNROLL for (int k = 0; k < 48; k++) out[k] = 0;
     if (S == 3) {
         uint32_t rec[8];
@@ -150,6 +203,16 @@ __host__ __device__ uint8_t stage_run(const PSrc& src, const ge* gtab, uint32_t 
         fe_to_le(out + 24, x); fe_to_le(out + 32, y); fe_to_le(out + 40, z);
         return 0;
     }
+    if (S == 16 || S == 17) {   // the ladder stopped after window arg (17: G only)
+        sc zero;
+        HD_UNROLL for (int k = 0; k < 8; k++) zero.v[k] = 0;
+        gej acc;
+        ladder_until(acc, R, u1, S == 17 ? zero : u2, gtab, arg);
+        fe x = acc.x, y = acc.y, z = acc.z;
+        fe_normalize(x); fe_normalize(y); fe_normalize(z);
+        fe_to_le(out, x); fe_to_le(out + 8, y); fe_to_le(out + 16, z);
+        return 0;
+    }
     gej Q;
     if (S == 14 || S == 15) {   // the ladder with one side only
         sc zero;
@@ -171,29 +234,30 @@ template <int W, int S>
 __global__ __launch_bounds__(256, W) void k_stage(uint32_t n, const uint32_t* __restrict__ dg,
                                                   const uint8_t* __restrict__ sig, const uint8_t* __restrict__ from,
                                                   const ge* __restrict__ gtab, uint32_t* __restrict__ out,
-                                                  uint8_t* __restrict__ verdict) {
+                                                  uint8_t* __restrict__ verdict, int arg) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     PSrc src{dg, sig, from, i};
     uint32_t o[48];
-    const uint8_t v = stage_run<S>(src, gtab, o);
+    const uint8_t v = stage_run<S>(src, gtab, o, arg);
     HD_UNROLL for (int k = 0; k < 48; k++) out[48 * (size_t)i + k] = o[k];
     verdict[i] = v;
 }
 
 template <int W>
 static void launch(int stage, uint32_t n, const uint32_t* dg, const uint8_t* sig, const uint8_t* from,
-                   const ge* gtab, uint32_t* out, uint8_t* verdict) {
+                   const ge* gtab, uint32_t* out, uint8_t* verdict, int arg) {
     const uint32_t b = (n + 255) / 256;
-#define HD_ST(S) else if (stage == S) k_stage<W, S><<<b, 256>>>(n, dg, sig, from, gtab, out, verdict)
+#define HD_ST(S) else if (stage == S) k_stage<W, S><<<b, 256>>>(n, dg, sig, from, gtab, out, verdict, arg)
     if (0) {}
     HD_ST(0); HD_ST(1); HD_ST(2); HD_ST(3); HD_ST(10); HD_ST(11); HD_ST(12); HD_ST(13); HD_ST(14); HD_ST(15);
+    HD_ST(16); HD_ST(17);
 #undef HD_ST
 }
 
 // host: digests (8 BE words per message), sigs (65 B), froms (32 B) -> out
 // (16 words per message) and verdicts, for waves W (3 or 4) and stage 0..3
-extern "C" int probe_run(int waves, int stage, uint32_t n, const uint32_t* dg, const uint8_t* sig,
+extern "C" int probe_run(int waves, int stage, int arg, uint32_t n, const uint32_t* dg, const uint8_t* sig,
                          const uint8_t* from, uint32_t* out, uint8_t* verdict) {
     static std::vector<ge> tab;
     if (tab.empty()) {
@@ -211,8 +275,8 @@ extern "C" int probe_run(int waves, int stage, uint32_t n, const uint32_t* dg, c
     hipMemcpy(d_dg, dg, 32 * (size_t)n, hipMemcpyHostToDevice);
     hipMemcpy(d_sig, sig, 65 * (size_t)n, hipMemcpyHostToDevice);
     hipMemcpy(d_from, from, 32 * (size_t)n, hipMemcpyHostToDevice);
-    if (waves == 4) launch<4>(stage, n, d_dg, d_sig, d_from, d_tab, d_out, d_v);
-    else launch<3>(stage, n, d_dg, d_sig, d_from, d_tab, d_out, d_v);
+    if (waves == 4) launch<4>(stage, n, d_dg, d_sig, d_from, d_tab, d_out, d_v, arg);
+    else launch<3>(stage, n, d_dg, d_sig, d_from, d_tab, d_out, d_v, arg);
     hipError_t e = hipDeviceSynchronize();
     if (e == hipSuccess) e = hipMemcpy(out, d_out, 192 * (size_t)n, hipMemcpyDeviceToHost);
     if (e == hipSuccess) e = hipMemcpy(verdict, d_v, n, hipMemcpyDeviceToHost);
@@ -226,8 +290,8 @@ extern "C" int probe_run(int waves, int stage, uint32_t n, const uint32_t* dg, c
 }
 
 // the same stages on the host (g++-equivalent host build of the headers)
-extern "C" int probe_host(int stage, uint32_t n, const uint32_t* dg, const uint8_t* sig, const uint8_t* from,
-                          uint32_t* out, uint8_t* verdict) {
+extern "C" int probe_host(int stage, int arg, uint32_t n, const uint32_t* dg, const uint8_t* sig,
+                          const uint8_t* from, uint32_t* out, uint8_t* verdict) {
     static std::vector<ge> tab;
     if (tab.empty()) {
         tab.resize(2 * HD_GLV_GTAB_N);
@@ -237,9 +301,10 @@ extern "C" int probe_host(int stage, uint32_t n, const uint32_t* dg, const uint8
         PSrc src{dg, sig, from, i};
         uint32_t o[48];
         uint8_t v = 0;
-#define HD_ST(S) else if (stage == S) v = stage_run<S>(src, tab.data(), o)
+#define HD_ST(S) else if (stage == S) v = stage_run<S>(src, tab.data(), o, arg)
         if (0) {}
         HD_ST(0); HD_ST(1); HD_ST(2); HD_ST(3); HD_ST(10); HD_ST(11); HD_ST(12); HD_ST(13); HD_ST(14); HD_ST(15);
+        HD_ST(16); HD_ST(17);
 #undef HD_ST
         for (int k = 0; k < 48; k++) out[48 * (size_t)i + k] = o[k];
         verdict[i] = v;

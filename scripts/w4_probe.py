@@ -40,21 +40,23 @@ def main():
     for var in variants:
         lib = ctypes.CDLL(os.path.join(HERE, f"w4_probe_{var}.so"))
         lib.probe_run.restype = ctypes.c_int
-        lib.probe_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint32] + [ctypes.c_void_p] * 5
-        lib.probe_host.argtypes = [ctypes.c_int, ctypes.c_uint32] + [ctypes.c_void_p] * 5
+        lib.probe_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32] + [ctypes.c_void_p] * 5
+        lib.probe_host.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint32] + [ctypes.c_void_p] * 5
         res = {}
-        for stage in (0, 1, 2, 3, 10, 11, 12, 13, 14, 15):
+        runs = [(st, 0) for st in (0, 1, 2, 3, 10, 11, 12, 13, 14, 15)]
+        runs += [(16, a) for a in (32, 31, 30, 29, 27, 24, 20, 16, 8, 0)] + [(17, a) for a in (32, 30, 27, 24, 0)]
+        for stage, arg in runs:
             outs = {}
             for w in (3, 4):
                 out = np.zeros((n, 48), np.uint32)
                 ver = np.zeros(n, np.uint8)
-                rc = lib.probe_run(w, stage, n, dg.ctypes.data, sig.ctypes.data, frm.ctypes.data,
+                rc = lib.probe_run(w, stage, arg, n, dg.ctypes.data, sig.ctypes.data, frm.ctypes.data,
                                    out.ctypes.data, ver.ctypes.data)
                 assert rc == 0, rc
                 outs[w] = (out, ver)
             out = np.zeros((n, 48), np.uint32)
             ver = np.zeros(n, np.uint8)
-            lib.probe_host(stage, n, dg.ctypes.data, sig.ctypes.data, frm.ctypes.data, out.ctypes.data,
+            lib.probe_host(stage, arg, n, dg.ctypes.data, sig.ctypes.data, frm.ctypes.data, out.ctypes.data,
                            ver.ctypes.data)
             outs["host"] = (out, ver)
             d = np.flatnonzero((outs[3][0] != outs[4][0]).any(1) | (outs[3][1] != outs[4][1]))
@@ -74,8 +76,8 @@ def main():
                     rec = outs[w][0][:, :8].astype(">u4").view(np.uint8).reshape(n, 32)
                     ok = gold_v == 0
                     ent[f"w{w}_rec_mismatch_on_valid"] = int((rec[ok] != gold_rec[ok]).any(1).sum())
-            res[stage] = ent
-            print(var, stage, json.dumps(ent)[:600], flush=True)
+            res[f"{stage}/{arg}"] = ent
+            print(var, stage, arg, json.dumps(ent)[:300], flush=True)
         report[var] = res
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/w4_probe.json", "w") as fh:

@@ -21,6 +21,11 @@ class COracle:
         self.lib.oracle_recover.restype = ctypes.c_int
         self.lib.oracle_digest.argtypes = [ctypes.c_uint8, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                            ctypes.c_char_p, ctypes.c_void_p]
+        self.lib.oracle_tally.restype = ctypes.c_int
+        self.lib.oracle_tally.argtypes = [ctypes.c_uint32] + [ctypes.c_void_p] * 6 + [ctypes.c_uint32, ctypes.c_void_p,
+                                                                                      ctypes.c_void_p, ctypes.c_void_p,
+                                                                                      ctypes.c_void_p, ctypes.c_void_p,
+                                                                                      ctypes.c_void_p]
 
     def sha256(self, b: bytes) -> bytes:
         out = ctypes.create_string_buffer(32)
@@ -48,3 +53,29 @@ class COracle:
                                           _p(adm), len(adm), int(compressed), _p(verdict), _p(rec), threads)
         assert rc == 0
         return verdict, rec
+
+    def tally(self, batch, verdict, f: int = 0, pv_by_hr=None, propose_value=None):
+        """First-wins tally + quorum decisions (oracle_tally).  Returns
+        {"counts": [k, 5] int64 (h, r, type, rep, n), "hr": [m, 6] int64 (h, r,
+        prevotes, precommits, any, rep), "decide": [m] uint8 bits}.
+        propose_value(h, r) -> 32 bytes or None gives the propose value of each
+        round (else pv_by_hr, else no propose)."""
+        n = len(batch)
+        verdict = np.ascontiguousarray(verdict, np.uint8)
+        counts = np.zeros((max(n, 1), 5), np.int64)
+        hr = np.zeros((max(n, 1), 6), np.int64)
+        nc, nh = ctypes.c_uint32(), ctypes.c_uint32()
+        rc = self.lib.oracle_tally(n, _p(batch.type), _p(batch.height), _p(batch.round), _p(batch.value),
+                                   _p(batch.frm), _p(verdict), 0, None, _p(counts), ctypes.byref(nc), _p(hr),
+                                   ctypes.byref(nh), None)
+        assert rc == 0
+        hr = hr[: nh.value]
+        if propose_value is not None:
+            pv_by_hr = np.array([np.frombuffer(propose_value(int(h), int(r)), np.uint8) for h, r in hr[:, :2]],
+                                np.uint8).reshape(-1, 32)
+        decide = np.zeros(max(nh.value, 1), np.uint8)
+        rc = self.lib.oracle_tally(n, _p(batch.type), _p(batch.height), _p(batch.round), _p(batch.value),
+                                   _p(batch.frm), _p(verdict), int(f), _p(pv_by_hr), _p(counts), ctypes.byref(nc),
+                                   _p(np.zeros((max(n, 1), 6), np.int64)), ctypes.byref(nh), _p(decide))
+        assert rc == 0
+        return {"counts": counts[: nc.value].copy(), "hr": hr.copy(), "decide": decide[: nh.value].copy()}

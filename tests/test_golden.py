@@ -139,3 +139,40 @@ def test_gpu_matches_golden(gpu, name):
                     assert fallback < len(b)
     finally:
         v.close()
+
+
+# Every kernel instantiation a context can select (include/hd_verify.h
+# HD_VAR_*), one at a time from the defaults; the first entry is the default.
+VARIANTS = [("default", None, None), ("verify_waves", "verify_waves", 2), ("sum_waves_2", "sum_waves", 2),
+            ("sum_prefetch_2", "sum_prefetch", 2), ("sum_digits_rows", "sum_digits", 1), ("split_k_0", "split_k", 0),
+            ("split_k_4", "split_k", 4), ("split_k_16", "split_k", 16), ("fast_waves_3", "split_k", 0),
+            ("recover_glv_g", "recover_g", 1), ("key_width_16", "key_width", 16), ("key_width_20", "key_width", 20)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("label,key,value", VARIANTS, ids=[v[0] for v in VARIANTS])
+def test_gpu_variants_match_golden(gpu, label, key, value):
+    """Each selectable k_verify / k_fast_sums / k_verify_fast / split-check
+    instantiation reproduces every golden fixture, through the full recovery
+    (pass 1) and the known-key check (pass 2)."""
+    for name in CASES:
+        b, z, _ = load_case(name)
+        v = gpu.Verifier(0, compressed=int(z["compressed"]))
+        try:
+            if key:
+                v.set_variant(key, value)
+            if label == "fast_waves_3":
+                v.set_variant("fast_waves", 3)
+            v.set_signatories(z["admitted"])
+            for rnd in range(2):
+                res = v.verify_batch(b)
+                assert res.verdict.tolist() == z["verdict"].tolist(), (label, name, rnd)
+                assert res.recovered.tobytes() == z["recovered"].tobytes(), (label, name, rnd)
+        finally:
+            v.close()
+
+
+def test_variant_api_rejects_bad_values():
+    import hyperdrive_amd._lib as L
+    lib = L.load()
+    assert lib.hd_ctx_set_variant(None, 0, 3) == L.HD_EINVAL

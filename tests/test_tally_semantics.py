@@ -46,3 +46,37 @@ def test_non_valid_and_proposes_are_not_candidates(oracle):
     t = oracle.tally(b, verdicts)
     assert t.distinct[(1, 0, oracle.PREVOTE)] == 4
     assert t.dup == [0, 3, 0, 3, 0, 0, 3]
+
+
+DECIDE_BITS = ("timeout_prevote", "precommit_nil", "timeout_precommit_reached", "timeout_precommit_exact", "skip",
+               "precommit_value", "commit")
+
+
+def test_c_oracle_tally_and_decisions(coracle, oracle):
+    """The C restatement of the tally and the quorum predicates (the CPU
+    baseline's tally leg, oracle/hd_oracle.c oracle_tally) equals the Python
+    restatement's rows and hyperdrive_amd.quorum.decide on every golden
+    fixture and tally scenario."""
+    import numpy as np
+    from test_golden import CASES, load_case
+    from test_multi_rank import tally_rows
+    from util import from_np
+    from hyperdrive_amd import quorum
+    batches = [(load_case(c)[0], load_case(c)[1]["verdict"]) for c in CASES]
+    from tally_cases import scenarios
+    from util import to_np
+    for sc in scenarios():
+        batches.append((to_np(sc.b), np.array([0 if i % 7 else 5 for i in range(len(sc.b))], np.uint8)))
+    for b, verdict in batches:
+        ob = from_np(b)
+        want = tally_rows(ob, verdict.tolist())
+        for f in (1, 2, 33):
+            pv = lambda h, r: oracle.canonical_value(h, r)
+            got = coracle.tally(b, verdict, f, propose_value=pv)
+            assert got["counts"].tolist() == want["counts"].tolist()
+            assert got["hr"].tolist() == want["hr"].tolist()
+            t = oracle.tally(ob, verdict.tolist())
+            for (h, r), d in zip(got["hr"][:, :2].tolist(), got["decide"].tolist()):
+                ref = quorum.decide(t, h, r, f, pv(h, r), True)
+                assert {k: bool(d >> j & 1) for j, k in enumerate(DECIDE_BITS)} == \
+                    {k: ref[k] for k in DECIDE_BITS}, (h, r, f)

@@ -641,7 +641,7 @@ def ingress_c5(v, keys, S, n, ws, dev, heights=64):
     ing.mq.drop_below(2 ** 62)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    verdicts = [ing.push_wire(t, wire, sub.n, stream=ws) for t, sub, wire in parts]
+    verdicts = ing.push_wires([(t, wire, sub.n) for t, sub, wire in parts])
     torch.cuda.synchronize()                          # push_ms includes the device work it queued
     t1 = time.perf_counter()
     delivered = 0

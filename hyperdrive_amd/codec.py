@@ -42,9 +42,11 @@ def marshal_device(v: Verifier, mtype: int, batch: DeviceBatch, with_sig: bool =
 
 
 def unmarshal_device(v: Verifier, mtype: int, buf, n: int, with_sig: bool = True,
-                     stream=None) -> Tuple[DeviceBatch, "object"]:
+                     stream=None, sync: bool = True) -> Tuple[DeviceBatch, "object"]:
     """Decode n `mtype` records from a device byte buffer into a DeviceBatch;
-    status[i] = 1 marks a record the buffer ended before."""
+    status[i] = 1 marks a record the buffer ended before.  sync=False leaves
+    the decode queued on `stream` (the caller orders what reads the batch
+    after it on that stream)."""
     torch = _torch()
     dev = buf.device
     out = DeviceBatch.empty(n, str(dev))
@@ -57,5 +59,6 @@ def unmarshal_device(v: Verifier, mtype: int, buf, n: int, with_sig: bool = True
                                        ctypes.byref(co), status.data_ptr(), ws.cuda_stream)
     if rc != 0:
         raise _lib.HDError(rc, "hd_unmarshal_batch_device", lib.hd_ctx_last_error(v.handle).decode())
-    ws.synchronize()
+    if sync:
+        ws.synchronize()
     return out, status[:n]

@@ -69,9 +69,11 @@ struct FbWork {
     struct Scratch {
         uint32_t* rows = nullptr;     // the split check's per-message rows (SplitRows, 62 words per message)
         size_t cap_rows = 0;
-        uint32_t* slow = nullptr;     // message index list for the full recovery
+        uint32_t* slow = nullptr;     // message index list: the known-key check's leftovers
         size_t cap_slow = 0;
-        uint32_t* count = nullptr;    // its length (device word)
+        uint32_t* count = nullptr;    // its length (device words: [0] leftovers, [1] after k_slow_lift)
+        uint32_t* slow2 = nullptr;    // the leftovers that pass the lift: the full recovery's list
+        size_t cap_slow2 = 0;
         hipEvent_t done = nullptr;    // recorded after the last call that used this set
         hipStream_t stream = nullptr; // that call's stream
         bool used = false;
@@ -671,6 +673,61 @@ __global__ __launch_bounds__(256) void k_fast_cmp(DevBatch b, SplitRows rows, co
     }
 }
 
+// Before the full recovery of the leftovers: the reference's first checks
+// and the lift of R (V >= 4, r / s range,
+// r + n >= p, x^3 + 7 a square), in recover_m's order.  A message that fails
+// one has its final verdict (nothing recovered) for one square-root chain,
+// ~7 % of a recovery -- the "x not on the curve" adversarial class, and the
+// malformed signatures of signatories without a known key; the rest go to
+// the compacted list `out` (*n_out) that k_verify walks.  Leftovers are ~10 %
+// of a 30 %-adversarial batch, so the saving is in the recovery's throughput
+// cost, which overlapping calls expose.
+__global__ __launch_bounds__(256) void k_slow_lift(DevBatch b, const uint32_t* __restrict__ list,
+                                                   const uint32_t* __restrict__ count, uint8_t* __restrict__ verdict,
+                                                   uint8_t* __restrict__ rec32, int32_t* __restrict__ signer,
+                                                   uint32_t* __restrict__ out, uint32_t* __restrict__ n_out) {
+    const uint32_t total = *count, stride = gridDim.x * blockDim.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += stride) {
+        const uint32_t p = base + threadIdx.x;
+        bool keep = false;
+        uint32_t i = 0;
+        if (p < total) {
+            i = list[p];
+            uint32_t r_be[8], s_be[8], v;
+            load_sig65(r_be, s_be, v, b.sig65, i, b.n);
+            sc r, s;
+            fe x;
+            uint8_t pre = sig_prefix(r, s, x, r_be, s_be, v);
+            if (pre == V_VALID) {
+                fe y2, y, seven;
+                fe_sqr(y2, x);
+                fe_mul(y2, y2, x);
+                fe_set_u32(seven, 7);
+                fe_add(y2, y2, seven);
+                if (!fe_sqrt(y, y2)) pre = V_NO_POINT;
+            }
+            keep = pre == V_VALID;
+            if (!keep) {
+                verdict[i] = pre;
+                if (rec32) {
+                    const uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                    store_row32_be(rec32, i, z);
+                }
+                if (signer) signer[i] = -1;
+            }
+        }
+        const unsigned long long bal = __ballot(keep);
+        if (bal) {
+            const uint32_t leader = (uint32_t)__ffsll((long long)bal) - 1;
+            uint32_t o = 0;
+            if (lane == leader) o = atomicAdd(n_out, (uint32_t)__popcll(bal));
+            o = __shfl(o, (int)leader);
+            if (keep) out[o + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = i;
+        }
+    }
+}
+
 __global__ void k_fb_bitmap(uint32_t n, const uint8_t* __restrict__ verdict, uint32_t* __restrict__ bitmap) {
     const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
     if (32 * w >= n) return;
@@ -981,7 +1038,7 @@ void hd_fb_release(hd_ctx* ctx) {
     for (hipEvent_t e : f->ev_sums) (void)hipEventDestroy(e);
     for (auto& sc : f->sc) {
         if (sc.done) (void)hipEventDestroy(sc.done);
-        void* sp[] = {sc.rows, sc.slow, sc.count};
+        void* sp[] = {sc.rows, sc.slow, sc.count, sc.slow2};
         for (void* p : sp)
             if (p) (void)hipFree(p);
     }
@@ -1180,7 +1237,7 @@ int hd_fb_verify(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_
     f->next = (j + 1) % FbWork::NSCRATCH;
     FbWork::Scratch& sc = f->sc[j];
     if (!sc.done) FBCHK(hipEventCreateWithFlags(&sc.done, hipEventDisableTiming), "fb scratch event");
-    if (!sc.count) FBCHK(hipMalloc(&sc.count, 4), "fb scratch count");
+    if (!sc.count) FBCHK(hipMalloc(&sc.count, 8), "fb scratch count");
     // see FbWork: in the steady state only this set's previous user orders
     // this call; otherwise the previous call does, on whatever stream
     const bool steady = f->nr_host && *(volatile uint32_t*)f->nr_host == 0;
@@ -1220,7 +1277,9 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
     if (rc) return rc;
     const uint32_t blocks = (b.n + 255) / 256;
     const uint32_t fast_blocks = ((b.n + 1) / 2 + 255) / 256;   // two messages per lane
-    FBCHK(hipMemsetAsync(sc.count, 0, 4, s), "fb count reset");
+    rc = hd_dev_grow(ctx, (void**)&sc.slow2, &sc.cap_slow2, 4 * (size_t)b.n);
+    if (rc) return rc;
+    FBCHK(hipMemsetAsync(sc.count, 0, 8, s), "fb count reset");
     if (ctx->n_adm > 0 && f->adm_slot && split_k_for(ctx, b.n) > 0) {
         // 62 words per message; the digit rows (the narrow width has more
         // windows) only for the HD_SUM_DIGITS=rows A/B form
@@ -1253,8 +1312,11 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         FBCHK(hipGetLastError(), "split check launch");
         // k_fast_cmp wrote the valid bitmap; the slow path sets the bits of
         // its VALID messages
-        const SlowCtl ctl{sc.slow, sc.count, f->adm_slot, f->state, f->pub, d_bitmap};
         const uint32_t slow_blocks = std::min(blocks, (uint32_t)std::max(ctx->n_cu, 1) * 4u);
+        k_slow_lift<<<slow_blocks, 256, 0, s>>>(b, sc.slow, sc.count, d_verdict, d_rec32, d_signer, sc.slow2,
+                                                sc.count + 1);
+        FBCHK(hipGetLastError(), "k_slow_lift");
+        const SlowCtl ctl{sc.slow2, sc.count + 1, f->adm_slot, f->state, f->pub, d_bitmap};
         rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl, slow_blocks, s);
         if (rc) return rc;
         return fb_learn(ctx, s);
@@ -1272,8 +1334,11 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         // the fallback list is usually short (its length is only known on the
         // device): a grid of 4 blocks per CU walks it, instead of one block
         // per 256 messages that would mostly start and exit
-        const SlowCtl ctl{sc.slow, sc.count, f->adm_slot, f->state, f->pub, nullptr};
         const uint32_t slow_blocks = std::min(blocks, (uint32_t)std::max(ctx->n_cu, 1) * 4u);
+        k_slow_lift<<<slow_blocks, 256, 0, s>>>(b, sc.slow, sc.count, d_verdict, d_rec32, d_signer, sc.slow2,
+                                                sc.count + 1);
+        FBCHK(hipGetLastError(), "k_slow_lift");
+        const SlowCtl ctl{sc.slow2, sc.count + 1, f->adm_slot, f->state, f->pub, nullptr};
         rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl, slow_blocks, s);
         if (rc) return rc;
         if (d_bitmap) {

@@ -67,7 +67,11 @@ HD void gej_dbl(gej& r, const gej& a) {
     fe_norm_weak(r.y);         // Y3                T
 }
 
-HD_NOINLINE void gej_dbl_slow(gej& r, const gej& a) { gej_dbl(r, a); }
+// the doubling of the rare a == b case of the additions, inlined like everything
+// else: a kernel with no device calls has no call frames next to its spill
+// slots (a called ladder miscompiled on gfx950, scripts/w4_probe.hip, DESIGN.md
+// §4 "Known issue, resolved")
+HD void gej_dbl_slow(gej& r, const gej& a) { gej_dbl(r, a); }
 
 // r = a + b, b affine and finite (madd-2007-bl shape, 8M + 3S with
 // Z3 = 2 Z1 H).  Handles a = inf (up front, so b is dead after the first

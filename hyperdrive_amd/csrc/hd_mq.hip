@@ -427,13 +427,14 @@ __global__ __launch_bounds__(1024) void k_mq_plan(uint32_t nsend, const int64_t*
 }
 
 // the delivered prefixes into the packed stage: block s copies sender s's
+// (rows at or past cap are not written: the consume then fails with HD_ECAP)
 __global__ __launch_bounds__(256) void k_mq_take(Pool p, const uint32_t* __restrict__ head,
                                                  const uint32_t* __restrict__ newhead, const uint32_t* __restrict__ off,
-                                                 const uint8_t* __restrict__ allow, Pool d) {
+                                                 const uint8_t* __restrict__ allow, uint32_t cap, Pool d) {
     const uint32_t s = blockIdx.x;
     if (!allow[s]) return;
     const uint32_t lo = head[s], n = newhead[s] - lo, o = off[s];
-    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
+    for (uint32_t j = threadIdx.x; j < n && o + j < cap; j += blockDim.x) {
         const uint32_t e = lo + j, k = o + j;
         d.sender[k] = p.sender[e];
         d.type[k] = p.type[e];
@@ -446,6 +447,13 @@ __global__ __launch_bounds__(256) void k_mq_take(Pool p, const uint32_t* __restr
         }
         for (int w = 0; w < 65; w++) d.sig[65 * (size_t)k + w] = p.sig[65 * (size_t)e + w];
     }
+}
+
+// the plan's heads become the queue's unless its delivered count exceeds cap
+__global__ void k_mq_commit(uint32_t nsend, const uint32_t* __restrict__ newhead, const uint32_t* __restrict__ totals,
+                            uint32_t cap, uint32_t* __restrict__ head) {
+    if (totals[0] > cap) return;
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nsend; s += gridDim.x * blockDim.x) head[s] = newhead[s];
 }
 
 // live pool entries (not in a consumed / dropped prefix)
@@ -882,6 +890,13 @@ static int mq_commit(hd_mq* q, uint32_t removed, hipStream_t s) {
     return HD_OK;
 }
 
+// Consume in one host round trip: allow flags -> plan -> the delivered rows
+// gathered into a stage of `cap` rows (the caller's capacity) -> heads
+// committed on the device if they fit -> ONE download of the plan totals and
+// the stage (a small consume is latency-bound: a second sync costs more than
+// the unused stage rows' bytes).  A stage larger than HD_MQ_STAGE_ROWS is
+// sized by a planning round trip first.
+#define HD_MQ_STAGE_ROWS 4096u
 int hd_mq_consume(hd_mq* q, int64_t h, const uint8_t* allowed32, uint32_t n_allowed, const hd_batch_out* out,
                   int32_t* out_sender, uint32_t cap, uint32_t* n_out, uint32_t* n_removed) {
     if (!q || !out || !n_out) return HD_EINVAL;
@@ -914,35 +929,55 @@ int hd_mq_consume(hd_mq* q, int64_t h, const uint8_t* allowed32, uint32_t n_allo
         be = 1;
     }
     if (na) k_mq_allow<<<nblk(na), 256, 0, s>>>(na, list, be, dict_of(q), allow);
-    uint32_t tot[2];
-    if ((rc = mq_plan(q, h, 0, allow, tot, s))) return rc;
-    const uint32_t c = tot[0], nr = tot[1];
+    const uint32_t ns = q->nsend;
+    uint32_t* newhead = (uint32_t*)qbuf(q, MQ_NEWHEAD, 4 * (size_t)ns, &rc);
+    uint32_t* off = (uint32_t*)qbuf(q, MQ_OFF, 4 * (size_t)ns, &rc);
+    uint32_t* tot = (uint32_t*)qbuf(q, MQ_TOT, 64, &rc);
+    if (rc) return rc;
+    uint32_t* head = (uint32_t*)q->buf[MQ_HEADS].p;
+    k_mq_plan<<<1, 1024, 0, s>>>(ns, q->pool.h, head, (const uint32_t*)q->buf[MQ_SEND].p, h, 0, allow, newhead, off,
+                                 tot);
+    QCHK(hipGetLastError(), "k_mq_plan");
+    // stage rows: the caller's room, at most HD_MQ_STAGE_ROWS without knowing
+    // the count (a larger delivery is planned first, then staged exactly)
+    uint32_t rows = std::min(cap, HD_MQ_STAGE_ROWS);
+    if (cap > HD_MQ_STAGE_ROWS) {
+        uint32_t t[2];
+        QCHK(hipMemcpyAsync(t, tot, 8, hipMemcpyDeviceToHost, s), "plan totals");
+        QCHK(hipStreamSynchronize(s), "plan sync");
+        rows = std::min(cap, t[0]);
+    }
+    const uint32_t r16 = (std::max(rows, 1u) + 15u) & ~15u;
+    const size_t bytes = pool_bytes(r16);
+    void* dst = qbuf(q, MQ_STAGE, bytes, &rc);
+    if (rc) return rc;
+    if (q->hstage_cap < bytes + 64) {
+        if (q->hstage) (void)hipHostFree(q->hstage);
+        q->hstage = nullptr;
+        q->hstage_cap = 0;
+        const size_t want = bytes + bytes / 2 + 64;
+        QCHK(hipHostMalloc(&q->hstage, want, hipHostMallocDefault), "mq host stage");
+        q->hstage_cap = want;
+    }
+    const Pool d = pool_view(dst, r16);
+    if (rows) k_mq_take<<<ns, 256, 0, s>>>(q->pool, head, newhead, off, allow, rows, d);
+    k_mq_commit<<<std::min(nblk(ns), 64u), 256, 0, s>>>(ns, newhead, tot, cap, head);
+    QCHK(hipGetLastError(), "consume kernels");
+    uint32_t* htot = (uint32_t*)q->hstage;                  // totals first, then the stage
+    void* hrows = (char*)q->hstage + 64;
+    QCHK(hipMemcpyAsync(htot, tot, 8, hipMemcpyDeviceToHost, s), "consume totals");
+    if (rows) QCHK(hipMemcpyAsync(hrows, dst, bytes, hipMemcpyDeviceToHost, s), "consume download");
+    QCHK(hipStreamSynchronize(s), "consume sync");
+    const uint32_t c = htot[0], nr = htot[1];
     *n_out = c;
     if (c > cap) return HD_ECAP;   // nothing committed
     if (n_removed) *n_removed = nr;
+    if (nr) {
+        q->live -= nr;
+        q->dead = true;
+    }
     if (c) {
-        // gather into a packed stage (the Pool layout at capacity c16) and
-        // bring it back in one copy
-        const uint32_t c16 = (c + 15u) & ~15u;
-        const size_t bytes = pool_bytes(c16);
-        void* dst = qbuf(q, MQ_STAGE, bytes, &rc);
-        if (rc) return rc;
-        if (q->hstage_cap < bytes) {
-            (void)hipHostFree(q->hstage);
-            q->hstage = nullptr;
-            q->hstage_cap = 0;
-            QCHK(hipHostMalloc(&q->hstage, bytes + bytes / 2, hipHostMallocDefault), "mq host stage");
-            q->hstage_cap = bytes + bytes / 2;
-        }
-        const Pool d = pool_view(dst, c16);
-        k_mq_take<<<q->nsend, 256, 0, s>>>(q->pool, (const uint32_t*)q->buf[MQ_HEADS].p,
-                                           (const uint32_t*)q->buf[MQ_NEWHEAD].p, (const uint32_t*)q->buf[MQ_OFF].p,
-                                           allow, d);
-        QCHK(hipGetLastError(), "k_mq_take");
-        QCHK(hipMemcpyAsync(q->hstage, dst, bytes, hipMemcpyDeviceToHost, s), "consume download");
-        if ((rc = mq_commit(q, nr, s))) return rc;
-        QCHK(hipStreamSynchronize(s), "consume sync");
-        const Pool hp = pool_view(q->hstage, c16);
+        const Pool hp = pool_view(hrows, r16);
         struct Cp { void* dst; const void* src; size_t sz; } cp[] = {
             {out->type, hp.type, (size_t)c},          {out->height, hp.h, 8 * (size_t)c},
             {out->round, hp.r, 8 * (size_t)c},        {out->valid_round, hp.vr, 8 * (size_t)c},
@@ -952,9 +987,8 @@ int hd_mq_consume(hd_mq* q, int64_t h, const uint8_t* allowed32, uint32_t n_allo
         for (auto& x : cp)
             if (x.dst) memcpy(x.dst, x.src, x.sz);
         if (out->adv_class) memset(out->adv_class, 0, c);
-        return HD_OK;
     }
-    return mq_commit(q, nr, s);
+    return HD_OK;
 }
 
 int hd_mq_drop_below(hd_mq* q, int64_t h) {

@@ -213,7 +213,8 @@ int hd_ctx_set_variant(hd_ctx* ctx, int which, int value) {
     if (!ctx || which < 0 || which >= HD_VAR__COUNT) return HD_EINVAL;
     bool ok = false;
     switch (which) {
-        case HD_VAR_VERIFY_WAVES: case HD_VAR_SUM_WAVES: case HD_VAR_FAST_WAVES: ok = value == 2 || value == 3; break;
+        case HD_VAR_VERIFY_WAVES: ok = value >= 2 && value <= 4; break;
+        case HD_VAR_SUM_WAVES: case HD_VAR_FAST_WAVES: ok = value == 2 || value == 3; break;
         case HD_VAR_SUM_PREFETCH: ok = value == 1 || value == 2; break;
         case HD_VAR_SUM_DIGITS: case HD_VAR_RECOVER_G: ok = value == 0 || value == 1; break;
         case HD_VAR_SPLIT_K: ok = value == -1 || value == 0 || value == 4 || value == 8 || value == 16; break;
@@ -297,12 +298,14 @@ int hd_launch_slow(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint
 #define HD_LAUNCH_VERIFY(C, W)                                                                                    \
     k_verify<C, W><<<blocks, 256, 0, s>>>(b, ctx->d_gtab, ctx->d_adm, ctx->d_adm_perm, ctx->n_adm, ctx->adm_steps, \
                                           d_verdict, d_rec32, d_signer, d_bitmap, d_digest, ctl, fbg)
-    // waves/SIMD the kernel is register-allocated for (HD_VERIFY_WAVES = 2/3, default 3)
+    // waves/SIMD the kernel is register-allocated for (HD_VAR_VERIFY_WAVES 2 / 3 / 4,
+    // default 3; the other pubkey formats are compiled for 3 only)
     const int w = ctx->verify_waves;
     // the fixed-base G table, when the context has one (HD_VAR_RECOVER_G 0)
     const gp* fbg = ctx->var[HD_VAR_RECOVER_G] ? nullptr : hd_fb_gtab(ctx);
     if (ctx->pkfmt == HD_PUBKEY_COMPRESSED) {
         if (w == 2) HD_LAUNCH_VERIFY(1, 2);
+        else if (w == 4) HD_LAUNCH_VERIFY(1, 4);
         else HD_LAUNCH_VERIFY(1, 3);
     } else if (ctx->pkfmt == HD_PUBKEY_RAW64) {
         HD_LAUNCH_VERIFY(2, 3);

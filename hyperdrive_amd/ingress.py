@@ -108,6 +108,40 @@ class Ingress:
         db, _ = unmarshal_device(self.v, mtype, buf, complete, with_sig, stream=stream)
         return self.push_device(db, stream=stream)
 
+    def push_wires(self, parts, with_sig: bool = True):
+        """Several wire buffers [(mtype, device byte buffer, n), ...] in
+        arrival order.  Each is unmarshalled and verified on one of two
+        streams, alternating, so the buffers' verify calls run concurrently on
+        the device (one call's fallback recoveries and inversion kernels leave
+        most SIMD slots to the other's); the mq inserts then follow in arrival
+        order.  Returns the verdicts of each buffer's complete records."""
+        torch = _torch()
+        if not parts:
+            return []
+        dev = parts[0][1].device
+        if getattr(self, "_streams", None) is None or self._streams[0].device != dev:
+            s0 = work_stream(dev)
+            self._streams = [s0, torch.cuda.Stream(device=dev, priority=s0.priority)]
+        staged = []
+        for k, (mtype, buf, n) in enumerate(parts):
+            s = self._streams[k % 2]
+            s.wait_stream(torch.cuda.current_stream(dev))
+            size = record_size(mtype, with_sig)
+            complete = min(n, buf.numel() // size) if size else 0
+            if complete == 0:
+                staged.append((None, torch.empty(0, dtype=torch.uint8, device=dev), s))
+                continue
+            db, _ = unmarshal_device(self.v, mtype, buf, complete, with_sig, stream=s, sync=False)
+            verdict = torch.empty(complete, dtype=torch.uint8, device=dev)
+            self.v.verify_batch_device(db.c_struct(), verdict.data_ptr(), None, None, None, s.cuda_stream)
+            staged.append((db, verdict, s))
+        out = []
+        for db, verdict, s in staged:
+            if db is not None:
+                self.mq.insert_verified_device(db, verdict, self.height, stream=s)
+            out.append(verdict)
+        return out
+
     def flush(self) -> FlushResult:
         """mq.Consume(CurrentHeight, ..., procsAllowed) with procsAllowed = the
         verifier's admitted set now, then the vote-log inserts."""

@@ -20,6 +20,8 @@ for step in "$@"; do
     gtest1) run pytest_gpu1 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "golden or c1 or host_pipeline or routed or multi" ;;
     bench_vs1) HD_BENCH_VSTREAMS=1 run bench_vs1 300 python bench.py --no-cpu --no-aux ;;
     bench_fast) run bench_fast 300 python bench.py --no-cpu --no-aux ;;
+    pipe) run pipe_c3 300 python scripts/pipe_probe.py C3 && run pipe_c2 300 python scripts/pipe_probe.py C2 && run pipe_c5 300 python scripts/pipe_probe.py C5 ;;
+    trace_c3) run trace_c3 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_c3 -o run -- python3 scripts/pipe_probe.py C3 6 ;;
     trace2) run trace2 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace2 -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub ;;
     fieldbench) run fieldbench 120 scripts/fieldbench 3 ;;
     gtest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;

@@ -187,6 +187,7 @@ def run_gpu(z, verifier):
     assert ing.f == rep.f
     try:
         for c in range(int(z["chunk"].max()) + 1):
+            parts = []
             for t in (PROPOSE, PREVOTE, PRECOMMIT):
                 idx = np.flatnonzero((z["chunk"] == c) & (z["type"] == t))
                 if not len(idx):
@@ -194,7 +195,13 @@ def run_gpu(z, verifier):
                 vr = z["valid_round"][idx] if t == PROPOSE else None
                 buf = SC.marshal_array(t, z["height"][idx], z["round"][idx], vr, z["value"][idx], z["frm"][idx],
                                        z["sig"][idx])
-                ing.push_wire(t, torch.frombuffer(bytearray(buf), dtype=torch.uint8).cuda(), len(idx))
+                parts.append((t, torch.frombuffer(bytearray(buf), dtype=torch.uint8).cuda(), len(idx)))
+            # even chunks one buffer at a time, odd chunks overlapped (push_wires)
+            if c % 2:
+                ing.push_wires(parts)
+            else:
+                for t, buf, n in parts:
+                    ing.push_wire(t, buf, n)
             while True:
                 res = ing.flush()
                 b = res.consumed

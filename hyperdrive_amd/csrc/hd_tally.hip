@@ -48,6 +48,8 @@ struct TallyWork {
     DevBuf b[13];
     void* host = nullptr;   // pinned download stage (hipHostMalloc)
     size_t host_cap = 0;
+    uint32_t* scalar = nullptr;   // pinned word (a partition's candidate count)
+    uint32_t guess_hr = 1024, guess_cnt = 1024;   // staged row capacities (the last call's counts + 1/4)
 };
 // T_G: the hash tables; T_C: the dense log cells; T_D: a partition's candidates;
 // T_SEL: the output stage;
@@ -237,8 +239,10 @@ __global__ void k_tally_rounds(DevBatch b, const uint32_t* __restrict__ cand, ui
 __global__ void k_tally_logs(DevBatch b, const uint32_t* __restrict__ cand, uint32_t m,
                              const uint32_t* __restrict__ gslot, const uint32_t* __restrict__ rank_of,
                              const uint32_t* __restrict__ adm, uint32_t S, int adm_steps, uint32_t* __restrict__ Dd,
-                             uint32_t* __restrict__ D, uint32_t mask, uint32_t* __restrict__ ref, int adm_in_lds) {
+                             const uint32_t* __restrict__ n_hr, size_t dcap, uint32_t* __restrict__ D, uint32_t mask,
+                             uint32_t* __restrict__ ref, int adm_in_lds) {
     extern __shared__ uint32_t sh_adm[];
+    if (Dd && (size_t)*n_hr * 2 * S > dcap) Dd = nullptr;   // more rounds than dense cells: all hashed
     if (adm_in_lds) adm_stage(sh_adm, adm, S);
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < m; q += stride) {
@@ -429,35 +433,52 @@ __global__ __launch_bounds__(256) void k_tally_chunk_write(uint32_t n, const uin
     }
 }
 
-__global__ void k_tally_emit_hr(uint32_t n_hr, const uint32_t* __restrict__ slot, const uint32_t* __restrict__ cand,
+// the dense log cells of the rounds found (n_hr x per words, n_hr on the
+// device), left alone when they exceed the allocation (k_tally_logs then
+// hashes every candidate)
+__global__ __launch_bounds__(256) void k_tally_dense_clear(uint32_t* __restrict__ Dd, const uint32_t* __restrict__ n_hr,
+                                                           uint32_t per, size_t cap) {
+    const size_t cells = (size_t)*n_hr * per;
+    if (cells > cap) return;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < cells; i += (size_t)gridDim.x * blockDim.x)
+        Dd[i] = kEmpty;
+}
+
+// Emit kernels: the first min(count, cap) groups in output order (count on
+// the device, cap the stage's capacity)
+__global__ void k_tally_emit_hr(const uint32_t* __restrict__ d_n, uint32_t cap, const uint32_t* __restrict__ slot,
+                                const uint32_t* __restrict__ cand,
                                 const uint32_t* __restrict__ gidx, GTab G, const int64_t* __restrict__ h,
                                 const int64_t* __restrict__ r, int64_t* __restrict__ oh, int64_t* __restrict__ orr,
                                 uint32_t* __restrict__ oprev, uint32_t* __restrict__ oprec, uint32_t* __restrict__ oany,
                                 uint32_t* __restrict__ orep) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n_hr) return;
-    const uint32_t s = slot[k], i = msg_of(cand, G.claim[s]);
-    orep[k] = gidx ? gidx[i] : i;
-    oh[k] = h[i];
-    orr[k] = r[i];
-    oprev[k] = G.nprev[s];
-    oprec[k] = G.nprec[s];
-    oany[k] = G.nprev[s] + G.nprec[s] - G.nboth[s];
+    const uint32_t n = min(*d_n, cap);
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const uint32_t s = slot[k], i = msg_of(cand, G.claim[s]);
+        orep[k] = gidx ? gidx[i] : i;
+        oh[k] = h[i];
+        orr[k] = r[i];
+        oprev[k] = G.nprev[s];
+        oprec[k] = G.nprec[s];
+        oany[k] = G.nprev[s] + G.nprec[s] - G.nboth[s];
+    }
 }
 
-__global__ void k_tally_emit_counts(uint32_t n_c, const uint32_t* __restrict__ slot, const uint32_t* __restrict__ cand,
+__global__ void k_tally_emit_counts(const uint32_t* __restrict__ d_n, uint32_t cap, const uint32_t* __restrict__ slot,
+                                    const uint32_t* __restrict__ cand,
                                     const uint32_t* __restrict__ gidx, CTab C, const int64_t* __restrict__ h,
                                     const int64_t* __restrict__ r, const uint8_t* __restrict__ type,
                                     int64_t* __restrict__ oh, int64_t* __restrict__ orr, uint8_t* __restrict__ ot,
                                     uint32_t* __restrict__ orep, uint32_t* __restrict__ on) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n_c) return;
-    const uint32_t s = slot[k], i = msg_of(cand, C.claim[s]);
-    oh[k] = h[i];
-    orr[k] = r[i];
-    ot[k] = type[i];
-    orep[k] = gidx ? gidx[i] : i;
-    on[k] = C.n[s];
+    const uint32_t n = min(*d_n, cap);
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const uint32_t s = slot[k], i = msg_of(cand, C.claim[s]);
+        oh[k] = h[i];
+        orr[k] = r[i];
+        ot[k] = type[i];
+        orep[k] = gidx ? gidx[i] : i;
+        on[k] = C.n[s];
+    }
 }
 
 // ---------------------------------------------------------- routing (C4)
@@ -590,6 +611,7 @@ void hd_tally_release(hd_ctx* ctx) {
     for (auto& b : ctx->tally->b)
         if (b.p) (void)hipFree(b.p);
     if (ctx->tally->host) (void)hipHostFree(ctx->tally->host);
+    if (ctx->tally->scalar) (void)hipHostFree(ctx->tally->scalar);
     delete ctx->tally;
     ctx->tally = nullptr;
 }
@@ -623,10 +645,20 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     int rc = 0;
     // blocks per CU of the probe passes (HD_TALLY_BPC, default 16)
     static const uint32_t bpc = getenv("HD_TALLY_BPC") ? (uint32_t)std::max(1, atoi(getenv("HD_TALLY_BPC"))) : 16u;
-    uint8_t* d_dup = out->dup ? (uint8_t*)tbuf(ctx, T_DUP, n, &rc) : nullptr;
+    // The output stage: [n_hr, n_cnt | per-message classification | per-round
+    // rows (32 B each, capacity H) | per-value rows (25 B each, capacity Cg)],
+    // downloaded with ONE copy after ONE host sync.  H and Cg are the previous
+    // call's counts plus a margin; a batch with more groups than that emits and
+    // downloads its rows a second time (the counts are known by then).
+    TallyWork* tw = ctx->tally;
+    const size_t dup_off = 64, rows_off = dup_off + (((out->dup ? (size_t)n : 0) + 63) & ~(size_t)63);
+    uint32_t H = tw->guess_hr, Cg = tw->guess_cnt;
+    auto stage_bytes = [&](uint32_t h, uint32_t c) { return rows_off + 32 * (size_t)h + 25 * (size_t)c + 64; };
+    char* st = (char*)tbuf(ctx, T_SEL, stage_bytes(H, Cg), &rc);
     uint32_t* at = (uint32_t*)tbuf(ctx, T_SORTK, 8 * (size_t)n, &rc);   // candidate flags; then at_g | at_c
     uint32_t* ccnt = (uint32_t*)tbuf(ctx, T_TMP, 4 * ((size_t)(n + HD_CHUNK - 1) / HD_CHUNK + 2), &rc);
     if (rc) return rc;
+    uint8_t* d_dup = out->dup ? (uint8_t*)(st + dup_off) : nullptr;
     // Items: the whole batch, or a partition's candidates compacted in batch
     // order (the rest of the tally then scales with the partition, not with
     // the replicated batch).
@@ -641,8 +673,10 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
         k_tally_chunk_counts<<<nch, 256, 0, s>>>(n, at, ccnt);
         k_tally_chunk_write<<<nch, 256, 0, s>>>(n, at, ccnt, cl, nullptr, ccnt + nch);
         TCHK(hipGetLastError(), "tally candidate kernels");
-        TCHK(hipMemcpyAsync(&m, ccnt + nch, 4, hipMemcpyDeviceToHost, s), "candidate count");
+        if (!tw->scalar) TCHK(hipHostMalloc((void**)&tw->scalar, 64, hipHostMallocDefault), "tally scalar");
+        TCHK(hipMemcpyAsync(tw->scalar, ccnt + nch, 4, hipMemcpyDeviceToHost, s), "candidate count");
         TCHK(hipStreamSynchronize(s), "candidate count sync");
+        m = tw->scalar[0];
         cand = cl;
     }
     if (m == 0) {   // nothing to tally here (dup: every message 3)
@@ -663,6 +697,12 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     uint32_t* gslot = (uint32_t*)tbuf(ctx, T_GSLOT, 4 * (size_t)m, &rc);
     uint32_t* ref = (uint32_t*)tbuf(ctx, T_DSLOT, 4 * (size_t)m, &rc);
     uint32_t* ord = (uint32_t*)tbuf(ctx, T_SORTV, 8 * (size_t)m, &rc);     // order_g | order_c
+    // dense log cells (n_hr x 2 x S, n_hr known on the device only) for
+    // admitted signatories, the hashed D table for the rest: room for every
+    // item's round up to HD_TALLY_DENSE_MAX words; the logs pass checks n_hr
+    const uint32_t S = ctx->n_adm;
+    const size_t dcap = S > 0 ? std::min<size_t>(HD_TALLY_DENSE_MAX, (size_t)m * 2 * S) : 0;
+    uint32_t* Dd = dcap ? (uint32_t*)tbuf(ctx, T_C, 4 * dcap, &rc) : nullptr;
     if (rc) return rc;
     const size_t K = cap;
     GTab G{tabs, tabs + 3 * K, tabs + 4 * K, tabs + 5 * K};
@@ -677,42 +717,48 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     k_tally_rounds<<<grid, 256, 0, s>>>(b, cand, m, d_verdict, d_bitmap, part, G, mask, gslot, d_dup);
     rc = table_order(ctx, m, cap, G.claim, at, ccnt, ord, rank_of, tot, s);
     if (rc) return rc;
-    uint32_t n_hr = 0;
-    TCHK(hipMemcpyAsync(&n_hr, tot, 4, hipMemcpyDeviceToHost, s), "round count");
-    TCHK(hipStreamSynchronize(s), "round count sync");
-    // dense log cells (n_hr x 2 x S) for admitted signatories, the hashed D
-    // table for the rest
-    const uint32_t S = ctx->n_adm;
-    const size_t cells = (size_t)n_hr * 2 * S;
-    uint32_t* Dd = nullptr;
-    if (S > 0 && cells <= HD_TALLY_DENSE_MAX) {
-        Dd = (uint32_t*)tbuf(ctx, T_C, 4 * cells, &rc);
-        if (rc) return rc;
-        TCHK(hipMemsetAsync(Dd, 0xFF, 4 * cells, s), "clear dense logs");
-    }
+    if (Dd)
+        k_tally_dense_clear<<<std::min<uint32_t>(nblk((uint32_t)dcap), (uint32_t)ctx->n_cu * 4u), 256, 0, s>>>(
+            Dd, tot, 2 * S, dcap);
     const size_t adm_lds = Dd ? adm_lds_bytes(S) : 0;
-    k_tally_logs<<<grid, 256, adm_lds, s>>>(b, cand, m, gslot, rank_of, ctx->d_adm, S, ctx->adm_steps, Dd, d, mask, ref,
-                                            adm_lds > 0);
+    k_tally_logs<<<grid, 256, adm_lds, s>>>(b, cand, m, gslot, rank_of, ctx->d_adm, S, ctx->adm_steps, Dd, tot, dcap, d,
+                                            mask, ref, adm_lds > 0);
     k_tally_values<<<grid, 256, 0, s>>>(b, cand, m, Dd, S, d, G, C, mask, gslot, ref, d_dup);
     TCHK(hipGetLastError(), "tally kernels");
     rc = table_order(ctx, m, cap, C.claim, at + m, ccnt, ord + m, nullptr, tot + 1, s);
     if (rc) return rc;
-    uint32_t n_cnt = 0;
-    TCHK(hipMemcpyAsync(&n_cnt, tot + 1, 4, hipMemcpyDeviceToHost, s), "group counts");
-    TCHK(hipStreamSynchronize(s), "group count sync");
-    out->n_hr = n_hr;
-    out->n_counts = n_cnt;
-    if (n_hr > out->cap_hr || n_cnt > out->cap_counts) return HD_ECAP;
-    // Every output into one device stage -- per-round rows (32 B each), the
-    // per-value rows (25 B each), the per-message classification -- and ONE
-    // download into a pinned host stage, then host copies into the caller's
-    // arrays (one blit instead of a dozen).
-    const size_t hr_bytes = 32 * (size_t)n_hr, cnt_bytes = 25 * (size_t)n_cnt;
-    const size_t dup_off = (hr_bytes + cnt_bytes + 63) & ~(size_t)63;
-    const size_t total = dup_off + (out->dup ? (size_t)n : 0);
-    char* st = (char*)tbuf(ctx, T_SEL, total + 64, &rc);
-    if (rc) return rc;
-    TallyWork* tw = ctx->tally;
+    // rows at capacity (H, Cg) in column arrays
+    struct Cols {
+        int64_t *o_h, *o_r, *c_h, *c_r;
+        uint32_t *o_prev, *o_prec, *o_any, *o_rep, *c_rep, *c_n;
+        uint8_t* c_t;
+    };
+    auto cols = [&](char* base, uint32_t h, uint32_t c) {
+        Cols x;
+        x.o_h = reinterpret_cast<int64_t*>(base);
+        x.o_r = x.o_h + h;
+        x.o_prev = reinterpret_cast<uint32_t*>(x.o_r + h);
+        x.o_prec = x.o_prev + h;
+        x.o_any = x.o_prec + h;
+        x.o_rep = x.o_any + h;
+        x.c_h = reinterpret_cast<int64_t*>(base + 32 * (size_t)h);
+        x.c_r = x.c_h + c;
+        x.c_rep = reinterpret_cast<uint32_t*>(x.c_r + c);
+        x.c_n = x.c_rep + c;
+        x.c_t = reinterpret_cast<uint8_t*>(x.c_n + c);
+        return x;
+    };
+    auto emit = [&](char* base, uint32_t h, uint32_t c) {
+        const Cols x = cols(base, h, c);
+        k_tally_emit_hr<<<std::min<uint32_t>(nblk(std::min(h, m)), (uint32_t)ctx->n_cu * 4u), 256, 0, s>>>(
+            tot, h, ord, cand, gidx, G, b.height, b.round, x.o_h, x.o_r, x.o_prev, x.o_prec, x.o_any, x.o_rep);
+        k_tally_emit_counts<<<std::min<uint32_t>(nblk(std::min(c, m)), (uint32_t)ctx->n_cu * 4u), 256, 0, s>>>(
+            tot + 1, c, ord + m, cand, gidx, C, b.height, b.round, b.type, x.c_h, x.c_r, x.c_t, x.c_rep, x.c_n);
+        return hipGetLastError();
+    };
+    TCHK(emit(st + rows_off, H, Cg), "tally emit");
+    TCHK(hipMemcpyAsync(st, tot, 8, hipMemcpyDeviceToDevice, s), "tally counts stage");
+    const size_t total = stage_bytes(H, Cg);
     if (tw->host_cap < total) {
         if (tw->host) (void)hipHostFree(tw->host);
         tw->host = nullptr;
@@ -720,43 +766,50 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
         TCHK(hipHostMalloc(&tw->host, total + (total >> 2), hipHostMallocDefault), "tally host stage");
         tw->host_cap = total + (total >> 2);
     }
-    int64_t* o_h = reinterpret_cast<int64_t*>(st);
-    int64_t* o_r = o_h + n_hr;
-    uint32_t* o_prev = reinterpret_cast<uint32_t*>(o_r + n_hr);
-    uint32_t* o_prec = o_prev + n_hr;
-    uint32_t* o_any = o_prec + n_hr;
-    uint32_t* o_rep = o_any + n_hr;
-    int64_t* c_h = reinterpret_cast<int64_t*>(st + hr_bytes);
-    int64_t* c_r = c_h + n_cnt;
-    uint32_t* c_rep = reinterpret_cast<uint32_t*>(c_r + n_cnt);
-    uint32_t* c_n = c_rep + n_cnt;
-    uint8_t* c_t = reinterpret_cast<uint8_t*>(c_n + n_cnt);
-    if (n_hr)
-        k_tally_emit_hr<<<nblk(n_hr), 256, 0, s>>>(n_hr, ord, cand, gidx, G, b.height, b.round, o_h, o_r, o_prev,
-                                                   o_prec, o_any, o_rep);
-    if (n_cnt)
-        k_tally_emit_counts<<<nblk(n_cnt), 256, 0, s>>>(n_cnt, ord + m, cand, gidx, C, b.height, b.round, b.type, c_h,
-                                                        c_r, c_t, c_rep, c_n);
-    TCHK(hipGetLastError(), "tally emit");
-    if (out->dup) TCHK(hipMemcpyAsync(st + dup_off, d_dup, (size_t)n, hipMemcpyDeviceToDevice, s), "dup stage");
     TCHK(hipMemcpyAsync(tw->host, st, total, hipMemcpyDeviceToHost, s), "tally download");
     TCHK(hipStreamSynchronize(s), "tally sync");
-    const char* hst = (const char*)tw->host;
-    auto put = [&](void* dst, const void* dev_src, size_t sz) {
-        if (dst && sz) memcpy(dst, hst + ((const char*)dev_src - st), sz);
+    const uint32_t n_hr = reinterpret_cast<const uint32_t*>(tw->host)[0];
+    const uint32_t n_cnt = reinterpret_cast<const uint32_t*>(tw->host)[1];
+    out->n_hr = n_hr;
+    out->n_counts = n_cnt;
+    tw->guess_hr = std::max<uint32_t>(1024u, n_hr + n_hr / 4);
+    tw->guess_cnt = std::max<uint32_t>(1024u, n_cnt + n_cnt / 4);
+    if (n_hr > out->cap_hr || n_cnt > out->cap_counts) return HD_ECAP;
+    if (out->dup) memcpy(out->dup, (const char*)tw->host + dup_off, (size_t)n);
+    const char* hrows = (const char*)tw->host + rows_off;
+    if (n_hr > H || n_cnt > Cg) {   // more groups than staged: emit and download the rows again
+        H = n_hr;
+        Cg = n_cnt;
+        const size_t rb = 32 * (size_t)H + 25 * (size_t)Cg;
+        char* st2 = (char*)tbuf(ctx, T_NSEL, rb + 64, &rc);
+        if (rc) return rc;
+        TCHK(emit(st2, H, Cg), "tally emit");
+        if (tw->host_cap < rb) {
+            (void)hipHostFree(tw->host);
+            tw->host = nullptr;
+            tw->host_cap = 0;
+            TCHK(hipHostMalloc(&tw->host, rb + (rb >> 2), hipHostMallocDefault), "tally host stage");
+            tw->host_cap = rb + (rb >> 2);
+        }
+        TCHK(hipMemcpyAsync(tw->host, st2, rb, hipMemcpyDeviceToHost, s), "tally download");
+        TCHK(hipStreamSynchronize(s), "tally sync");
+        hrows = (const char*)tw->host;
+    }
+    const Cols x = cols(const_cast<char*>(hrows), H, Cg);
+    auto put = [&](void* dst, const void* src, size_t sz) {
+        if (dst && sz) memcpy(dst, src, sz);
     };
-    put(out->hr_height, o_h, 8 * (size_t)n_hr);
-    put(out->hr_round, o_r, 8 * (size_t)n_hr);
-    put(out->hr_prevotes, o_prev, 4 * (size_t)n_hr);
-    put(out->hr_precommits, o_prec, 4 * (size_t)n_hr);
-    put(out->hr_any, o_any, 4 * (size_t)n_hr);
-    put(out->hr_rep, o_rep, 4 * (size_t)n_hr);
-    put(out->count_height, c_h, 8 * (size_t)n_cnt);
-    put(out->count_round, c_r, 8 * (size_t)n_cnt);
-    put(out->count_type, c_t, (size_t)n_cnt);
-    put(out->count_rep, c_rep, 4 * (size_t)n_cnt);
-    put(out->count_n, c_n, 4 * (size_t)n_cnt);
-    if (out->dup) memcpy(out->dup, hst + dup_off, (size_t)n);
+    put(out->hr_height, x.o_h, 8 * (size_t)n_hr);
+    put(out->hr_round, x.o_r, 8 * (size_t)n_hr);
+    put(out->hr_prevotes, x.o_prev, 4 * (size_t)n_hr);
+    put(out->hr_precommits, x.o_prec, 4 * (size_t)n_hr);
+    put(out->hr_any, x.o_any, 4 * (size_t)n_hr);
+    put(out->hr_rep, x.o_rep, 4 * (size_t)n_hr);
+    put(out->count_height, x.c_h, 8 * (size_t)n_cnt);
+    put(out->count_round, x.c_r, 8 * (size_t)n_cnt);
+    put(out->count_type, x.c_t, (size_t)n_cnt);
+    put(out->count_rep, x.c_rep, 4 * (size_t)n_cnt);
+    put(out->count_n, x.c_n, 4 * (size_t)n_cnt);
     return HD_OK;
 }
 

@@ -20,7 +20,9 @@ for step in "$@"; do
     gtest1) run pytest_gpu1 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "golden or c1 or host_pipeline or routed or multi" ;;
     bench_vs1) HD_BENCH_VSTREAMS=1 run bench_vs1 300 python bench.py --no-cpu --no-aux ;;
     bench_fast) run bench_fast 300 python bench.py --no-cpu --no-aux ;;
-    pipe) run pipe_c3 300 python scripts/pipe_probe.py C3 && run pipe_c2 300 python scripts/pipe_probe.py C2 && run pipe_c5 300 python scripts/pipe_probe.py C5 ;;
+    pipe) run pipe_c3 300 python scripts/pipe_probe.py C3 40 && run pipe_c2 300 python scripts/pipe_probe.py C2 30 && run pipe_c5 300 python scripts/pipe_probe.py C5 20 ;;
+    tally) run tally_c2 200 python scripts/tally_probe.py C2 && run tally_c3 200 python scripts/tally_probe.py C3 ;;
+    tally_trace) run tally_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/tally_trace -o run -- python3 scripts/tally_probe.py C2 20 ;;
     trace_c3) run trace_c3 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_c3 -o run -- python3 scripts/pipe_probe.py C3 6 ;;
     rehearse) run rehearse2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29561 bench.py --gpus 2 --dist-backend gloo --steps 4 --warmup 1 --no-cpu --no-aux --no-sub && run rehearse3_c4 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 3 --master-addr 127.0.0.1 --master-port 29562 bench.py --gpus 3 --dist-backend gloo --global-batch 3145728 --steps 3 --warmup 1 --no-cpu --no-aux --no-sub ;;
     trace2) run trace2 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace2 -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub ;;

@@ -22,8 +22,10 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
     v = hd.Verifier(0)
-    ws = work_stream(dev, priority=-1)
-    ts = torch.cuda.Stream(device=dev)
+    ws_hi = work_stream(dev, priority=-1)
+    ws_lo = torch.cuda.Stream(device=dev, priority=0)
+    ts_hi = torch.cuda.Stream(device=dev, priority=-1)
+    ts_lo = torch.cuda.Stream(device=dev, priority=0)
     S = 1000 if wl == "C3" else 100
     keys = v.gen_keys(S)
     v.set_signatories(keys[0])
@@ -34,14 +36,18 @@ def main():
         n = 1 << 20
         db, _, _ = generate(v, 0, n, S, 30 if wl == "C5" else 0, keys=keys, device=str(dev))
     res = {}
-    for vs in (1, 2, 3):
-        for tally in (True, False):
-            bench.Pipeline.VSTREAMS = vs
-            p = bench.Pipeline(v, db, n, 0, 0, 1, None, ws, ts, tally=tally)
-            p.run(3)
-            el = bench.timed(p, steps, None, dev)
-            res[f"vs{vs}_{'tally' if tally else 'notally'}"] = round(el / steps * 1e3, 4)
-            print(wl, vs, tally, res, flush=True)
+    # (verify streams, tally on, verify priority high, tally priority high)
+    settings = [(1, False, True, False), (1, True, True, False), (1, True, False, True),
+                (2, False, True, False), (2, True, True, False), (2, True, False, True),
+                (3, False, True, False), (3, True, True, False), (3, True, False, True)]
+    for vs, tally, vhi, thi in settings:
+        bench.Pipeline.VSTREAMS = vs
+        p = bench.Pipeline(v, db, n, 0, 0, 1, None, ws_hi if vhi else ws_lo, ts_hi if thi else ts_lo, tally=tally)
+        p.run(3)
+        el = bench.timed(p, steps, None, dev)
+        key = f"vs{vs}_" + (("tally_" + ("thi" if thi else "vhi")) if tally else "notally")
+        res[key] = round(el / steps * 1e3, 4)
+        print(wl, key, res[key], flush=True)
     print({"workload": wl, "messages": n, "ms_per_step": res}, flush=True)
     v.close()
 

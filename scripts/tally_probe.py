@@ -1,13 +1,16 @@
-"""The tally alone on the C2 batch (1M verified votes, 100 signatories): wall
-time per hd_tally_device_bitmap call (host syncs included), for the kernel
-breakdown run it under rocprofv3 --kernel-trace --stats."""
+"""Measurement aid (not product code): the tally alone on a verified batch --
+hd_tally_device_bitmap called back to back on one stream -- so a
+`rocprofv3 --kernel-trace --stats` run shows each tally kernel's own
+duration without verify kernels competing for the CUs.
+
+Usage: python scripts/tally_probe.py C2|C3|C5 [calls]"""
 import ctypes
-import json
 import os
 import sys
 import time
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
 def main():
@@ -15,30 +18,41 @@ def main():
     import hyperdrive_amd as hd
     from hyperdrive_amd import _lib
     from hyperdrive_amd.device import generate, work_stream
-    N, S = int(os.environ.get("TP_N", 1 << 20)), int(os.environ.get("TP_S", 100))
-    adv = int(os.environ.get("TP_ADV", 0))
+    wl = sys.argv[1] if len(sys.argv) > 1 else "C2"
+    calls = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
     v = hd.Verifier(0)
-    sigs, foreign = v.gen_keys(S)
-    v.set_signatories(sigs)
-    db, _, _ = generate(v, 0, N, S, adv, keys=(sigs, foreign))
-    ws = work_stream()
-    verdict = torch.empty(N, dtype=torch.uint8, device="cuda")
-    bitmap = torch.zeros(N // 32, dtype=torch.int32, device="cuda")
-    cb = db.c_struct()
-    v.verify_batch_device(cb, verdict.data_ptr(), None, None, bitmap.data_ptr(), ws.cuda_stream)
-    ws.synchronize()
+    ws = work_stream(dev)
+    S = 1000 if wl == "C3" else 100
+    keys = v.gen_keys(S)
+    v.set_signatories(keys[0])
+    if wl == "C3":
+        n = (64 * (2 * S + 1) + 31) // 32 * 32
+        db, _, _ = generate(v, 1, n, S, 0, keys=keys, device=str(dev))
+    else:
+        n = 1 << 20
+        db, _, _ = generate(v, 0, n, S, 30 if wl == "C5" else 0, keys=keys, device=str(dev))
+    shard = db.c_struct()
+    verdict = torch.empty(n, dtype=torch.uint8, device=dev)
+    bitmap = torch.zeros(n // 32, dtype=torch.int32, device=dev)
+    for _ in range(2):
+        v.verify_batch_device(shard, verdict.data_ptr(), None, None, bitmap.data_ptr(), ws.cuda_stream)
+    torch.cuda.synchronize()
+    t_out, _ = v._tally_struct(n, pinned=True)
     lib = _lib.load()
-    t_out, _ = v._tally_struct(N)
-    ms = []
-    for k in range(int(os.environ.get("TP_CALLS", 20))):
-        torch.cuda.synchronize()
+    times = []
+    for k in range(calls):
         t = time.perf_counter()
-        rc = lib.hd_tally_device_bitmap(v.handle, ctypes.byref(cb), bitmap.data_ptr(), ctypes.byref(t_out),
+        rc = lib.hd_tally_device_bitmap(v.handle, ctypes.byref(shard), bitmap.data_ptr(), ctypes.byref(t_out),
                                         ws.cuda_stream)
+        times.append(time.perf_counter() - t)
         assert rc == 0, rc
-        ms.append(round((time.perf_counter() - t) * 1e3, 3))
-    print(json.dumps({"n": N, "signers": S, "adv": adv, "tally_ms": ms, "median_ms": sorted(ms)[len(ms) // 2],
-                      "n_hr": t_out.n_hr, "n_counts": t_out.n_counts}), flush=True)
+    times.sort()
+    print({"workload": wl, "messages": n, "n_hr": t_out.n_hr, "n_counts": t_out.n_counts,
+           "tally_ms_median": round(times[len(times) // 2] * 1e3, 4), "tally_ms_min": round(times[0] * 1e3, 4)},
+          flush=True)
+    v.close()
 
 
 if __name__ == "__main__":

@@ -267,11 +267,12 @@ def test_pairwise_check_equals_single(fb, oracle):
 @pytest.mark.gpu
 @pytest.mark.parametrize("width", [16, 20])
 def test_key_table_widths_equal_full_recovery(gpu, monkeypatch, width):
-    """Both per-key table widths (HD_FB_PW: 16-bit windows, 16 additions for
-    u2; 20-bit, 13 additions) give the full recovery's outputs on the
-    adversarial mix, a ragged batch (n not a multiple of the 8 messages per
-    lane of the split check), and after the admitted set is re-mapped at the
-    other width (every key is learned again)."""
+    """Both per-key table widths (HD_FB_PW at context creation, then the
+    key_width variant: 16-bit windows, 16 additions for u2; 20-bit, 13
+    additions) give the full recovery's outputs on the adversarial mix, a
+    ragged batch (n not a multiple of the 8 messages per lane of the split
+    check), and after the admitted set is re-mapped at the other width (every
+    key is learned again)."""
     import torch
     from hyperdrive_amd.device import generate
     from hyperdrive_amd.verify import Verifier
@@ -289,7 +290,8 @@ def test_key_table_widths_equal_full_recovery(gpu, monkeypatch, width):
         got = _run(fast, db, n)
         assert all(torch.equal(a, b) for a, b in zip(ref, got))
     assert fast.known_keys() > 0 and fast.fastpath_stats()[1] <= int((ref[0] != 0).sum())
-    monkeypatch.setenv("HD_FB_PW", str(36 - width))
+    assert fast.variant("key_width") == width
+    fast.set_variant("key_width", 36 - width)      # (the environment is read at creation only)
     fast.set_signatories(ks[0])
     assert fast.known_keys() == 0
     for _ in range(2):

@@ -835,8 +835,21 @@ def pmc_traffic():
     return None
 
 
+def cgroup_cpu_quota():
+    """CPUs' worth of time the cgroup v2 quota grants (cpu.max), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, period = fh.read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        return None
+
+
 def host_cpu_info():
-    """(CPU model, cores this process may run on, online CPUs of the host)."""
+    """(CPU model, cores this process may use, online CPUs of the host): the
+    affinity mask bounded by the cgroup's CPU quota (a GPU box shows every
+    CPU of the machine in its mask but grants one GPU's share of time; more
+    threads than the quota only queue)."""
     model = ""
     try:
         with open("/proc/cpuinfo") as fh:
@@ -850,6 +863,9 @@ def host_cpu_info():
         allowed = len(os.sched_getaffinity(0))
     except AttributeError:
         allowed = os.cpu_count() or 1
+    quota = cgroup_cpu_quota()
+    if quota:
+        allowed = min(allowed, quota)
     return model, allowed, os.cpu_count() or allowed
 
 
@@ -878,7 +894,10 @@ def run_cpu_baseline(args, v, db, sigs, gpu_verdict, gpu_recovered):
     f = len(sigs) // 3
     pv = lambda h, r: O.canonical_value(h, r)
     figures = {}
-    for label, threads in (("all_threads", args.cpu_threads or allowed), ("per_gpu_share", share)):
+    legs = [("all_threads", args.cpu_threads or allowed), ("per_gpu_share", share)]
+    if legs[0][1] == share:
+        legs = legs[1:]
+    for label, threads in legs:
         t0 = time.perf_counter()
         verdict, rec = co.verify(sample, sigs, True, threads=threads)
         t1 = time.perf_counter()
@@ -898,10 +917,13 @@ def run_cpu_baseline(args, v, db, sigs, gpu_verdict, gpu_recovered):
                  {k: quorum.decide(gt, int(h), int(r), f, pv(int(h), int(r)), True)[k] for k in bits}
                  for (h, r), d in zip(tal["hr"][:, :2].tolist(), tal["decide"].tolist()))
     exact_tally = c_counts == gt.count and c_any == gt.distinct_any
-    best = figures["all_threads"]
+    figures.setdefault("all_threads", figures["per_gpu_share"])
+    best = max(figures.values(), key=lambda fig: fig["msgs_per_s"])
     return {"value": best["msgs_per_s"], "unit": "msgs/s", "cores": best["threads"], "kind": "port",
             "cpu_model": model, "host_cpus_allowed": allowed, "host_cpus_online": online,
-            "per_gpu_share": figures["per_gpu_share"], "all_threads": best,
+            "cgroup_cpu_quota": cgroup_cpu_quota(),
+            "per_gpu_share": figures["per_gpu_share"], "all_threads": figures["all_threads"],
+            "value_from": "the faster of the all-threads and per-GPU-share runs",
             "bit_exact_vs_gpu": bool(exact_verify and exact_tally and dec_ok),
             "bit_exact_detail": {"verdicts_and_signatories": bool(exact_verify), "tally_rows": bool(exact_tally),
                                  "decisions": bool(dec_ok), "rounds_decided": int(len(tal["hr"])),

@@ -271,7 +271,15 @@ struct SplitRows {
     uint32_t* pre;   // 9n: prefix products of s, then s^-1 R (radix 2^29); later of Z, then Z^-1
     uint32_t* xyz;   // 27n: the Jacobian sum
     uint32_t* dig;   // (NWIN(WG) + NWIN(W)) n: window digits as table references (fb_ref)
+    int prio;        // wave priority of the short kernels (HD_VAR_WAVE_PRIO)
 };
+
+// s_setprio takes an immediate: a uniform branch per level
+HD void wave_prio(int p) {
+    if (p == 1) __builtin_amdgcn_s_setprio(1);
+    else if (p == 2) __builtin_amdgcn_s_setprio(2);
+    else if (p >= 3) __builtin_amdgcn_s_setprio(3);
+}
 
 // a Booth digit of window w as a reference into the base's table: entry
 // index | HD_REF_NEG for a negative digit, HD_REF_ZERO for 0 (entry 0 of the
@@ -294,6 +302,7 @@ __global__ __launch_bounds__(256) void k_fast_prep(DevBatch b, const uint8_t* __
                                                    const uint32_t* __restrict__ adm, uint32_t n_adm, int adm_steps,
                                                    SplitRows rows, int adm_in_lds) {
     extern __shared__ uint32_t sh_adm[];
+    wave_prio(rows.prio);
     if (adm_in_lds) adm_stage(sh_adm, adm, n_adm);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = b.n;
@@ -352,6 +361,7 @@ __global__ __launch_bounds__(256) void k_fast_prep(DevBatch b, const uint8_t* __
 // n / K lanes there are too few waves to hide a load per step.
 template <int K>
 __global__ __launch_bounds__(256) void k_fast_sinv(uint32_t n, uint32_t T, SplitRows rows) {
+    wave_prio(rows.prio);
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
     sc sv[K];
@@ -563,6 +573,7 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
 template <int K>
 __global__ __launch_bounds__(256) void k_fast_zinv(uint32_t n, uint32_t T, SplitRows rows) {
     static_assert(K >= 2 && (K & (K - 1)) == 0, "K: a power of two");
+    wave_prio(rows.prio);
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
     const uint32_t* zrow = rows.xyz + 18 * (size_t)n;
@@ -623,6 +634,7 @@ __global__ __launch_bounds__(256) void k_fast_cmp(DevBatch b, SplitRows rows, co
                                                   uint8_t* __restrict__ verdict, uint8_t* __restrict__ rec32,
                                                   int32_t* __restrict__ signer, uint32_t* __restrict__ slow,
                                                   uint32_t* __restrict__ n_slow, uint32_t* __restrict__ bitmap) {
+    wave_prio(rows.prio);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = b.n;
     const bool present = i < n;
@@ -685,7 +697,9 @@ __global__ __launch_bounds__(256) void k_fast_cmp(DevBatch b, SplitRows rows, co
 __global__ __launch_bounds__(256) void k_slow_lift(DevBatch b, const uint32_t* __restrict__ list,
                                                    const uint32_t* __restrict__ count, uint8_t* __restrict__ verdict,
                                                    uint8_t* __restrict__ rec32, int32_t* __restrict__ signer,
-                                                   uint32_t* __restrict__ out, uint32_t* __restrict__ n_out) {
+                                                   uint32_t* __restrict__ out, uint32_t* __restrict__ n_out,
+                                                   int prio) {
+    wave_prio(prio);
     const uint32_t total = *count, stride = gridDim.x * blockDim.x;
     const uint32_t lane = threadIdx.x & 63u;
     for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += stride) {
@@ -1296,6 +1310,7 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         rows.pre = sc.rows + 26 * (size_t)n;
         rows.xyz = sc.rows + 35 * (size_t)n;
         rows.dig = sums_digits_lds(ctx) ? nullptr : sc.rows + 62 * (size_t)n;
+        rows.prio = ctx->var[HD_VAR_WAVE_PRIO];
         const int k = split_k_for(ctx, n);
         f->last_k = k;
 #define HD_SPLIT(K, WP) launch_split<K, WP>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, sc, s)
@@ -1314,7 +1329,7 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         // its VALID messages
         const uint32_t slow_blocks = std::min(blocks, (uint32_t)std::max(ctx->n_cu, 1) * 4u);
         k_slow_lift<<<slow_blocks, 256, 0, s>>>(b, sc.slow, sc.count, d_verdict, d_rec32, d_signer, sc.slow2,
-                                                sc.count + 1);
+                                                sc.count + 1, ctx->var[HD_VAR_WAVE_PRIO]);
         FBCHK(hipGetLastError(), "k_slow_lift");
         const SlowCtl ctl{sc.slow2, sc.count + 1, f->adm_slot, f->state, f->pub, d_bitmap};
         rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl, slow_blocks, s);
@@ -1336,7 +1351,7 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         // per 256 messages that would mostly start and exit
         const uint32_t slow_blocks = std::min(blocks, (uint32_t)std::max(ctx->n_cu, 1) * 4u);
         k_slow_lift<<<slow_blocks, 256, 0, s>>>(b, sc.slow, sc.count, d_verdict, d_rec32, d_signer, sc.slow2,
-                                                sc.count + 1);
+                                                sc.count + 1, ctx->var[HD_VAR_WAVE_PRIO]);
         FBCHK(hipGetLastError(), "k_slow_lift");
         const SlowCtl ctl{sc.slow2, sc.count + 1, f->adm_slot, f->state, f->pub, nullptr};
         rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl, slow_blocks, s);

@@ -121,6 +121,11 @@ def tally_part_device(v, dbatch, d_bitmap: int, part: int, nparts: int, stream, 
     from . import _lib
     lib = _lib.load()
     t, a = out
+    # the previous call's uploads may still be reading the pinned stage that
+    # the library is about to overwrite: wait for them first
+    prev = getattr(t, "_uploads_done", None)
+    if prev is not None:
+        prev.synchronize()
     rc = lib.hd_tally_device_bitmap_part(v.handle, ctypes.byref(dbatch), d_bitmap, part, nparts, ctypes.byref(t),
                                          stream)
     if rc != 0:
@@ -131,7 +136,12 @@ def tally_part_device(v, dbatch, d_bitmap: int, part: int, nparts: int, stream, 
             return torch.zeros((0, len(cols)), dtype=torch.int64, device=device)
         return torch.stack([torch.from_numpy(a[c][:k].astype(np.int64, copy=False)).to(device, non_blocking=True)
                             for c in cols], 1)
-    return {"counts": rows(COUNT_COLS, t.n_counts), "hr": rows(HR_COLS, t.n_hr)}
+    res = {"counts": rows(COUNT_COLS, t.n_counts), "hr": rows(HR_COLS, t.n_hr)}
+    if torch.device(device).type == "cuda":
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        t._uploads_done = ev
+    return res
 
 
 def gather_tally_device(local, world: int, group=None):

@@ -151,7 +151,11 @@ int hd_ctx_profile(hd_ctx* ctx, int enable);
 #define HD_VAR_FAST_WAVES 6     /* k_verify_fast (split K = 0): 2 (default) or 3 [HD_FAST_WAVES] */
 #define HD_VAR_KEY_WIDTH 7      /* per-key table windows: 0 by the table budget (default), 16 or 20; applies from
                                    the next hd_set_signatories [HD_FB_PW] */
-#define HD_VAR__COUNT 8
+#define HD_VAR_WAVE_PRIO 8      /* wave issue priority (s_setprio 0..3) of the known-key check's short kernels
+                                   (prep, s / Z inversions, comparison, lift): above k_fast_sums' 0 they keep
+                                   their SIMD share while the next call's sums waves share the SIMD
+                                   [HD_WAVE_PRIO] */
+#define HD_VAR__COUNT 9
 int hd_ctx_set_variant(hd_ctx* ctx, int which, int value);
 int hd_ctx_get_variant(hd_ctx* ctx, int which, int* value);
 int hd_ctx_profile_read(hd_ctx* ctx, uint32_t* calls, double* verify_ms, uint32_t* sums_launches, double* sums_ms);

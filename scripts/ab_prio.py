@@ -1,0 +1,69 @@
+"""A/B of the short kernels' wave priority (HD_VAR_WAVE_PRIO) x verify streams,
+interleaved in one process, through bench.py's Pipeline (verify + tally):
+C2 (1M, 100 signatories), C5 (30 % adversarial) and C3 (1000 signatories,
+128,064 messages).  Prints one JSON line per workload: ms/step per setting
+and round."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+import torch
+
+import bench
+import hyperdrive_amd as hd
+from hyperdrive_amd.device import generate, work_stream
+
+PRIOS = [int(p) for p in os.environ.get("AB_PRIOS", "0,1,3").split(",")]
+STREAMS = [int(p) for p in os.environ.get("AB_STREAMS", "1,2").split(",")]
+ROUNDS = int(os.environ.get("AB_ROUNDS", "3"))
+STEPS = int(os.environ.get("AB_STEPS", "20"))
+which = sys.argv[1:] or ["C2", "C5", "C3"]
+
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(0)
+ws = work_stream(dev, priority=-1)
+torch.cuda.set_stream(ws)
+ts = torch.cuda.Stream(device=dev, priority=0)
+
+
+def ab(name, v, db, n):
+    pipe = bench.Pipeline(v, db, n, 0, 0, 1, None, ws, ts)
+    extra = [torch.cuda.Stream(device=dev, priority=ws.priority) for _ in range(max(STREAMS) - 1)]
+    pipe.run(3)
+    res = {f"p{p}_s{s}": [] for p in PRIOS for s in STREAMS}
+    for _ in range(ROUNDS):
+        for p in PRIOS:
+            v.set_variant("wave_prio", p)
+            for s in STREAMS:
+                pipe.wss = [ws] + extra[: s - 1]
+                pipe.run(2)
+                el = bench.timed(pipe, STEPS, None, dev)
+                res[f"p{p}_s{s}"].append(round(el / STEPS * 1e3, 4))
+    vd, _, _ = pipe.last(STEPS)
+    hist = torch.bincount(vd.long(), minlength=8).cpu().tolist()
+    best = {k: round(n / min(x) * 1e-3, 1) for k, x in res.items()}
+    print(json.dumps({"workload": name, "messages": n, "ms_per_step": res, "best_M_msgs_per_s": best,
+                      "verdicts": hist}), flush=True)
+
+
+v = hd.Verifier(0)
+sigs, foreign = v.gen_keys(100)
+v.set_signatories(sigs)
+B = 1 << 20
+if "C2" in which:
+    db, _, _ = generate(v, 0, B, 100, 0, keys=(sigs, foreign), device=str(dev))
+    ab("C2", v, db, B)
+    del db
+if "C5" in which:
+    db, _, _ = generate(v, 0, B, 100, 30, keys=(sigs, foreign), device=str(dev))
+    ab("C5", v, db, B)
+    del db
+if "C3" in which:
+    v.close()
+    v3 = hd.Verifier(0)
+    k3 = v3.gen_keys(1000)
+    v3.set_signatories(k3[0])
+    n3 = (64 * 2001 + 31) // 32 * 32
+    db3, _, _ = generate(v3, 1, n3, 1000, 0, keys=k3, device=str(dev))
+    ab("C3", v3, db3, n3)

@@ -635,8 +635,7 @@ def ingress_c5(v, keys, S, n, ws, dev, heights=64):
                                                          "sig")))
         parts.append((t, sub, marshal_device(v, t, sub, with_sig=True, stream=ws)))
     ing = Ingress(v, height=1, max_capacity=1000)
-    for t, sub, wire in parts:                        # warm (allocations)
-        ing.push_wire(t, wire, sub.n, stream=ws)
+    ing.push_wires([(t, wire, sub.n) for t, sub, wire in parts])   # warm (allocations on both streams)
     ing.votes.reset(1)
     ing.mq.drop_below(2 ** 62)
     torch.cuda.synchronize()

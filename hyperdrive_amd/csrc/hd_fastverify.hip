@@ -89,6 +89,15 @@ struct FbWork {
     // or the key format changes; UINT32_MAX = unknown.
     uint32_t* nr_host = nullptr;
     uint32_t* nr_dev = nullptr;
+    // The fallback list lengths of the latest calls ([0] leftovers of the
+    // check, [1] those past the lift), stored by k_slow_lift / k_verify into
+    // pinned host memory: they size the next calls' fallback grids (both
+    // kernels walk their list grid-stride, so any size is correct; a grid
+    // sized by the last list instead of the batch keeps ~2,000 blocks that
+    // would only start and exit from queueing for SIMD slots behind a
+    // concurrent call's k_fast_sums).  UINT32_MAX = none seen yet.
+    uint32_t* est_host = nullptr;
+    uint32_t* est_dev = nullptr;
     // Ordering between calls (hd_fb_verify): a call waits (on the device) for
     // the last call that used its scratch set.  While keys can still be
     // learned (nr_host != 0), or on the first call after the last key became
@@ -698,9 +707,10 @@ __global__ __launch_bounds__(256) void k_slow_lift(DevBatch b, const uint32_t* _
                                                    const uint32_t* __restrict__ count, uint8_t* __restrict__ verdict,
                                                    uint8_t* __restrict__ rec32, int32_t* __restrict__ signer,
                                                    uint32_t* __restrict__ out, uint32_t* __restrict__ n_out,
-                                                   int prio) {
+                                                   int prio, uint32_t* __restrict__ est) {
     wave_prio(prio);
     const uint32_t total = *count, stride = gridDim.x * blockDim.x;
+    if (est && blockIdx.x == 0 && threadIdx.x == 0) est[0] = total;
     const uint32_t lane = threadIdx.x & 63u;
     for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += stride) {
         const uint32_t p = base + threadIdx.x;
@@ -1036,6 +1046,9 @@ int hd_fb_init(hd_ctx* ctx) {
     FBCHK(hipHostMalloc((void**)&f->nr_host, 4, hipHostMallocMapped | hipHostMallocCoherent), "fb ready count");
     *f->nr_host = 0xFFFFFFFFu;
     FBCHK(hipHostGetDevicePointer((void**)&f->nr_dev, f->nr_host, 0), "fb ready count map");
+    FBCHK(hipHostMalloc((void**)&f->est_host, 8, hipHostMallocMapped | hipHostMallocCoherent), "fb list estimate");
+    f->est_host[0] = f->est_host[1] = 0xFFFFFFFFu;
+    FBCHK(hipHostGetDevicePointer((void**)&f->est_dev, f->est_host, 0), "fb list estimate map");
     int rc = fb_alloc_slots(ctx);
     if (rc) return rc;
     return fb_g_table(ctx, &f->gtab);
@@ -1060,6 +1073,7 @@ void hd_fb_release(hd_ctx* ctx) {
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (f->nr_host) (void)hipHostFree(f->nr_host);
+    if (f->est_host) (void)hipHostFree(f->est_host);
     delete f;
     ctx->fb = nullptr;
 }
@@ -1196,6 +1210,25 @@ static hipEvent_t* fb_prof_pair(std::vector<hipEvent_t>& ev, size_t& used, bool 
     return &ev[2 * used++];
 }
 
+// Blocks of a grid-stride fallback kernel (k_slow_lift, k_verify over a
+// list) for the latest list length seen (FbWork::est_host): 1.25x its
+// blocks, at least 64 (a sudden burst of leftovers costs a few grid-stride
+// rounds once), at most `full`.
+static uint32_t fallback_blocks(uint32_t est, uint32_t full) {
+    if (est == 0xFFFFFFFFu) return full;
+    const uint64_t want = ((uint64_t)est * 5 / 4 + 255) / 256;
+    return (uint32_t)std::min<uint64_t>(full, std::max<uint64_t>(want, std::min(64u, full)));
+}
+
+// Dynamic LDS that caps k_fast_sums at `cap` blocks per CU (HD_VAR_SUM_CAP):
+// with `stat` bytes of static LDS per block, a block reserves just over
+// 1 / (cap + 1) of the CU's 160 KiB.
+static size_t sums_cap_lds(int cap, size_t stat) {
+    if (cap <= 0) return 0;
+    const size_t per = ((160u * 1024u) / (size_t)(cap + 1) + 1 + 511) & ~(size_t)511;
+    return per > stat ? per - stat : 0;
+}
+
 // k_fast_sums occupancy (HD_VAR_SUM_WAVES), prefetch depth
 // (HD_VAR_SUM_PREFETCH) and where the window digits come from (DL:
 // HD_VAR_SUM_DIGITS 0 = computed into LDS, 1 = a k_fast_digits pass)
@@ -1203,12 +1236,14 @@ template <int WP, bool DL>
 static void launch_sums(const hd_ctx* ctx, uint32_t blocks, hipStream_t s, uint32_t n, const gp* gtab,
                         const gp* const* tab, const SplitRows& rows) {
     const int w = ctx->var[HD_VAR_SUM_WAVES], pf = ctx->var[HD_VAR_SUM_PREFETCH];
+    constexpr size_t stat = DL ? 4 * 256 * (size_t)(FbL<HD_FB_WG>::NWIN + FbL<WP>::NWIN) : 4;
+    const size_t dyn = sums_cap_lds(ctx->var[HD_VAR_SUM_CAP], stat);
     if (pf == 2) {
-        if (w == 3) k_fast_sums<3, WP, 2, DL><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
-        else k_fast_sums<2, WP, 2, DL><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
+        if (w == 3) k_fast_sums<3, WP, 2, DL><<<blocks, 256, dyn, s>>>(n, gtab, tab, rows);
+        else k_fast_sums<2, WP, 2, DL><<<blocks, 256, dyn, s>>>(n, gtab, tab, rows);
     } else {
-        if (w == 2) k_fast_sums<2, WP, 1, DL><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
-        else k_fast_sums<3, WP, 1, DL><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
+        if (w == 2) k_fast_sums<2, WP, 1, DL><<<blocks, 256, dyn, s>>>(n, gtab, tab, rows);
+        else k_fast_sums<3, WP, 1, DL><<<blocks, 256, dyn, s>>>(n, gtab, tab, rows);
     }
 }
 static bool sums_digits_lds(const hd_ctx* ctx) { return ctx->var[HD_VAR_SUM_DIGITS] == 0; }
@@ -1327,12 +1362,14 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         FBCHK(hipGetLastError(), "split check launch");
         // k_fast_cmp wrote the valid bitmap; the slow path sets the bits of
         // its VALID messages
-        const uint32_t slow_blocks = std::min(blocks, (uint32_t)std::max(ctx->n_cu, 1) * 4u);
-        k_slow_lift<<<slow_blocks, 256, 0, s>>>(b, sc.slow, sc.count, d_verdict, d_rec32, d_signer, sc.slow2,
-                                                sc.count + 1, ctx->var[HD_VAR_WAVE_PRIO]);
+        const uint32_t full = std::min(blocks, (uint32_t)std::max(ctx->n_cu, 1) * 4u);
+        const uint32_t lift_blocks = fallback_blocks(f->est_host[0], full);
+        k_slow_lift<<<lift_blocks, 256, 0, s>>>(b, sc.slow, sc.count, d_verdict, d_rec32, d_signer, sc.slow2,
+                                                sc.count + 1, ctx->var[HD_VAR_WAVE_PRIO], f->est_dev);
         FBCHK(hipGetLastError(), "k_slow_lift");
-        const SlowCtl ctl{sc.slow2, sc.count + 1, f->adm_slot, f->state, f->pub, d_bitmap};
-        rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl, slow_blocks, s);
+        const SlowCtl ctl{sc.slow2, sc.count + 1, f->adm_slot, f->state, f->pub, d_bitmap, f->est_dev + 1};
+        rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl,
+                            fallback_blocks(f->est_host[1], full), s);
         if (rc) return rc;
         return fb_learn(ctx, s);
     }
@@ -1351,9 +1388,9 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         // per 256 messages that would mostly start and exit
         const uint32_t slow_blocks = std::min(blocks, (uint32_t)std::max(ctx->n_cu, 1) * 4u);
         k_slow_lift<<<slow_blocks, 256, 0, s>>>(b, sc.slow, sc.count, d_verdict, d_rec32, d_signer, sc.slow2,
-                                                sc.count + 1, ctx->var[HD_VAR_WAVE_PRIO]);
+                                                sc.count + 1, ctx->var[HD_VAR_WAVE_PRIO], nullptr);
         FBCHK(hipGetLastError(), "k_slow_lift");
-        const SlowCtl ctl{sc.slow2, sc.count + 1, f->adm_slot, f->state, f->pub, nullptr};
+        const SlowCtl ctl{sc.slow2, sc.count + 1, f->adm_slot, f->state, f->pub, nullptr, nullptr};
         rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl, slow_blocks, s);
         if (rc) return rc;
         if (d_bitmap) {
@@ -1364,7 +1401,7 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
     }
     // no admitted set: every message takes the full recovery (it ends in
     // NOT_ADMITTED at best), nothing to learn
-    const SlowCtl none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    const SlowCtl none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     return hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, none, blocks, s);
 }
 

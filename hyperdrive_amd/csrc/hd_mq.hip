@@ -456,6 +456,92 @@ __global__ void k_mq_commit(uint32_t nsend, const uint32_t* __restrict__ newhead
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nsend; s += gridDim.x * blockDim.x) head[s] = newhead[s];
 }
 
+// A consume in one launch, for queues of at most 1024 senders (the usual
+// case: one queue per validator): procsAllowed flags in LDS (the dict looked
+// up for each allowed signatory), the plan (k_mq_plan's cut per sender and the
+// scan of the delivered counts), the delivered rows packed into the stage as
+// 160-byte records in delivery order (so the host downloads only a prefix),
+// and the heads committed when the delivery fits `cap`.  The stage starts
+// with a 64-byte header: {delivered, removed}.
+#define HD_MQ_ROW 160
+#define HD_MQ_HDR 64
+__device__ __forceinline__ void mq_row_put(uint8_t* __restrict__ row, const Pool& p, uint32_t e) {
+    uint64_t* w = reinterpret_cast<uint64_t*>(row);
+    w[0] = (uint64_t)p.h[e];
+    w[1] = (uint64_t)p.r[e];
+    w[2] = (uint64_t)p.vr[e];
+    const uint32_t* val = reinterpret_cast<const uint32_t*>(p.value + 32 * (size_t)e);
+    const uint32_t* frm = reinterpret_cast<const uint32_t*>(p.from + 32 * (size_t)e);
+    uint32_t* o = reinterpret_cast<uint32_t*>(row + 24);
+    for (int j = 0; j < 8; j++) o[j] = val[j];
+    for (int j = 0; j < 8; j++) o[8 + j] = frm[j];
+    for (int j = 0; j < 65; j++) row[88 + j] = p.sig[65 * (size_t)e + j];
+    row[153] = p.type[e];
+    *reinterpret_cast<int32_t*>(row + 156) = p.sender[e];
+}
+__global__ __launch_bounds__(1024) void k_mq_consume1(uint32_t nsend, Pool p, uint32_t* __restrict__ head,
+                                                      const uint32_t* __restrict__ send, int64_t h, uint32_t na,
+                                                      const uint32_t* __restrict__ list, int be_words, Dict d,
+                                                      uint32_t rows, uint32_t cap, uint8_t* __restrict__ stage) {
+    typedef hipcub::BlockScan<uint32_t, 1024> Scan;
+    typedef hipcub::BlockReduce<uint32_t, 1024> Red;
+    __shared__ typename Scan::TempStorage ts;
+    __shared__ typename Red::TempStorage rs;
+    __shared__ uint8_t allow[1024];
+    __shared__ uint32_t off[1024], lo_of[1024];
+    __shared__ uint32_t tot_d;
+    const uint32_t t = threadIdx.x;
+    allow[t] = 0;
+    __syncthreads();
+    for (uint32_t k = t; k < na; k += 1024) {
+        uint32_t w[8];
+        for (int j = 0; j < 8; j++) {
+            const uint32_t x = list[8 * (size_t)k + j];
+            w[j] = be_words ? __builtin_bswap32(x) : x;
+        }
+        const uint32_t id = dict_find(d, make_uint4(w[0], w[1], w[2], w[3]), make_uint4(w[4], w[5], w[6], w[7]));
+        if (id != kEmpty) allow[id] = 1;
+    }
+    __syncthreads();
+    uint32_t rem = 0, del = 0, cut = 0, h0 = 0;
+    if (t < nsend) {
+        uint32_t lo = head[t], hi = send[t];
+        h0 = lo;
+        while (lo < hi) {   // first index with the height past the cut
+            const uint32_t mid = lo + (hi - lo) / 2;
+            if (p.h[mid] <= h) lo = mid + 1;
+            else hi = mid;
+        }
+        cut = lo;
+        rem = lo - h0;
+        del = allow[t] ? rem : 0u;
+    }
+    uint32_t o = 0, agg = 0;
+    Scan(ts).ExclusiveSum(del, o, agg);
+    const uint32_t rsum = Red(rs).Sum(rem);
+    off[t] = t < nsend ? o : agg;       // entries past nsend sort after every row
+    lo_of[t] = h0;
+    if (t == 0) {
+        tot_d = agg;
+        reinterpret_cast<uint32_t*>(stage)[0] = agg;
+        reinterpret_cast<uint32_t*>(stage)[1] = rsum;
+    }
+    __syncthreads();
+    const uint32_t total = tot_d, nw = total < rows ? total : rows;
+    uint8_t* out = stage + HD_MQ_HDR;
+    for (uint32_t k = t; k < nw; k += 1024) {
+        // the sender of delivered row k: the last s with off[s] <= k whose run is non-empty
+        uint32_t a = 0, b = nsend;      // off is non-decreasing over [0, nsend)
+        while (b - a > 1) {
+            const uint32_t m = (a + b) / 2;
+            if (off[m] <= k) a = m;
+            else b = m;
+        }
+        mq_row_put(out + (size_t)HD_MQ_ROW * k, p, lo_of[a] + (k - off[a]));
+    }
+    if (total <= cap && t < nsend) head[t] = cut;
+}
+
 // live pool entries (not in a consumed / dropped prefix)
 __global__ void k_mq_live(uint32_t M, const int32_t* __restrict__ snd, const uint32_t* __restrict__ head,
                           uint8_t* __restrict__ keep) {
@@ -496,6 +582,7 @@ struct hd_mq {
     // pinned host stage of consume (the packed outputs + the plan totals)
     void* hstage = nullptr;
     size_t hstage_cap = 0;
+    uint32_t last_deliv = 0;    // the previous consume's delivery: sizes the next one's first download
 };
 
 #define QCHK(expr, what)                                           \
@@ -890,6 +977,65 @@ static int mq_commit(hd_mq* q, uint32_t removed, hipStream_t s) {
     return HD_OK;
 }
 
+// Consume of a queue with at most 1024 senders and a capacity of at most
+// HD_MQ_FUSED_ROWS: one kernel (k_mq_consume1), then a download of the
+// header and of as many 160-byte rows as the previous consume delivered
+// (twice that, at least 64), and a second copy only when this delivery is
+// larger.  The rows are unpacked into the caller's SoA arrays on the host.
+#define HD_MQ_FUSED_ROWS 65536u   // larger deliveries take the multi-block path
+static int mq_consume1(hd_mq* q, int64_t h, const uint32_t* list, uint32_t na, int be, const hd_batch_out* out,
+                       int32_t* out_sender, uint32_t cap, uint32_t* n_out, uint32_t* n_removed) {
+    hipStream_t s = q->ctx->stream;
+    int rc = 0;
+    const uint32_t rows = std::max(cap, 1u);
+    const size_t bytes = HD_MQ_HDR + (size_t)HD_MQ_ROW * rows;
+    uint8_t* dst = (uint8_t*)qbuf(q, MQ_STAGE, bytes, &rc);
+    if (rc) return rc;
+    if (q->hstage_cap < bytes) {
+        if (q->hstage) (void)hipHostFree(q->hstage);
+        q->hstage = nullptr;
+        q->hstage_cap = 0;
+        const size_t want = std::max(bytes, (size_t)1 << 16);
+        QCHK(hipHostMalloc(&q->hstage, want, hipHostMallocDefault), "mq host stage");
+        q->hstage_cap = want;
+    }
+    k_mq_consume1<<<1, 1024, 0, s>>>(q->nsend, q->pool, (uint32_t*)q->buf[MQ_HEADS].p,
+                                     (const uint32_t*)q->buf[MQ_SEND].p, h, na, list, be, dict_of(q), rows, cap, dst);
+    QCHK(hipGetLastError(), "k_mq_consume1");
+    const uint32_t guess = std::min(rows, std::max(64u, 2 * q->last_deliv));
+    uint8_t* hs = (uint8_t*)q->hstage;
+    QCHK(hipMemcpyAsync(hs, dst, HD_MQ_HDR + (size_t)HD_MQ_ROW * guess, hipMemcpyDeviceToHost, s), "consume download");
+    QCHK(hipStreamSynchronize(s), "consume sync");
+    const uint32_t c = ((const uint32_t*)hs)[0], nr = ((const uint32_t*)hs)[1];
+    *n_out = c;
+    if (c > cap) return HD_ECAP;   // nothing committed
+    if (c > guess) {
+        const size_t o = HD_MQ_HDR + (size_t)HD_MQ_ROW * guess;
+        QCHK(hipMemcpyAsync(hs + o, dst + o, (size_t)HD_MQ_ROW * (c - guess), hipMemcpyDeviceToHost, s),
+             "consume download rest");
+        QCHK(hipStreamSynchronize(s), "consume sync");
+    }
+    q->last_deliv = c;
+    if (n_removed) *n_removed = nr;
+    if (nr) {
+        q->live -= nr;
+        q->dead = true;
+    }
+    const uint8_t* row = hs + HD_MQ_HDR;
+    for (uint32_t k = 0; k < c; k++, row += HD_MQ_ROW) {
+        out->type[k] = row[153];
+        memcpy(out->height + k, row, 8);
+        memcpy(out->round + k, row + 8, 8);
+        if (out->valid_round) memcpy(out->valid_round + k, row + 16, 8);
+        memcpy(out->value32 + 32 * (size_t)k, row + 24, 32);
+        memcpy(out->from32 + 32 * (size_t)k, row + 56, 32);
+        if (out->sig65) memcpy(out->sig65 + 65 * (size_t)k, row + 88, 65);
+        if (out_sender) memcpy(out_sender + k, row + 156, 4);
+    }
+    if (out->adv_class && c) memset(out->adv_class, 0, c);
+    return HD_OK;
+}
+
 // Consume in one host round trip: allow flags -> plan -> the delivered rows
 // gathered into a stage of `cap` rows (the caller's capacity) -> heads
 // committed on the device if they fit -> ONE download of the plan totals and
@@ -908,10 +1054,7 @@ int hd_mq_consume(hd_mq* q, int64_t h, const uint8_t* allowed32, uint32_t n_allo
     (void)hipSetDevice(q->ctx->device);
     hipStream_t s = q->ctx->stream;
     int rc = 0;
-    // procsAllowed as one flag per sender queue
-    uint8_t* allow = (uint8_t*)qbuf(q, MQ_ALLOW, q->nsend, &rc);
-    if (rc) return rc;
-    QCHK(hipMemsetAsync(allow, 0, q->nsend, s), "clear allow");
+    // procsAllowed: the allowed list (uploaded) or the ctx's admitted set
     const uint32_t* list = nullptr;
     uint32_t na = 0;
     int be = 0;
@@ -928,8 +1071,13 @@ int hd_mq_consume(hd_mq* q, int64_t h, const uint8_t* allowed32, uint32_t n_allo
         list = q->ctx->d_adm;
         be = 1;
     }
-    if (na) k_mq_allow<<<nblk(na), 256, 0, s>>>(na, list, be, dict_of(q), allow);
     const uint32_t ns = q->nsend;
+    if (ns <= 1024 && cap <= HD_MQ_FUSED_ROWS) return mq_consume1(q, h, list, na, be, out, out_sender, cap, n_out,
+                                                                   n_removed);
+    uint8_t* allow = (uint8_t*)qbuf(q, MQ_ALLOW, q->nsend, &rc);
+    if (rc) return rc;
+    QCHK(hipMemsetAsync(allow, 0, q->nsend, s), "clear allow");
+    if (na) k_mq_allow<<<nblk(na), 256, 0, s>>>(na, list, be, dict_of(q), allow);
     uint32_t* newhead = (uint32_t*)qbuf(q, MQ_NEWHEAD, 4 * (size_t)ns, &rc);
     uint32_t* off = (uint32_t*)qbuf(q, MQ_OFF, 4 * (size_t)ns, &rc);
     uint32_t* tot = (uint32_t*)qbuf(q, MQ_TOT, 64, &rc);

@@ -62,6 +62,7 @@ __global__ __launch_bounds__(256, WAVES) void k_verify(DevBatch b, const ge* __r
                                                 SlowCtl ctl, const gp* __restrict__ fbg) {
     const uint32_t stride = gridDim.x * blockDim.x;
     const uint32_t total = ctl.list ? *ctl.count : b.n;
+    if (ctl.est_out && blockIdx.x == 0 && threadIdx.x == 0) ctl.est_out[0] = total;
     for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += stride) {
         const uint32_t p = base + threadIdx.x;
         const bool active = p < total;
@@ -161,7 +162,7 @@ int hd_ctx_create(int device, hd_ctx** out) {
         {HD_VAR_VERIFY_WAVES, "HD_VERIFY_WAVES"}, {HD_VAR_SUM_WAVES, "HD_SUM_WAVES"},
         {HD_VAR_SUM_PREFETCH, "HD_SUM_PF"},       {HD_VAR_SPLIT_K, "HD_FAST_K"},
         {HD_VAR_FAST_WAVES, "HD_FAST_WAVES"},     {HD_VAR_KEY_WIDTH, "HD_FB_PW"},
-        {HD_VAR_WAVE_PRIO, "HD_WAVE_PRIO"},
+        {HD_VAR_WAVE_PRIO, "HD_WAVE_PRIO"},       {HD_VAR_SUM_CAP, "HD_SUM_CAP"},
     };
     for (auto& ev : envs)
         if (const char* e = getenv(ev.env)) (void)hd_ctx_set_variant(ctx, ev.key, atoi(e));
@@ -221,6 +222,7 @@ int hd_ctx_set_variant(hd_ctx* ctx, int which, int value) {
         case HD_VAR_SPLIT_K: ok = value == -1 || value == 0 || value == 4 || value == 8 || value == 16; break;
         case HD_VAR_KEY_WIDTH: ok = value == 0 || value == HD_FB_W || value == HD_FB_WW; break;
         case HD_VAR_WAVE_PRIO: ok = value >= 0 && value <= 3; break;
+        case HD_VAR_SUM_CAP: ok = value == 0 || value == 2; break;
     }
     if (!ok) return HD_EINVAL;
     ctx->var[which] = value;
@@ -335,7 +337,7 @@ int launch_verify(hd_ctx* ctx, const hd_batch* db, const uint8_t* d_digest, uint
     // than a resident-sized grid looping over the batch (measured on 1M:
     // 13.2 ms vs 13.5 ms at 2x resident blocks, 14.3 ms at 1x)
     const uint32_t blocks = (db->n + 255) / 256;
-    const SlowCtl none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    const SlowCtl none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     const int rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_recovered32, d_signer, d_valid_bitmap, none, blocks, s);
     if (rc) return rc;
     hipError_t e = ctx->ev_slow ? hipSuccess : hipEventCreateWithFlags(&ctx->ev_slow, hipEventDisableTiming);

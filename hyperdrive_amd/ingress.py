@@ -122,10 +122,16 @@ class Ingress:
         if getattr(self, "_streams", None) is None or self._streams[0].device != dev:
             s0 = work_stream(dev)
             self._streams = [s0, torch.cuda.Stream(device=dev, priority=s0.priority)]
+        # every stream waits for the caller's work queued so far (the wire
+        # buffers), not for each other: with the caller's stream being one of
+        # the two, waiting on "the current stream" inside the loop would chain
+        # each buffer's verification behind the previous one's
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(dev))
         staged = []
         for k, (mtype, buf, n) in enumerate(parts):
             s = self._streams[k % 2]
-            s.wait_stream(torch.cuda.current_stream(dev))
+            s.wait_event(ready)
             size = record_size(mtype, with_sig)
             complete = min(n, buf.numel() // size) if size else 0
             if complete == 0:

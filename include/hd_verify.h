@@ -155,7 +155,11 @@ int hd_ctx_profile(hd_ctx* ctx, int enable);
                                    (prep, s / Z inversions, comparison, lift): above k_fast_sums' 0 they keep
                                    their SIMD share while the next call's sums waves share the SIMD
                                    [HD_WAVE_PRIO] */
-#define HD_VAR__COUNT 9
+#define HD_VAR_SUM_CAP 9        /* k_fast_sums residency: 0 as registers allow (3 waves per SIMD, default), 2 at
+                                   most 2 blocks per CU (2 waves per SIMD, by an LDS reservation), leaving a
+                                   slot per SIMD to the short kernels of a concurrent call and the tally
+                                   [HD_SUM_CAP] */
+#define HD_VAR__COUNT 10
 int hd_ctx_set_variant(hd_ctx* ctx, int which, int value);
 int hd_ctx_get_variant(hd_ctx* ctx, int which, int* value);
 int hd_ctx_profile_read(hd_ctx* ctx, uint32_t* calls, double* verify_ms, uint32_t* sums_launches, double* sums_ms);

@@ -1,8 +1,10 @@
-"""A/B of the short kernels' wave priority (HD_VAR_WAVE_PRIO) x verify streams,
-interleaved in one process, through bench.py's Pipeline (verify + tally):
-C2 (1M, 100 signatories), C5 (30 % adversarial) and C3 (1000 signatories,
-128,064 messages).  Prints one JSON line per workload: ms/step per setting
-and round."""
+"""A/B of context variants x verify streams, interleaved in one process,
+through bench.py's Pipeline (verify + tally): C2 (1M, 100 signatories), C5
+(30 % adversarial) and C3 (1000 signatories, 128,064 messages).  Prints one
+JSON line per workload: ms/step per setting and round.
+
+AB_VARS="wave_prio=0,3;sum_cap=0,2" (Verifier.VARIANTS names; every
+combination), AB_STREAMS="1,2"."""
 import json
 import os
 import sys
@@ -14,8 +16,13 @@ import bench
 import hyperdrive_amd as hd
 from hyperdrive_amd.device import generate, work_stream
 
-PRIOS = [int(p) for p in os.environ.get("AB_PRIOS", "0,1,3").split(",")]
+import itertools
+
+VARS = [(kv.split("=")[0], [int(x) for x in kv.split("=")[1].split(",")])
+        for kv in os.environ.get("AB_VARS", "wave_prio=0,3").split(";") if kv]
+COMBOS = list(itertools.product(*[[(k, x) for x in vals] for k, vals in VARS]))
 STREAMS = [int(p) for p in os.environ.get("AB_STREAMS", "1,2").split(",")]
+TALLY = os.environ.get("AB_TALLY", "on").split(",")      # on, off, nodup
 ROUNDS = int(os.environ.get("AB_ROUNDS", "3"))
 STEPS = int(os.environ.get("AB_STEPS", "20"))
 which = sys.argv[1:] or ["C2", "C5", "C3"]
@@ -31,15 +38,24 @@ def ab(name, v, db, n):
     pipe = bench.Pipeline(v, db, n, 0, 0, 1, None, ws, ts)
     extra = [torch.cuda.Stream(device=dev, priority=ws.priority) for _ in range(max(STREAMS) - 1)]
     pipe.run(3)
-    res = {f"p{p}_s{s}": [] for p in PRIOS for s in STREAMS}
+    label = lambda combo, s, t: "_".join(f"{k}{x}" for k, x in combo) + f"_s{s}_t{t}"
+    res = {label(c, s, t): [] for c in COMBOS for s in STREAMS for t in TALLY}
+    dup = pipe.t_out.dup
     for _ in range(ROUNDS):
-        for p in PRIOS:
-            v.set_variant("wave_prio", p)
+        for combo in COMBOS:
+            for k, x in combo:
+                v.set_variant(k, x)
             for s in STREAMS:
-                pipe.wss = [ws] + extra[: s - 1]
-                pipe.run(2)
-                el = bench.timed(pipe, STEPS, None, dev)
-                res[f"p{p}_s{s}"].append(round(el / STEPS * 1e3, 4))
+                for t in TALLY:
+                    pipe.wss = [ws] + extra[: s - 1]
+                    pipe.do_tally = t != "off"
+                    pipe.t_out.dup = dup if t == "on" else None
+                    pipe.run(2)
+                    el = bench.timed(pipe, STEPS, None, dev)
+                    res[label(combo, s, t)].append(round(el / STEPS * 1e3, 4))
+    pipe.do_tally, pipe.t_out.dup = True, dup
+    for k, vals in VARS:
+        v.set_variant(k, vals[0])
     vd, _, _ = pipe.last(STEPS)
     hist = torch.bincount(vd.long(), minlength=8).cpu().tolist()
     best = {k: round(n / min(x) * 1e-3, 1) for k, x in res.items()}

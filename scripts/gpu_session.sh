@@ -26,6 +26,19 @@ for step in "$@"; do
     trace_c3) run trace_c3 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_c3 -o run -- python3 scripts/pipe_probe.py C3 6 ;;
     rehearse) run rehearse2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29561 bench.py --gpus 2 --dist-backend gloo --steps 4 --warmup 1 --no-cpu --no-aux --no-sub && run rehearse3_c4 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 3 --master-addr 127.0.0.1 --master-port 29562 bench.py --gpus 3 --dist-backend gloo --global-batch 3145728 --steps 3 --warmup 1 --no-cpu --no-aux --no-sub ;;
     trace2) run trace2 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace2 -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub ;;
+    mqtest) run pytest_mq 600 python -u -m pytest tests/test_mq.py tests/test_ingress.py tests/test_c1_network.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    golden) run pytest_golden 600 python -u -m pytest tests/test_golden.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    abprio) run ab_prio 900 python -u scripts/ab_prio.py ;;
+    absplit) AB_VARS="wave_prio=0,3;split_k=-1,8" AB_STREAMS=2 run ab_split 900 python -u scripts/ab_prio.py ;;
+    abtally) AB_VARS="sum_cap=0" AB_STREAMS=1,2 AB_TALLY=on,off,nodup AB_ROUNDS=4 run ab_tally 900 python -u scripts/ab_prio.py C2 C3 ;;
+    abcapk) AB_VARS="sum_cap=0,2;split_k=-1,4,8;wave_prio=3" AB_STREAMS=2 run ab_capk 900 python -u scripts/ab_prio.py ;;
+    abcap) AB_VARS="sum_cap=0,2;wave_prio=0,3" AB_STREAMS=1,2 run ab_cap 900 python -u scripts/ab_prio.py ;;
+    trace_cap) HD_SUM_CAP=2 HD_WAVE_PRIO=3 run trace_cap 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_cap -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub ;;
+    ingress) run ingress_probe 300 python -u scripts/ingress_probe.py ;;
+    ingress_trace) run ingress_trace 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ingress_trace -o run -- python3 scripts/ingress_probe.py ;;
+    pipe2) run pipe_c2 300 python scripts/pipe_probe.py C2 20 ;;
+    trace_prio) HD_WAVE_PRIO=3 run trace_prio 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_prio -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub ;;
+    pcie) run pcie 120 scripts/pcie_probe && HSA_ENABLE_SDMA=0 run pcie_nosdma 120 scripts/pcie_probe ;;
     fieldbench) run fieldbench 120 scripts/fieldbench 3 ;;
     gtest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     gputest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;

@@ -20,10 +20,10 @@ __global__ __launch_bounds__(256) void k_probe(uint32_t iters, uint32_t seed, ui
     uint64_t acc[CHAINS];
     uint32_t x[CHAINS], y[CHAINS];
     double f[CHAINS];
-    uint64_t cy[CHAINS];
+    uint64_t cy[CHAINS], z64[CHAINS];
 #pragma unroll
     for (int k = 0; k < CHAINS; k++) {
-        acc[k] = a + k; x[k] = a ^ (k * 0x9E3779B9u); y[k] = x[k] * 3u; cy[k] = 0; f[k] = (double)x[k];
+        acc[k] = a + k; z64[k] = a ^ k; x[k] = a ^ (k * 0x9E3779B9u); y[k] = x[k] * 3u; cy[k] = 0; f[k] = (double)x[k];
     }
     double fb = 1.0000001;
     uint64_t t0 = clock64(), w0 = wall_clock64();
@@ -64,6 +64,11 @@ __global__ __launch_bounds__(256) void k_probe(uint32_t iters, uint32_t seed, ui
                 if (OP == 25) asm volatile("s_nop 0\n\tv_add_u32 %0, %0, %1" : "+v"(x[k]) : "v"(b));
                 if (OP == 26) asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0\n\tv_mad_u64_u32 %0, %1, %2, %3, %0"
                                            : "+v"(acc[k]), "=s"(cy[k]) : "v"(x[k]), "v"(b));
+                if (OP == 27) asm volatile("v_lshl_add_u64 %0, %0, 3, %1" : "+v"(acc[k]) : "v"(z64[k]));
+                if (OP == 28) asm volatile("v_add_co_u32 %0, vcc, %0, %2\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"
+                                           : "+v"(x[k]), "+v"(y[k]) : "v"(b) : "vcc");
+                if (OP == 29) asm volatile("v_mad_u64_u32 %0, %1, %3, %4, %0\n\tv_lshl_add_u64 %2, %2, 3, %0"
+                                           : "+v"(acc[k]), "=s"(cy[k]), "+v"(z64[k]) : "v"(x[k]), "v"(b));
             }
         }
     }
@@ -71,7 +76,7 @@ __global__ __launch_bounds__(256) void k_probe(uint32_t iters, uint32_t seed, ui
     uint32_t r = 0;
 #pragma unroll
     for (int k = 0; k < CHAINS; k++)
-        r ^= (uint32_t)cy[k] ^ x[k] ^ y[k] ^ (uint32_t)acc[k] ^ (uint32_t)(acc[k] >> 32) ^ (uint32_t)f[k];
+        r ^= (uint32_t)cy[k] ^ (uint32_t)z64[k] ^ x[k] ^ y[k] ^ (uint32_t)acc[k] ^ (uint32_t)(acc[k] >> 32) ^ (uint32_t)f[k];
     if (r == 0x12345678u) out[0] = r;
     if (threadIdx.x == 0 && blockIdx.x == 0) { clk[0] = t1 - t0; clk[1] = w1 - w0; }
 }
@@ -82,9 +87,10 @@ static const char* NAMES[] = {"v_add_u32", "v_mad_u64_u32", "v_mul_lo_u32", "v_m
                               "v_lshl_add_u32", "v_mul_u32_u24", "mad_u64 + add_u32 (2 instr)", "v_dot2_u32_u16",
                               "v_cndmask_b32", "v_lshrrev_b32", "mad_u64 + add + and (3 instr)", "v_add_co_u32",
                               "v_lshlrev_b64", "v_mov_b32", "v_bfe_u32", "mad + s_nop 0 (1 VALU)",
-                              "s_nop 0 + v_add_u32 (1 VALU)", "mad -> dependent mad (2 instr)"};
-static const int NINSTR[] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1, 1, 2, 1, 1, 1, 3, 1, 1, 1, 1, 1, 1, 2};
-#define NOPS 27
+                              "s_nop 0 + v_add_u32 (1 VALU)", "mad -> dependent mad (2 instr)", "v_lshl_add_u64",
+                              "add_co + addc (2 instr)", "mad + lshl_add_u64 (2 instr)"};
+static const int NINSTR[] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1, 1, 2, 1, 1, 1, 3, 1, 1, 1, 1, 1, 1, 2, 1, 2, 2};
+#define NOPS 30
 
 template <int OP>
 static void run(int blocks, uint32_t iters, uint32_t* d, uint64_t* clk, int ncu) {

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -53,6 +54,52 @@ namespace {
         hipError_t e_ = (expr);                                   \
         if (e_ != hipSuccess) return hd_ctx_fail(ctx, e_, what);  \
     } while (0)
+
+// Outputs go to host memory by a kernel's stores over PCIe (the pinned
+// buffer mapped into the device's address space), not by DMA: the DMA
+// engine runs copies in the order they were queued, so a download queued
+// behind batch k's kernels would hold back batch k+1's upload queued after
+// it, and every batch's upload, kernels and download would run in series
+// (rocprofv3 memory-copy trace, round 3).  With the downloads on the compute
+// queue the engine carries only uploads, and batch k+1's upload runs under
+// batch k's kernels.  HD_HOST_D2H=dma restores the copies for A/B.
+struct HostOut {
+    uint8_t* dst[3];
+    const uint8_t* src[3];
+    size_t n[3];
+};
+__global__ __launch_bounds__(256) void k_host_store(HostOut o) {
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
+    for (int k = 0; k < 3; k++) {
+        if (!o.dst[k]) continue;
+        const size_t n = o.n[k];
+        // 16-byte words where both ends are 16-byte aligned, bytes otherwise
+        if ((((uintptr_t)o.dst[k] | (uintptr_t)o.src[k]) & 15) == 0) {
+            const size_t w = n / 16;
+            const uint4* s4 = reinterpret_cast<const uint4*>(o.src[k]);
+            uint4* d4 = reinterpret_cast<uint4*>(o.dst[k]);
+            for (size_t i = t; i < w; i += stride) d4[i] = s4[i];
+            for (size_t i = 16 * w + t; i < n; i += stride) o.dst[k][i] = o.src[k][i];
+        } else {
+            for (size_t i = t; i < n; i += stride) o.dst[k][i] = o.src[k][i];
+        }
+    }
+}
+
+// the device address of pinned host memory (NULL if it is not mapped)
+void* host_dev_ptr(void* p) {
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return d;
+}
+
+bool d2h_by_kernel() {
+    static const bool k = !(getenv("HD_HOST_D2H") && strcmp(getenv("HD_HOST_D2H"), "dma") == 0);
+    return k;
+}
 
 bool is_pinned(const void* p) {
     hipPointerAttribute_t a;
@@ -209,16 +256,30 @@ int hd_verify_submit(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8
     if (ostage && (rc = grow_pinned(ctx, &s.hout, &s.hout_cap, ostage))) return rc;
     off = 0;
     s.deliver.clear();
-    for (const Out& o : outs) {
+    HostOut ho{};
+    int nk = 0;
+    for (int k = 0; k < 3; k++) {
+        const Out& o = outs[k];
         if (!o.dst) continue;
-        if (is_pinned(o.dst)) {
-            HCHK(hipMemcpyAsync(o.dst, o.dev, o.sz, hipMemcpyDeviceToHost, s.stream), "submit download");
-        } else {
-            void* st = (char*)s.hout + off;
+        void* dst = o.dst;
+        if (!is_pinned(o.dst)) {   // into staging, delivered at completion
+            dst = (char*)s.hout + off;
             off += (o.sz + 255) & ~(size_t)255;
-            HCHK(hipMemcpyAsync(st, o.dev, o.sz, hipMemcpyDeviceToHost, s.stream), "submit download");
-            s.deliver.push_back({o.dst, st, o.sz});
+            s.deliver.push_back({o.dst, dst, o.sz});
         }
+        void* ddev = d2h_by_kernel() ? host_dev_ptr(dst) : nullptr;
+        if (ddev) {
+            ho.dst[k] = (uint8_t*)ddev;
+            ho.src[k] = (const uint8_t*)o.dev;
+            ho.n[k] = o.sz;
+            nk++;
+        } else {
+            HCHK(hipMemcpyAsync(dst, o.dev, o.sz, hipMemcpyDeviceToHost, s.stream), "submit download");
+        }
+    }
+    if (nk) {
+        k_host_store<<<std::max(ctx->n_cu, 1) * 2, 256, 0, s.stream>>>(ho);
+        HCHK(hipGetLastError(), "k_host_store");
     }
     HCHK(hipEventRecord(s.done, s.stream), "submit record");
     s.ticket = t;

@@ -29,7 +29,7 @@ which = sys.argv[1:] or ["C2", "C5", "C3"]
 
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(0)
-ws = work_stream(dev, priority=-1)
+ws = work_stream(dev, priority=int(os.environ.get("AB_VPRIO", "-1")))
 torch.cuda.set_stream(ws)
 ts = torch.cuda.Stream(device=dev, priority=0)
 

@@ -16,7 +16,7 @@ from hyperdrive_amd.ingress import Ingress
 
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(0)
-ws = work_stream(dev, priority=-1)
+ws = work_stream(dev, priority=int(os.environ.get("AB_VPRIO", "-1")))
 torch.cuda.set_stream(ws)
 v = hd.Verifier(0)
 sigs, foreign = v.gen_keys(100)

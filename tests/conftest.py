@@ -44,8 +44,13 @@ def build_coracle() -> str:
 
 def build_hostmath(bounds: bool = False) -> str:
     """bounds=True builds with -DHD_BOUNDS: every field element then carries
-    interval bounds that each operation checks (hd_field.h)."""
-    out = os.path.join(NATIVE_DIR, "_build", "libhdhost_bounds.so" if bounds else "libhdhost.so")
+    interval bounds that each operation checks (hd_field.h).  With
+    HD_HOST_SANITIZE=1 in the environment the build adds UBSan
+    (-fsanitize=undefined, any finding aborts), so the host-math suite runs
+    the device headers under the sanitizer."""
+    san = os.environ.get("HD_HOST_SANITIZE") == "1"
+    name = ("libhdhost_bounds" if bounds else "libhdhost") + ("_ubsan" if san else "") + ".so"
+    out = os.path.join(NATIVE_DIR, "_build", name)
     csrc = os.path.join(ROOT, "hyperdrive_amd", "csrc")
     srcs = [os.path.join(NATIVE_DIR, "hd_host_check.cpp")] + [os.path.join(csrc, f) for f in os.listdir(csrc)
                                                               if f.endswith(".h")]
@@ -55,6 +60,8 @@ def build_hostmath(bounds: bool = False) -> str:
         # product's 16-bit tables (17 x 32768) take ~10 s per key to build on
         # one host core; the algorithm is the same for every window width
         flags = (["-DHD_BOUNDS"] if bounds else []) + ["-DHD_FB_W=12", "-DHD_FB_WG=12"]
+        if san:
+            flags += ["-fsanitize=undefined", "-fno-sanitize-recover=all", "-g"]
         subprocess.run(["g++", "-O2", "-fPIC", "-shared", "-std=c++17", "-Wall", "-Wno-unused-function", *flags, "-o",
                         out, srcs[0]], check=True)
     return out

@@ -42,14 +42,16 @@ def marshal_device(v: Verifier, mtype: int, batch: DeviceBatch, with_sig: bool =
 
 
 def unmarshal_device(v: Verifier, mtype: int, buf, n: int, with_sig: bool = True,
-                     stream=None, sync: bool = True) -> Tuple[DeviceBatch, "object"]:
+                     stream=None, sync: bool = True, out: DeviceBatch = None) -> Tuple[DeviceBatch, "object"]:
     """Decode n `mtype` records from a device byte buffer into a DeviceBatch;
     status[i] = 1 marks a record the buffer ended before.  sync=False leaves
     the decode queued on `stream` (the caller orders what reads the batch
-    after it on that stream)."""
+    after it on that stream).  out: decode into this batch (n rows, e.g. a
+    view into a larger one; its sig rows must start 16-byte aligned)."""
     torch = _torch()
     dev = buf.device
-    out = DeviceBatch.empty(n, str(dev))
+    if out is None:
+        out = DeviceBatch.empty(n, str(dev))
     status = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
     co = out.c_out()
     lib = _lib.load()

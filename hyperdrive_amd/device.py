@@ -68,6 +68,12 @@ class DeviceBatch:
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
         return cls(len(b), t(b.type), t(b.height), t(b.round), t(vr), t(b.value), t(b.frm), t(b.sig))
 
+    def rows(self, lo: int, n: int) -> "DeviceBatch":
+        """Rows lo .. lo + n - 1 as views (no copy)."""
+        f = lambda t: t[lo: lo + n] if t is not None else None
+        return DeviceBatch(n, f(self.type), f(self.height), f(self.round), f(self.valid_round), f(self.value),
+                           f(self.frm), f(self.sig), f(self.adv_class))
+
     def c_struct(self) -> HdBatch:
         return HdBatch(self.n, self.type.data_ptr(), self.height.data_ptr(), self.round.data_ptr(),
                        self.valid_round.data_ptr(), self.value.data_ptr(), self.frm.data_ptr(), self.sig.data_ptr())

@@ -27,6 +27,7 @@ for step in "$@"; do
     rehearse) run rehearse2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29561 bench.py --gpus 2 --dist-backend gloo --steps 4 --warmup 1 --no-cpu --no-aux --no-sub && run rehearse3_c4 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 3 --master-addr 127.0.0.1 --master-port 29562 bench.py --gpus 3 --dist-backend gloo --global-batch 3145728 --steps 3 --warmup 1 --no-cpu --no-aux --no-sub ;;
     trace2) run trace2 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace2 -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub ;;
     mqtest) run pytest_mq 600 python -u -m pytest tests/test_mq.py tests/test_ingress.py tests/test_c1_network.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    burst) run pytest_burst 300 python -u -m pytest tests/test_gpu_verify.py -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread -k "burst or adversarial" ;;
     golden) run pytest_golden 600 python -u -m pytest tests/test_golden.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     abprio) run ab_prio 900 python -u scripts/ab_prio.py ;;
     absplit) AB_VARS="wave_prio=0,3;split_k=-1,8" AB_STREAMS=2 run ab_split 900 python -u scripts/ab_prio.py ;;
@@ -47,6 +48,7 @@ for step in "$@"; do
     gputest_all) run pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 600 python bench.py ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
+    prof1) HD_BENCH_VSTREAMS=1 run rocprof1 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof1 -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-aux --no-sub ;;
     pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 0 --no-cpu --no-aux --no-sub ;;
     pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 3 --warmup 0 --no-cpu --no-aux --no-sub ;;

@@ -152,6 +152,37 @@ def test_adversarial_full_mix_vs_c_oracle(gpu, oracle, coracle):
         v.close()
 
 
+def test_fallback_burst_after_clean_batches(gpu, coracle):
+    """The fallback kernels (k_slow_lift, k_verify over the leftover list) size
+    their grids by the latest list length seen (hd_fastverify.hip
+    fallback_blocks).  After honest batches (no leftovers: the smallest grid)
+    a 30 %-adversarial batch on the same context has ~10k leftovers that the
+    small grids walk grid-stride; every verdict and signatory must still
+    equal the C oracle, and the next adversarial batch too (grids sized by
+    the burst)."""
+    from hyperdrive_amd.device import generate
+    N, S = 65536, 100
+    v = gpu.Verifier(0)
+    try:
+        ks = v.gen_keys(S)
+        v.set_signatories(ks[0])
+        clean, _, _ = generate(v, 0, N, S, 0, keys=ks)
+        hc = clean.to_host()
+        for _ in range(3):                          # learn the keys, then two calls with no leftovers
+            v.verify_batch(hc)
+        assert v.fastpath_stats()[1] == 0
+        adv, _, _ = generate(v, 0, N, S, 30, keys=ks, start=N)
+        ha = adv.to_host()
+        cv, crec = coracle.verify(ha, ks[0], True, threads=16)
+        for rnd in range(2):
+            res = v.verify_batch(ha)
+            assert res.verdict.tolist() == cv.tolist(), rnd
+            assert res.recovered.tobytes() == crec.tobytes(), rnd
+        assert v.fastpath_stats()[1] > 1000
+    finally:
+        v.close()
+
+
 def test_c4_16m_sharded_emulation(verifier, coracle):
     """BASELINE configs[3] (16M messages, sharded over 8 GPUs) on one GPU: the
     8 rank shards (shard_range) verified one after another into their bitmap

@@ -153,6 +153,11 @@ SIGNATURES = {
     "hd_mq_consume": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_uint32,
                                      ctypes.POINTER(HdBatchOut), ctypes.c_void_p, ctypes.c_uint32,
                                      ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
+    "hd_mq_consume_votes": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                           ctypes.c_uint32, ctypes.POINTER(HdBatchOut), ctypes.c_void_p,
+                                           ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                                           ctypes.POINTER(ctypes.c_uint32), ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
     "hd_mq_drop_below": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     # include/hd_digest.h
     "hd_digest_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(HdBatch),

@@ -36,6 +36,7 @@
 #include <new>
 
 #include "../../include/hd_mq.h"
+#include "../../include/hd_votes.h"
 #include "hd_internal.h"
 
 using namespace hd;
@@ -1137,6 +1138,19 @@ int hd_mq_consume(hd_mq* q, int64_t h, const uint8_t* allowed32, uint32_t n_allo
         if (out->adv_class) memset(out->adv_class, 0, c);
     }
     return HD_OK;
+}
+
+int hd_mq_consume_votes(hd_mq* q, struct hd_votes* v, int64_t h, const uint8_t* allowed32, uint32_t n_allowed,
+                        const hd_batch_out* out, int32_t* out_sender, uint32_t cap, uint32_t* n_out,
+                        uint32_t* n_removed, uint8_t* status, uint32_t* double_of, uint8_t* events,
+                        uint32_t* n_inserted) {
+    if (!v || !n_out) return HD_EINVAL;
+    if (n_inserted) *n_inserted = 0;
+    int rc = hd_mq_consume(q, h, allowed32, n_allowed, out, out_sender, cap, n_out, n_removed);
+    if (rc || *n_out == 0) return rc;
+    const hd_batch b{*n_out, out->type, out->height, out->round, out->valid_round, out->value32, out->from32,
+                     out->sig65};
+    return hd_votes_insert_batch(v, &b, nullptr, status, double_of, events, n_inserted);
 }
 
 int hd_mq_drop_below(hd_mq* q, int64_t h) {

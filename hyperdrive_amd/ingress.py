@@ -151,10 +151,9 @@ class Ingress:
     def flush(self) -> FlushResult:
         """mq.Consume(CurrentHeight, ..., procsAllowed) with procsAllowed = the
         verifier's admitted set now, then the vote-log inserts."""
-        b, senders = self.mq.consume(self.height, allowed=None)
+        b, senders, status, double_of, events = self.mq.consume_votes(self.height, self.votes)
+        self.votes.last_events = events
         self._clean = (self.height, self.mq.inserts)
-        status, double_of = self.votes.insert_batch(b)
-        events = np.asarray(self.votes.last_events, np.uint8) if len(b) else np.zeros(0, np.uint8)
         return FlushResult(b, senders, status, double_of, np.flatnonzero(b.type == PROPOSE), self.mq.last_removed,
                            events)
 

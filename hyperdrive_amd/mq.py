@@ -145,5 +145,36 @@ class MessageQueue:
                   a["value"][:k].copy(), a["frm"][:k].copy(), a["sig"][:k].copy())
         return b, snd[:k].copy()
 
+    def consume_votes(self, height: int, votes) -> Tuple[Batch, np.ndarray, np.ndarray, np.ndarray, np.ndarray]:
+        """consume(height) with procsAllowed = the verifier's admitted set,
+        and the delivered messages inserted into the vote logs `votes`
+        (votes.VoteLog) in the same foreign call (include/hd_mq.h
+        hd_mq_consume_votes).  Returns (batch, senders, status, double_of,
+        events), each per delivered message."""
+        got, removed, ins = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        a, snd, out = self._out_arrays(1024)
+        while True:
+            st, dbl, ev = self._vote_arrays()
+            rc = self._lib.hd_mq_consume_votes(self._q, votes._v, int(height), None, 0, ctypes.byref(out),
+                                               snd.ctypes.data, self._cap, ctypes.byref(got), ctypes.byref(removed),
+                                               st.ctypes.data, dbl.ctypes.data, ev.ctypes.data, ctypes.byref(ins))
+            if rc != _lib.HD_ECAP:
+                break
+            a, snd, out = self._out_arrays(int(got.value))
+        self._check(rc, "hd_mq_consume_votes")
+        k = int(got.value)
+        self.last_removed = int(removed.value)
+        b = Batch(a["type"][:k].copy(), a["height"][:k].copy(), a["round"][:k].copy(), a["valid_round"][:k].copy(),
+                  a["value"][:k].copy(), a["frm"][:k].copy(), a["sig"][:k].copy())
+        return b, snd[:k].copy(), st[:k].copy(), dbl[:k].copy(), ev[:k].copy()
+
+    def _vote_arrays(self):
+        if getattr(self, "_vcap", 0) < self._cap:
+            self._vst = np.empty(self._cap, np.uint8)
+            self._vdbl = np.empty(self._cap, np.uint32)
+            self._vev = np.empty(self._cap, np.uint8)
+            self._vcap = self._cap
+        return self._vst, self._vdbl, self._vev
+
     def drop_below(self, height: int) -> None:
         self._check(self._lib.hd_mq_drop_below(self._q, int(height)), "hd_mq_drop_below")

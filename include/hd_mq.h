@@ -71,6 +71,19 @@ int hd_mq_senders(hd_mq* q, uint32_t* n);
 int hd_mq_consume(hd_mq* q, int64_t h, const uint8_t* allowed32, uint32_t n_allowed, const hd_batch_out* out,
                   int32_t* out_sender, uint32_t cap, uint32_t* n_out, uint32_t* n_removed);
 
+/* The replica's flush (replica.go:251-264: Consume the current height into
+ * the Process) in one call: hd_mq_consume into *out, then
+ * hd_votes_insert_batch of the delivered messages into the vote logs v
+ * (status / double_of / events per delivered message, as
+ * hd_votes_insert_batch; proposes get HD_VOTE_NOT_VOTE and are left to the
+ * caller).  One host round trip and one foreign call per flush.  HD_ECAP as
+ * hd_mq_consume (nothing removed or inserted). */
+struct hd_votes;
+int hd_mq_consume_votes(hd_mq* q, struct hd_votes* v, int64_t h, const uint8_t* allowed32, uint32_t n_allowed,
+                        const hd_batch_out* out, int32_t* out_sender, uint32_t cap, uint32_t* n_out,
+                        uint32_t* n_removed, uint8_t* status, uint32_t* double_of, uint8_t* events,
+                        uint32_t* n_inserted);
+
 /* DropMessagesBelowHeight (mq.go:70-83): remove every message with height < h */
 int hd_mq_drop_below(hd_mq* q, int64_t h);
 

@@ -621,6 +621,106 @@ __global__ __launch_bounds__(256) void k_fast_zinv(uint32_t n, uint32_t T, Split
     });
 }
 
+// Lean forms of the two inversion kernels (HD_VAR_LEAN_INV): the same
+// products, one inversion per lane, the same results, but the lane's prefix
+// products go to the pre row of each message (which later receives that
+// message's inverse) and the inputs are loaded again on the walk back,
+// instead of K inputs and K prefixes held in registers.  ~110 VGPRs instead
+// of 368 / 397: with k_fast_sums resident on a SIMD (160 VGPRs per wave)
+// the register-held forms cannot start until the SIMD has no sums wave left;
+// the lean forms fit beside two.  The walk is linear (the zinv product tree
+// needs its nodes in registers), K - 1 products deep.
+template <int K>
+__global__ __launch_bounds__(256) void k_fast_sinv_lean(uint32_t n, uint32_t T, SplitRows rows) {
+    wave_prio(rows.prio);
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    uint32_t live = 0;
+    sm acc;
+    HD_NOUNROLL for (int j = 0; j < K; j++) {
+        const uint32_t i = (uint32_t)j * T + t;
+        if (i >= n) break;
+        if ((rows.aux[i] & 0xFFu) != HD_FAST_LIVE) continue;
+        sc sv;
+        soa_load(sv.v, rows.s, n, i);
+        sm ss;
+        sm_from_sc(ss, sv);
+        if (live) sm_mul(acc, acc, ss);
+        else acc = ss;
+        live |= 1u << j;
+        soa_store(rows.pre, n, i, acc.n);   // the product of the live messages up to j
+    }
+    if (!live) return;
+    sm inv;
+    {
+        sc p, pinv;
+        sm_to_sc(p, acc);
+        sc_inv_divsteps(pinv, p);
+        sm_from_sc(inv, pinv);
+        sm r2;
+        sm_r2(r2);
+        sm_mul(inv, inv, r2);
+    }
+    HD_NOUNROLL for (int j = K - 1; j >= 0; j--) {
+        if (!((live >> j) & 1u)) continue;
+        const uint32_t i = (uint32_t)j * T + t;
+        const uint32_t below = live & ((1u << j) - 1u);
+        if (below) {
+            const uint32_t jp = 31u - (uint32_t)__builtin_clz(below);   // the previous live message
+            sm prev, sinv, ss;
+            soa_load(prev.n, rows.pre, n, jp * T + t);
+            sm_mul(sinv, inv, prev);
+            sc sv;
+            soa_load(sv.v, rows.s, n, i);
+            sm_from_sc(ss, sv);
+            sm_mul(inv, inv, ss);
+            soa_store(rows.pre, n, i, sinv.n);
+        } else {
+            soa_store(rows.pre, n, i, inv.n);
+        }
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_fast_zinv_lean(uint32_t n, uint32_t T, SplitRows rows) {
+    wave_prio(rows.prio);
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const uint32_t* zrow = rows.xyz + 18 * (size_t)n;
+    uint32_t live = 0;
+    fe acc;
+    HD_NOUNROLL for (int j = 0; j < K; j++) {
+        const uint32_t i = (uint32_t)j * T + t;
+        if (i >= n) break;
+        if ((rows.aux[i] & 0xFFu) != HD_FAST_LIVE) continue;
+        fe z;
+        soa_load(z.n, zrow, n, i);
+        if (live) fe_mul(acc, acc, z);
+        else acc = z;
+        live |= 1u << j;
+        soa_store(rows.pre, n, i, acc.n);
+    }
+    if (!live) return;
+    fe inv;
+    fe_inv_divsteps(inv, acc);   // a product of non-zero Z: never 0
+    HD_NOUNROLL for (int j = K - 1; j >= 0; j--) {
+        if (!((live >> j) & 1u)) continue;
+        const uint32_t i = (uint32_t)j * T + t;
+        const uint32_t below = live & ((1u << j) - 1u);
+        if (below) {
+            const uint32_t jp = 31u - (uint32_t)__builtin_clz(below);
+            fe prev, zi, z;
+            soa_load(prev.n, rows.pre, n, jp * T + t);
+            fe_mul(zi, inv, prev);
+            soa_load(z.n, zrow, n, i);
+            fe_mul(inv, inv, z);
+            soa_store(rows.pre, n, i, zi.n);
+        } else {
+            soa_store(rows.pre, n, i, inv.n);
+        }
+    }
+}
+
 // x = r (+ n when v & 2) as a field element: the x coordinate of R (the range
 // checks of sig_prefix passed in k_fast_prep)
 HD void fast_rx(fe& x, const sc& r, uint32_t v) {
@@ -1260,7 +1360,9 @@ static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest
     const size_t adm_lds = adm_lds_bytes(ctx->n_adm);
     k_fast_prep<<<nb, 256, adm_lds, s>>>(b, d_digest, f->state, f->adm_slot, ctx->d_adm, ctx->n_adm, ctx->adm_steps,
                                          rows, adm_lds > 0);
-    k_fast_sinv<K><<<tb, 256, 0, s>>>(n, T, rows);
+    const bool lean = ctx->var[HD_VAR_LEAN_INV] != 0;
+    if (lean) k_fast_sinv_lean<K><<<tb, 256, 0, s>>>(n, T, rows);
+    else k_fast_sinv<K><<<tb, 256, 0, s>>>(n, T, rows);
     const bool dl = sums_digits_lds(ctx);
     if (!dl) k_fast_digits<WP><<<nb, 256, 0, s>>>(n, rows);
     hipEvent_t* pe = fb_prof_pair(f->ev_sums, f->n_sums, f->prof);
@@ -1268,7 +1370,8 @@ static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest
     if (dl) launch_sums<WP, true>(ctx, nb, s, n, f->gtab, f->tabs, rows);
     else launch_sums<WP, false>(ctx, nb, s, n, f->gtab, f->tabs, rows);
     if (pe) (void)hipEventRecord(pe[1], s);
-    k_fast_zinv<K><<<tb, 256, 0, s>>>(n, T, rows);
+    if (lean) k_fast_zinv_lean<K><<<tb, 256, 0, s>>>(n, T, rows);
+    else k_fast_zinv<K><<<tb, 256, 0, s>>>(n, T, rows);
     // whole blocks of 256: every wavefront's 64 messages are one bitmap word pair
     k_fast_cmp<<<nb, 256, 0, s>>>(b, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer, sc.slow, sc.count,
                                   d_bitmap);

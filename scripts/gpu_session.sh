@@ -37,6 +37,8 @@ for step in "$@"; do
     abvprio) AB_VARS="wave_prio=0" AB_STREAMS=1,2 AB_ROUNDS=2 run ab_vprio_hi 600 python -u scripts/ab_prio.py && AB_VPRIO=0 AB_VARS="wave_prio=0" AB_STREAMS=1,2 AB_ROUNDS=2 run ab_vprio_lo 600 python -u scripts/ab_prio.py && AB_VPRIO=0 run ingress_vprio_lo 300 python -u scripts/ingress_probe.py ;;
     tallytest) run pytest_tally 600 python -u -m pytest tests/test_gpu_tally.py tests/test_golden.py tests/test_multi_gpu.py tests/test_ingress.py tests/test_c1_network.py tests/test_mq.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     abtsize) AB_VARS="wave_prio=0" AB_STREAMS=1,2 AB_ROUNDS=3 run ab_tsize_new 600 python -u scripts/ab_prio.py C2 C3 && HD_TALLY_SAFE_TABLES=1 AB_VARS="wave_prio=0" AB_STREAMS=1,2 AB_ROUNDS=3 run ab_tsize_old 600 python -u scripts/ab_prio.py C2 C3 ;;
+    ablean) AB_VARS="lean_inv=0,1;sum_cap=0,2" AB_STREAMS=1,2 AB_ROUNDS=3 run ab_lean 900 python -u scripts/ab_prio.py ;;
+    trace_lean) HD_LEAN_INV=1 HD_SUM_CAP=2 run trace_lean 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_lean -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub ;;
     abcap) AB_VARS="sum_cap=0,2;wave_prio=0,3" AB_STREAMS=1,2 run ab_cap 900 python -u scripts/ab_prio.py ;;
     trace_cap) HD_SUM_CAP=2 HD_WAVE_PRIO=3 run trace_cap 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_cap -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub ;;
     ingress) run ingress_probe 300 python -u scripts/ingress_probe.py ;;

@@ -565,105 +565,6 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
     soa_store(rows.xyz + 18 * (size_t)n, n, i, acc.z.n);
 }
 
-// Two lanes per message (HD_VAR_SUM_PAIRS), for batches too small to fill
-// the SIMDs twice over, where k_fast_sums is one addition chain's latency:
-// the even lane sums the G windows (u1 G), the odd lane the key's windows
-// (u2 P), each from its own digits (one Montgomery product each in the
-// prologue); the odd lane's partial sum crosses to the even lane by
-// shuffles and one Jacobian addition (gej_add: exceptional cases handled)
-// joins them.  The chain is max(NG, NP) - 1 additions deep instead of
-// NG + NP - 1 (C3: 15 + 1 join instead of 26), for ~12-27 % more additions
-// in all.  The same point as k_fast_sums (the group law), so the same
-// verdicts; a degenerate partial sum (Z = 0) or join sends the message to
-// the full recovery, as there.
-template <int WP>
-__global__ __launch_bounds__(256, 3) void k_fast_sums_pair(uint32_t n, const gp* __restrict__ gtab,
-                                                          const gp* const* __restrict__ tabs, SplitRows rows) {
-    constexpr int NG = FbL<HD_FB_WG>::NWIN, NP = FbL<WP>::NWIN, NMAX = NG > NP ? NG : NP;
-    __shared__ uint32_t sdig[NMAX * 256];
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t i = t >> 1;
-    const bool odd = (t & 1u) != 0;
-    if (i >= n) return;   // both lanes of a pair
-    const uint32_t a = rows.aux[i];
-    if ((a & 0xFFu) != HD_FAST_LIVE) return;
-    const gp* __restrict__ tab = odd ? tabs[a >> 8] : gtab;
-    const int nw = odd ? NP : NG;
-    uint32_t* dp = sdig + threadIdx.x;   // this lane's column; no barrier
-    {
-        sm sinv, x;
-        soa_load(sinv.n, rows.pre, n, i);
-        sc u;
-        soa_load(u.v, odd ? rows.u2 : rows.u1, n, i);
-        sm_from_sc(x, u);
-        sm_mul(x, x, sinv);
-        sm_to_sc(u, x);
-        if (odd) {
-            HD_UNROLL for (int w = 0; w < NP; w++) dp[w * 256] = fb_ref<WP>(fb_digit<WP>(u, w), w);
-        } else {
-            HD_UNROLL for (int w = 0; w < NG; w++) dp[w * 256] = fb_ref<HD_FB_WG>(fb_digit<HD_FB_WG>(u, w), w);
-        }
-    }
-    uint32_t e = dp[0];
-    gej acc;
-    ge p0;
-    gp_unpack(p0, tab[e & HD_REF_IDX]);
-    if (e & HD_REF_NEG) fe_neg(p0.y, p0.y);
-    fe_norm_weak(p0.y);
-    gej_set_ge(acc, p0);
-    bool started = !(e & HD_REF_ZERO);
-    if (!started) gej_set_inf(acc);
-    uint32_t c1 = dp[256];
-    gp q1 = tab[c1 & HD_REF_IDX];
-    {
-        ge g;
-        gp_unpack(g, q1);
-        uint32_t ec = c1;
-        if (2 < nw) {   // the next window's point, one addition ahead
-            c1 = dp[2 * 256];
-            q1 = tab[c1 & HD_REF_IDX];
-        }
-        sum_first(acc, started, p0, g, ec);
-    }
-    HD_NOUNROLL for (int j = 2; j < NMAX; j++) {
-        if (j < nw) {
-            ge g;
-            gp_unpack(g, q1);
-            const uint32_t ec = c1;
-            if (j + 1 < nw) {
-                c1 = dp[(j + 1) * 256];
-                q1 = tab[c1 & HD_REF_IDX];
-            }
-            sum_step(acc, started, g, ec);
-        }
-    }
-    // the odd lane's partial sum to the even lane
-    gej o;
-    HD_UNROLL for (int k = 0; k < 9; k++) {
-        o.x.n[k] = (uint32_t)__shfl_xor((int)acc.x.n[k], 1);
-        o.y.n[k] = (uint32_t)__shfl_xor((int)acc.y.n[k], 1);
-        o.z.n[k] = (uint32_t)__shfl_xor((int)acc.z.n[k], 1);
-    }
-    const bool ostarted = __shfl_xor((int)started, 1) != 0;
-    if (odd) return;
-    bool bad = !started && !ostarted;
-    if ((started && gej_is_inf(acc)) || (ostarted && gej_is_inf(o))) bad = true;
-    gej sum;
-    if (!bad) {
-        if (!ostarted) sum = acc;
-        else if (!started) sum = o;
-        else gej_add(sum, acc, o);
-        bad = gej_is_inf(sum);
-    }
-    if (bad) {
-        rows.aux[i] = (a & ~0xFFu) | HD_NEEDS_SLOW;
-        return;
-    }
-    soa_store(rows.xyz, n, i, sum.x.n);
-    soa_store(rows.xyz + 9 * (size_t)n, n, i, sum.y.n);
-    soa_store(rows.xyz + 18 * (size_t)n, n, i, sum.z.n);
-}
-
 // Batch inversion over the K messages of a lane as a product tree (K a power
 // of two), node[i] = node[2i] node[2i+1] with the leaves at K .. 2K-1: K - 1
 // products up, one inversion of the root, 2 (K - 1) products down
@@ -718,106 +619,6 @@ __global__ __launch_bounds__(256) void k_fast_zinv(uint32_t n, uint32_t T, Split
         constexpr int j = decltype(jc)::value;
         if ((live >> j) & 1u) soa_store(rows.pre, n, (uint32_t)j * T + t, node[K + j].n);
     });
-}
-
-// Lean forms of the two inversion kernels (HD_VAR_LEAN_INV): the same
-// products, one inversion per lane, the same results, but the lane's prefix
-// products go to the pre row of each message (which later receives that
-// message's inverse) and the inputs are loaded again on the walk back,
-// instead of K inputs and K prefixes held in registers.  ~110 VGPRs instead
-// of 368 / 397: with k_fast_sums resident on a SIMD (160 VGPRs per wave)
-// the register-held forms cannot start until the SIMD has no sums wave left;
-// the lean forms fit beside two.  The walk is linear (the zinv product tree
-// needs its nodes in registers), K - 1 products deep.
-template <int K>
-__global__ __launch_bounds__(256) void k_fast_sinv_lean(uint32_t n, uint32_t T, SplitRows rows) {
-    wave_prio(rows.prio);
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= T) return;
-    uint32_t live = 0;
-    sm acc;
-    HD_NOUNROLL for (int j = 0; j < K; j++) {
-        const uint32_t i = (uint32_t)j * T + t;
-        if (i >= n) break;
-        if ((rows.aux[i] & 0xFFu) != HD_FAST_LIVE) continue;
-        sc sv;
-        soa_load(sv.v, rows.s, n, i);
-        sm ss;
-        sm_from_sc(ss, sv);
-        if (live) sm_mul(acc, acc, ss);
-        else acc = ss;
-        live |= 1u << j;
-        soa_store(rows.pre, n, i, acc.n);   // the product of the live messages up to j
-    }
-    if (!live) return;
-    sm inv;
-    {
-        sc p, pinv;
-        sm_to_sc(p, acc);
-        sc_inv_divsteps(pinv, p);
-        sm_from_sc(inv, pinv);
-        sm r2;
-        sm_r2(r2);
-        sm_mul(inv, inv, r2);
-    }
-    HD_NOUNROLL for (int j = K - 1; j >= 0; j--) {
-        if (!((live >> j) & 1u)) continue;
-        const uint32_t i = (uint32_t)j * T + t;
-        const uint32_t below = live & ((1u << j) - 1u);
-        if (below) {
-            const uint32_t jp = 31u - (uint32_t)__builtin_clz(below);   // the previous live message
-            sm prev, sinv, ss;
-            soa_load(prev.n, rows.pre, n, jp * T + t);
-            sm_mul(sinv, inv, prev);
-            sc sv;
-            soa_load(sv.v, rows.s, n, i);
-            sm_from_sc(ss, sv);
-            sm_mul(inv, inv, ss);
-            soa_store(rows.pre, n, i, sinv.n);
-        } else {
-            soa_store(rows.pre, n, i, inv.n);
-        }
-    }
-}
-
-template <int K>
-__global__ __launch_bounds__(256) void k_fast_zinv_lean(uint32_t n, uint32_t T, SplitRows rows) {
-    wave_prio(rows.prio);
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= T) return;
-    const uint32_t* zrow = rows.xyz + 18 * (size_t)n;
-    uint32_t live = 0;
-    fe acc;
-    HD_NOUNROLL for (int j = 0; j < K; j++) {
-        const uint32_t i = (uint32_t)j * T + t;
-        if (i >= n) break;
-        if ((rows.aux[i] & 0xFFu) != HD_FAST_LIVE) continue;
-        fe z;
-        soa_load(z.n, zrow, n, i);
-        if (live) fe_mul(acc, acc, z);
-        else acc = z;
-        live |= 1u << j;
-        soa_store(rows.pre, n, i, acc.n);
-    }
-    if (!live) return;
-    fe inv;
-    fe_inv_divsteps(inv, acc);   // a product of non-zero Z: never 0
-    HD_NOUNROLL for (int j = K - 1; j >= 0; j--) {
-        if (!((live >> j) & 1u)) continue;
-        const uint32_t i = (uint32_t)j * T + t;
-        const uint32_t below = live & ((1u << j) - 1u);
-        if (below) {
-            const uint32_t jp = 31u - (uint32_t)__builtin_clz(below);
-            fe prev, zi, z;
-            soa_load(prev.n, rows.pre, n, jp * T + t);
-            fe_mul(zi, inv, prev);
-            soa_load(z.n, zrow, n, i);
-            fe_mul(inv, inv, z);
-            soa_store(rows.pre, n, i, zi.n);
-        } else {
-            soa_store(rows.pre, n, i, inv.n);
-        }
-    }
 }
 
 // x = r (+ n when v & 2) as a field element: the x coordinate of R (the range
@@ -1446,13 +1247,6 @@ static void launch_sums(const hd_ctx* ctx, uint32_t blocks, hipStream_t s, uint3
     }
 }
 static bool sums_digits_lds(const hd_ctx* ctx) { return ctx->var[HD_VAR_SUM_DIGITS] == 0; }
-// two lanes per message (k_fast_sums_pair): HD_VAR_SUM_PAIRS 1, or (-1, the
-// default) when the batch fills fewer than two rounds of 3 waves per SIMD
-static bool sums_pairs(const hd_ctx* ctx, uint32_t n) {
-    const int v = ctx->var[HD_VAR_SUM_PAIRS];
-    if (v >= 0 || !sums_digits_lds(ctx)) return v > 0 && sums_digits_lds(ctx);
-    return (uint64_t)n < 2ull * 3 * 4 * 64 * (uint64_t)std::max(ctx->n_cu, 1);
-}
 
 template <int K, int WP>
 static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict,
@@ -1466,19 +1260,15 @@ static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest
     const size_t adm_lds = adm_lds_bytes(ctx->n_adm);
     k_fast_prep<<<nb, 256, adm_lds, s>>>(b, d_digest, f->state, f->adm_slot, ctx->d_adm, ctx->n_adm, ctx->adm_steps,
                                          rows, adm_lds > 0);
-    const bool lean = ctx->var[HD_VAR_LEAN_INV] != 0;
-    if (lean) k_fast_sinv_lean<K><<<tb, 256, 0, s>>>(n, T, rows);
-    else k_fast_sinv<K><<<tb, 256, 0, s>>>(n, T, rows);
+    k_fast_sinv<K><<<tb, 256, 0, s>>>(n, T, rows);
     const bool dl = sums_digits_lds(ctx);
     if (!dl) k_fast_digits<WP><<<nb, 256, 0, s>>>(n, rows);
     hipEvent_t* pe = fb_prof_pair(f->ev_sums, f->n_sums, f->prof);
     if (pe) (void)hipEventRecord(pe[0], s);
-    if (sums_pairs(ctx, n)) k_fast_sums_pair<WP><<<(2 * n + 255) / 256, 256, 0, s>>>(n, f->gtab, f->tabs, rows);
-    else if (dl) launch_sums<WP, true>(ctx, nb, s, n, f->gtab, f->tabs, rows);
+    if (dl) launch_sums<WP, true>(ctx, nb, s, n, f->gtab, f->tabs, rows);
     else launch_sums<WP, false>(ctx, nb, s, n, f->gtab, f->tabs, rows);
     if (pe) (void)hipEventRecord(pe[1], s);
-    if (lean) k_fast_zinv_lean<K><<<tb, 256, 0, s>>>(n, T, rows);
-    else k_fast_zinv<K><<<tb, 256, 0, s>>>(n, T, rows);
+    k_fast_zinv<K><<<tb, 256, 0, s>>>(n, T, rows);
     // whole blocks of 256: every wavefront's 64 messages are one bitmap word pair
     k_fast_cmp<<<nb, 256, 0, s>>>(b, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer, sc.slow, sc.count,
                                   d_bitmap);

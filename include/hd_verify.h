@@ -159,14 +159,7 @@ int hd_ctx_profile(hd_ctx* ctx, int enable);
                                    most 2 blocks per CU (2 waves per SIMD, by an LDS reservation), leaving a
                                    slot per SIMD to the short kernels of a concurrent call and the tally
                                    [HD_SUM_CAP] */
-#define HD_VAR_LEAN_INV 10      /* the known-key check's inversion kernels: 0 with the lane's inputs and prefixes
-                                   in registers (default), 1 the lean forms (prefixes in the rows, inputs
-                                   reloaded; ~110 VGPRs, so they fit beside a running k_fast_sums)
-                                   [HD_LEAN_INV] */
-#define HD_VAR_SUM_PAIRS 11     /* k_fast_sums with two lanes per message (u1 G and u2 P summed apart, then
-                                   joined): -1 when the batch fills fewer than two rounds of the SIMDs,
-                                   0 never (default), 1 always [HD_SUM_PAIRS] */
-#define HD_VAR__COUNT 12
+#define HD_VAR__COUNT 10
 int hd_ctx_set_variant(hd_ctx* ctx, int which, int value);
 int hd_ctx_get_variant(hd_ctx* ctx, int which, int* value);
 int hd_ctx_profile_read(hd_ctx* ctx, uint32_t* calls, double* verify_ms, uint32_t* sums_launches, double* sums_ms);

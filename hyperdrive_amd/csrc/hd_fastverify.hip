@@ -492,7 +492,7 @@ template <int WAVES, int WP, int PF, bool DL>
 __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* __restrict__ gtab,
                                                           const gp* const* __restrict__ tabs, SplitRows rows) {
     constexpr int NG = FbL<HD_FB_WG>::NWIN, NT = NG + FbL<WP>::NWIN;
-    static_assert(PF == 1 || PF == 2, "prefetch depth");
+    static_assert(PF >= 0 && PF <= 2, "prefetch depth");
     __shared__ uint32_t sdig[DL ? NT * 256 : 1];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -516,14 +516,21 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
     // digit of the window after those is read one addition earlier still, so
     // no load waits on another load inside an addition.
     uint32_t c1 = dp[dstride], c2 = 0, dn = 0;
-    gp q1 = gtab[c1 & HD_REF_IDX], q2;
+    gp q1, q2;
+    if (PF > 0) q1 = gtab[c1 & HD_REF_IDX];
     if (PF == 2) {
         c2 = dp[2 * dstride];
         q2 = (2 < NG ? gtab : ptab)[c2 & HD_REF_IDX];
     }
-    if (PF + 1 < NT) dn = dp[(size_t)(PF + 1) * dstride];
+    if (PF > 0 && PF + 1 < NT) dn = dp[(size_t)(PF + 1) * dstride];
     // window j's point and digit reference, advancing the prefetch queue
+    // (PF = 0: loaded when used; the other waves of the SIMD cover the wait)
     auto advance = [&](int j, gp& cur, uint32_t& ec) {
+        if (PF == 0) {
+            ec = j == 1 ? c1 : dp[(size_t)j * dstride];
+            cur = (j < NG ? gtab : ptab)[ec & HD_REF_IDX];
+            return;
+        }
         cur = q1;
         ec = c1;
         if (PF == 2) {
@@ -1235,14 +1242,20 @@ static size_t sums_cap_lds(int cap, size_t stat) {
 template <int WP, bool DL>
 static void launch_sums(const hd_ctx* ctx, uint32_t blocks, hipStream_t s, uint32_t n, const gp* gtab,
                         const gp* const* tab, const SplitRows& rows) {
-    const int w = ctx->var[HD_VAR_SUM_WAVES], pf = ctx->var[HD_VAR_SUM_PREFETCH];
+    // 0 (the default): 4 waves per SIMD for a batch that fills fewer than two
+    // rounds at 3 (C3's 128k messages: +5 %; measured 3 % slower per 1M, where
+    // 3 waves keep the loaded-ahead table points)
+    int w = ctx->var[HD_VAR_SUM_WAVES];
+    const int pf = ctx->var[HD_VAR_SUM_PREFETCH];
+    if (w == 0) w = (uint64_t)n < 2ull * 3 * 4 * 64 * (uint64_t)std::max(ctx->n_cu, 1) ? 4 : 3;
     constexpr size_t stat = DL ? 4 * 256 * (size_t)(FbL<HD_FB_WG>::NWIN + FbL<WP>::NWIN) : 4;
     const size_t dyn = sums_cap_lds(ctx->var[HD_VAR_SUM_CAP], stat);
     if (pf == 2) {
-        if (w == 3) k_fast_sums<3, WP, 2, DL><<<blocks, 256, dyn, s>>>(n, gtab, tab, rows);
-        else k_fast_sums<2, WP, 2, DL><<<blocks, 256, dyn, s>>>(n, gtab, tab, rows);
+        if (w == 2) k_fast_sums<2, WP, 2, DL><<<blocks, 256, dyn, s>>>(n, gtab, tab, rows);
+        else k_fast_sums<3, WP, 2, DL><<<blocks, 256, dyn, s>>>(n, gtab, tab, rows);   // (no 4-wave form)
     } else {
         if (w == 2) k_fast_sums<2, WP, 1, DL><<<blocks, 256, dyn, s>>>(n, gtab, tab, rows);
+        else if (w == 4) k_fast_sums<4, WP, 0, DL><<<blocks, 256, dyn, s>>>(n, gtab, tab, rows);
         else k_fast_sums<3, WP, 1, DL><<<blocks, 256, dyn, s>>>(n, gtab, tab, rows);
     }
 }

@@ -216,7 +216,8 @@ int hd_ctx_set_variant(hd_ctx* ctx, int which, int value) {
     bool ok = false;
     switch (which) {
         case HD_VAR_VERIFY_WAVES: ok = value >= 2 && value <= 4; break;
-        case HD_VAR_SUM_WAVES: case HD_VAR_FAST_WAVES: ok = value == 2 || value == 3; break;
+        case HD_VAR_SUM_WAVES: ok = value == 0 || (value >= 2 && value <= 4); break;
+        case HD_VAR_FAST_WAVES: ok = value == 2 || value == 3; break;
         case HD_VAR_SUM_PREFETCH: ok = value == 1 || value == 2; break;
         case HD_VAR_SUM_DIGITS: case HD_VAR_RECOVER_G: ok = value == 0 || value == 1; break;
         case HD_VAR_SPLIT_K: ok = value == -1 || value == 0 || value == 4 || value == 8 || value == 16; break;

@@ -140,7 +140,8 @@ int hd_ctx_profile(hd_ctx* ctx, int enable);
  * HD_EINVAL for an unknown key or value. */
 #define HD_VAR_VERIFY_WAVES 0   /* k_verify register budget, waves per SIMD: 2, 3 (default) or 4 (compressed
                                    pubkeys; the other formats run the 3-wave build) [HD_VERIFY_WAVES] */
-#define HD_VAR_SUM_WAVES 1      /* k_fast_sums: 2 or 3 (default) [HD_SUM_WAVES] */
+#define HD_VAR_SUM_WAVES 1      /* k_fast_sums waves per SIMD: 2, 3 or 4 (128 VGPRs, table points loaded when
+                                   used); 0 (default) 4 for batches under two rounds at 3, else 3 [HD_SUM_WAVES] */
 #define HD_VAR_SUM_PREFETCH 2   /* k_fast_sums table-point prefetch depth: 1 (default) or 2 [HD_SUM_PF] */
 #define HD_VAR_SUM_DIGITS 3     /* window digits: 0 in k_fast_sums' LDS (default), 1 a k_fast_digits pass
                                    [HD_SUM_DIGITS=rows] */

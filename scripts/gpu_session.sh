@@ -40,6 +40,8 @@ for step in "$@"; do
     ablean) AB_VARS="lean_inv=0,1;sum_cap=0,2" AB_STREAMS=1,2 AB_ROUNDS=3 run ab_lean 900 python -u scripts/ab_prio.py ;;
     trace_lean) HD_LEAN_INV=1 HD_SUM_CAP=2 run trace_lean 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_lean -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub ;;
     abpairs) AB_VARS="sum_pairs=0,1" AB_STREAMS=1,2 AB_ROUNDS=3 run ab_pairs 900 python -u scripts/ab_prio.py C3 C2 ;;
+    abw4) AB_VARS="sum_waves=3,4" AB_STREAMS=1,2 AB_ROUNDS=3 run ab_w4 900 python -u scripts/ab_prio.py ;;
+    benchw) run bench_w3a 300 python bench.py --no-cpu --no-aux && HD_SUM_WAVES=4 run bench_w4a 300 python bench.py --no-cpu --no-aux && run bench_w3b 300 python bench.py --no-cpu --no-aux && HD_SUM_WAVES=4 run bench_w4b 300 python bench.py --no-cpu --no-aux ;;
     abcap) AB_VARS="sum_cap=0,2;wave_prio=0,3" AB_STREAMS=1,2 run ab_cap 900 python -u scripts/ab_prio.py ;;
     trace_cap) HD_SUM_CAP=2 HD_WAVE_PRIO=3 run trace_cap 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_cap -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub ;;
     ingress) run ingress_probe 300 python -u scripts/ingress_probe.py ;;

@@ -144,7 +144,7 @@ def test_gpu_matches_golden(gpu, name):
 # Every kernel instantiation a context can select (include/hd_verify.h
 # HD_VAR_*), one at a time from the defaults; the first entry is the default.
 VARIANTS = [("default", None, None), ("verify_waves_2", "verify_waves", 2), ("verify_waves_4", "verify_waves", 4),
-            ("sum_waves_2", "sum_waves", 2),
+            ("sum_waves_2", "sum_waves", 2), ("sum_waves_3", "sum_waves", 3), ("sum_waves_4", "sum_waves", 4),
             ("sum_prefetch_2", "sum_prefetch", 2), ("sum_digits_rows", "sum_digits", 1), ("split_k_0", "split_k", 0),
             ("split_k_4", "split_k", 4), ("split_k_16", "split_k", 16), ("fast_waves_3", "split_k", 0),
             ("recover_glv_g", "recover_g", 1), ("key_width_16", "key_width", 16), ("key_width_20", "key_width", 20),

@@ -94,6 +94,8 @@ SIGNATURES = {
                                        ctypes.c_void_p, ctypes.c_void_p]),
     "hd_verify_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "hd_authenticate_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
+                                                    ctypes.c_void_p]),
     "hd_verify_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "hd_verify_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),

@@ -42,12 +42,17 @@ def marshal_device(v: Verifier, mtype: int, batch: DeviceBatch, with_sig: bool =
 
 
 def unmarshal_device(v: Verifier, mtype: int, buf, n: int, with_sig: bool = True,
-                     stream=None, sync: bool = True, out: DeviceBatch = None) -> Tuple[DeviceBatch, "object"]:
+                     stream=None, sync: bool = True, out: DeviceBatch = None,
+                     wait: bool = True) -> Tuple[DeviceBatch, "object"]:
     """Decode n `mtype` records from a device byte buffer into a DeviceBatch;
     status[i] = 1 marks a record the buffer ended before.  sync=False leaves
     the decode queued on `stream` (the caller orders what reads the batch
     after it on that stream).  out: decode into this batch (n rows, e.g. a
-    view into a larger one; its sig rows must start 16-byte aligned)."""
+    view into a larger one; its sig rows must start 16-byte aligned).
+    wait=False: `stream` does not first wait for the current stream (the
+    caller has ordered the buffer's producer before it, e.g. push_wires'
+    event: otherwise a second buffer's decode on another stream would queue
+    behind the first buffer's verification)."""
     torch = _torch()
     dev = buf.device
     if out is None:
@@ -56,7 +61,8 @@ def unmarshal_device(v: Verifier, mtype: int, buf, n: int, with_sig: bool = True
     co = out.c_out()
     lib = _lib.load()
     ws = stream or work_stream(dev)
-    ws.wait_stream(torch.cuda.current_stream(ws.device))
+    if wait:
+        ws.wait_stream(torch.cuda.current_stream(ws.device))
     rc = lib.hd_unmarshal_batch_device(v.handle, mtype, 1 if with_sig else 0, buf.data_ptr(), buf.numel(), n,
                                        ctypes.byref(co), status.data_ptr(), ws.cuda_stream)
     if rc != 0:

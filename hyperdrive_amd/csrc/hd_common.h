@@ -55,6 +55,7 @@ enum Verdict : uint8_t {
     V_SIGNATORY_MISMATCH = 5,
     V_NOT_ADMITTED = 6,
     V_BAD_TYPE = 7,
+    V_NOT_AUTHENTIC = 8,   // hd_authenticate_batch_device only: failed the known-key check
 };
 
 // process/message.go:11-22

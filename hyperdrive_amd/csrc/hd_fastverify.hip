@@ -649,7 +649,8 @@ HD void fast_rx(fe& x, const sc& r, uint32_t v) {
 __global__ __launch_bounds__(256) void k_fast_cmp(DevBatch b, SplitRows rows, const int32_t* __restrict__ adm_perm,
                                                   uint8_t* __restrict__ verdict, uint8_t* __restrict__ rec32,
                                                   int32_t* __restrict__ signer, uint32_t* __restrict__ slow,
-                                                  uint32_t* __restrict__ n_slow, uint32_t* __restrict__ bitmap) {
+                                                  uint32_t* __restrict__ n_slow, uint32_t* __restrict__ bitmap,
+                                                  bool auth) {
     wave_prio(rows.prio);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = b.n;
@@ -669,6 +670,9 @@ __global__ __launch_bounds__(256) void k_fast_cmp(DevBatch b, SplitRows rows, co
             const uint32_t sv = b.sig65[65 * (size_t)i + 64];
             fast_rx(x, r, sv);
             v = fast_final(s, zi, x, sv);
+            // authentication only: From's key does not give R, so the
+            // recovered key is not From's -- final, without the recovery
+            if (auth && v == HD_NEEDS_SLOW) v = V_NOT_AUTHENTIC;
         }
         if (v != HD_NEEDS_SLOW) {
             const bool ok = v == V_VALID;
@@ -1264,7 +1268,7 @@ static bool sums_digits_lds(const hd_ctx* ctx) { return ctx->var[HD_VAR_SUM_DIGI
 template <int K, int WP>
 static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict,
                          uint8_t* d_rec32, int32_t* d_signer, uint32_t* d_bitmap, const SplitRows& rows,
-                         const FbWork::Scratch& sc, hipStream_t s) {
+                         const FbWork::Scratch& sc, hipStream_t s, bool auth) {
     FbWork* f = ctx->fb;
     const uint32_t n = b.n;
     // lanes of the K-per-lane kernels, a multiple of 64 (k_fast_final's bitmap words)
@@ -1284,15 +1288,15 @@ static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest
     k_fast_zinv<K><<<tb, 256, 0, s>>>(n, T, rows);
     // whole blocks of 256: every wavefront's 64 messages are one bitmap word pair
     k_fast_cmp<<<nb, 256, 0, s>>>(b, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer, sc.slow, sc.count,
-                                  d_bitmap);
+                                  d_bitmap, auth);
 }
 
 static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict,
                           uint8_t* d_rec32, int32_t* d_signer, uint32_t* d_bitmap, FbWork::Scratch& sc,
-                          hipStream_t s);
+                          hipStream_t s, bool auth);
 
 int hd_fb_verify(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict, uint8_t* d_rec32,
-                 int32_t* d_signer, uint32_t* d_bitmap, hipStream_t s) {
+                 int32_t* d_signer, uint32_t* d_bitmap, hipStream_t s, bool auth) {
     FbWork* f = ctx->fb;
     if (!f->done) FBCHK(hipEventCreateWithFlags(&f->done, hipEventDisableTiming), "fb event");
     const int j = f->next;
@@ -1307,7 +1311,7 @@ int hd_fb_verify(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_
     if (f->any && f->last != s && !(steady && f->steady)) FBCHK(hipStreamWaitEvent(s, f->done, 0), "fb stream order");
     hipEvent_t* pe = fb_prof_pair(f->ev_call, f->n_call, f->prof);
     if (pe) (void)hipEventRecord(pe[0], s);
-    const int rc = fb_verify_impl(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, sc, s);
+    const int rc = fb_verify_impl(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, sc, s, auth);
     if (pe) (void)hipEventRecord(pe[1], s);
     FBCHK(hipEventRecord(sc.done, s), "fb scratch record");
     FBCHK(hipEventRecord(f->done, s), "fb event record");
@@ -1333,7 +1337,7 @@ int hd_fb_quiesce(hd_ctx* ctx) {
 
 static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict,
                           uint8_t* d_rec32, int32_t* d_signer, uint32_t* d_bitmap, FbWork::Scratch& sc,
-                          hipStream_t s) {
+                          hipStream_t s, bool auth) {
     FbWork* f = ctx->fb;
     int rc = hd_dev_grow(ctx, (void**)&sc.slow, &sc.cap_slow, 4 * (size_t)b.n);
     if (rc) return rc;
@@ -1361,7 +1365,7 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         rows.prio = ctx->var[HD_VAR_WAVE_PRIO];
         const int k = split_k_for(ctx, n);
         f->last_k = k;
-#define HD_SPLIT(K, WP) launch_split<K, WP>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, sc, s)
+#define HD_SPLIT(K, WP) launch_split<K, WP>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, sc, s, auth)
         if (f->wp == HD_FB_WW) {
             if (k == 16) HD_SPLIT(16, HD_FB_WW);
             else if (k == 4) HD_SPLIT(4, HD_FB_WW);

@@ -74,8 +74,9 @@ const hd::gp* hd_fb_gtab(const hd_ctx* ctx);    // the shared fixed-base G table
 int hd_fb_map_signatories(hd_ctx* ctx, const uint8_t* sorted_sigs32, uint32_t m);  // after hd_set_signatories
 int hd_fb_clear_keys(hd_ctx* ctx);               // pubkey format changed: learned keys no longer apply
 // fast kernel + slow recovery of the rest + learning; the whole verify of a device batch
+// (auth: hd_authenticate_batch_device -- a failed known-key check is final, NOT_AUTHENTIC)
 int hd_fb_verify(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict, uint8_t* d_rec32,
-                 int32_t* d_signer, uint32_t* d_bitmap, hipStream_t s);
+                 int32_t* d_signer, uint32_t* d_bitmap, hipStream_t s, bool auth = false);
 
 // slow-path control for k_verify (hd_verify.hip): an index list and key learning
 struct SlowCtl {

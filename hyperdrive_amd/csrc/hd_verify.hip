@@ -327,12 +327,12 @@ int hd_launch_slow(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint
 
 namespace {
 int launch_verify(hd_ctx* ctx, const hd_batch* db, const uint8_t* d_digest, uint8_t* d_verdict, uint8_t* d_recovered32,
-                  int32_t* d_signer, uint32_t* d_valid_bitmap, void* stream) {
+                  int32_t* d_signer, uint32_t* d_valid_bitmap, void* stream, bool auth = false) {
     (void)hipSetDevice(ctx->device);
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
     DevBatch b{db->n, db->type, db->height, db->round, db->valid_round, db->value32, db->from32, db->sig65};
     if (ctx->fastpath && ctx->fb)
-        return hd_fb_verify(ctx, b, d_digest, d_verdict, d_recovered32, d_signer, d_valid_bitmap, s);
+        return hd_fb_verify(ctx, b, d_digest, d_verdict, d_recovered32, d_signer, d_valid_bitmap, s, auth);
     // one block per 256 messages, no grid-stride: the dispatcher hands a CU a
     // new block whenever one retires, which balances the last round better
     // than a resident-sized grid looping over the batch (measured on 1M:
@@ -363,6 +363,14 @@ int hd_verify_batch_device(hd_ctx* ctx, const hd_batch* db, uint8_t* d_verdict, 
     if (!d_verdict) return HD_EINVAL;
     if (!db->type || !db->height || !db->round || !db->value32 || !db->from32 || !db->sig65) return HD_EINVAL;
     return launch_verify(ctx, db, nullptr, d_verdict, d_recovered32, d_signer, d_valid_bitmap, stream);
+}
+
+int hd_authenticate_batch_device(hd_ctx* ctx, const hd_batch* db, uint8_t* d_verdict, void* stream) {
+    if (!ctx || !db) return HD_EINVAL;
+    if (db->n == 0) return HD_OK;
+    if (!d_verdict) return HD_EINVAL;
+    if (!db->type || !db->height || !db->round || !db->value32 || !db->from32 || !db->sig65) return HD_EINVAL;
+    return launch_verify(ctx, db, nullptr, d_verdict, nullptr, nullptr, nullptr, stream, true);
 }
 
 int hd_verify_batch_digest_device(hd_ctx* ctx, const hd_batch* db, const uint8_t* d_digest32, uint8_t* d_verdict,

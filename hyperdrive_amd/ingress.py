@@ -82,9 +82,10 @@ class Ingress:
         self.votes.close()
 
     def push_device(self, batch: DeviceBatch, stream=None):
-        """Verify a device batch and buffer its authenticated messages (VALID
-        or NOT_ADMITTED) with height >= the current height.  Returns the
-        device verdict tensor."""
+        """Authenticate a device batch and buffer its authenticated messages
+        (VALID or NOT_ADMITTED) with height >= the current height.  Returns
+        the device verdict tensor (authenticate_batch_device's: a message
+        that fails its From's known-key check is NOT_AUTHENTIC, unclassified)."""
         torch = _torch()
         dev = batch.height.device
         n = batch.n
@@ -93,7 +94,7 @@ class Ingress:
             return verdict[:0]
         ws = stream or work_stream(dev)
         ws.wait_stream(torch.cuda.current_stream(ws.device))
-        self.v.verify_batch_device(batch.c_struct(), verdict.data_ptr(), None, None, None, ws.cuda_stream)
+        self.v.authenticate_batch_device(batch.c_struct(), verdict.data_ptr(), ws.cuda_stream)
         self.mq.insert_verified_device(batch, verdict, self.height, stream=ws)
         return verdict[:n]
 
@@ -137,9 +138,9 @@ class Ingress:
             if complete == 0:
                 staged.append((None, torch.empty(0, dtype=torch.uint8, device=dev), s))
                 continue
-            db, _ = unmarshal_device(self.v, mtype, buf, complete, with_sig, stream=s, sync=False)
+            db, _ = unmarshal_device(self.v, mtype, buf, complete, with_sig, stream=s, sync=False, wait=False)
             verdict = torch.empty(complete, dtype=torch.uint8, device=dev)
-            self.v.verify_batch_device(db.c_struct(), verdict.data_ptr(), None, None, None, s.cuda_stream)
+            self.v.authenticate_batch_device(db.c_struct(), verdict.data_ptr(), s.cuda_stream)
             staged.append((db, verdict, s))
         out = []
         for db, verdict, s in staged:

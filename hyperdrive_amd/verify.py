@@ -36,8 +36,9 @@ INFINITY = 4
 SIGNATORY_MISMATCH = 5
 NOT_ADMITTED = 6
 BAD_TYPE = 7
+NOT_AUTHENTIC = 8     # authenticate_batch_device only (include/hd_verify.h)
 VERDICT_NAMES = ["VALID", "BAD_RECID", "BAD_RS", "NO_POINT", "INFINITY", "SIGNATORY_MISMATCH",
-                 "NOT_ADMITTED", "BAD_TYPE"]
+                 "NOT_ADMITTED", "BAD_TYPE", "NOT_AUTHENTIC"]
 
 PROPOSE, PREVOTE, PRECOMMIT = 1, 2, 3
 
@@ -244,6 +245,15 @@ class Verifier:
         """Device-resident variant: every pointer is a device address."""
         self._check(self._lib.hd_verify_batch_device(self._ctx, ctypes.byref(dbatch), d_verdict, d_recovered,
                                                      d_signer, d_bitmap, stream), "hd_verify_batch_device")
+
+    def authenticate_batch_device(self, dbatch: HdBatch, d_verdict: int, stream: Optional[int] = None) -> None:
+        """Verdicts for the replica ingress (hd_authenticate_batch_device):
+        VALID and NOT_ADMITTED exactly as verify_batch_device; a message whose
+        From has a known key that does not verify its signature is final as
+        NOT_AUTHENTIC, without the recovery that would classify it (the
+        reference drops every unauthenticated message, process/process.go:95-98)."""
+        self._check(self._lib.hd_authenticate_batch_device(self._ctx, ctypes.byref(dbatch), d_verdict, stream),
+                    "hd_authenticate_batch_device")
 
     # ---- tally -------------------------------------------------------
     @staticmethod

@@ -64,6 +64,11 @@ extern "C" {
 #define HD_VERDICT_SIGNATORY_MISMATCH 5 /* recovered signatory != From                */
 #define HD_VERDICT_NOT_ADMITTED 6       /* From not in the admitted signatory set     */
 #define HD_VERDICT_BAD_TYPE 7           /* type not Propose/Prevote/Precommit         */
+#define HD_VERDICT_NOT_AUTHENTIC 8      /* hd_authenticate_batch_device only: From's
+                                           known key does not verify the signature;
+                                           the recovery that would name the reason
+                                           (NO_POINT, INFINITY or SIGNATORY_MISMATCH)
+                                           was skipped                                 */
 
 typedef struct hd_ctx hd_ctx;
 
@@ -186,6 +191,17 @@ int hd_verify_batch(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8_
  * learned, a call on another stream first waits for the previous call. */
 int hd_verify_batch_device(hd_ctx* ctx, const hd_batch* dbatch, uint8_t* d_verdict, uint8_t* d_recovered32,
                            int32_t* d_signer, uint32_t* d_valid_bitmap, void* stream);
+
+/* Authentication only, for the replica ingress: the reference buffers a
+ * message only once it is authenticated (process/process.go:95-98,
+ * mq/mq.go:85-101) and drops it otherwise, whatever the reason.  Same inputs
+ * and ordering as hd_verify_batch_device with verdicts only.  VALID and
+ * NOT_ADMITTED are exactly hd_verify_batch_device's; every other message gets
+ * a verdict that is neither of them: the same as hd_verify_batch_device's, or
+ * HD_VERDICT_NOT_AUTHENTIC where From's key is known and the known-key check
+ * fails (then the recovered key is not From's, so the message is not
+ * authentic; the full recovery that would classify it is skipped). */
+int hd_authenticate_batch_device(hd_ctx* ctx, const hd_batch* dbatch, uint8_t* d_verdict, void* stream);
 
 /* Asynchronous host-buffer verification (the cgo caller's path,
  * replica/replica.go:156-181, without its synchronous upload -> verify ->

@@ -59,6 +59,14 @@ for rep in range(3):
         _, rec[f"verify_{t}"] = clock(lambda: v.verify_batch_device(dbu.c_struct(), verdict.data_ptr(), None, None,
                                                                     None, ws.cuda_stream))
         _, rec[f"insert_{t}"] = clock(lambda: ing.mq.insert_verified_device(dbu, verdict, 1, stream=ws))
+        for k in range(2):      # authentication only (the ingress's call); the second run sizes by the first
+            _, rec[f"auth_{t}"] = clock(lambda: v.authenticate_batch_device(dbu.c_struct(), verdict.data_ptr(),
+                                                                          ws.cuda_stream))
+        rec[f"auth_fallback_{t}"] = v.fastpath_stats()[1]
+        for k in range(2):
+            _, rec[f"verify2_{t}"] = clock(lambda: v.verify_batch_device(dbu.c_struct(), verdict.data_ptr(), None,
+                                                                       None, None, ws.cuda_stream))
+        rec[f"verify_fallback_{t}"] = v.fastpath_stats()[1]
     ing.mq.drop_below(2 ** 62)
     _, rec["push_wire_x2"] = clock(lambda: [ing.push_wire(t, wire, sub.n, stream=ws) for t, sub, wire in parts])
     ing.mq.drop_below(2 ** 62)

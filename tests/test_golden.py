@@ -141,6 +141,40 @@ def test_gpu_matches_golden(gpu, name):
         v.close()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", CASES)
+def test_gpu_authenticate_golden(gpu, name):
+    """hd_authenticate_batch_device on each fixture, after a verify pass has
+    taught the context the keys: VALID and NOT_ADMITTED exactly the golden
+    verdicts, every other message its golden verdict or NOT_AUTHENTIC (8),
+    and NOT_AUTHENTIC only for Froms in the admitted set."""
+    import torch
+    from hyperdrive_amd.device import DeviceBatch, work_stream
+    b, z, _ = load_case(name)
+    if len(b) == 0:
+        return
+    v = gpu.Verifier(0, compressed=int(z["compressed"]))
+    try:
+        v.set_signatories(z["admitted"])
+        v.verify_batch(b)
+        db = DeviceBatch.from_host(b, "cuda")
+        out = torch.full((len(b),), 255, dtype=torch.uint8, device="cuda")
+        ws = work_stream()
+        ws.wait_stream(torch.cuda.current_stream())
+        v.authenticate_batch_device(db.c_struct(), out.data_ptr(), ws.cuda_stream)
+        ws.synchronize()
+        va, want = out.cpu().numpy(), z["verdict"]
+        auth = np.isin(want, (0, 6))
+        assert (va[auth] == want[auth]).all()
+        assert not np.isin(va[~auth], (0, 6)).any()
+        na = va == 8
+        assert ((va == want) | na).all()
+        adm = {bytes(x) for x in np.asarray(z["admitted"]).reshape(-1, 32)}
+        assert all(b.frm[i].tobytes() in adm for i in np.flatnonzero(na))
+    finally:
+        v.close()
+
+
 # Every kernel instantiation a context can select (include/hd_verify.h
 # HD_VAR_*), one at a time from the defaults; the first entry is the default.
 VARIANTS = [("default", None, None), ("verify_waves_2", "verify_waves", 2), ("verify_waves_4", "verify_waves", 4),

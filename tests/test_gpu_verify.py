@@ -152,6 +152,53 @@ def test_adversarial_full_mix_vs_c_oracle(gpu, oracle, coracle):
         v.close()
 
 
+def test_authenticate_vs_c_oracle(gpu, coracle):
+    """hd_authenticate_batch_device (the replica ingress's call) on the 30 %
+    adversarial mix: before the keys are known every verdict is the oracle's
+    (full recovery); once they are, VALID and NOT_ADMITTED are still exactly
+    the oracle's, every other message is the oracle's verdict or
+    NOT_AUTHENTIC, NOT_AUTHENTIC only where From is admitted, and the
+    fallback list shrinks to what the known-key check cannot decide (Froms
+    outside the admitted set, the early verdicts' lift checks).  A full
+    verify on the same context afterwards is unaffected."""
+    import torch
+    from hyperdrive_amd.device import DeviceBatch, generate, work_stream
+    N, S = 65536, 100
+    v = gpu.Verifier(0)
+    try:
+        ks = v.gen_keys(S)
+        v.set_signatories(ks[0])
+        db, _, _ = generate(v, 0, N, S, 30, keys=ks)
+        hb = db.to_host()
+        cv, crec = coracle.verify(hb, ks[0], True, threads=16)
+        admitted = {x.tobytes() for x in ks[0]}
+        from_adm = np.array([hb.frm[i].tobytes() in admitted for i in range(N)])
+        ws = work_stream()
+        out = torch.empty(N, dtype=torch.uint8, device="cuda")
+        fallbacks = []
+        for rnd in range(3):
+            out.fill_(255)
+            v.authenticate_batch_device(db.c_struct(), out.data_ptr(), ws.cuda_stream)
+            ws.synchronize()
+            va = out.cpu().numpy()
+            fallbacks.append(v.fastpath_stats()[1])
+            if rnd == 0:
+                assert va.tolist() == cv.tolist()          # no key known yet: the full recovery
+                continue
+            auth = np.isin(cv, (0, 6))
+            assert (va[auth] == cv[auth]).all()
+            assert not np.isin(va[~auth], (0, 6)).any()
+            na = va == 8
+            assert ((va == cv) | na).all()
+            assert na.sum() > 0.05 * N and from_adm[na].all()
+        assert fallbacks[2] < 0.5 * int((cv != 0).sum())
+        res = v.verify_batch(hb)
+        assert res.verdict.tolist() == cv.tolist()
+        assert res.recovered.tobytes() == crec.tobytes()
+    finally:
+        v.close()
+
+
 def test_fallback_burst_after_clean_batches(gpu, coracle):
     """The fallback kernels (k_slow_lift, k_verify over the leftover list) size
     their grids by the latest list length seen (hd_fastverify.hip

@@ -32,6 +32,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <new>
 
@@ -467,23 +468,32 @@ __global__ void k_mq_commit(uint32_t nsend, const uint32_t* __restrict__ newhead
 #define HD_MQ_ROW 160
 #define HD_MQ_HDR 64
 __device__ __forceinline__ void mq_row_put(uint8_t* __restrict__ row, const Pool& p, uint32_t e) {
-    uint64_t* w = reinterpret_cast<uint64_t*>(row);
-    w[0] = (uint64_t)p.h[e];
-    w[1] = (uint64_t)p.r[e];
-    w[2] = (uint64_t)p.vr[e];
+    // whole dwords only (the stage may be mapped host memory: one PCIe write
+    // per dword instead of per byte); bytes 152..155 = sig[64], type, 0, 0
+    uint32_t* o = reinterpret_cast<uint32_t*>(row);
+    const uint64_t hv = (uint64_t)p.h[e], rv = (uint64_t)p.r[e], vv = (uint64_t)p.vr[e];
+    o[0] = (uint32_t)hv;
+    o[1] = (uint32_t)(hv >> 32);
+    o[2] = (uint32_t)rv;
+    o[3] = (uint32_t)(rv >> 32);
+    o[4] = (uint32_t)vv;
+    o[5] = (uint32_t)(vv >> 32);
     const uint32_t* val = reinterpret_cast<const uint32_t*>(p.value + 32 * (size_t)e);
     const uint32_t* frm = reinterpret_cast<const uint32_t*>(p.from + 32 * (size_t)e);
-    uint32_t* o = reinterpret_cast<uint32_t*>(row + 24);
-    for (int j = 0; j < 8; j++) o[j] = val[j];
-    for (int j = 0; j < 8; j++) o[8 + j] = frm[j];
-    for (int j = 0; j < 65; j++) row[88 + j] = p.sig[65 * (size_t)e + j];
-    row[153] = p.type[e];
-    *reinterpret_cast<int32_t*>(row + 156) = p.sender[e];
+    for (int j = 0; j < 8; j++) o[6 + j] = val[j];
+    for (int j = 0; j < 8; j++) o[14 + j] = frm[j];
+    const uint8_t* sg = p.sig + 65 * (size_t)e;
+    for (int j = 0; j < 16; j++)
+        o[22 + j] = (uint32_t)sg[4 * j] | ((uint32_t)sg[4 * j + 1] << 8) | ((uint32_t)sg[4 * j + 2] << 16) |
+                    ((uint32_t)sg[4 * j + 3] << 24);
+    o[38] = (uint32_t)sg[64] | ((uint32_t)p.type[e] << 8);
+    o[39] = (uint32_t)p.sender[e];
 }
 __global__ __launch_bounds__(1024) void k_mq_consume1(uint32_t nsend, Pool p, uint32_t* __restrict__ head,
                                                       const uint32_t* __restrict__ send, int64_t h, uint32_t na,
                                                       const uint32_t* __restrict__ list, int be_words, Dict d,
-                                                      uint32_t rows, uint32_t cap, uint8_t* __restrict__ stage) {
+                                                      uint32_t rows, uint32_t cap, uint8_t* __restrict__ stage,
+                                                      uint32_t seq) {
     typedef hipcub::BlockScan<uint32_t, 1024> Scan;
     typedef hipcub::BlockReduce<uint32_t, 1024> Red;
     __shared__ typename Scan::TempStorage ts;
@@ -541,6 +551,14 @@ __global__ __launch_bounds__(1024) void k_mq_consume1(uint32_t nsend, Pool p, ui
         mq_row_put(out + (size_t)HD_MQ_ROW * k, p, lo_of[a] + (k - off[a]));
     }
     if (total <= cap && t < nsend) head[t] = cut;
+    if (seq) {
+        // mapped host stage: every row and the header reach host memory
+        // before the sequence word the host spins on
+        __threadfence_system();
+        __syncthreads();
+        if (t == 0) __hip_atomic_store(reinterpret_cast<uint32_t*>(stage) + 2, seq, __ATOMIC_RELEASE,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // live pool entries (not in a consumed / dropped prefix)
@@ -584,6 +602,13 @@ struct hd_mq {
     void* hstage = nullptr;
     size_t hstage_cap = 0;
     uint32_t last_deliv = 0;    // the previous consume's delivery: sizes the next one's first download
+    // mapped (device-written) host stage of the fused consume: no download,
+    // the host spins on a sequence word (HD_MQ_MAPPED=0: the download path)
+    void* mstage = nullptr;
+    uint8_t* mstage_dev = nullptr;
+    size_t mstage_cap = 0;
+    uint32_t seq = 0;
+    bool mapped = true;
 };
 
 #define QCHK(expr, what)                                           \
@@ -882,6 +907,7 @@ int hd_mq_create(hd_ctx* ctx, uint32_t max_capacity, hd_mq** out) {
     q->max_cap = max_capacity;
     q->seed = (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count() * 0x9E3779B97F4A7C15ull ^
               (uint64_t)(uintptr_t)q;
+    if (const char* e = getenv("HD_MQ_MAPPED")) q->mapped = atoi(e) != 0;
     *out = q;
     return HD_OK;
 }
@@ -897,6 +923,7 @@ int hd_mq_destroy(hd_mq* q) {
     for (auto& b : q->buf)
         if (b.p) (void)hipFree(b.p);
     if (q->hstage) (void)hipHostFree(q->hstage);
+    if (q->mstage) (void)hipHostFree(q->mstage);
     delete q;
     return HD_OK;
 }
@@ -990,31 +1017,75 @@ static int mq_consume1(hd_mq* q, int64_t h, const uint32_t* list, uint32_t na, i
     int rc = 0;
     const uint32_t rows = std::max(cap, 1u);
     const size_t bytes = HD_MQ_HDR + (size_t)HD_MQ_ROW * rows;
-    uint8_t* dst = (uint8_t*)qbuf(q, MQ_STAGE, bytes, &rc);
-    if (rc) return rc;
-    if (q->hstage_cap < bytes) {
-        if (q->hstage) (void)hipHostFree(q->hstage);
-        q->hstage = nullptr;
-        q->hstage_cap = 0;
-        const size_t want = std::max(bytes, (size_t)1 << 16);
-        QCHK(hipHostMalloc(&q->hstage, want, hipHostMallocDefault), "mq host stage");
-        q->hstage_cap = want;
-    }
-    k_mq_consume1<<<1, 1024, 0, s>>>(q->nsend, q->pool, (uint32_t*)q->buf[MQ_HEADS].p,
-                                     (const uint32_t*)q->buf[MQ_SEND].p, h, na, list, be, dict_of(q), rows, cap, dst);
-    QCHK(hipGetLastError(), "k_mq_consume1");
-    const uint32_t guess = std::min(rows, std::max(64u, 2 * q->last_deliv));
-    uint8_t* hs = (uint8_t*)q->hstage;
-    QCHK(hipMemcpyAsync(hs, dst, HD_MQ_HDR + (size_t)HD_MQ_ROW * guess, hipMemcpyDeviceToHost, s), "consume download");
-    QCHK(hipStreamSynchronize(s), "consume sync");
-    const uint32_t c = ((const uint32_t*)hs)[0], nr = ((const uint32_t*)hs)[1];
-    *n_out = c;
-    if (c > cap) return HD_ECAP;   // nothing committed
-    if (c > guess) {
-        const size_t o = HD_MQ_HDR + (size_t)HD_MQ_ROW * guess;
-        QCHK(hipMemcpyAsync(hs + o, dst + o, (size_t)HD_MQ_ROW * (c - guess), hipMemcpyDeviceToHost, s),
-             "consume download rest");
+    uint8_t* hs = nullptr;
+    uint32_t c = 0, nr = 0;
+    if (q->mapped) {
+        // the kernel writes the header and rows straight into mapped host
+        // memory and, last, the call's sequence number: no copy, no stream
+        // synchronisation on the common path
+        if (q->mstage_cap < bytes) {
+            if (q->mstage) (void)hipHostFree(q->mstage);
+            q->mstage = nullptr;
+            q->mstage_cap = 0;
+            const size_t want = std::max(bytes, (size_t)1 << 16);
+            QCHK(hipHostMalloc(&q->mstage, want, hipHostMallocMapped | hipHostMallocCoherent), "mq mapped stage");
+            void* dp = nullptr;
+            QCHK(hipHostGetDevicePointer(&dp, q->mstage, 0), "mq mapped stage pointer");
+            q->mstage_dev = (uint8_t*)dp;
+            q->mstage_cap = want;
+        }
+        const uint32_t seq = ++q->seq ? q->seq : ++q->seq;   // never 0 (0 = no signal)
+        k_mq_consume1<<<1, 1024, 0, s>>>(q->nsend, q->pool, (uint32_t*)q->buf[MQ_HEADS].p,
+                                         (const uint32_t*)q->buf[MQ_SEND].p, h, na, list, be, dict_of(q), rows, cap,
+                                         q->mstage_dev, seq);
+        QCHK(hipGetLastError(), "k_mq_consume1");
+        hs = (uint8_t*)q->mstage;
+        volatile uint32_t* word = (volatile uint32_t*)hs + 2;
+        // spin for the sequence word; past ~0.2 s, wait for the stream (a
+        // fault surfaces there) and read it once more
+        const auto t0 = std::chrono::steady_clock::now();
+        while (*word != seq) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+                QCHK(hipStreamSynchronize(s), "consume sync");
+                if (*word != seq) return hd_ctx_fail(q->ctx, hipErrorUnknown, "consume signal");
+                break;
+            }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        c = ((const uint32_t*)hs)[0];
+        nr = ((const uint32_t*)hs)[1];
+        *n_out = c;
+        if (c > cap) return HD_ECAP;   // nothing committed
+    } else {
+        uint8_t* dst = (uint8_t*)qbuf(q, MQ_STAGE, bytes, &rc);
+        if (rc) return rc;
+        if (q->hstage_cap < bytes) {
+            if (q->hstage) (void)hipHostFree(q->hstage);
+            q->hstage = nullptr;
+            q->hstage_cap = 0;
+            const size_t want = std::max(bytes, (size_t)1 << 16);
+            QCHK(hipHostMalloc(&q->hstage, want, hipHostMallocDefault), "mq host stage");
+            q->hstage_cap = want;
+        }
+        k_mq_consume1<<<1, 1024, 0, s>>>(q->nsend, q->pool, (uint32_t*)q->buf[MQ_HEADS].p,
+                                         (const uint32_t*)q->buf[MQ_SEND].p, h, na, list, be, dict_of(q), rows, cap,
+                                         dst, 0u);
+        QCHK(hipGetLastError(), "k_mq_consume1");
+        const uint32_t guess = std::min(rows, std::max(64u, 2 * q->last_deliv));
+        hs = (uint8_t*)q->hstage;
+        QCHK(hipMemcpyAsync(hs, dst, HD_MQ_HDR + (size_t)HD_MQ_ROW * guess, hipMemcpyDeviceToHost, s),
+             "consume download");
         QCHK(hipStreamSynchronize(s), "consume sync");
+        c = ((const uint32_t*)hs)[0];
+        nr = ((const uint32_t*)hs)[1];
+        *n_out = c;
+        if (c > cap) return HD_ECAP;   // nothing committed
+        if (c > guess) {
+            const size_t o = HD_MQ_HDR + (size_t)HD_MQ_ROW * guess;
+            QCHK(hipMemcpyAsync(hs + o, dst + o, (size_t)HD_MQ_ROW * (c - guess), hipMemcpyDeviceToHost, s),
+                 "consume download rest");
+            QCHK(hipStreamSynchronize(s), "consume sync");
+        }
     }
     q->last_deliv = c;
     if (n_removed) *n_removed = nr;

@@ -568,6 +568,40 @@ __global__ void k_mq_live(uint32_t M, const int32_t* __restrict__ snd, const uin
     if (e < M) keep[e] = e >= head[snd[e]];
 }
 
+// min and max of the three sort keys in one pass: out[0..4] = min of
+// (rk, ~rk, hk, ~hk, ~sk) in the order-preserving unsigned form (signed x ->
+// x ^ 2^63), all initialised to ~0; max(x) = ~min(~x)
+__device__ __forceinline__ uint64_t mq_ord(int64_t x) { return (uint64_t)x ^ 0x8000000000000000ull; }
+__global__ __launch_bounds__(256) void k_mq_minmax3(uint32_t T, const int64_t* __restrict__ rk,
+                                                   const int64_t* __restrict__ hk, const uint32_t* __restrict__ sk,
+                                                   unsigned long long* __restrict__ out) {
+    uint64_t m[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < T; e += gridDim.x * blockDim.x) {
+        const uint64_t r = mq_ord(rk[e]), hh = mq_ord(hk[e]), ss = ~(uint64_t)sk[e];
+        m[0] = r < m[0] ? r : m[0];
+        m[1] = ~r < m[1] ? ~r : m[1];
+        m[2] = hh < m[2] ? hh : m[2];
+        m[3] = ~hh < m[3] ? ~hh : m[3];
+        m[4] = ss < m[4] ? ss : m[4];
+    }
+    // wavefront, then block minima; one atomic per block and field
+    __shared__ uint64_t part[4][5];
+    for (int k = 0; k < 5; k++) {
+        uint64_t x = m[k];
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t y = __shfl_xor(x, o);
+            x = y < x ? y : x;
+        }
+        if ((threadIdx.x & 63u) == 0) part[threadIdx.x >> 6][k] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < 5) {
+        uint64_t x = part[0][threadIdx.x];
+        for (int w = 1; w < 4; w++) x = part[w][threadIdx.x] < x ? part[w][threadIdx.x] : x;
+        atomicMin(out + threadIdx.x, (unsigned long long)x);
+    }
+}
+
 inline uint32_t nblk(uint32_t n) { return (n + 255) / 256; }
 
 int bits_of(uint64_t range) {
@@ -629,26 +663,6 @@ static void* qbuf(hd_mq* q, int slot, size_t bytes, int* rc) {
 
 static Dict dict_of(const hd_mq* q) { return Dict{q->keys, q->slots, q->tcap - 1, q->seed}; }
 
-template <typename T>
-static int dev_minmax(hd_mq* q, const T* d, uint32_t n, T* mn, T* mx, hipStream_t s) {
-    int rc = 0;
-    T* red = (T*)qbuf(q, MQ_RED, 2 * sizeof(T), &rc);
-    if (rc) return rc;
-    size_t need = 0, need2 = 0;
-    QCHK(hipcub::DeviceReduce::Min(nullptr, need, d, red, n, s), "reduce size");
-    QCHK(hipcub::DeviceReduce::Max(nullptr, need2, d, red + 1, n, s), "reduce size");
-    void* tmp = qbuf(q, MQ_TMP, std::max(need, need2), &rc);
-    if (rc) return rc;
-    QCHK(hipcub::DeviceReduce::Min(tmp, need, d, red, n, s), "reduce min");
-    QCHK(hipcub::DeviceReduce::Max(tmp, need2, d, red + 1, n, s), "reduce max");
-    T host[2];
-    QCHK(hipMemcpyAsync(host, red, 2 * sizeof(T), hipMemcpyDeviceToHost, s), "minmax");
-    QCHK(hipStreamSynchronize(s), "minmax sync");
-    *mn = host[0];
-    *mx = host[1];
-    return HD_OK;
-}
-
 // select-flagged over [0, n) -> out indices, returns count (synchronises)
 // Indices of the set flags, in order.  The count lands in *count after a
 // stream sync when wait is set; with wait unset it is only queued (the caller
@@ -671,11 +685,31 @@ static int select_idx(hd_mq* q, const uint8_t* flag, uint32_t n, uint32_t* out, 
     return HD_OK;
 }
 
-// stable sort of perm (DoubleBuffer) by a 64-bit field rebased to its min
-static int sort_pass64(hd_mq* q, hipcub::DoubleBuffer<uint32_t>& perm, const int64_t* field, uint32_t T, hipStream_t s) {
-    int64_t mn = 0, mx = 0;
-    int rc = dev_minmax(q, field, T, &mn, &mx, s);
+static int key_ranges(hd_mq* q, uint32_t T, const int64_t* rk, const int64_t* hk, const uint32_t* sk, int64_t* rmn,
+                      int64_t* rmx, int64_t* hmn, int64_t* hmx, uint32_t* smx, hipStream_t s) {
+    int rc = 0;
+    unsigned long long* red = (unsigned long long*)qbuf(q, MQ_RED, 5 * sizeof(uint64_t), &rc);
     if (rc) return rc;
+    QCHK(hipMemsetAsync(red, 0xFF, 5 * sizeof(uint64_t), s), "key ranges init");
+    const uint32_t blocks = std::min(nblk(T), 256u);
+    k_mq_minmax3<<<blocks, 256, 0, s>>>(T, rk, hk, sk, red);
+    QCHK(hipGetLastError(), "k_mq_minmax3");
+    uint64_t host[5];
+    QCHK(hipMemcpyAsync(host, red, sizeof(host), hipMemcpyDeviceToHost, s), "key ranges");
+    QCHK(hipStreamSynchronize(s), "key ranges sync");
+    const uint64_t sign = 0x8000000000000000ull;
+    *rmn = (int64_t)(host[0] ^ sign);
+    *rmx = (int64_t)(~host[1] ^ sign);
+    *hmn = (int64_t)(host[2] ^ sign);
+    *hmx = (int64_t)(~host[3] ^ sign);
+    *smx = (uint32_t)~host[4];
+    return HD_OK;
+}
+
+// stable sort of perm (DoubleBuffer) by a 64-bit field rebased to its min
+static int sort_pass64(hd_mq* q, hipcub::DoubleBuffer<uint32_t>& perm, const int64_t* field, uint32_t T, hipStream_t s,
+                       int64_t mn, int64_t mx) {
+    int rc = 0;
     const int bits = bits_of((uint64_t)mx - (uint64_t)mn);
     if (bits == 0) return HD_OK;
     uint64_t* ka = (uint64_t*)qbuf(q, MQ_K64A, 8 * (size_t)T, &rc);
@@ -692,10 +726,8 @@ static int sort_pass64(hd_mq* q, hipcub::DoubleBuffer<uint32_t>& perm, const int
 }
 
 static int sort_pass32(hd_mq* q, hipcub::DoubleBuffer<uint32_t>& perm, const uint32_t* field, uint32_t T,
-                       hipStream_t s) {
-    uint32_t mn = 0, mx = 0;
-    int rc = dev_minmax(q, field, T, &mn, &mx, s);
-    if (rc) return rc;
+                       hipStream_t s, uint32_t mx) {
+    int rc = 0;
     const int bits = bits_of(mx);
     if (bits == 0) return HD_OK;
     uint32_t* ka = (uint32_t*)qbuf(q, MQ_K32A, 4 * (size_t)T, &rc);
@@ -861,10 +893,14 @@ static int mq_insert_flagged(hd_mq* q, const hd_batch* d_batch, const uint8_t* f
     k_mq_keys<<<nblk(T), 256, 0, s>>>(src, T, hk, rk, sk, p0);
     // 4. stable LSD passes: round, height, sender (mq.go:120-128 order; the
     //    stability keeps arrival order among equal keys)
+    //    (the three keys' ranges in one reduction and one host round trip)
+    int64_t rmn, rmx, hmn, hmx;
+    uint32_t smx;
+    if ((rc = key_ranges(q, T, rk, hk, sk, &rmn, &rmx, &hmn, &hmx, &smx, s))) return rc;
     hipcub::DoubleBuffer<uint32_t> perm(p0, p1);
-    if ((rc = sort_pass64(q, perm, rk, T, s))) return rc;
-    if ((rc = sort_pass64(q, perm, hk, T, s))) return rc;
-    if ((rc = sort_pass32(q, perm, sk, T, s))) return rc;
+    if ((rc = sort_pass64(q, perm, rk, T, s, rmn, rmx))) return rc;
+    if ((rc = sort_pass64(q, perm, hk, T, s, hmn, hmx))) return rc;
+    if ((rc = sort_pass32(q, perm, sk, T, s, smx))) return rc;
     // 5. per-sender capacity: keep the first max_cap of every sender run
     uint32_t* head = (uint32_t*)qbuf(q, MQ_HEAD, 4 * (size_t)T, &rc);
     uint8_t* keep = (uint8_t*)qbuf(q, MQ_KEEP, T, &rc);

@@ -303,6 +303,18 @@ __global__ void k_mq_rekey32(uint32_t T, const uint32_t* __restrict__ perm, cons
     if (k < T) key[k] = field[perm[k]];
 }
 
+// one sort key for (sender, height, round), each rebased to its minimum and
+// packed high to low, when the three ranges fit 64 bits together (element e
+// in the merged sequence's order: the sort is stable, so ties keep arrival)
+__global__ void k_mq_combine(uint32_t T, const int64_t* __restrict__ rk, const int64_t* __restrict__ hk,
+                             const uint32_t* __restrict__ sk, int64_t rmn, int64_t hmn, int rb, int hb,
+                             uint64_t* __restrict__ key) {
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= T) return;
+    const uint64_t r = (uint64_t)rk[e] - (uint64_t)rmn, h = (uint64_t)hk[e] - (uint64_t)hmn;
+    key[e] = ((((uint64_t)sk[e] << hb) | h) << rb) | r;
+}
+
 // position of each sorted element's sender run start (inclusive max-scan input)
 __global__ void k_mq_heads(uint32_t T, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ sk,
                            uint32_t* __restrict__ head) {
@@ -898,9 +910,28 @@ static int mq_insert_flagged(hd_mq* q, const hd_batch* d_batch, const uint8_t* f
     uint32_t smx;
     if ((rc = key_ranges(q, T, rk, hk, sk, &rmn, &rmx, &hmn, &hmx, &smx, s))) return rc;
     hipcub::DoubleBuffer<uint32_t> perm(p0, p1);
-    if ((rc = sort_pass64(q, perm, rk, T, s, rmn, rmx))) return rc;
-    if ((rc = sort_pass64(q, perm, hk, T, s, hmn, hmx))) return rc;
-    if ((rc = sort_pass32(q, perm, sk, T, s, smx))) return rc;
+    const int rb = bits_of((uint64_t)rmx - (uint64_t)rmn), hb = bits_of((uint64_t)hmx - (uint64_t)hmn),
+              sb = bits_of(smx);
+    if (rb + hb + sb <= 64) {
+        // one radix sort over the packed key (usually ~25 bits: 3-4 digit
+        // passes instead of three sorts' worth)
+        if (rb + hb + sb > 0) {
+            uint64_t* ka = (uint64_t*)qbuf(q, MQ_K64A, 8 * (size_t)T, &rc);
+            uint64_t* kb = (uint64_t*)qbuf(q, MQ_K64B, 8 * (size_t)T, &rc);
+            if (rc) return rc;
+            k_mq_combine<<<nblk(T), 256, 0, s>>>(T, rk, hk, sk, rmn, hmn, rb, hb, ka);
+            hipcub::DoubleBuffer<uint64_t> keys(ka, kb);
+            size_t need = 0;
+            QCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, need, keys, perm, T, 0, rb + hb + sb, s), "sort size");
+            void* tmp = qbuf(q, MQ_TMP, need, &rc);
+            if (rc) return rc;
+            QCHK(hipcub::DeviceRadixSort::SortPairs(tmp, need, keys, perm, T, 0, rb + hb + sb, s), "sort keys");
+        }
+    } else {
+        if ((rc = sort_pass64(q, perm, rk, T, s, rmn, rmx))) return rc;
+        if ((rc = sort_pass64(q, perm, hk, T, s, hmn, hmx))) return rc;
+        if ((rc = sort_pass32(q, perm, sk, T, s, smx))) return rc;
+    }
     // 5. per-sender capacity: keep the first max_cap of every sender run
     uint32_t* head = (uint32_t*)qbuf(q, MQ_HEAD, 4 * (size_t)T, &rc);
     uint8_t* keep = (uint8_t*)qbuf(q, MQ_KEEP, T, &rc);

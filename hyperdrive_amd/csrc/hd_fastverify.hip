@@ -1384,7 +1384,8 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         k_slow_lift<<<lift_blocks, 256, 0, s>>>(b, sc.slow, sc.count, d_verdict, d_rec32, d_signer, sc.slow2,
                                                 sc.count + 1, ctx->var[HD_VAR_WAVE_PRIO], f->est_dev);
         FBCHK(hipGetLastError(), "k_slow_lift");
-        const SlowCtl ctl{sc.slow2, sc.count + 1, f->adm_slot, f->state, f->pub, d_bitmap, f->est_dev + 1};
+        const SlowCtl ctl{sc.slow2, sc.count + 1, f->adm_slot, f->state, f->pub, d_bitmap, f->est_dev + 1,
+                          ctx->var[HD_VAR_WAVE_PRIO]};
         rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl,
                             fallback_blocks(f->est_host[1], full), s);
         if (rc) return rc;
@@ -1407,7 +1408,8 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         k_slow_lift<<<slow_blocks, 256, 0, s>>>(b, sc.slow, sc.count, d_verdict, d_rec32, d_signer, sc.slow2,
                                                 sc.count + 1, ctx->var[HD_VAR_WAVE_PRIO], nullptr);
         FBCHK(hipGetLastError(), "k_slow_lift");
-        const SlowCtl ctl{sc.slow2, sc.count + 1, f->adm_slot, f->state, f->pub, nullptr, nullptr};
+        const SlowCtl ctl{sc.slow2, sc.count + 1, f->adm_slot, f->state, f->pub, nullptr, nullptr,
+                          ctx->var[HD_VAR_WAVE_PRIO]};
         rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl, slow_blocks, s);
         if (rc) return rc;
         if (d_bitmap) {
@@ -1418,7 +1420,7 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
     }
     // no admitted set: every message takes the full recovery (it ends in
     // NOT_ADMITTED at best), nothing to learn
-    const SlowCtl none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    const SlowCtl none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
     return hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, none, blocks, s);
 }
 

@@ -87,6 +87,7 @@ struct SlowCtl {
     hd::ge* fb_pub;
     uint32_t* bitmap_or;      // list mode: set the valid bit of each VALID message (the rest already written)
     uint32_t* est_out;        // list mode: the list length is stored here (host-mapped; sizes later grids)
+    int prio;                 // wave issue priority (s_setprio 0..3; HD_VAR_WAVE_PRIO) of the list mode
 };
 int hd_launch_slow(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict, uint8_t* d_rec32,
                    int32_t* d_signer, uint32_t* d_bitmap, const SlowCtl& ctl, uint32_t blocks, hipStream_t s);

@@ -60,6 +60,10 @@ __global__ __launch_bounds__(256, WAVES) void k_verify(DevBatch b, const ge* __r
                                                 uint8_t* __restrict__ rec32, int32_t* __restrict__ signer,
                                                 uint32_t* __restrict__ bitmap, const uint8_t* __restrict__ digest_in,
                                                 SlowCtl ctl, const gp* __restrict__ fbg) {
+    // s_setprio takes an immediate: a uniform branch per level
+    if (ctl.prio == 1) __builtin_amdgcn_s_setprio(1);
+    else if (ctl.prio == 2) __builtin_amdgcn_s_setprio(2);
+    else if (ctl.prio >= 3) __builtin_amdgcn_s_setprio(3);
     const uint32_t stride = gridDim.x * blockDim.x;
     const uint32_t total = ctl.list ? *ctl.count : b.n;
     if (ctl.est_out && blockIdx.x == 0 && threadIdx.x == 0) ctl.est_out[0] = total;
@@ -338,7 +342,7 @@ int launch_verify(hd_ctx* ctx, const hd_batch* db, const uint8_t* d_digest, uint
     // than a resident-sized grid looping over the batch (measured on 1M:
     // 13.2 ms vs 13.5 ms at 2x resident blocks, 14.3 ms at 1x)
     const uint32_t blocks = (db->n + 255) / 256;
-    const SlowCtl none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    const SlowCtl none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
     const int rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_recovered32, d_signer, d_valid_bitmap, none, blocks, s);
     if (rc) return rc;
     hipError_t e = ctx->ev_slow ? hipSuccess : hipEventCreateWithFlags(&ctx->ev_slow, hipEventDisableTiming);

@@ -158,7 +158,8 @@ int hd_ctx_profile(hd_ctx* ctx, int enable);
 #define HD_VAR_KEY_WIDTH 7      /* per-key table windows: 0 by the table budget (default), 16 or 20; applies from
                                    the next hd_set_signatories [HD_FB_PW] */
 #define HD_VAR_WAVE_PRIO 8      /* wave issue priority (s_setprio 0..3) of the known-key check's short kernels
-                                   (prep, s / Z inversions, comparison, lift): above k_fast_sums' 0 they keep
+                                   (prep, s / Z inversions, comparison, lift, the leftovers' k_verify): above
+                                   k_fast_sums' 0 they keep
                                    their SIMD share while the next call's sums waves share the SIMD
                                    [HD_WAVE_PRIO] */
 #define HD_VAR_SUM_CAP 9        /* k_fast_sums residency: 0 as registers allow (3 waves per SIMD, default), 2 at

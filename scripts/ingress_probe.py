@@ -69,6 +69,13 @@ for rep in range(3):
         rec[f"verify_fallback_{t}"] = v.fastpath_stats()[1]
     ing.mq.drop_below(2 ** 62)
     _, rec["push_wire_x2"] = clock(lambda: [ing.push_wire(t, wire, sub.n, stream=ws) for t, sub, wire in parts])
+    for k in range(3):          # interleaved A/B of the fallback's wave priority (HD_VAR_WAVE_PRIO)
+        for prio in (0, 2):
+            v.set_variant("wave_prio", prio)
+            ing.mq.drop_below(2 ** 62)
+            _, rec[f"push_wires_prio{prio}_{k}"] = clock(
+                lambda: ing.push_wires([(t, wire, sub.n) for t, sub, wire in parts]))
+    v.set_variant("wave_prio", 0)
     ing.mq.drop_below(2 ** 62)
     _, rec["push_wires"] = clock(lambda: ing.push_wires([(t, wire, sub.n) for t, sub, wire in parts]))
     t0 = time.perf_counter()

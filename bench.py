@@ -636,30 +636,38 @@ def ingress_c5(v, keys, S, n, ws, dev, heights=64):
         parts.append((t, sub, marshal_device(v, t, sub, with_sig=True, stream=ws)))
     ing = Ingress(v, height=1, max_capacity=1000)
     ing.push_wires([(t, wire, sub.n) for t, sub, wire in parts])   # warm (allocations on both streams)
-    ing.votes.reset(1)
-    ing.mq.drop_below(2 ** 62)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    verdicts = ing.push_wires([(t, wire, sub.n) for t, sub, wire in parts])
-    torch.cuda.synchronize()                          # push_ms includes the device work it queued
-    t1 = time.perf_counter()
-    delivered = 0
-    for h in range(1, heights + 1):
-        if h > 1:
-            ing.reset_height(h)
-        delivered += len(ing.flush().consumed)
-    t2 = time.perf_counter()
+    reps = []
+    for rep in range(3):        # three timed cycles; the median one is reported
+        ing.height = 1
+        ing.votes.reset(1)
+        ing._clean = None
+        ing.mq.drop_below(2 ** 62)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        verdicts = ing.push_wires([(t, wire, sub.n) for t, sub, wire in parts])
+        torch.cuda.synchronize()                      # push_ms includes the device work it queued
+        t1 = time.perf_counter()
+        delivered = 0
+        for h in range(1, heights + 1):
+            if h > 1:
+                ing.reset_height(h)
+            delivered += len(ing.flush().consumed)
+        t2 = time.perf_counter()
+        reps.append((t2 - t0, t1 - t0, t2 - t1))
+    tot, push, flush = sorted(reps)[1]
     want = sum(int(((vd == 0) & (sub.height >= 1) & (sub.height <= heights)).sum())
                for vd, (_, sub, _) in zip(verdicts, parts))
-    vh = torch.bincount(torch.cat(verdicts).long(), minlength=8).cpu().tolist()
+    vh = torch.bincount(torch.cat(verdicts).long(), minlength=9).cpu().tolist()
     buffered = len(ing.mq)
     ing.close()
-    return {"messages": n, "push_ms": (t1 - t0) * 1e3, "push_msgs_per_s": n / (t1 - t0),
-            "flushes": heights, "flush_ms": (t2 - t1) * 1e3, "total_msgs_per_s": n / (t2 - t0),
+    return {"messages": n, "push_ms": push * 1e3, "push_msgs_per_s": n / push,
+            "flushes": heights, "flush_ms": flush * 1e3, "total_msgs_per_s": n / tot,
+            "reps_total_ms": [round(r[0] * 1e3, 3) for r in reps],
             "verdicts": vh, "delivered": delivered, "delivered_equals_valid_at_flushed_heights": delivered == want,
             "buffered_after": buffered,
             "note": "30 % adversarial C2 batch in random order (heights out of order), prevote and precommit wire "
-                    "buffers; wall time of the synchronous ingress calls"}
+                    "buffers; wall time of the synchronous ingress calls (authenticate -> filterHeight -> mq "
+                    "insert, then the flushes), median of 3 cycles"}
 
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured float4 copy)

@@ -588,6 +588,21 @@ __global__ __launch_bounds__(1024) void k_mq_consume1(uint32_t nsend, Pool p, ui
     if (t < nsend) {
         uint32_t lo = head[t], hi = send[t];
         h0 = lo;
+        // a flush per height cuts a few messages off each run's front: look at
+        // the first four at once (independent loads), search only past them
+        {
+            uint32_t c = 0;
+            bool past = false;
+            HD_UNROLL for (uint32_t j = 0; j < 4; j++) {
+                const bool in = lo + j < hi;
+                const int64_t hv = in ? p.h[lo + j] : 0;
+                const bool le = in && hv <= h;
+                c += (!past && le) ? 1u : 0u;
+                past = past || !le;
+            }
+            if (past) hi = lo + c;   // the cut is within the first four
+            lo += c;
+        }
         while (lo < hi) {   // first index with the height past the cut
             const uint32_t mid = lo + (hi - lo) / 2;
             if (p.h[mid] <= h) lo = mid + 1;

@@ -120,6 +120,17 @@ struct FbWork {
     int last_k = 8;               // messages per inversion of the last split check (split_k_for)
     double budget = 0;            // table bytes allowed (HD_FB_MAX_BYTES), shared per device
     size_t bytes = 0;             // table bytes this context holds
+    // Foreign keys (HD_VAR_FOREIGN_KEYS): fcap slots fbase .. reserved once
+    // (a contiguous block, kept across set changes) for authenticated Froms
+    // outside the admitted set; fdict maps such a From to its slot (emptied
+    // on every set change).  k_verify stores the claim count into fpend_host;
+    // a change since fseen makes the next call build the new tables.
+    uint32_t* fdict = nullptr;
+    uint32_t* fnext = nullptr;
+    uint32_t fbase = 0, fcap = 0;
+    uint32_t* fpend_host = nullptr;
+    uint32_t* fpend_dev = nullptr;
+    uint32_t fseen = 0;
 };
 
 namespace {
@@ -309,7 +320,7 @@ __global__ __launch_bounds__(256) void k_fast_prep(DevBatch b, const uint8_t* __
                                                    const uint32_t* __restrict__ state,
                                                    const int32_t* __restrict__ adm_slot,
                                                    const uint32_t* __restrict__ adm, uint32_t n_adm, int adm_steps,
-                                                   SplitRows rows, int adm_in_lds) {
+                                                   SplitRows rows, int adm_in_lds, const uint32_t* __restrict__ fdict) {
     extern __shared__ uint32_t sh_adm[];
     wave_prio(rows.prio);
     if (adm_in_lds) adm_stage(sh_adm, adm, n_adm);
@@ -326,7 +337,13 @@ __global__ __launch_bounds__(256) void k_fast_prep(DevBatch b, const uint8_t* __
         uint32_t from_be[8];
         src.from_words(from_be);
         idx = adm_in_lds ? admitted_find(sh_adm, n_adm, adm_steps, from_be) : admitted_find(adm, n_adm, adm_steps, from_be);
-        const int32_t sl = idx >= 0 ? adm_slot[idx] : -1;
+        int32_t sl = idx >= 0 ? adm_slot[idx] : -1;
+        if (idx < 0 && fdict) {
+            // an authenticated From outside the admitted set with a known key:
+            // the check's success means NOT_ADMITTED (idx -2 marks it)
+            sl = fdict_find(fdict, from_be);
+            if (sl >= 0) idx = -2;
+        }
         if (sl >= 0 && state[sl] == HD_FB_READY) {
             slot = (uint32_t)sl;
             FastIn in;
@@ -673,13 +690,14 @@ __global__ __launch_bounds__(256) void k_fast_cmp(DevBatch b, SplitRows rows, co
             // authentication only: From's key does not give R, so the
             // recovered key is not From's -- final, without the recovery
             if (auth && v == HD_NEEDS_SLOW) v = V_NOT_AUTHENTIC;
+            if (v == V_VALID && rows.idx[i] == -2) v = V_NOT_ADMITTED;   // a foreign key's check
         }
         if (v != HD_NEEDS_SLOW) {
             const bool ok = v == V_VALID;
             verdict[i] = v;
             if (rec32) {
                 uint32_t f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                if (ok) load_row32_be(f, b.from32, i);
+                if (ok || (v == V_NOT_ADMITTED && rows.idx[i] == -2)) load_row32_be(f, b.from32, i);
                 store_row32_be(rec32, i, f);
             }
             if (signer) signer[i] = ok ? adm_perm[rows.idx[i]] : -1;
@@ -890,12 +908,15 @@ __global__ __launch_bounds__(256) void k_fb_runs(const uint32_t* __restrict__ li
 }
 
 __global__ void k_fb_ready(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
-                           uint32_t* __restrict__ state, uint32_t* not_ready) {
+                           uint32_t* __restrict__ state, uint32_t* not_ready, uint32_t f0, uint32_t f1) {
     const uint32_t c = *count;
     for (uint32_t k = threadIdx.x; k < c; k += blockDim.x) state[list[k]] = HD_FB_READY;
     if (threadIdx.x == 0 && c && not_ready) {
+        // not_ready counts admitted slots: the foreign block [f0, f1) is not in it
+        uint32_t ca = 0;
+        for (uint32_t k = 0; k < c; k++) ca += (list[k] >= f0 && list[k] < f1) ? 0u : 1u;
         const uint32_t v = *(volatile uint32_t*)not_ready;
-        *(volatile uint32_t*)not_ready = v >= c ? v - c : 0u;
+        *(volatile uint32_t*)not_ready = v >= ca ? v - ca : 0u;
     }
 }
 
@@ -979,9 +1000,16 @@ size_t fb_run_scratch_bytes(const hd_ctx* ctx) { return (size_t)HD_FB_RUN * 9 * 
 
 // build the tables of every LEARNED slot, stream-ordered (nothing to launch
 // once every mapped key is READY)
+// a foreign key claimed since the last build (HD_VAR_FOREIGN_KEYS)
+static bool fb_foreign_pending(const FbWork* f) {
+    return f->fcap && f->fpend_host && *(volatile uint32_t*)f->fpend_host != f->fseen;
+}
+
 int fb_learn(hd_ctx* ctx, hipStream_t s) {
     FbWork* f = ctx->fb;
-    if (f->nr_host && *(volatile uint32_t*)f->nr_host == 0) return HD_OK;
+    const bool fnew = fb_foreign_pending(f);
+    if (f->nr_host && *(volatile uint32_t*)f->nr_host == 0 && !fnew) return HD_OK;
+    if (fnew) f->fseen = *(volatile uint32_t*)f->fpend_host;
     const uint32_t g = (uint32_t)std::max(ctx->n_cu, 1) * 4u;
     k_fb_list<<<1, 256, 0, s>>>(f->nslots, f->state, f->list, f->counts);
     if (f->wp == HD_FB_WW) {
@@ -991,7 +1019,7 @@ int fb_learn(hd_ctx* ctx, hipStream_t s) {
         k_fb_bases<HD_FB_W><<<g, 256, 0, s>>>(f->list, f->counts, f->pub, f->base);
         k_fb_runs<HD_FB_W><<<fb_run_blocks(ctx), 256, 0, s>>>(f->list, f->counts, f->base, f->tabs, f->zr);
     }
-    k_fb_ready<<<1, 256, 0, s>>>(f->list, f->counts, f->state, f->nr_dev);
+    k_fb_ready<<<1, 256, 0, s>>>(f->list, f->counts, f->state, f->nr_dev, f->fbase, f->fbase + f->fcap);
     FBCHK(hipGetLastError(), "fb table kernels");
     return HD_OK;
 }
@@ -1060,6 +1088,9 @@ int hd_fb_init(hd_ctx* ctx) {
     FBCHK(hipHostMalloc((void**)&f->est_host, 8, hipHostMallocMapped | hipHostMallocCoherent), "fb list estimate");
     f->est_host[0] = f->est_host[1] = 0xFFFFFFFFu;
     FBCHK(hipHostGetDevicePointer((void**)&f->est_dev, f->est_host, 0), "fb list estimate map");
+    FBCHK(hipHostMalloc((void**)&f->fpend_host, 4, hipHostMallocMapped | hipHostMallocCoherent), "fb foreign claims");
+    *f->fpend_host = 0;
+    FBCHK(hipHostGetDevicePointer((void**)&f->fpend_dev, f->fpend_host, 0), "fb foreign claims map");
     int rc = fb_alloc_slots(ctx);
     if (rc) return rc;
     return fb_g_table(ctx, &f->gtab);
@@ -1080,11 +1111,12 @@ void hd_fb_release(hd_ctx* ctx) {
         for (void* p : sp)
             if (p) (void)hipFree(p);
     }
-    void* ptrs[] = {f->counts, f->adm_slot, f->zr};
+    void* ptrs[] = {f->counts, f->adm_slot, f->zr, f->fdict, f->fnext};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (f->nr_host) (void)hipHostFree(f->nr_host);
     if (f->est_host) (void)hipHostFree(f->est_host);
+    if (f->fpend_host) (void)hipHostFree(f->fpend_host);
     delete f;
     ctx->fb = nullptr;
 }
@@ -1146,6 +1178,7 @@ int hd_fb_map_signatories(hd_ctx* ctx, const uint8_t* sorted, uint32_t m) {
         f->slot_of.clear();
         f->free_slots.clear();
         f->used = 1;
+        f->fcap = 0;   // the foreign block goes with the tables
         f->wp = wp;
         f->max_slots = (uint32_t)std::max(1.0, std::min(1e6, f->budget / fb_slot_bytes(wp)));
         int ra = fb_alloc_slots(ctx);
@@ -1184,10 +1217,28 @@ int hd_fb_map_signatories(hd_ctx* ctx, const uint8_t* sorted, uint32_t m) {
         f->slot_of.emplace(std::string(reinterpret_cast<const char*>(sorted + 32 * (size_t)k), 32), slot);
         fresh.push_back(slot);
     }
+    // foreign keys: a block of slots reserved once, after the admitted ones
+    // of the first set that asks for it; emptied (dictionary and states) on
+    // every set change -- a From that leaves or joins the set is learned again
+    const uint32_t want = (uint32_t)std::max(0, ctx->var[HD_VAR_FOREIGN_KEYS]);
+    if (want && !f->fcap && f->used + want <= f->max_slots) {
+        f->fbase = f->used;
+        f->fcap = want;
+        f->used += want;
+    }
     int rc = fb_grow_slots(ctx, f->used);
     if (rc) return rc;
     hipStream_t s = ctx->stream;
     for (uint32_t slot : fresh) FBCHK(hipMemsetAsync(f->state + slot, 0, 4, s), "fb slot reset");
+    if (f->fcap) {
+        if (!f->fdict) FBCHK(hipMalloc(&f->fdict, 4 * (size_t)HD_FD_WORDS), "fb foreign dictionary");
+        if (!f->fnext) FBCHK(hipMalloc(&f->fnext, 4), "fb foreign count");
+        FBCHK(hipMemsetAsync(f->fdict, 0, 4 * (size_t)HD_FD_WORDS, s), "fb foreign reset");
+        FBCHK(hipMemsetAsync(f->fnext, 0, 4, s), "fb foreign reset");
+        FBCHK(hipMemsetAsync(f->state + f->fbase, 0, 4 * (size_t)f->fcap, s), "fb foreign reset");
+        *(volatile uint32_t*)f->fpend_host = 0;
+        f->fseen = 0;
+    }
     rc = hd_dev_grow(ctx, (void**)&f->adm_slot, &f->cap_adm_slot, 4 * adm_slot.size());
     if (rc) return rc;
     FBCHK(hipMemcpyAsync(f->adm_slot, adm_slot.data(), 4 * adm_slot.size(), hipMemcpyHostToDevice, s), "fb adm_slot");
@@ -1200,7 +1251,15 @@ int hd_fb_clear_keys(hd_ctx* ctx) {
     int rq = hd_ctx_quiesce(ctx);
     if (rq) return rq;
     if (f->nslots > 1) FBCHK(hipMemsetAsync(f->state + 1, 0, 4 * (size_t)(f->nslots - 1), ctx->stream), "fb clear");
+    if (f->fcap && f->fdict) {   // the foreign keys are learned again too
+        FBCHK(hipMemsetAsync(f->fdict, 0, 4 * (size_t)HD_FD_WORDS, ctx->stream), "fb clear");
+        FBCHK(hipMemsetAsync(f->fnext, 0, 4, ctx->stream), "fb clear");
+    }
     FBCHK(hipStreamSynchronize(ctx->stream), "fb clear");
+    if (f->fcap) {
+        *(volatile uint32_t*)f->fpend_host = 0;
+        f->fseen = 0;
+    }
     return fb_count_not_ready(ctx);
 }
 
@@ -1276,7 +1335,7 @@ static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest
     const uint32_t tb = (T + 255) / 256, nb = (n + 255) / 256;
     const size_t adm_lds = adm_lds_bytes(ctx->n_adm);
     k_fast_prep<<<nb, 256, adm_lds, s>>>(b, d_digest, f->state, f->adm_slot, ctx->d_adm, ctx->n_adm, ctx->adm_steps,
-                                         rows, adm_lds > 0);
+                                         rows, adm_lds > 0, f->fcap ? f->fdict : nullptr);
     k_fast_sinv<K><<<tb, 256, 0, s>>>(n, T, rows);
     const bool dl = sums_digits_lds(ctx);
     if (!dl) k_fast_digits<WP><<<nb, 256, 0, s>>>(n, rows);
@@ -1306,7 +1365,7 @@ int hd_fb_verify(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_
     if (!sc.count) FBCHK(hipMalloc(&sc.count, 8), "fb scratch count");
     // see FbWork: in the steady state only this set's previous user orders
     // this call; otherwise the previous call does, on whatever stream
-    const bool steady = f->nr_host && *(volatile uint32_t*)f->nr_host == 0;
+    const bool steady = f->nr_host && *(volatile uint32_t*)f->nr_host == 0 && !fb_foreign_pending(f);
     if (sc.used && sc.stream != s) FBCHK(hipStreamWaitEvent(s, sc.done, 0), "fb scratch order");
     if (f->any && f->last != s && !(steady && f->steady)) FBCHK(hipStreamWaitEvent(s, f->done, 0), "fb stream order");
     hipEvent_t* pe = fb_prof_pair(f->ev_call, f->n_call, f->prof);
@@ -1385,7 +1444,8 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
                                                 sc.count + 1, ctx->var[HD_VAR_WAVE_PRIO], f->est_dev);
         FBCHK(hipGetLastError(), "k_slow_lift");
         const SlowCtl ctl{sc.slow2, sc.count + 1, f->adm_slot, f->state, f->pub, d_bitmap, f->est_dev + 1,
-                          ctx->var[HD_VAR_WAVE_PRIO]};
+                          ctx->var[HD_VAR_WAVE_PRIO], f->fcap ? f->fdict : nullptr, f->fnext, f->fbase, f->fcap,
+                          f->fpend_dev};
         rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl,
                             fallback_blocks(f->est_host[1], full), s);
         if (rc) return rc;
@@ -1409,7 +1469,7 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
                                                 sc.count + 1, ctx->var[HD_VAR_WAVE_PRIO], nullptr);
         FBCHK(hipGetLastError(), "k_slow_lift");
         const SlowCtl ctl{sc.slow2, sc.count + 1, f->adm_slot, f->state, f->pub, nullptr, nullptr,
-                          ctx->var[HD_VAR_WAVE_PRIO]};
+                          ctx->var[HD_VAR_WAVE_PRIO], nullptr, nullptr, 0, 0, nullptr};
         rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl, slow_blocks, s);
         if (rc) return rc;
         if (d_bitmap) {
@@ -1420,7 +1480,7 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
     }
     // no admitted set: every message takes the full recovery (it ends in
     // NOT_ADMITTED at best), nothing to learn
-    const SlowCtl none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+    const SlowCtl none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, 0, 0, nullptr};
     return hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, none, blocks, s);
 }
 
@@ -1504,7 +1564,8 @@ int hd_ctx_fastpath_stats(hd_ctx* ctx, uint32_t* known_keys, uint32_t* last_fall
     if (known_keys && f->nslots > 1) {
         std::vector<uint32_t> st(f->nslots);
         FBCHK(hipMemcpy(st.data(), f->state, 4 * (size_t)f->nslots, hipMemcpyDeviceToHost), "state read");
-        for (uint32_t k = 1; k < f->nslots; k++) *known_keys += st[k] == HD_FB_READY;
+        for (uint32_t k = 1; k < f->nslots; k++)   // admitted keys (not the foreign block)
+            *known_keys += st[k] == HD_FB_READY && !(k >= f->fbase && k < f->fbase + f->fcap);
     }
     if (last_fallback && f->last_set >= 0)
         FBCHK(hipMemcpy(last_fallback, f->sc[f->last_set].count, 4, hipMemcpyDeviceToHost), "fallback read");

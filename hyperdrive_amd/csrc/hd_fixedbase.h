@@ -54,6 +54,33 @@ struct FbL {
 #define HD_FB_TAB (FbL<HD_FB_W>::TAB)
 #define HD_NEEDS_SLOW 0xFEu
 
+// The foreign-key dictionary (HD_VAR_FOREIGN_KEYS): Froms outside the
+// admitted set whose key a NOT_ADMITTED recovery has shown, each with a table
+// slot.  HD_FD_BUCKETS buckets, linear probing over at most 8: words
+// [0, B) claim (0 empty, 1 being written, 2 written), [B, 2B) slot (or
+// 0xFFFFFFFF: no slot was left), then 8 big-endian From words per bucket.
+#define HD_FD_BUCKETS 128u
+#define HD_FD_WORDS (10u * HD_FD_BUCKETS)
+HD uint32_t fdict_bucket(const uint32_t w[8]) {
+    return (w[0] ^ (w[3] * 0x9E3779B1u) ^ (w[7] * 0x85EBCA77u)) & (HD_FD_BUCKETS - 1u);
+}
+// slot of a known foreign From, or -1
+HD int32_t fdict_find(const uint32_t* fd, const uint32_t from_be[8]) {
+    uint32_t b = fdict_bucket(from_be);
+    for (int p = 0; p < 8; p++, b = (b + 1u) & (HD_FD_BUCKETS - 1u)) {
+        const uint32_t c = fd[b];
+        if (c == 0u) return -1;
+        if (c != 2u) continue;
+        uint32_t diff = 0;
+        HD_UNROLL for (int w = 0; w < 8; w++) diff |= fd[2u * HD_FD_BUCKETS + 8u * b + w] ^ from_be[w];
+        if (!diff) {
+            const uint32_t s = fd[HD_FD_BUCKETS + b];
+            return s == 0xFFFFFFFFu ? -1 : (int32_t)s;
+        }
+    }
+    return -1;
+}
+
 // slot states of the per-signatory tables (device memory, hd_fastverify.hip)
 #define HD_FB_EMPTY 0u     // no key known
 #define HD_FB_CLAIMED 1u   // a recovering lane is writing the key

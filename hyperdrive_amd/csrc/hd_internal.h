@@ -36,7 +36,7 @@ struct hd_ctx {
     int device = 0;
     int n_cu = 256;
     int verify_waves = 3;   // register budget of k_verify (waves per SIMD)
-    int var[HD_VAR__COUNT] = {3, 0, 1, 0, -1, 0, 2, 0, 0, 0};   // hd_ctx_set_variant (var[0] mirrors verify_waves)
+    int var[HD_VAR__COUNT] = {3, 0, 1, 0, -1, 0, 2, 0, 0, 0, 16};   // hd_ctx_set_variant (var[0] mirrors verify_waves)
     hipStream_t stream = nullptr;
     int pkfmt = HD_PUBKEY_COMPRESSED;   // id.NewSignatory's pubkey encoding (hd_ctx_set_pubkey_format)
     hd::ge* d_gtab = nullptr;
@@ -88,6 +88,12 @@ struct SlowCtl {
     uint32_t* bitmap_or;      // list mode: set the valid bit of each VALID message (the rest already written)
     uint32_t* est_out;        // list mode: the list length is stored here (host-mapped; sizes later grids)
     int prio;                 // wave issue priority (s_setprio 0..3; HD_VAR_WAVE_PRIO) of the list mode
+    // foreign keys (HD_VAR_FOREIGN_KEYS): a NOT_ADMITTED recovery publishes
+    // its key into one of the fcap reserved slots fbase .. (fdict: hd_fixedbase.h)
+    uint32_t* fdict;
+    uint32_t* fnext;
+    uint32_t fbase, fcap;
+    uint32_t* fpend;          // host-mapped: the claim count, so the host builds the new tables
 };
 int hd_launch_slow(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict, uint8_t* d_rec32,
                    int32_t* d_signer, uint32_t* d_bitmap, const SlowCtl& ctl, uint32_t blocks, hipStream_t s);

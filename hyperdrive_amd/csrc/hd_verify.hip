@@ -49,6 +49,38 @@ struct DevSrc {
     __device__ __forceinline__ uint32_t digest(int w) const { return load_be32(dg + 32 * (size_t)i + 4 * w); }
 };
 
+// A NOT_ADMITTED recovery's key into the foreign-key dictionary (once per
+// From; a bucket another lane is writing is left alone -- learning is only an
+// optimisation) and, while reserved slots last, into its own table slot.
+__device__ void fdict_learn(const SlowCtl& ctl, const uint32_t from_be[8], const ge& q) {
+    uint32_t* fd = ctl.fdict;
+    uint32_t b = fdict_bucket(from_be);
+    for (int p = 0; p < 8; p++, b = (b + 1u) & (HD_FD_BUCKETS - 1u)) {
+        const uint32_t c = atomicCAS(&fd[b], 0u, 1u);
+        if (c == 0u) {
+            const uint32_t j = atomicAdd(ctl.fnext, 1u);
+            uint32_t slot = 0xFFFFFFFFu;
+            if (j < ctl.fcap) {
+                slot = ctl.fbase + j;
+                ctl.fb_pub[slot] = q;
+                __threadfence();
+                atomicExch(&ctl.fb_state[slot], HD_FB_LEARNED);
+            }
+            HD_UNROLL for (int w = 0; w < 8; w++) fd[2u * HD_FD_BUCKETS + 8u * b + w] = from_be[w];
+            fd[HD_FD_BUCKETS + b] = slot;
+            __threadfence();
+            atomicExch(&fd[b], 2u);
+            if (slot != 0xFFFFFFFFu)
+                __hip_atomic_store(ctl.fpend, j + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+        if (c != 2u) return;
+        uint32_t diff = 0;
+        HD_UNROLL for (int w = 0; w < 8; w++) diff |= fd[2u * HD_FD_BUCKETS + 8u * b + w] ^ from_be[w];
+        if (!diff) return;
+    }
+}
+
 // With ctl.list, lane p verifies message ctl.list[p] for p < *ctl.count (the
 // known-key fast path's leftovers); with ctl.adm_slot, a VALID message whose
 // signatory has no known key yet publishes its recovered key to the
@@ -85,6 +117,11 @@ __global__ __launch_bounds__(256, WAVES) void k_verify(DevBatch b, const ge* __r
             }
             if (signer) signer[i] = s >= 0 ? adm_perm[s] : -1;
             if (ctl.bitmap_or && v == V_VALID) atomicOr(&ctl.bitmap_or[i >> 5], 1u << (i & 31));
+            if (ctl.fdict && v == V_NOT_ADMITTED) {
+                uint32_t from_be[8];
+                HD_UNROLL for (int w = 0; w < 8; w++) from_be[w] = src.from(w);
+                fdict_learn(ctl, from_be, q);
+            }
             if (ctl.adm_slot && v == V_VALID) {
                 const int32_t slot = ctl.adm_slot[s];
                 if (slot >= 0 && ctl.fb_state[slot] == HD_FB_EMPTY &&
@@ -167,6 +204,7 @@ int hd_ctx_create(int device, hd_ctx** out) {
         {HD_VAR_SUM_PREFETCH, "HD_SUM_PF"},       {HD_VAR_SPLIT_K, "HD_FAST_K"},
         {HD_VAR_FAST_WAVES, "HD_FAST_WAVES"},     {HD_VAR_KEY_WIDTH, "HD_FB_PW"},
         {HD_VAR_WAVE_PRIO, "HD_WAVE_PRIO"},       {HD_VAR_SUM_CAP, "HD_SUM_CAP"},
+        {HD_VAR_FOREIGN_KEYS, "HD_FOREIGN_KEYS"},
     };
     for (auto& ev : envs)
         if (const char* e = getenv(ev.env)) (void)hd_ctx_set_variant(ctx, ev.key, atoi(e));
@@ -228,6 +266,7 @@ int hd_ctx_set_variant(hd_ctx* ctx, int which, int value) {
         case HD_VAR_KEY_WIDTH: ok = value == 0 || value == HD_FB_W || value == HD_FB_WW; break;
         case HD_VAR_WAVE_PRIO: ok = value >= 0 && value <= 3; break;
         case HD_VAR_SUM_CAP: ok = value == 0 || value == 2; break;
+        case HD_VAR_FOREIGN_KEYS: ok = value >= 0 && value <= 64; break;
     }
     if (!ok) return HD_EINVAL;
     ctx->var[which] = value;
@@ -342,7 +381,7 @@ int launch_verify(hd_ctx* ctx, const hd_batch* db, const uint8_t* d_digest, uint
     // than a resident-sized grid looping over the batch (measured on 1M:
     // 13.2 ms vs 13.5 ms at 2x resident blocks, 14.3 ms at 1x)
     const uint32_t blocks = (db->n + 255) / 256;
-    const SlowCtl none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+    const SlowCtl none{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, 0, 0, nullptr};
     const int rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_recovered32, d_signer, d_valid_bitmap, none, blocks, s);
     if (rc) return rc;
     hipError_t e = ctx->ev_slow ? hipSuccess : hipEventCreateWithFlags(&ctx->ev_slow, hipEventDisableTiming);

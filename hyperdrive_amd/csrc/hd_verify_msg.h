@@ -118,13 +118,13 @@ HD uint8_t verify_msg_src(const Src& src, GTab gtab, AdmTab adm, uint32_t n_adm,
         diff |= rec_be[i] ^ from_be[i];
     }
     if (diff) return V_SIGNATORY_MISMATCH;
-    int32_t idx = admitted_find(adm, n_adm, adm_steps, from_be);
-    if (idx < 0) return V_NOT_ADMITTED;
-    signer = idx;
-    if (qout) {  // the recovered key, for the known-key tables (hd_fixedbase.h)
+    if (qout) {  // the recovered key (== From's), for the known-key tables (hd_fixedbase.h)
         qout->x = qx;
         qout->y = qy;
     }
+    int32_t idx = admitted_find(adm, n_adm, adm_steps, from_be);
+    if (idx < 0) return V_NOT_ADMITTED;
+    signer = idx;
     return V_VALID;
 }
 

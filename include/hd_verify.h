@@ -166,7 +166,13 @@ int hd_ctx_profile(hd_ctx* ctx, int enable);
                                    most 2 blocks per CU (2 waves per SIMD, by an LDS reservation), leaving a
                                    slot per SIMD to the short kernels of a concurrent call and the tally
                                    [HD_SUM_CAP] */
-#define HD_VAR__COUNT 10
+#define HD_VAR_FOREIGN_KEYS 10  /* table slots (0..64) reserved for authenticated Froms outside the admitted set:
+                                   a NOT_ADMITTED recovery teaches the context its key, and later messages of
+                                   that From take the known-key check (verdict NOT_ADMITTED, identical to the
+                                   recovery's); applies from the next hd_set_signatories (reserved once per
+                                   context, when the table budget allows); 16 (default), 0 = off
+                                   [HD_FOREIGN_KEYS] */
+#define HD_VAR__COUNT 11
 int hd_ctx_set_variant(hd_ctx* ctx, int which, int value);
 int hd_ctx_get_variant(hd_ctx* ctx, int which, int* value);
 int hd_ctx_profile_read(hd_ctx* ctx, uint32_t* calls, double* verify_ms, uint32_t* sums_launches, double* sums_ms);

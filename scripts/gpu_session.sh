@@ -45,6 +45,8 @@ for step in "$@"; do
     abcap) AB_VARS="sum_cap=0,2;wave_prio=0,3" AB_STREAMS=1,2 run ab_cap 900 python -u scripts/ab_prio.py ;;
     trace_cap) HD_SUM_CAP=2 HD_WAVE_PRIO=3 run trace_cap 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_cap -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub ;;
     auth) run pytest_auth 600 python -u -m pytest tests/test_gpu_verify.py tests/test_golden.py tests/test_ingress.py tests/test_c1_network.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "authenticate or ingress or c1" ;;
+    foreign) run pytest_foreign 600 python -u -m pytest tests/test_gpu_verify.py tests/test_golden.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "foreign or authenticate or adversarial or burst or matches_golden" ;;
+    ingress_fk) HD_FOREIGN_KEYS=16 run ingress_probe_fk 300 python -u scripts/ingress_probe.py ;;
     flushprobe) run flush_probe 300 python -u scripts/flush_probe.py ;;
     ingress) run ingress_probe 300 python -u scripts/ingress_probe.py ;;
     ingress_trace) run ingress_trace 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ingress_trace -o run -- python3 scripts/ingress_probe.py ;;

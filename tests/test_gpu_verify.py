@@ -199,6 +199,58 @@ def test_authenticate_vs_c_oracle(gpu, coracle):
         v.close()
 
 
+def test_foreign_keys_vs_c_oracle(gpu, coracle):
+    """HD_VAR_FOREIGN_KEYS: the 30 % adversarial mix's authenticated senders
+    outside the admitted set (16 foreign keys) are learned from their
+    NOT_ADMITTED recoveries; once their tables are built their messages take
+    the known-key check.  Every pass equals the C oracle (verdicts and
+    recovered signatories, NOT_ADMITTED included), the fallback list shrinks by
+    the foreign share, and authenticate_batch_device then needs no full
+    recovery for them either."""
+    import torch
+    from hyperdrive_amd.device import generate, work_stream
+    N, S = 65536, 100
+    v = gpu.Verifier(0)
+    try:
+        v.set_variant("foreign_keys", 16)
+        ks = v.gen_keys(S)
+        v.set_signatories(ks[0])
+        db, _, _ = generate(v, 0, N, S, 30, keys=ks)
+        hb = db.to_host()
+        cv, crec = coracle.verify(hb, ks[0], True, threads=16)
+        fallback = []
+        for rnd in range(4):
+            res = v.verify_batch(hb)
+            assert res.verdict.tolist() == cv.tolist(), rnd
+            assert res.recovered.tobytes() == crec.tobytes(), rnd
+            bits = np.unpackbits(res.valid_bitmap.view(np.uint8), bitorder="little")[:N]
+            assert bits.tolist() == (cv == 0).astype(int).tolist()
+            fallback.append(v.fastpath_stats()[1])
+        n_foreign = int((cv == 6).sum())
+        assert n_foreign > 1000
+        # the same batch on a context without foreign keys: its steady fallback
+        # includes every NOT_ADMITTED message, this one's none of them
+        v0 = gpu.Verifier(0)
+        try:
+            v0.set_signatories(ks[0])
+            for _ in range(2):
+                v0.verify_batch(hb)
+            base = v0.fastpath_stats()[1]
+        finally:
+            v0.close()
+        assert all(f <= base - n_foreign + 5 for f in fallback[1:]), (fallback, base, n_foreign)
+        ws = work_stream()
+        out = torch.empty(N, dtype=torch.uint8, device="cuda")
+        v.authenticate_batch_device(db.c_struct(), out.data_ptr(), ws.cuda_stream)
+        ws.synchronize()
+        va = out.cpu().numpy()
+        auth = np.isin(cv, (0, 6))
+        assert (va[auth] == cv[auth]).all() and not np.isin(va[~auth], (0, 6)).any()
+        assert v.fastpath_stats()[1] <= 5          # nothing left for the full recovery
+    finally:
+        v.close()
+
+
 def test_fallback_burst_after_clean_batches(gpu, coracle):
     """The fallback kernels (k_slow_lift, k_verify over the leftover list) size
     their grids by the latest list length seen (hd_fastverify.hip

@@ -170,7 +170,7 @@ int hd_ctx_profile(hd_ctx* ctx, int enable);
                                    a NOT_ADMITTED recovery teaches the context its key, and later messages of
                                    that From take the known-key check (verdict NOT_ADMITTED, identical to the
                                    recovery's); applies from the next hd_set_signatories (reserved once per
-                                   context, when the table budget allows); 16 (default), 0 = off
+                                   context, when the table budget allows); 0 = off (default), 16 = the measured setting
                                    [HD_FOREIGN_KEYS] */
 #define HD_VAR__COUNT 11
 int hd_ctx_set_variant(hd_ctx* ctx, int which, int value);

@@ -44,22 +44,25 @@ W_OPS_PER_MSG = 6.06e5          # algorithmic int32 ops per Prevo
 # the known-key check R == s^-1 (m G + r P) that VALID messages of known
 # signatories take, for the geometry the context reports
 # (hd_ctx_fastpath_geometry): one table point per window, the first loaded and
-# the rest mixed additions (8M + 3S = 11 M each); s^-1 mod n (296 M, as
-# SURVEY's r^-1) and Z^-1 mod p (274 M) once per `per_inv` messages;
-# Montgomery's trick (3 M per message and kind), u1 and u2 (2 M), the affine
-# comparison (1S + 3M); one SHA-256 compression (2,200 ops).
+# the rest mixed additions in XYZZ coordinates (8M + 2S = 10 M each, round 4;
+# 8M + 3S = 11 M in Jacobian before); s^-1 mod n (296 M, as SURVEY's r^-1) and
+# the inverse of ZZ ZZZ mod p (274 M) once per `per_inv` messages; Montgomery's
+# trick (3 M per message and kind), u1 and u2 (2 M), the affine form (3 M) and
+# comparison (2 M); one SHA-256 compression (2,200 ops).
 M_OPS = 160
+M_PER_ADD = 10                  # an XYZZ mixed addition, 8M + 2S (hd_fixedbase.h gxz_add_ge_nx)
 
 
 def fast_ops_per_msg(g_windows, key_windows, per_inv):
     adds = g_windows + key_windows - 1
-    return (adds * 11 + (296 + 274) / per_inv + 2 * 3 + 2 + 4) * M_OPS + 2200
+    return (adds * M_PER_ADD + (296 + 274) / per_inv + 2 * 3 + 2 + 5) * M_OPS + 2200
 
 
 def sums_ops_per_msg(g_windows, key_windows):
-    """k_fast_sums alone: the mixed additions, 11 M each, and (from round 2b)
-    its prologue's u1 = m / s and u2 = r / s, 2 M."""
-    return ((g_windows + key_windows - 1) * 11 + 2) * M_OPS
+    """k_fast_sums alone: the mixed additions, 10 M each, its prologue's
+    u1 = m / s and u2 = r / s, 2 M, and the stored form (X ZZZ, Y ZZ, ZZ ZZZ),
+    3 M."""
+    return ((g_windows + key_windows - 1) * M_PER_ADD + 2 + 3) * M_OPS
 
 
 BYTES_PER_MSG = 146 + 33        # SURVEY §8(d): HBM in + out per message
@@ -105,6 +108,15 @@ def cpu_baseline(args, S):
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
     from oracle_c import COracle
     return COracle(os.path.join(ROOT, "oracle", "_build", "liboracle.so"))
+
+
+def glv_port():
+    """The 'port-glv' CPU baseline (oracle/glv_port.cpp; the baseline leg only)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    from oracle_c import GlvPort
+    return GlvPort(os.path.join(ROOT, "oracle", "_build", "libglvport.so"))
 
 
 class Pipeline:
@@ -409,7 +421,7 @@ def main():
                 "kernel_ms": sums_avg,
                 "launches_timed": sums_launches,
                 "algorithmic_ops_per_msg": w_sums,
-                "ops_model": "((g_windows + key_windows - 1) mixed additions x 11 M + u1, u2 2 M) x 160 int32 ops "
+                "ops_model": "((g_windows + key_windows - 1) XYZZ mixed additions x 10 M + u1, u2 2 M + the stored form 3 M) x 160 int32 ops "
                              "(SURVEY §8(d) M); messages per launch = batch - fallback",
                 "verify_call": {
                     "ms": call_avg,
@@ -495,8 +507,9 @@ def sub_benchmarks(args, v, sigs, foreign, dev, ws, ts):
     p5 = Pipeline(v, db5, B, 0, 0, 1, None, ws, ts)
     p5.run(2)
     el = timed(p5, args.sub_steps, None, dev)
-    vd, _, _ = p5.last(args.sub_steps)
-    out["C5_adversarial_30pct"] = {"messages": B, "msgs_per_s": B * args.sub_steps / el,
+    vd, rec5, _ = p5.last(args.sub_steps)
+    out["C5_adversarial_30pct"] = {"oracle_sample_check": oracle_sample_check(db5, vd, rec5, sigs),
+                                   "messages": B, "msgs_per_s": B * args.sub_steps / el,
                                    "ms_per_step": el / args.sub_steps * 1e3,
                                    "verdicts": torch.bincount(vd.long(), minlength=8).cpu().tolist(),
                                    "fallback_msgs": v.fastpath_stats()[1], "tally": p5.tally_info}
@@ -549,8 +562,9 @@ def sub_benchmarks(args, v, sigs, foreign, dev, ws, ts):
     cold3 = time.perf_counter() - t0
     p3.run(2)
     el = timed(p3, args.sub_steps, None, dev)
-    vd, _, _ = p3.last(args.sub_steps)
+    vd, rec3, _ = p3.last(args.sub_steps)
     out["C3_1000_signatories_64_rounds"] = {
+        "oracle_sample_check": oracle_sample_check(db3, vd, rec3, k3[0]),
         "messages": n3p, "msgs_per_s": n3p * args.sub_steps / el, "ms_per_step": el / args.sub_steps * 1e3,
         "verdicts": torch.bincount(vd.long(), minlength=8).cpu().tolist(), "fallback_msgs": v3.fastpath_stats()[1],
         "known_signatories": v3.fastpath_stats()[0], "key_windows": v3.fastpath_geometry()[1],
@@ -560,7 +574,7 @@ def sub_benchmarks(args, v, sigs, foreign, dev, ws, ts):
     return out
 
 
-def host_buffers(v, args, sigs, foreign, dev, steps=8):
+def host_buffers(v, args, sigs, foreign, dev, steps=12):
     """The cgo caller's path (replica.go:156-181 hands over host messages):
     the C2 batch in host memory through hd_verify_submit / hd_verify_wait,
     two tickets in flight, so batch k+1's upload runs under batch k's
@@ -570,41 +584,59 @@ def host_buffers(v, args, sigs, foreign, dev, steps=8):
     import numpy as np
     import torch
     from hyperdrive_amd.device import generate
-    from hyperdrive_amd.verify import Batch
+    from hyperdrive_amd.verify import Batch, CompactBatch
     B = args.batch
+    INFLIGHT = 3    # tickets queued (the library keeps HD_HOST_SLOTS = 4 pipelines)
     db, _, _ = generate(v, 0, B, args.signers, 0, keys=(sigs, foreign), device=str(dev))
     hb = db.to_host()
+    if np.isin(hb.type, (2, 3)).all():
+        hb.valid_round = None   # votes only: a cgo caller passes no valid_round column (-1 = InvalidRound)
     keep = []
 
     def pinned(a):
         t = torch.empty(a.shape, dtype={np.uint8: torch.uint8, np.int64: torch.int64,
-                                         np.uint32: torch.int32}[a.dtype.type], pin_memory=True)
+                                         np.uint16: torch.int16, np.uint32: torch.int32}[a.dtype.type], pin_memory=True)
         keep.append(t)
         o = t.numpy().view(a.dtype)
         o[...] = a
         return o
 
     res = {}
-    for name, mk in (("pinned", pinned), ("pageable", lambda a: a.copy())):
-        src = Batch(*(mk(a) for a in (hb.type, hb.height, hb.round, hb.valid_round, hb.value, hb.frm, hb.sig)))
+    cb = CompactBatch.from_batch(hb, sigs)
+    for name, mk in (("pinned", pinned), ("pageable", lambda a: a.copy()), ("compact_pinned", pinned),
+                     ("compact_pageable", lambda a: a.copy())):
+        compact = name.startswith("compact")
+        if compact:
+            src = CompactBatch(*(mk(a) if a is not None else None for a in
+                                 (cb.type, cb.height, cb.round, cb.valid_round, cb.from_idx, cb.value_idx, cb.sig,
+                                  cb.escape, cb.values)))
+            submit = v.submit_compact
+            up = 86 * B + 32 * (len(cb.escape) + len(cb.values))
+        else:
+            src = Batch(*(mk(a) if a is not None else None for a in
+                          (hb.type, hb.height, hb.round, hb.valid_round, hb.value, hb.frm, hb.sig)))
+            submit = v.submit
+            up = 146 * B
         outs = [(mk(np.zeros(B, np.uint8)), mk(np.zeros((B, 32), np.uint8)),
-                 mk(np.zeros((B + 31) // 32, np.uint32))) for _ in range(2)]
-        for k in range(2):                               # warm: staging and device buffers
-            v.wait(v.submit(src, *outs[k % 2]))
+                 mk(np.zeros((B + 31) // 32, np.uint32))) for _ in range(INFLIGHT)]
+        for k in range(INFLIGHT):                        # warm: staging and device buffers
+            v.wait(submit(src, *outs[k % INFLIGHT]))
         t0 = time.perf_counter()
-        prev = None
+        pending = []
         for k in range(steps):
-            t = v.submit(src, *outs[k % 2])
-            if prev is not None:
-                v.wait(prev)
-            prev = t
-        v.wait(prev)
+            pending.append(submit(src, *outs[k % INFLIGHT]))
+            if len(pending) == INFLIGHT:              # at most INFLIGHT tickets queued
+                v.wait(pending.pop(0))
+        for t in pending:
+            v.wait(t)
         dt = time.perf_counter() - t0
         ok = bool((outs[0][0] == 0).all() and (outs[0][1] == hb.frm).all())
         res[name] = {"msgs_per_s": B * steps / dt, "ms_per_batch": dt / steps * 1e3,
-                     "h2d_GBs": B * 146 * steps / dt / 1e9, "outputs_ok": ok}
-    res.update({"messages": B, "batches": steps, "in_flight": 2,
-                "note": "PCIe-inclusive: 146 B up and 33 B + bitmap down per message; bounded by the host link, "
+                     "h2d_bytes_per_batch": up, "h2d_GBs": up * steps / dt / 1e9, "outputs_ok": ok}
+    res.update({"messages": B, "batches": steps, "in_flight": INFLIGHT, "compact_values": len(cb.values),
+                "compact_escape_rows": len(cb.escape),
+                "note": "PCIe-inclusive: 146 B up (compact form: 86 B, From and value as 16-bit indices, "
+                        "hd_verify_submit_compact) and 33 B + bitmap down per message; bounded by the host link, "
                         "not by the kernels"})
     return res
 
@@ -926,7 +958,28 @@ def run_cpu_baseline(args, v, db, sigs, gpu_verdict, gpu_recovered):
     exact_tally = c_counts == gt.count and c_any == gt.distinct_any
     figures.setdefault("all_threads", figures["per_gpu_share"])
     best = max(figures.values(), key=lambda fig: fig["msgs_per_s"])
-    return {"value": best["msgs_per_s"], "unit": "msgs/s", "cores": best["threads"], "kind": "port",
+    # the GLV port (oracle/glv_port.cpp: the repository's own recovery with
+    # GLV and 12-bit G tables, built for the host) on the same sample and
+    # threads, then the same tally; bit-exact against the GPU as well
+    glv = {}
+    try:
+        gp = glv_port()
+        threads = best["threads"]
+        t0 = time.perf_counter()
+        gverdict, grec = gp.verify(sample, sigs, True, threads=threads)
+        t1 = time.perf_counter()
+        co.tally(sample, gverdict, f, propose_value=pv)
+        t2 = time.perf_counter()
+        glv = {"threads": threads, "msgs_per_s": n / (t2 - t0), "verify_s": t1 - t0, "tally_decide_s": t2 - t1,
+               "bit_exact_vs_gpu": bool(gverdict.tolist() == gv.tolist()
+                                        and grec.tobytes() == gpu_recovered[:n].cpu().numpy().tobytes())}
+    except Exception as e:  # reported, never fatal
+        glv = {"error": repr(e)}
+    kind, value, cores = "port", best["msgs_per_s"], best["threads"]
+    if glv.get("msgs_per_s", 0) > value and glv.get("bit_exact_vs_gpu"):
+        kind, value, cores = "port-glv", glv["msgs_per_s"], glv["threads"]
+    return {"value": value, "unit": "msgs/s", "cores": cores, "kind": kind,
+            "port_glv": glv, "port_naive": {"msgs_per_s": best["msgs_per_s"], "threads": best["threads"]},
             "cpu_model": model, "host_cpus_allowed": allowed, "host_cpus_online": online,
             "cgroup_cpu_quota": cgroup_cpu_quota(),
             "per_gpu_share": figures["per_gpu_share"], "all_threads": figures["all_threads"],
@@ -937,9 +990,12 @@ def run_cpu_baseline(args, v, db, sigs, gpu_verdict, gpu_recovered):
                                  "commits": int(sum(d >> 6 & 1 for d in tal["decide"].tolist()))},
             "sample": f"first {n} messages of the same C2 workload: verify (digest+recover+signatory+membership) "
                       f"on the host threads, then the first-wins tally and every round's quorum decisions",
-            "note": "C restatement with naive 4x64-bit-limb arithmetic (no GLV, no precomputed tables): slower "
-                    "than libsecp256k1, which the reference reaches through go-ethereum's cgo and which cannot "
-                    "be built here; a lower bound for the reference's CPU path",
+            "note": "value = the faster of two bit-exact host ports: 'port' is the C restatement with naive "
+                    "4x64-bit-limb arithmetic (no GLV, no tables); 'port-glv' is the repository's own recovery "
+                    "(GLV split, 12-bit G / lambda G tables, divstep inversions) built for the host, whose "
+                    "radix-2^29 limbs suit the GPU's 32-bit multiplier rather than the host's 64-bit one.  Both "
+                    "are slower per core than libsecp256k1, which the reference reaches through go-ethereum's cgo "
+                    "and which cannot be built here: a lower bound for the reference's CPU path",
             "valid": int((verdict == 0).sum())}
 
 

@@ -39,6 +39,23 @@ class HdBatch(ctypes.Structure):
     ]
 
 
+class HdBatchCompact(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_uint32),
+        ("type", ctypes.c_void_p),
+        ("height", ctypes.c_void_p),
+        ("round", ctypes.c_void_p),
+        ("valid_round", ctypes.c_void_p),
+        ("from_idx", ctypes.c_void_p),
+        ("value_idx", ctypes.c_void_p),
+        ("sig65", ctypes.c_void_p),
+        ("n_escape", ctypes.c_uint32),
+        ("escape32", ctypes.c_void_p),
+        ("n_values", ctypes.c_uint32),
+        ("values32", ctypes.c_void_p),
+    ]
+
+
 class HdBatchOut(ctypes.Structure):
     _fields_ = [
         ("type", ctypes.c_void_p),
@@ -98,6 +115,8 @@ SIGNATURES = {
                                                     ctypes.c_void_p]),
     "hd_verify_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
+    "hd_verify_submit_compact": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatchCompact), ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "hd_verify_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
     "hd_host_alloc": (ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
     "hd_host_free": (ctypes.c_int, [ctypes.c_void_p]),

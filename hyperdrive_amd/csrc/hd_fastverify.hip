@@ -120,14 +120,16 @@ struct FbWork {
     int last_k = 8;               // messages per inversion of the last split check (split_k_for)
     double budget = 0;            // table bytes allowed (HD_FB_MAX_BYTES), shared per device
     size_t bytes = 0;             // table bytes this context holds
-    // Foreign keys (HD_VAR_FOREIGN_KEYS): fcap slots fbase .. reserved once
+    // Foreign keys (HD_VAR_FOREIGN_KEYS): fres slots fbase .. reserved once
     // (a contiguous block, kept across set changes) for authenticated Froms
-    // outside the admitted set; fdict maps such a From to its slot (emptied
+    // outside the admitted set, of which the first fcap are in use (fcap is
+    // re-read from the variant at every set change: 0 turns learning off,
+    // the block stays reserved); fdict maps such a From to its slot (emptied
     // on every set change).  k_verify stores the claim count into fpend_host;
     // a change since fseen makes the next call build the new tables.
     uint32_t* fdict = nullptr;
     uint32_t* fnext = nullptr;
-    uint32_t fbase = 0, fcap = 0;
+    uint32_t fbase = 0, fcap = 0, fres = 0;
     uint32_t* fpend_host = nullptr;
     uint32_t* fpend_dev = nullptr;
     uint32_t fseen = 0;
@@ -262,7 +264,7 @@ __global__ __launch_bounds__(256, WAVES) void k_verify_fast(DevBatch b, const ui
 //                   s^-1 of each message
 //   k_fast_digits   one per lane: u1 = m / s, u2 = r / s as window digits
 //   k_fast_sums     one per lane: u1 G + u2 P (the first window's point
-//                   loaded, one mixed addition per further window)
+//                   loaded, one XYZZ mixed addition per further window)
 //   k_fast_zinv     K per lane: prefix products of Z, one inversion mod p,
 //                   Z^-1 of each message
 //   k_fast_cmp      one per lane: the comparison, the outputs, the valid
@@ -289,7 +291,7 @@ struct SplitRows {
     uint32_t* u2;    // 8n: r
     uint32_t* s;     // 8n: s
     uint32_t* pre;   // 9n: prefix products of s, then s^-1 R (radix 2^29); later of Z, then Z^-1
-    uint32_t* xyz;   // 27n: the Jacobian sum
+    uint32_t* xyz;   // 27n: the XYZZ sum as (X ZZZ, Y ZZ, Z = ZZ ZZZ) (gxz_finish)
     uint32_t* dig;   // (NWIN(WG) + NWIN(W)) n: window digits as table references (fb_ref)
     int prio;        // wave priority of the short kernels (HD_VAR_WAVE_PRIO)
 };
@@ -447,29 +449,30 @@ __global__ __launch_bounds__(256) void k_fast_sinv(uint32_t n, uint32_t T, Split
 // wavefront that has one (a uniform branch); every other step is the bare
 // addition.  (Sending such messages to the full recovery instead costs a
 // whole recovery's latency per verify call: measured 1.95 -> 3.0 ms per 1M.)
-HD void sum_step_sel(gej& acc, bool& started, const ge& cur, bool nz) {
-    gej s;
-    gej_add_ge_nx(s, acc, cur);
-    gej first;
-    gej_set_ge(first, cur);
+// The sums are XYZZ (gxz, hd_fixedbase.h: 8M + 2S per addition).
+HD void sum_step_sel(gxz& acc, bool& started, const ge& cur, bool nz) {
+    gxz s;
+    gxz_add_ge_nx(s, acc, cur);
+    gxz first;
+    gxz_set_ge(first, cur);
     fe_norm_weak(first.y);
-    gej_cmov(s, first, !started);
-    gej_cmov(acc, s, nz);
+    gxz_cmov(s, first, !started);
+    gxz_cmov(acc, s, nz);
     started = started || nz;
 }
-HD void sum_step(gej& acc, bool& started, ge cur, uint32_t ec) {
+HD void sum_step(gxz& acc, bool& started, ge cur, uint32_t ec) {
     if (ec & HD_REF_NEG) fe_neg(cur.y, cur.y);
     const bool nz = !(ec & HD_REF_ZERO);
-    if (__ballot(!(started && nz)) == 0ull) gej_add_ge_nx(acc, acc, cur);
+    if (__ballot(!(started && nz)) == 0ull) gxz_add_ge_nx(acc, acc, cur);
     else sum_step_sel(acc, started, cur, nz);
 }
 
 // the first addition: the accumulator is still the first window's affine
 // point p0, so the cheaper affine + affine formula applies (4M + 2S)
-HD void sum_first(gej& acc, bool& started, const ge& p0, ge cur, uint32_t ec) {
+HD void sum_first(gxz& acc, bool& started, const ge& p0, ge cur, uint32_t ec) {
     if (ec & HD_REF_NEG) fe_neg(cur.y, cur.y);
     const bool nz = !(ec & HD_REF_ZERO);
-    if (__ballot(!(started && nz)) == 0ull) gej_add_ge_z1(acc, p0, cur);
+    if (__ballot(!(started && nz)) == 0ull) gxz_add_ge_z1(acc, p0, cur);
     else sum_step_sel(acc, started, cur, nz);
 }
 
@@ -521,14 +524,13 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
     const uint32_t* dp = DL ? sdig + threadIdx.x : rows.dig + i;
     if (DL) fast_digit_refs<WP>(sdig + threadIdx.x, 256, rows, n, i);
     uint32_t e = dp[0];
-    gej acc;
+    gxz acc;
     ge p0;
     gp_unpack(p0, gtab[e & HD_REF_IDX]);
     if (e & HD_REF_NEG) fe_neg(p0.y, p0.y);
     fe_norm_weak(p0.y);
-    gej_set_ge(acc, p0);
-    bool started = !(e & HD_REF_ZERO);
-    if (!started) gej_set_inf(acc);
+    gxz_set_ge(acc, p0);
+    bool started = !(e & HD_REF_ZERO);   // (while not started, acc is never read)
     // The next PF windows' points, packed (16 words each) until used; the
     // digit of the window after those is read one addition earlier still, so
     // no load waits on another load inside an addition.
@@ -579,14 +581,17 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
         gp_unpack(g, cur);
         sum_step(acc, started, g, ec);
     }
-    // infinity, or a degenerate addition on the way (Z = 0): full recovery
-    if (!started || gej_is_inf(acc)) {
+    // infinity, or a degenerate addition on the way (ZZ = 0): full recovery
+    if (!started || gxz_is_inf(acc)) {
         rows.aux[i] = (a & ~0xFFu) | HD_NEEDS_SLOW;
         return;
     }
-    soa_store(rows.xyz, n, i, acc.x.n);
-    soa_store(rows.xyz + 9 * (size_t)n, n, i, acc.y.n);
-    soa_store(rows.xyz + 18 * (size_t)n, n, i, acc.z.n);
+    // (X ZZZ, Y ZZ, ZZ ZZZ): k_fast_zinv inverts the third like a Jacobian Z
+    fe xn, yn, t;
+    gxz_finish(xn, yn, t, acc);
+    soa_store(rows.xyz, n, i, xn.n);
+    soa_store(rows.xyz + 9 * (size_t)n, n, i, yn.n);
+    soa_store(rows.xyz + 18 * (size_t)n, n, i, t.n);
 }
 
 // Batch inversion over the K messages of a lane as a product tree (K a power
@@ -676,17 +681,15 @@ __global__ __launch_bounds__(256) void k_fast_cmp(DevBatch b, SplitRows rows, co
     if (present) {
         v = (uint8_t)(rows.aux[i] & 0xFFu);
         if (v == HD_FAST_LIVE) {
-            gej s;
-            fe zi, x;
-            soa_load(s.x.n, rows.xyz, n, i);
-            soa_load(s.y.n, rows.xyz + 9 * (size_t)n, n, i);
-            fe_clear(s.z);   // fast_final reads x, y and Z^-1 only
-            soa_load(zi.n, rows.pre, n, i);
+            fe xn, yn, w, x;
+            soa_load(xn.n, rows.xyz, n, i);
+            soa_load(yn.n, rows.xyz + 9 * (size_t)n, n, i);
+            soa_load(w.n, rows.pre, n, i);
             sc r;
             soa_load(r.v, rows.u2, n, i);
             const uint32_t sv = b.sig65[65 * (size_t)i + 64];
             fast_rx(x, r, sv);
-            v = fast_final(s, zi, x, sv);
+            v = fast_final_xz(xn, yn, w, x, sv);
             // authentication only: From's key does not give R, so the
             // recovered key is not From's -- final, without the recovery
             if (auth && v == HD_NEEDS_SLOW) v = V_NOT_AUTHENTIC;
@@ -907,14 +910,26 @@ __global__ __launch_bounds__(256) void k_fb_runs(const uint32_t* __restrict__ li
     }
 }
 
+// One block.  not_ready counts admitted slots only: the foreign block
+// [f0, f1) is left out, counted inside the parallel walk (one LDS atomic per
+// thread), so a set change that builds 10^5-10^6 admitted tables pays no
+// serial walk over the list.
 __global__ void k_fb_ready(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
                            uint32_t* __restrict__ state, uint32_t* not_ready, uint32_t f0, uint32_t f1) {
+    __shared__ uint32_t sh_admitted;
     const uint32_t c = *count;
-    for (uint32_t k = threadIdx.x; k < c; k += blockDim.x) state[list[k]] = HD_FB_READY;
+    if (threadIdx.x == 0) sh_admitted = 0;
+    __syncthreads();
+    uint32_t mine = 0;
+    for (uint32_t k = threadIdx.x; k < c; k += blockDim.x) {
+        const uint32_t sl = list[k];
+        state[sl] = HD_FB_READY;
+        mine += (sl >= f0 && sl < f1) ? 0u : 1u;
+    }
+    if (mine) atomicAdd(&sh_admitted, mine);
+    __syncthreads();
     if (threadIdx.x == 0 && c && not_ready) {
-        // not_ready counts admitted slots: the foreign block [f0, f1) is not in it
-        uint32_t ca = 0;
-        for (uint32_t k = 0; k < c; k++) ca += (list[k] >= f0 && list[k] < f1) ? 0u : 1u;
+        const uint32_t ca = sh_admitted;
         const uint32_t v = *(volatile uint32_t*)not_ready;
         *(volatile uint32_t*)not_ready = v >= ca ? v - ca : 0u;
     }
@@ -1019,7 +1034,7 @@ int fb_learn(hd_ctx* ctx, hipStream_t s) {
         k_fb_bases<HD_FB_W><<<g, 256, 0, s>>>(f->list, f->counts, f->pub, f->base);
         k_fb_runs<HD_FB_W><<<fb_run_blocks(ctx), 256, 0, s>>>(f->list, f->counts, f->base, f->tabs, f->zr);
     }
-    k_fb_ready<<<1, 256, 0, s>>>(f->list, f->counts, f->state, f->nr_dev, f->fbase, f->fbase + f->fcap);
+    k_fb_ready<<<1, 256, 0, s>>>(f->list, f->counts, f->state, f->nr_dev, f->fbase, f->fbase + f->fres);
     FBCHK(hipGetLastError(), "fb table kernels");
     return HD_OK;
 }
@@ -1178,7 +1193,7 @@ int hd_fb_map_signatories(hd_ctx* ctx, const uint8_t* sorted, uint32_t m) {
         f->slot_of.clear();
         f->free_slots.clear();
         f->used = 1;
-        f->fcap = 0;   // the foreign block goes with the tables
+        f->fcap = f->fres = 0;   // the foreign block goes with the tables
         f->wp = wp;
         f->max_slots = (uint32_t)std::max(1.0, std::min(1e6, f->budget / fb_slot_bytes(wp)));
         int ra = fb_alloc_slots(ctx);
@@ -1221,21 +1236,22 @@ int hd_fb_map_signatories(hd_ctx* ctx, const uint8_t* sorted, uint32_t m) {
     // of the first set that asks for it; emptied (dictionary and states) on
     // every set change -- a From that leaves or joins the set is learned again
     const uint32_t want = (uint32_t)std::max(0, ctx->var[HD_VAR_FOREIGN_KEYS]);
-    if (want && !f->fcap && f->used + want <= f->max_slots) {
+    if (want && !f->fres && f->used + want <= f->max_slots) {
         f->fbase = f->used;
-        f->fcap = want;
+        f->fres = want;
         f->used += want;
     }
+    f->fcap = std::min(want, f->fres);   // 0: no foreign learning until a set change asks again
     int rc = fb_grow_slots(ctx, f->used);
     if (rc) return rc;
     hipStream_t s = ctx->stream;
     for (uint32_t slot : fresh) FBCHK(hipMemsetAsync(f->state + slot, 0, 4, s), "fb slot reset");
-    if (f->fcap) {
+    if (f->fres) {
         if (!f->fdict) FBCHK(hipMalloc(&f->fdict, 4 * (size_t)HD_FD_WORDS), "fb foreign dictionary");
         if (!f->fnext) FBCHK(hipMalloc(&f->fnext, 4), "fb foreign count");
         FBCHK(hipMemsetAsync(f->fdict, 0, 4 * (size_t)HD_FD_WORDS, s), "fb foreign reset");
         FBCHK(hipMemsetAsync(f->fnext, 0, 4, s), "fb foreign reset");
-        FBCHK(hipMemsetAsync(f->state + f->fbase, 0, 4 * (size_t)f->fcap, s), "fb foreign reset");
+        FBCHK(hipMemsetAsync(f->state + f->fbase, 0, 4 * (size_t)f->fres, s), "fb foreign reset");
         *(volatile uint32_t*)f->fpend_host = 0;
         f->fseen = 0;
     }
@@ -1251,12 +1267,12 @@ int hd_fb_clear_keys(hd_ctx* ctx) {
     int rq = hd_ctx_quiesce(ctx);
     if (rq) return rq;
     if (f->nslots > 1) FBCHK(hipMemsetAsync(f->state + 1, 0, 4 * (size_t)(f->nslots - 1), ctx->stream), "fb clear");
-    if (f->fcap && f->fdict) {   // the foreign keys are learned again too
+    if (f->fres && f->fdict) {   // the foreign keys are learned again too
         FBCHK(hipMemsetAsync(f->fdict, 0, 4 * (size_t)HD_FD_WORDS, ctx->stream), "fb clear");
         FBCHK(hipMemsetAsync(f->fnext, 0, 4, ctx->stream), "fb clear");
     }
     FBCHK(hipStreamSynchronize(ctx->stream), "fb clear");
-    if (f->fcap) {
+    if (f->fres) {
         *(volatile uint32_t*)f->fpend_host = 0;
         f->fseen = 0;
     }
@@ -1565,7 +1581,7 @@ int hd_ctx_fastpath_stats(hd_ctx* ctx, uint32_t* known_keys, uint32_t* last_fall
         std::vector<uint32_t> st(f->nslots);
         FBCHK(hipMemcpy(st.data(), f->state, 4 * (size_t)f->nslots, hipMemcpyDeviceToHost), "state read");
         for (uint32_t k = 1; k < f->nslots; k++)   // admitted keys (not the foreign block)
-            *known_keys += st[k] == HD_FB_READY && !(k >= f->fbase && k < f->fbase + f->fcap);
+            *known_keys += st[k] == HD_FB_READY && !(k >= f->fbase && k < f->fbase + f->fres);
     }
     if (last_fallback && f->last_set >= 0)
         FBCHK(hipMemcpy(last_fallback, f->sc[f->last_set].count, 4, hipMemcpyDeviceToHost), "fallback read");

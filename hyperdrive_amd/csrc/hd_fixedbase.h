@@ -193,6 +193,99 @@ HD void gej_add_ge_z1(gej& r, const ge& a, const ge& b) {
     r = o;
 }
 
+// ---- XYZZ sums (k_fast_sums) ------------------------------------------------
+// The known-key check's fixed-base sums accumulate in XYZZ coordinates
+// ("extended Jacobian"): x = X / ZZ, y = Y / ZZZ with ZZ^3 = ZZZ^2, and
+// ZZ = 0 for infinity.  A mixed addition is 8M + 2S
+// (madd-2008-s) against 8M + 3S for Jacobian (gej_add_ge_nx), and the loop
+// carries X and Y unnormalised (limb classes below), which saves two weak
+// normalisations per addition as well.  The sum leaves the loop as
+// (X ZZZ, Y ZZ, ZZ ZZZ): one inversion w of the last gives x = X ZZZ w and
+// y = Y ZZ w (xz_finish / fast_final_xz).
+//
+// Limb classes (hd_field.h): X <= 5T, Y <= 3T, ZZ and ZZZ tight; the table
+// point's x is T and its y T or 2T (negated).  tests/test_field_bounds.py
+// certifies every step for all inputs of these classes.
+struct gxz { fe x, y, zz, zzz; };
+
+HD void gxz_set_ge(gxz& r, const ge& a) {
+    r.x = a.x;
+    r.y = a.y;
+    fe_set_u32(r.zz, 1);
+    fe_set_u32(r.zzz, 1);
+}
+HD void gxz_cmov(gxz& r, const gxz& a, bool flag) {
+    fe_cmov(r.x, a.x, flag);
+    fe_cmov(r.y, a.y, flag);
+    fe_cmov(r.zz, a.zz, flag);
+    fe_cmov(r.zzz, a.zzz, flag);
+}
+HD bool gxz_is_inf(const gxz& a) { return fe_is_zero(a.zz); }
+
+// X3, Y3 of both XYZZ additions from P, R and X1, Y1 (the shared tail):
+// X3 = R^2 - PPP - 2Q, Y3 = R (Q - X3) - Y1 PPP with Q = X1 PP.  zz / zzz:
+// ZZ1 and ZZZ1 (in: nullptr for an affine a), multiplied by PP and PPP as
+// soon as those exist, so that ZZ1 and ZZZ1 die early (k_fast_sums runs at
+// 168 VGPRs for 3 waves per SIMD).
+HD void gxz_add_tail(gxz& o, const fe& x1, const fe& y1, const fe& p, const fe& R, const fe* zz1, const fe* zzz1) {
+    fe pp, ppp, q, t;
+    fe_sqr(pp, p);             // PP               T
+    fe_mul(q, x1, pp);         // Q = X1 PP        T (5T x T)
+    fe_mul(ppp, p, pp);        // PPP              T
+    if (zz1) {
+        fe_mul(o.zz, *zz1, pp);       // ZZ3 = ZZ1 PP      T
+        fe_mul(o.zzz, *zzz1, ppp);    // ZZZ3 = ZZZ1 PPP   T
+    } else {
+        o.zz = pp;
+        o.zzz = ppp;
+    }
+    fe_sqr(o.x, R);            // R^2              T
+    fe_add(t, q, q);
+    fe_add(t, t, ppp);         // 2Q + PPP         3T
+    fe_sub_k<4>(o.x, o.x, t);  // X3               5T
+    fe_sub_k<6>(t, q, o.x);    // Q - X3           7T
+    fe_mul(t, R, t);           // R (Q - X3)       T (T x 7T)
+    fe_mul(q, y1, ppp);        // Y1 PPP           T (3T x T)
+    fe_sub_k<2>(o.y, t, q);    // Y3               3T
+}
+
+// a + b for a finite XYZZ a and an affine b, no exceptional branches: if
+// a = +-b then P = 0, so ZZ3 = ZZZ3 = 0 and every later ZZ is a multiple of
+// it; the sum ends with ZZ = 0 and the message takes the full recovery, as
+// with gej_add_ge_nx.
+HD void gxz_add_ge_nx(gxz& r, const gxz& a, const ge& b) {
+    fe u2, s2, p, R;
+    fe_mul(u2, b.x, a.zz);     // U2 = X2 ZZ1      T
+    fe_mul(s2, b.y, a.zzz);    // S2 = Y2 ZZZ1     T (2T x T)
+    fe_sub_k<6>(p, u2, a.x);
+    fe_norm_weak(p);           // P = U2 - X1      T
+    fe_sub_k<4>(R, s2, a.y);
+    fe_norm_weak(R);           // R = S2 - Y1      T
+    gxz o;
+    gxz_add_tail(o, a.x, a.y, p, R, &a.zz, &a.zzz);
+    r = o;
+}
+
+// a + b for two affine points (a.y weakly normalised, b.y T or 2T): ZZ1 =
+// ZZZ1 = 1, 4M + 2S; a = +-b gives ZZ3 = 0 like gxz_add_ge_nx.
+HD void gxz_add_ge_z1(gxz& r, const ge& a, const ge& b) {
+    fe p, R;
+    fe_sub_k<2>(p, b.x, a.x);
+    fe_norm_weak(p);           // P = X2 - X1      T
+    fe_sub_k<2>(R, b.y, a.y);
+    fe_norm_weak(R);           // R = Y2 - Y1      T
+    gxz o;
+    gxz_add_tail(o, a.x, a.y, p, R, nullptr, nullptr);
+    r = o;
+}
+
+// the sum as k_fast_sums stores it: X ZZZ, Y ZZ and the value to invert, ZZ ZZZ
+HD void gxz_finish(fe& xn, fe& yn, fe& t, const gxz& a) {
+    fe_mul(xn, a.x, a.zzz);
+    fe_mul(yn, a.y, a.zz);
+    fe_mul(t, a.zz, a.zzz);
+}
+
 // Booth digit j of u for the table width: bits [W j - 1, W j + W - 1] of u
 // (bits outside [0, 256) read 0).  The words are picked with selects over
 // the 8 limbs instead of a runtime array index, which would put u in scratch.
@@ -367,6 +460,19 @@ HD uint8_t fast_final(const gej& acc, const fe& zinv, const fe& x, uint32_t v) {
     fe_mul(ax, acc.x, z2);
     fe_mul(z2, z2, zinv);
     fe_mul(ay, acc.y, z2);
+    fe_normalize(ax);
+    fe_normalize(ay);
+    uint32_t diff = (ay.n[0] & 1u) ^ (v & 1u);
+    HD_UNROLL for (int i = 0; i < 9; i++) diff |= ax.n[i] ^ x.n[i];
+    return diff ? HD_NEEDS_SLOW : V_VALID;
+}
+
+// fast_final for a sum stored by gxz_finish: w = (ZZ ZZZ)^-1, so x = (X ZZZ) w
+// and y = (Y ZZ) w
+HD uint8_t fast_final_xz(const fe& xn, const fe& yn, const fe& w, const fe& x, uint32_t v) {
+    fe ax, ay;
+    fe_mul(ax, xn, w);
+    fe_mul(ay, yn, w);
     fe_normalize(ax);
     fe_normalize(ay);
     uint32_t diff = (ay.n[0] & 1u) ^ (v & 1u);

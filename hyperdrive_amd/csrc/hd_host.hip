@@ -24,7 +24,9 @@
 
 namespace {
 
-enum { HC_TYPE, HC_H, HC_R, HC_VR, HC_VALUE, HC_FROM, HC_SIG, HC_N };
+// device columns of a pipeline: the hd_batch fields, then the compact
+// batch's index columns and dictionaries (hd_verify_submit_compact)
+enum { HC_TYPE, HC_H, HC_R, HC_VR, HC_VALUE, HC_FROM, HC_SIG, HC_FIDX, HC_VIDX, HC_ESC, HC_VALS, HC_N };
 
 struct HostSlot {
     hipStream_t stream = nullptr;
@@ -84,6 +86,33 @@ __global__ __launch_bounds__(256) void k_host_store(HostOut o) {
             for (size_t i = t; i < n; i += stride) o.dst[k][i] = o.src[k][i];
         }
     }
+}
+
+// The compact batch's From and value columns, expanded on the device: row i
+// of from32 is the caller's signatory from_idx[i] (the array last passed to
+// hd_set_signatories, caller order) or escape row from_idx[i] - n_sig; row i
+// of value32 is values row value_idx[i].  One lane per 16-byte half row, so
+// a wavefront reads and writes whole 16-byte words.  Indices were range
+// checked on the host.
+__global__ __launch_bounds__(256) void k_compact_expand(uint32_t n, const uint16_t* __restrict__ from_idx,
+                                                        const uint16_t* __restrict__ value_idx,
+                                                        const uint4* __restrict__ sigs, uint32_t n_sig,
+                                                        const uint4* __restrict__ esc,
+                                                        const uint4* __restrict__ vals, uint4* __restrict__ from32,
+                                                        uint4* __restrict__ value32) {
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= 2 * (size_t)n) return;
+    const uint32_t i = (uint32_t)(t >> 1), h = (uint32_t)(t & 1);
+    const uint32_t f = from_idx[i];
+    from32[t] = f < n_sig ? sigs[2 * (size_t)f + h] : esc[2 * (size_t)(f - n_sig) + h];
+    value32[t] = vals[2 * (size_t)value_idx[i] + h];
+}
+
+// largest element of a host index column (the range check before the upload)
+uint32_t max_u16(const uint16_t* a, size_t n) {
+    uint16_t m = 0;
+    for (size_t i = 0; i < n; i++) m = a[i] > m ? a[i] : m;
+    return m;
 }
 
 // the device address of pinned host memory (NULL if it is not mapped)
@@ -177,14 +206,17 @@ void hd_host_release(hd_ctx* ctx) {
     ctx->host = nullptr;
 }
 
-extern "C" {
+namespace {
 
-int hd_verify_submit(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8_t* recovered32,
-                     uint32_t* valid_bitmap, uint64_t* ticket) {
-    if (!ctx || !batch || !verdict || !ticket) return HD_EINVAL;
-    if (batch->n && (!batch->type || !batch->height || !batch->round || !batch->value32 || !batch->from32 ||
-                     !batch->sig65))
-        return HD_EINVAL;
+// One submit: the host columns `cols` (NULL src: absent) go to the slot's
+// device columns (pinned ones by DMA, pageable ones through the staging);
+// with `cb` the compact batch's From / value columns are expanded on the
+// device first; then hd_verify_batch_device and the outputs.
+struct Col { const void* src; size_t sz; };
+struct CompactInfo { uint32_t n_sig, n_esc; };
+
+int submit_impl(hd_ctx* ctx, uint32_t n, const Col (&cols)[HC_N], const CompactInfo* cb, uint8_t* verdict,
+                uint8_t* recovered32, uint32_t* valid_bitmap, uint64_t* ticket) {
     (void)hipSetDevice(ctx->device);
     if (!ctx->host) ctx->host = new (std::nothrow) HostPipe();
     if (!ctx->host) return HD_ENOMEM;
@@ -195,17 +227,7 @@ int hd_verify_submit(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8
     if (rc) return rc;
     if ((rc = slot_init(ctx, s))) return rc;
     *ticket = t;
-    const uint32_t n = batch->n;
     if (n == 0) return HD_OK;
-    // inputs: pinned columns by DMA, pageable ones through the staging
-    struct Col { const void* src; size_t sz; };
-    const Col cols[HC_N] = {{batch->type, n},
-                            {batch->height, 8 * (size_t)n},
-                            {batch->round, 8 * (size_t)n},
-                            {batch->valid_round, 8 * (size_t)n},
-                            {batch->value32, 32 * (size_t)n},
-                            {batch->from32, 32 * (size_t)n},
-                            {batch->sig65, 65 * (size_t)n}};
     size_t stage = 0;
     bool pinned[HC_N];
     for (int k = 0; k < HC_N; k++) {
@@ -228,6 +250,19 @@ int hd_verify_submit(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8
         }
         HCHK(hipMemcpyAsync(s.col[k].p, src, cols[k].sz, hipMemcpyHostToDevice, s.stream), "submit upload");
         dst[k] = s.col[k].p;
+    }
+    if (cb) {
+        // From and value rows from the uploaded indices and dictionaries
+        if ((rc = hd_dev_grow(ctx, &s.col[HC_FROM].p, &s.col[HC_FROM].cap, 32 * (size_t)n))) return rc;
+        if ((rc = hd_dev_grow(ctx, &s.col[HC_VALUE].p, &s.col[HC_VALUE].cap, 32 * (size_t)n))) return rc;
+        dst[HC_FROM] = s.col[HC_FROM].p;
+        dst[HC_VALUE] = s.col[HC_VALUE].p;
+        const uint32_t blocks = (uint32_t)((2 * (size_t)n + 255) / 256);
+        k_compact_expand<<<blocks, 256, 0, s.stream>>>(
+            n, (const uint16_t*)dst[HC_FIDX], (const uint16_t*)dst[HC_VIDX], (const uint4*)ctx->d_sig_caller,
+            cb->n_sig, (const uint4*)dst[HC_ESC], (const uint4*)dst[HC_VALS], (uint4*)s.col[HC_FROM].p,
+            (uint4*)s.col[HC_VALUE].p);
+        HCHK(hipGetLastError(), "k_compact_expand");
     }
     hd_batch db{n,
                 (const uint8_t*)dst[HC_TYPE],
@@ -284,6 +319,61 @@ int hd_verify_submit(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8
     HCHK(hipEventRecord(s.done, s.stream), "submit record");
     s.ticket = t;
     return HD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hd_verify_submit(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8_t* recovered32,
+                     uint32_t* valid_bitmap, uint64_t* ticket) {
+    if (!ctx || !batch || !verdict || !ticket) return HD_EINVAL;
+    if (batch->n && (!batch->type || !batch->height || !batch->round || !batch->value32 || !batch->from32 ||
+                     !batch->sig65))
+        return HD_EINVAL;
+    const uint32_t n = batch->n;
+    const Col cols[HC_N] = {{batch->type, n},
+                            {batch->height, 8 * (size_t)n},
+                            {batch->round, 8 * (size_t)n},
+                            {batch->valid_round, 8 * (size_t)n},
+                            {batch->value32, 32 * (size_t)n},
+                            {batch->from32, 32 * (size_t)n},
+                            {batch->sig65, 65 * (size_t)n},
+                            {nullptr, 0}, {nullptr, 0}, {nullptr, 0}, {nullptr, 0}};
+    return submit_impl(ctx, n, cols, nullptr, verdict, recovered32, valid_bitmap, ticket);
+}
+
+int hd_verify_submit_compact(hd_ctx* ctx, const hd_batch_compact* batch, uint8_t* verdict, uint8_t* recovered32,
+                             uint32_t* valid_bitmap, uint64_t* ticket) {
+    if (!ctx || !batch || !verdict || !ticket) return HD_EINVAL;
+    const uint32_t n = batch->n;
+    if (n && (!batch->type || !batch->height || !batch->round || !batch->from_idx || !batch->value_idx ||
+              !batch->sig65 || !batch->values32 || batch->n_values == 0))
+        return HD_EINVAL;
+    if ((batch->n_escape && !batch->escape32) || (size_t)ctx->n_sig_caller + batch->n_escape > 65536u ||
+        batch->n_values > 65536u)
+        return HD_EINVAL;
+    if (n) {
+        // every index names a row (the expansion reads no further)
+        if (max_u16(batch->from_idx, n) >= ctx->n_sig_caller + batch->n_escape) return HD_EINVAL;
+        if (max_u16(batch->value_idx, n) >= batch->n_values) return HD_EINVAL;
+    }
+    const CompactInfo ci{ctx->n_sig_caller, batch->n_escape};
+    // (an empty escape list still gets a device row: the kernel's pointer is never NULL)
+    static const uint8_t zero32[32] = {0};
+    const Col cols[HC_N] = {{batch->type, n},
+                            {batch->height, 8 * (size_t)n},
+                            {batch->round, 8 * (size_t)n},
+                            {batch->valid_round, 8 * (size_t)n},
+                            {nullptr, 0},
+                            {nullptr, 0},
+                            {batch->sig65, 65 * (size_t)n},
+                            {batch->from_idx, 2 * (size_t)n},
+                            {batch->value_idx, 2 * (size_t)n},
+                            {batch->n_escape ? (const void*)batch->escape32 : (const void*)zero32,
+                             32 * (size_t)std::max(batch->n_escape, 1u)},
+                            {batch->values32, 32 * (size_t)batch->n_values}};
+    return submit_impl(ctx, n, cols, &ci, verdict, recovered32, valid_bitmap, ticket);
 }
 
 int hd_verify_wait(hd_ctx* ctx, uint64_t ticket) {

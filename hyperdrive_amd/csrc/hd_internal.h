@@ -36,7 +36,7 @@ struct hd_ctx {
     int device = 0;
     int n_cu = 256;
     int verify_waves = 3;   // register budget of k_verify (waves per SIMD)
-    int var[HD_VAR__COUNT] = {3, 0, 1, 0, -1, 0, 2, 0, 0, 0, 0};   // hd_ctx_set_variant (var[0] mirrors verify_waves)
+    int var[HD_VAR__COUNT] = {3, 0, 1, 0, -1, 0, 2, 0, 0, 0, 16};   // hd_ctx_set_variant (var[0] mirrors verify_waves)
     hipStream_t stream = nullptr;
     int pkfmt = HD_PUBKEY_COMPRESSED;   // id.NewSignatory's pubkey encoding (hd_ctx_set_pubkey_format)
     hd::ge* d_gtab = nullptr;
@@ -44,6 +44,11 @@ struct hd_ctx {
     int32_t* d_adm_perm = nullptr;  // sorted index -> caller's index
     size_t cap_adm = 0, cap_adm_perm = 0;
     uint32_t n_adm = 0;
+    // the hd_set_signatories array as given (caller order, duplicates kept):
+    // the From rows of the compact host batch (hd_verify_submit_compact)
+    uint8_t* d_sig_caller = nullptr;
+    size_t cap_sig_caller = 0;
+    uint32_t n_sig_caller = 0;
     int adm_steps = 0;
     DevBuf bufs[BUF__COUNT];
     TallyWork* tally = nullptr;

@@ -502,15 +502,28 @@ struct RouteRow {          // 64 B
 static_assert(sizeof(RouteRow) == 64, "route row");
 #define HD_ROUTE_MAX_PARTS 64u
 
-// per block and owner: the number of candidates (o-major: cnt[o * nb + blk])
+// per block and owner: the number of candidates (o-major: cnt[o * nb + blk]);
+// *outside counts candidates whose From is not in the context's admitted set
+// (possible when the set changed since verification): a row carries the
+// admitted index, not the From, so such a candidate cannot be routed
 __global__ __launch_bounds__(256) void k_route_count(DevBatch b, const uint32_t* __restrict__ bitmap, uint32_t nparts,
-                                                     uint32_t* __restrict__ cnt) {
+                                                     const uint32_t* __restrict__ adm, uint32_t n_adm, int adm_steps,
+                                                     int adm_in_lds, uint32_t* __restrict__ cnt,
+                                                     uint32_t* __restrict__ outside) {
+    extern __shared__ uint32_t sh_adm[];
     __shared__ uint32_t c[HD_ROUTE_MAX_PARTS];
+    if (adm_in_lds) adm_stage(sh_adm, adm, n_adm);
     if (threadIdx.x < nparts) c[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < b.n && candidate(b, nullptr, bitmap, i, Part{0, 1}))
+    if (i < b.n && candidate(b, nullptr, bitmap, i, Part{0, 1})) {
         atomicAdd(&c[part_of(hash_hr(b.height[i], b.round[i]), nparts)], 1u);
+        uint32_t from_be[8];
+        load_row32_be(from_be, b.from32, i);
+        const int32_t sg = adm_in_lds ? admitted_find(sh_adm, n_adm, adm_steps, from_be)
+                                      : admitted_find(adm, n_adm, adm_steps, from_be);
+        if (sg < 0) atomicAdd(outside, 1u);
+    }
     __syncthreads();
     if (threadIdx.x < nparts) cnt[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = c[threadIdx.x];
 }
@@ -550,8 +563,8 @@ __global__ __launch_bounds__(256) void k_route_write(DevBatch b, const uint32_t*
     row.value[0] = vp[0];
     row.value[1] = vp[1];
     row.gidx = base + i;
-    // a VALID message's From is admitted (NOT_ADMITTED otherwise); a caller
-    // set changed since verification routes it as "not admitted" (0xFFFFFF)
+    // a VALID message's From is admitted (NOT_ADMITTED otherwise); a batch
+    // with a candidate outside the current set was refused before this kernel
     row.signer_type = ((uint32_t)(sg >= 0 ? sg : 0xFFFFFF) << 8) | b.type[i];
     row.pad[0] = row.pad[1] = 0;
     rows[pos] = row;
@@ -885,29 +898,39 @@ int hd_route_candidates_device(hd_ctx* ctx, const hd_batch* dshard, const uint32
     const uint32_t nb = nblk(n);
     const size_t cells = (size_t)nparts * nb;
     int rc = 0;
-    uint32_t* cnt = (uint32_t*)tbuf(ctx, T_ROUTE, 4 * (2 * cells + nparts + 1) + 4096, &rc);
+    // starts[0 .. nparts] and, after them, the count of candidates outside the set
+    uint32_t* cnt = (uint32_t*)tbuf(ctx, T_ROUTE, 4 * (2 * cells + nparts + 2) + 4096, &rc);
     if (rc) return rc;
     uint32_t* off = cnt + cells;
     uint32_t* starts = off + cells;
-    void* tmp = (void*)(starts + nparts + 1);
+    void* tmp = (void*)(starts + nparts + 2);
     size_t tmp_bytes = 0;
     TCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, off, (int)cells, s), "route scan size");
     // the scan's temporary storage after the counts (grown with them)
-    cnt = (uint32_t*)tbuf(ctx, T_ROUTE, 4 * (2 * cells + nparts + 1) + 64 + tmp_bytes, &rc);
+    cnt = (uint32_t*)tbuf(ctx, T_ROUTE, 4 * (2 * cells + nparts + 2) + 64 + tmp_bytes, &rc);
     if (rc) return rc;
     off = cnt + cells;
     starts = off + cells;
-    tmp = (void*)(((uintptr_t)(starts + nparts + 1) + 63) & ~(uintptr_t)63);
-    k_route_count<<<nb, 256, 0, s>>>(b, d_valid_bitmap, nparts, cnt);
+    tmp = (void*)(((uintptr_t)(starts + nparts + 2) + 63) & ~(uintptr_t)63);
+    const size_t adm_lds = adm_lds_bytes(ctx->n_adm);
+    TCHK(hipMemsetAsync(starts + nparts + 1, 0, 4, s), "route outside count");
+    k_route_count<<<nb, 256, adm_lds, s>>>(b, d_valid_bitmap, nparts, ctx->d_adm, ctx->n_adm, ctx->adm_steps,
+                                           adm_lds > 0, cnt, starts + nparts + 1);
     TCHK(hipGetLastError(), "k_route_count");
     TCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, (int)cells, s), "route scan");
     k_route_starts<<<1, 64, 0, s>>>(off, cnt, nparts, nb, starts);
-    std::vector<uint32_t> st(nparts + 1);
-    TCHK(hipMemcpyAsync(st.data(), starts, 4 * (nparts + 1), hipMemcpyDeviceToHost, s), "route counts");
+    std::vector<uint32_t> st(nparts + 2);
+    TCHK(hipMemcpyAsync(st.data(), starts, 4 * (nparts + 2), hipMemcpyDeviceToHost, s), "route counts");
     TCHK(hipStreamSynchronize(s), "route counts");
+    if (st[nparts + 1]) {
+        // a VALID candidate whose From left the set since verification: its
+        // row could not name it (the tally keys on the From), so refuse
+        ctx->last_error = "hd_route_candidates_device: " + std::to_string(st[nparts + 1]) +
+                          " candidates whose From is not in the current admitted set";
+        return HD_EINVAL;
+    }
     for (uint32_t o = 0; o < nparts; o++) counts[o] = st[o + 1] - st[o];
     if (st[nparts] > cap_rows) return HD_ECAP;
-    const size_t adm_lds = adm_lds_bytes(ctx->n_adm);
     k_route_write<<<nb, 256, adm_lds, s>>>(b, d_valid_bitmap, nparts, base_index, off, ctx->d_adm, ctx->n_adm,
                                            ctx->adm_steps, adm_lds > 0, reinterpret_cast<RouteRow*>(d_rows));
     TCHK(hipGetLastError(), "k_route_write");

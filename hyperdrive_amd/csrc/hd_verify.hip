@@ -240,7 +240,7 @@ int hd_ctx_destroy(hd_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hd_ctx_quiesce(ctx);
     if (ctx->ev_slow) (void)hipEventDestroy(ctx->ev_slow);
-    void* ptrs[] = {ctx->d_gtab, ctx->d_adm, ctx->d_adm_perm};
+    void* ptrs[] = {ctx->d_gtab, ctx->d_adm, ctx->d_adm_perm, ctx->d_sig_caller};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& b : ctx->bufs)
@@ -319,15 +319,20 @@ int hd_set_signatories(hd_ctx* ctx, const uint8_t* sigs32, uint32_t n) {
     rc = hd_dev_grow(ctx, (void**)&ctx->d_adm_perm, &cap_p, 4 * (size_t)std::max(m, 1u));
     if (rc) return rc;
     ctx->cap_adm_perm = cap_p;
+    rc = hd_dev_grow(ctx, (void**)&ctx->d_sig_caller, &ctx->cap_sig_caller, 32 * (size_t)std::max(n, 1u));
+    if (rc) return rc;
     hipError_t e = hipSuccess;
     if (m) {
         e = hipMemcpyAsync(ctx->d_adm, words.data(), 32 * (size_t)m, hipMemcpyHostToDevice, ctx->stream);
         if (e == hipSuccess)
             e = hipMemcpyAsync(ctx->d_adm_perm, perm.data(), 4 * (size_t)m, hipMemcpyHostToDevice, ctx->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(ctx->d_sig_caller, sigs32, 32 * (size_t)n, hipMemcpyHostToDevice, ctx->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     }
     if (e != hipSuccess) return hd_ctx_fail(ctx, e, "set_signatories upload");
     ctx->n_adm = m;
+    ctx->n_sig_caller = n;
     int steps = 0;
     while ((1u << steps) < m) steps++;
     ctx->adm_steps = steps;

@@ -95,6 +95,57 @@ class Batch:
 
 
 @dataclass
+class CompactBatch:
+    """The PCIe-lean host batch (hd_batch_compact): From and value as 16-bit
+    indices into the signatory array of the context (then escape rows) and
+    into a per-batch value dictionary."""
+    type: np.ndarray          # uint8[n]
+    height: np.ndarray        # int64[n]
+    round: np.ndarray         # int64[n]
+    valid_round: Optional[np.ndarray]
+    from_idx: np.ndarray      # uint16[n]
+    value_idx: np.ndarray     # uint16[n]
+    sig: np.ndarray           # uint8[n, 65]
+    escape: np.ndarray        # uint8[n_escape, 32]
+    values: np.ndarray        # uint8[n_values, 32]
+
+    def __len__(self):
+        return len(self.type)
+
+    @staticmethod
+    def from_batch(b: "Batch", signatories) -> "CompactBatch":
+        """Index form of a Batch against the signatory array the context was
+        given (the first row of a repeated signatory is used; Froms outside
+        it become escape rows, values the batch's dictionary)."""
+        sig = np.ascontiguousarray(_as_rows(signatories, 32))
+        n, ns = len(b), len(sig)
+        key = lambda rows: rows.view(np.dtype((np.void, 32))).ravel()
+        skeys = key(sig)
+        order = np.argsort(skeys, kind="stable")
+        fk = key(b.frm)
+        pos = np.searchsorted(skeys[order], fk)
+        pos = np.minimum(pos, max(ns - 1, 0))
+        hit = (skeys[order][pos] == fk) if ns else np.zeros(n, bool)
+        from_idx = np.zeros(n, np.int64)
+        from_idx[hit] = order[pos[hit]]
+        esc_rows, esc_inv = np.unique(fk[~hit], return_inverse=True)
+        from_idx[~hit] = ns + esc_inv.ravel()
+        vals, vinv = np.unique(key(b.value), return_inverse=True)
+        if ns + len(esc_rows) > 65536 or len(vals) > 65536:
+            raise ValueError("more than 65536 From rows or values: split the batch")
+        return CompactBatch(b.type, b.height, b.round, b.valid_round, from_idx.astype(np.uint16),
+                            vinv.ravel().astype(np.uint16), b.sig,
+                            np.frombuffer(esc_rows.tobytes(), np.uint8).reshape(-1, 32).copy(),
+                            np.frombuffer(vals.tobytes(), np.uint8).reshape(-1, 32).copy())
+
+    def c_struct(self):
+        from ._lib import HdBatchCompact
+        return HdBatchCompact(len(self), _ptr(self.type), _ptr(self.height), _ptr(self.round), _ptr(self.valid_round),
+                              _ptr(self.from_idx), _ptr(self.value_idx), _ptr(self.sig), len(self.escape),
+                              _ptr(self.escape) if len(self.escape) else None, len(self.values), _ptr(self.values))
+
+
+@dataclass
 class VerifyResult:
     verdict: np.ndarray       # uint8[n]
     recovered: np.ndarray     # uint8[n, 32]
@@ -235,6 +286,16 @@ class Verifier:
         t = ctypes.c_uint64()
         self._check(self._lib.hd_verify_submit(self._ctx, ctypes.byref(cb), _ptr(verdict), _ptr(recovered),
                                                _ptr(bitmap), ctypes.byref(t)), "hd_verify_submit")
+        return t.value
+
+    def submit_compact(self, batch: CompactBatch, verdict: np.ndarray, recovered: Optional[np.ndarray] = None,
+                       bitmap: Optional[np.ndarray] = None) -> int:
+        """hd_verify_submit_compact: as submit, with From and value as indices
+        (CompactBatch.from_batch); the outputs are the expanded batch's."""
+        cb = batch.c_struct()
+        t = ctypes.c_uint64()
+        self._check(self._lib.hd_verify_submit_compact(self._ctx, ctypes.byref(cb), _ptr(verdict), _ptr(recovered),
+                                                       _ptr(bitmap), ctypes.byref(t)), "hd_verify_submit_compact")
         return t.value
 
     def wait(self, ticket: int) -> None:

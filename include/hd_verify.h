@@ -170,8 +170,8 @@ int hd_ctx_profile(hd_ctx* ctx, int enable);
                                    a NOT_ADMITTED recovery teaches the context its key, and later messages of
                                    that From take the known-key check (verdict NOT_ADMITTED, identical to the
                                    recovery's); applies from the next hd_set_signatories (reserved once per
-                                   context, when the table budget allows); 0 = off (default), 16 = the measured setting
-                                   [HD_FOREIGN_KEYS] */
+                                   context, when the table budget allows; a later 0 stops using the block); 16 (default),
+                                   0 = off [HD_FOREIGN_KEYS] */
 #define HD_VAR__COUNT 11
 int hd_ctx_set_variant(hd_ctx* ctx, int which, int value);
 int hd_ctx_get_variant(hd_ctx* ctx, int which, int* value);
@@ -223,10 +223,42 @@ int hd_authenticate_batch_device(hd_ctx* ctx, const hd_batch* dbatch, uint8_t* d
  * stay unchanged, and the output buffers valid, until the ticket's wait
  * returns.  A submit that reuses a pipeline first completes its previous
  * ticket.  Tickets start at 1; waiting on a completed ticket returns at once. */
-#define HD_HOST_SLOTS 2
+#define HD_HOST_SLOTS 4   /* a caller keeps up to 3 in flight: upload, verify and output store of three
+                             batches overlap (2 in flight serialise upload + verify + store) */
 int hd_verify_submit(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8_t* recovered32,
                      uint32_t* valid_bitmap, uint64_t* ticket);
 int hd_verify_wait(hd_ctx* ctx, uint64_t ticket);
+/* Compact host batch (PCIe-lean form of hd_verify_submit, 86 B per vote
+ * instead of 146 B).  A replica knows its signatory set and a batch carries
+ * few distinct values, so From and value cross PCIe as 16-bit indices:
+ *   from_idx[i] <  n_sig: From = row from_idx[i] of the array last passed to
+ *                         hd_set_signatories (caller order, duplicates kept;
+ *                         n_sig = its length)
+ *   from_idx[i] >= n_sig: From = escape32 row from_idx[i] - n_sig (senders
+ *                         outside the set, e.g. the NOT_ADMITTED ones)
+ *   value_idx[i]:         value = values32 row value_idx[i]
+ * The rows are expanded on the device, then verified as hd_verify_submit
+ * verifies the expanded batch: verdicts, recovered signatories and bitmaps
+ * are byte-identical.  HD_EINVAL (nothing queued) when an index names no
+ * row, n_sig + n_escape > 65536 or n_values is 0 or > 65536.  Same ticket
+ * semantics as hd_verify_submit; the dictionaries must stay unchanged until
+ * the ticket's wait returns too. */
+typedef struct {
+    uint32_t n;
+    const uint8_t* type;
+    const int64_t* height;
+    const int64_t* round;
+    const int64_t* valid_round;   /* NULL: no Proposes (-1 = InvalidRound) */
+    const uint16_t* from_idx;     /* n */
+    const uint16_t* value_idx;    /* n */
+    const uint8_t* sig65;         /* n x 65 */
+    uint32_t n_escape;
+    const uint8_t* escape32;      /* n_escape x 32 (may be NULL when 0) */
+    uint32_t n_values;
+    const uint8_t* values32;      /* n_values x 32 */
+} hd_batch_compact;
+int hd_verify_submit_compact(hd_ctx* ctx, const hd_batch_compact* batch, uint8_t* verdict, uint8_t* recovered32,
+                             uint32_t* valid_bitmap, uint64_t* ticket);
 /* pinned (page-locked) host memory for inputs the caller fills directly */
 int hd_host_alloc(size_t bytes, void** out);
 int hd_host_free(void* p);
@@ -351,7 +383,11 @@ int hd_gen_batch_device(hd_ctx* ctx, uint32_t kind, uint64_t start, uint32_t n, 
  * grouped by the owner rank of their round (hd_tally_partition_of(h, r,
  * nparts), nparts <= 64) and in index order inside each group; counts[nparts]
  * (host) gets the group sizes (group o starts at row sum(counts[0..o))).
- * Synchronous (one small download); HD_ECAP when cap_rows is too small.
+ * Synchronous (one small download); HD_ECAP when cap_rows is too small;
+ * HD_EINVAL (nothing written) when a candidate's From is not in the context's
+ * current admitted set (the set changed since verification): a row names its
+ * signer by admitted index, so such a vote could not be told apart from
+ * another non-admitted signer's on the owner.
  * The rows cross xGMI (grouped ncclSend/Recv or an all-to-all); the owner
  * concatenates what it received in source-rank order (= global index order)
  * and calls hd_unroute_device: a device batch (type, height, round, value32,

@@ -54,8 +54,10 @@ for step in "$@"; do
     trace_prio) HD_WAVE_PRIO=3 run trace_prio 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_prio -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub ;;
     pcie) run pcie 120 scripts/pcie_probe && HSA_ENABLE_SDMA=0 run pcie_nosdma 120 scripts/pcie_probe ;;
     fieldbench) run fieldbench 120 scripts/fieldbench 3 ;;
+    swappc) run swappc 120 scripts/swappc_repro ;;
     gtest_fk) HD_FOREIGN_KEYS=16 run pytest_gpu_fk 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     bench_fk) HD_FOREIGN_KEYS=16 run bench_fk 600 python bench.py ;;
+    abxyzz) run ab_xyzz 900 python -u scripts/ab_fast.py "HD_LIB=hyperdrive_amd/_lib/var/libhd_base.so" "HD_SUM_WAVES=3" "HD_SUM_WAVES=2" "HD_LIB=hyperdrive_amd/_lib/var/libhd_base.so" "HD_SUM_WAVES=3" "HD_SUM_WAVES=2" "HD_LIB=hyperdrive_amd/_lib/var/libhd_base.so AB_ADV=30" "HD_SUM_WAVES=3 AB_ADV=30" "HD_SUM_WAVES=2 AB_ADV=30" ;;
     gtest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     gputest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     gputest_all) run pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;

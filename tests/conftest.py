@@ -47,9 +47,14 @@ def build_hostmath(bounds: bool = False) -> str:
     interval bounds that each operation checks (hd_field.h).  With
     HD_HOST_SANITIZE=1 in the environment the build adds UBSan
     (-fsanitize=undefined, any finding aborts), so the host-math suite runs
-    the device headers under the sanitizer."""
-    san = os.environ.get("HD_HOST_SANITIZE") == "1"
-    name = ("libhdhost_bounds" if bounds else "libhdhost") + ("_ubsan" if san else "") + ".so"
+    the device headers under the sanitizer.  HD_HOST_SANITIZE=asan adds
+    AddressSanitizer as well; the interpreter then needs the ASan runtime
+    preloaded:
+        LD_PRELOAD=$(gcc -print-file-name=libasan.so) ASAN_OPTIONS=detect_leaks=0 \
+        HD_HOST_SANITIZE=asan python -m pytest tests -m "not gpu" -k <host-math tests>"""
+    mode = os.environ.get("HD_HOST_SANITIZE", "")
+    san = mode in ("1", "asan")
+    name = ("libhdhost_bounds" if bounds else "libhdhost") + {"1": "_ubsan", "asan": "_asan"}.get(mode, "") + ".so"
     out = os.path.join(NATIVE_DIR, "_build", name)
     csrc = os.path.join(ROOT, "hyperdrive_amd", "csrc")
     srcs = [os.path.join(NATIVE_DIR, "hd_host_check.cpp")] + [os.path.join(csrc, f) for f in os.listdir(csrc)
@@ -62,6 +67,8 @@ def build_hostmath(bounds: bool = False) -> str:
         flags = (["-DHD_BOUNDS"] if bounds else []) + ["-DHD_FB_W=12", "-DHD_FB_WG=12"]
         if san:
             flags += ["-fsanitize=undefined", "-fno-sanitize-recover=all", "-g"]
+        if mode == "asan":
+            flags += ["-fsanitize=address", "-fno-omit-frame-pointer"]
         subprocess.run(["g++", "-O2", "-fPIC", "-shared", "-std=c++17", "-Wall", "-Wno-unused-function", *flags, "-o",
                         out, srcs[0]], check=True)
     return out

@@ -281,6 +281,40 @@ extern "C" int hdh_bound_certify(const uint8_t* px, const uint8_t* py, const uin
         fe_neg(qb.y, Q.y); set_class(qb.y, 2);
         gej_add_ge_z1(r, pa, qb);
     }
+    // the XYZZ sums of k_fast_sums: the loop invariant (X 5T, Y 3T, ZZ and
+    // ZZZ tight in; the same classes out) for a table point y of T and 2T,
+    // the affine first addition, the zero-digit select, the stored form
+    {
+        gxz xa;
+        xa.x = a.x; xa.y = a.y; xa.zz = a.z; xa.zzz = a.z;
+        set_class(xa.x, 5); set_class(xa.y, 3); set_class(xa.zz, 1); set_class(xa.zzz, 1);
+        ge pb = Q; set_class(pb.x, 1); set_class(pb.y, 1);
+        ge nb = Q; fe_neg(nb.y, Q.y); set_class(nb.y, 2);
+        gxz o;
+        auto in_class = [](const gxz& g) {
+            for (int i = 0; i < 9; i++) {
+                HD_BREQ(g.x.b[i] <= 5ull * fe_t_limb(i), "gxz: X out of its 5T class");
+                HD_BREQ(g.y.b[i] <= 3ull * fe_t_limb(i), "gxz: Y out of its 3T class");
+                HD_BREQ(g.zz.b[i] <= fe_t_limb(i) && g.zzz.b[i] <= fe_t_limb(i), "gxz: ZZ / ZZZ not tight");
+            }
+        };
+        gxz_add_ge_nx(o, xa, pb); in_class(o);
+        gxz_add_ge_nx(o, xa, nb); in_class(o);
+        ge pa = P; set_class(pa.x, 1); set_class(pa.y, 1);
+        gxz_add_ge_z1(o, pa, pb); in_class(o);
+        gxz_add_ge_z1(o, pa, nb); in_class(o);
+        gxz first;
+        gxz_set_ge(first, nb);
+        fe_norm_weak(first.y);
+        gxz s = o;
+        gxz_cmov(s, first, true);
+        gxz_cmov(xa, s, true); in_class(xa);
+        fe xn, yn, t;
+        gxz_finish(xn, yn, t, xa);
+        fe w = t;
+        fe xr = P.x; set_class(xr, 1);
+        (void)fast_final_xz(xn, yn, w, xr, 0);
+    }
     // isomorphic-curve additions (G side of the ladder) and the R table build
     fe zg = b.z; set_class(zg, 1);
     gej_add_ge_zinv(r, a, qn, zg);
@@ -449,6 +483,55 @@ extern "C" int hdh_add_affine(const uint8_t* ax, const uint8_t* ay, const uint8_
     gej_to_ge(x, y, r);
     fe_out(out64, x);
     fe_out(out64 + 32, y);
+    return 0;
+}
+
+// k_fast_sums' XYZZ accumulation on the host: n affine points (x || y
+// big-endian, 64 B each), point k negated when neg[k] and skipped when
+// skip[k] (a zero digit), summed the way the kernel does it (the first
+// non-skipped point starts the sum, the affine first addition when the
+// second window's digit is non-zero, then gxz_add_ge_nx); the result through
+// gxz_finish, one inversion and fast_final_xz's products.  Returns 1 for a
+// degenerate sum (ZZ = 0 or nothing started), else out = affine x || y.
+extern "C" int hdh_xyzz_sum(const uint8_t* pts, const int* neg, const int* skip, int n, uint8_t* out64) {
+    gxz acc;
+    bool started = false;
+    for (int k = 0; k < n; k++) {
+        ge cur;
+        fe_in(cur.x, pts + 64 * k);
+        fe_in(cur.y, pts + 64 * k + 32);
+        if (neg[k]) fe_neg(cur.y, cur.y);
+        const bool nz = !skip[k];
+        if (k == 0) {
+            fe_norm_weak(cur.y);
+            gxz_set_ge(acc, cur);
+            started = nz;
+            continue;
+        }
+        if (k == 1 && started && nz) {
+            ge p0;
+            p0.x = acc.x;
+            p0.y = acc.y;
+            gxz_add_ge_z1(acc, p0, cur);
+            continue;
+        }
+        gxz s;
+        gxz_add_ge_nx(s, acc, cur);
+        gxz first;
+        gxz_set_ge(first, cur);
+        fe_norm_weak(first.y);
+        gxz_cmov(s, first, !started);
+        gxz_cmov(acc, s, nz);
+        started = started || nz;
+    }
+    if (!started || gxz_is_inf(acc)) return 1;
+    fe xn, yn, t, w, ax, ay;
+    gxz_finish(xn, yn, t, acc);
+    fe_inv(w, t);
+    fe_mul(ax, xn, w);
+    fe_mul(ay, yn, w);
+    fe_out(out64, ax);
+    fe_out(out64 + 32, ay);
     return 0;
 }
 

@@ -95,6 +95,59 @@ def test_first_step_addition(fb, oracle):
     assert fb.hdh_add_affine(b32(a[0]), b32(a[1]), b32(a[0]), b32(a[1]), out) == 1
 
 
+def _xyzz_sum(fb, pts, neg, skip):
+    fb.hdh_xyzz_sum.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
+    fb.hdh_xyzz_sum.restype = ctypes.c_int
+    n = len(pts)
+    out = ctypes.create_string_buffer(64)
+    ng = np.asarray(neg, np.int32)
+    sk = np.asarray(skip, np.int32)
+    deg = fb.hdh_xyzz_sum(b"".join(_pub64(p) for p in pts), ng.ctypes.data, sk.ctypes.data, n, out)
+    return None if deg else (int.from_bytes(out.raw[:32], "big"), int.from_bytes(out.raw[32:], "big"))
+
+
+def test_xyzz_sums(fb, oracle):
+    """k_fast_sums' XYZZ accumulation (gxz_add_ge_z1, gxz_add_ge_nx, the
+    zero-digit selects, gxz_finish) on the host against oracle point
+    addition: 24 points (the 11 + 13 windows of C2) with random signs and
+    rare skips, skipped first windows, and the degenerate sums (a partial sum
+    equal to +-the next point) that must end with ZZ = 0."""
+    O = oracle
+    rng = random.Random(77)
+    G = (O.GX, O.GY)
+    for t in range(30):
+        n = 24
+        pts = [O.point_mul(rng.randrange(1, O.N), G) for _ in range(n)]
+        neg = [rng.random() < 0.5 for _ in range(n)]
+        skip = [rng.random() < (0.3 if t % 5 == 0 else 0.02) for _ in range(n)]
+        if t % 7 == 0:
+            skip[0] = True
+        if t % 11 == 0:
+            skip[0] = skip[1] = True
+        want = None
+        for p, ng, sk in zip(pts, neg, skip):
+            if sk:
+                continue
+            q = O.point_neg(p) if ng else p
+            want = q if want is None else O.point_add(want, q)
+        got = _xyzz_sum(fb, pts, [int(x) for x in neg], [int(x) for x in skip])
+        if want is None:
+            assert got is None
+        else:
+            assert got == want, t
+    # degenerate: the partial sum equals +-the next point (doubling / cancel)
+    a = O.point_mul(12345, G)
+    b = O.point_mul(777, G)
+    ab = O.point_add(a, b)
+    for nxt, ng in [(ab, 0), (ab, 1)]:
+        assert _xyzz_sum(fb, [a, b, nxt, O.point_mul(5, G)], [0, 0, ng, 0], [0, 0, 0, 0]) is None
+    # the affine first addition's own degenerate cases
+    assert _xyzz_sum(fb, [a, a], [0, 1], [0, 0]) is None
+    assert _xyzz_sum(fb, [a, a, b], [0, 0, 0], [0, 0, 0]) is None
+    # a skipped second window, then the general addition from an affine start
+    assert _xyzz_sum(fb, [a, b, b], [0, 0, 1], [0, 1, 0]) == O.point_add(a, O.point_neg(b))
+
+
 def test_fast_path_agrees_with_recovery(fb, oracle):
     O = oracle
     rng = random.Random(12)

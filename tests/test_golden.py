@@ -182,7 +182,7 @@ VARIANTS = [("default", None, None), ("verify_waves_2", "verify_waves", 2), ("ve
             ("sum_prefetch_2", "sum_prefetch", 2), ("sum_digits_rows", "sum_digits", 1), ("split_k_0", "split_k", 0),
             ("split_k_4", "split_k", 4), ("split_k_16", "split_k", 16), ("fast_waves_3", "split_k", 0),
             ("recover_glv_g", "recover_g", 1), ("key_width_16", "key_width", 16), ("key_width_20", "key_width", 20),
-            ("wave_prio_2", "wave_prio", 2), ("sum_cap_2", "sum_cap", 2), ("foreign_keys_16", "foreign_keys", 16)]
+            ("wave_prio_2", "wave_prio", 2), ("sum_cap_2", "sum_cap", 2), ("foreign_keys_0", "foreign_keys", 0)]
 
 
 @pytest.mark.gpu
@@ -200,8 +200,9 @@ def test_gpu_variants_match_golden(gpu, label, key, value):
             if label == "fast_waves_3":
                 v.set_variant("fast_waves", 3)
             v.set_signatories(z["admitted"])
-            # (foreign keys: pass 1 learns them, pass 2 builds their tables, pass 3 checks with them)
-            for rnd in range(3 if key == "foreign_keys" else 2):
+            # (foreign keys, on by default: pass 1 learns them, pass 2 builds
+            # their tables, pass 3 checks with them)
+            for rnd in range(2 if key == "foreign_keys" else 3):
                 res = v.verify_batch(b)
                 assert res.verdict.tolist() == z["verdict"].tolist(), (label, name, rnd)
                 assert res.recovered.tobytes() == z["recovered"].tobytes(), (label, name, rnd)

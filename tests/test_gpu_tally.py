@@ -45,15 +45,23 @@ def test_scenarios_match_oracle(verifier, oracle, sc):
 
 
 @pytest.mark.parametrize("kind,n,S,adv", [(0, 65536, 100, 30), (1, 128064, 1000, 10)])
-def test_generated_batches_match_oracle(verifier, oracle, kind, n, S, adv):
+def test_generated_batches_match_oracle(verifier, oracle, coracle, kind, n, S, adv):
     """GPU verify -> GPU tally == oracle tally over the same verdicts; the
-    C3 shape (kind 1) is the 1000-signatory, 64-round config."""
+    C3 shape (kind 1) is the 1000-signatory, 64-round config.  Every GPU
+    verdict and recovered signatory of the batch is the C oracle's too, on the
+    full-recovery pass and on the known-key pass (process.go:823-892 consumes
+    exactly these verdicts)."""
     from hyperdrive_amd.device import generate
     ks = verifier.gen_keys(S)
     verifier.set_signatories(ks[0])
     db, _, _ = generate(verifier, kind, n, S, adv, keys=ks)
     hb = db.to_host()
-    res, tal = verifier.process_batch(hb)
+    cv, crec = coracle.verify(hb, ks[0], True, threads=16)
+    for _ in range(2):      # the first pass learns the keys, the second checks with them
+        res, tal = verifier.process_batch(hb)
+        assert res.verdict.tolist() == cv.tolist()
+        assert res.recovered.tobytes() == crec.tobytes()
+    assert (cv == 0).sum() > n // 2
     ot = oracle.tally(from_np(hb), res.verdict.tolist())
     _same(tal, ot)
     f = quorum.thresholds(S)[0]

@@ -230,15 +230,35 @@ def test_foreign_keys_vs_c_oracle(gpu, coracle):
         assert n_foreign > 1000
         # the same batch on a context without foreign keys: its steady fallback
         # includes every NOT_ADMITTED message, this one's none of them
+        # (foreign keys are on by default: turned off here before the set, so
+        # the baseline does not depend on the environment)
         v0 = gpu.Verifier(0)
         try:
+            v0.set_variant("foreign_keys", 0)
             v0.set_signatories(ks[0])
-            for _ in range(2):
+            for _ in range(3):
                 v0.verify_batch(hb)
             base = v0.fastpath_stats()[1]
         finally:
             v0.close()
+        assert base >= n_foreign, (base, n_foreign)
         assert all(f <= base - n_foreign + 5 for f in fallback[1:]), (fallback, base, n_foreign)
+        # turning the variant off at the next set change stops the foreign
+        # check (the reserved block stays, unused): every NOT_ADMITTED message
+        # takes the full recovery again, with the same outputs
+        v.set_variant("foreign_keys", 0)
+        v.set_signatories(ks[0])
+        for _ in range(3):
+            res = v.verify_batch(hb)
+            assert res.verdict.tolist() == cv.tolist()
+            assert res.recovered.tobytes() == crec.tobytes()
+        assert v.fastpath_stats()[1] >= n_foreign
+        v.set_variant("foreign_keys", 16)
+        v.set_signatories(ks[0])
+        for _ in range(3):   # learn the foreign keys again, build, check
+            res = v.verify_batch(hb)
+            assert res.verdict.tolist() == cv.tolist()
+        assert v.fastpath_stats()[1] <= base - n_foreign + 5
         ws = work_stream()
         out = torch.empty(N, dtype=torch.uint8, device="cuda")
         v.authenticate_batch_device(db.c_struct(), out.data_ptr(), ws.cuda_stream)

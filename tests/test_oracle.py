@@ -7,6 +7,7 @@ crypto tests), OpenSSL 3's independent ECDSA implementation, and the
 reference's own property tests (sign -> Signatory(&hash) -> Equal,
 process/message_test.go:145-158; hash determinism :133-143)."""
 import hashlib
+import os
 import random
 import struct
 
@@ -134,3 +135,21 @@ def test_oracle_openssl_on_all_valid_messages(oracle):
             r = int.from_bytes(ob.sig[i][:32], "big")
             s = int.from_bytes(ob.sig[i][32:64], "big")
             assert ossl.verify(d, r, s, oracle.pubkey_bytes(Q, False)), i
+
+
+def test_glv_port_baseline_equals_c_oracle(coracle, hostmath):
+    """The 'port-glv' CPU baseline (oracle/glv_port.cpp, bench.py's
+    cpu_baseline) gives the C oracle's verdicts and recovered signatories on
+    the 30 % adversarial mix, on one and on several threads."""
+    import subprocess
+    from oracle_c import GlvPort
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "oracle")], check=True)
+    gp = GlvPort(os.path.join(root, "oracle", "_build", "libglvport.so"))
+    sigs, foreign = hostmath.keys(50, True)
+    b, _ = hostmath.gen(0, 3, 3000, 50, 30, (sigs, foreign))
+    cv, crec = coracle.verify(b, sigs, True, threads=4)
+    for th in (1, 5):
+        v, rec = gp.verify(b, sigs, True, threads=th)
+        assert v.tolist() == cv.tolist()
+        assert rec.tobytes() == crec.tobytes()

@@ -586,7 +586,7 @@ def host_buffers(v, args, sigs, foreign, dev, steps=12):
     from hyperdrive_amd.device import generate
     from hyperdrive_amd.verify import Batch, CompactBatch
     B = args.batch
-    INFLIGHT = 3    # tickets queued (the library keeps HD_HOST_SLOTS = 4 pipelines)
+    INFLIGHT = 3    # tickets queued (the library keeps HD_HOST_SLOTS = 3 pipelines)
     db, _, _ = generate(v, 0, B, args.signers, 0, keys=(sigs, foreign), device=str(dev))
     hb = db.to_host()
     if np.isin(hb.type, (2, 3)).all():

@@ -15,6 +15,7 @@ import os
 import shutil
 import subprocess
 import sys
+import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
@@ -48,16 +49,21 @@ def _mtime(p):
         return -1.0
 
 
-def _compile(src: str, force: bool) -> str:
+def _compile(src: str, force: bool):
+    """(object path, whether it was compiled now)"""
     obj = os.path.join(OBJDIR, os.path.basename(src) + ".o")
     newest = max([_mtime(src)] + [_mtime(d) for d in _deps()])
     if not force and _mtime(obj) >= newest:
-        return obj
+        return obj, False
     cmd = [HIPCC, *CFLAGS, "-c", src, "-o", obj]
+    t0 = time.time()
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")
-    return obj
+    # the object is as old as the sources it was compiled from: a source
+    # edited while hipcc ran is newer than it, so the next build recompiles
+    os.utime(obj, (t0, t0))
+    return obj, True
 
 
 def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> str:
@@ -67,8 +73,9 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
     jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 4)))
     jobs = min(jobs, 16)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force), srcs))
-    if force or _mtime(LIB) < max(_mtime(o) for o in objs):
+        done = list(ex.map(lambda s: _compile(s, force), srcs))
+    objs = [o for o, _ in done]
+    if force or any(c for _, c in done) or _mtime(LIB) < max(_mtime(o) for o in objs):
         tmp = LIB + ".tmp"
         # librccl: the hd_multi_* exchange (hd_multi.hip)
         r = subprocess.run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", *objs, "-L" + ROCM_LIB, "-lrccl",

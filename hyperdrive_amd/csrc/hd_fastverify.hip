@@ -735,11 +735,18 @@ __global__ __launch_bounds__(256) void k_fast_cmp(DevBatch b, SplitRows rows, co
 // the compacted list `out` (*n_out) that k_verify walks.  Leftovers are ~10 %
 // of a 30 %-adversarial batch, so the saving is in the recovery's throughput
 // cost, which overlapping calls expose.
+//
+// Round 4: a leftover that went through the known-key check (aux code still
+// HD_FAST_LIVE, so m and s are in the rows) and lifts is tested for the
+// INFINITY verdict with the fixed-base G table (fb_is_infinity: R == (m / s) G).
+// That class -- cheap for anyone to craft (R = k G, s = m / k) -- then costs a
+// scalar inversion and 11 additions instead of a full recovery each.
 __global__ __launch_bounds__(256) void k_slow_lift(DevBatch b, const uint32_t* __restrict__ list,
                                                    const uint32_t* __restrict__ count, uint8_t* __restrict__ verdict,
                                                    uint8_t* __restrict__ rec32, int32_t* __restrict__ signer,
                                                    uint32_t* __restrict__ out, uint32_t* __restrict__ n_out,
-                                                   int prio, uint32_t* __restrict__ est) {
+                                                   int prio, uint32_t* __restrict__ est, SplitRows rows,
+                                                   const gp* __restrict__ gtab) {
     wave_prio(prio);
     const uint32_t total = *count, stride = gridDim.x * blockDim.x;
     if (est && blockIdx.x == 0 && threadIdx.x == 0) est[0] = total;
@@ -761,7 +768,17 @@ __global__ __launch_bounds__(256) void k_slow_lift(DevBatch b, const uint32_t* _
                 fe_mul(y2, y2, x);
                 fe_set_u32(seven, 7);
                 fe_add(y2, y2, seven);
-                if (!fe_sqrt(y, y2)) pre = V_NO_POINT;
+                if (!fe_sqrt(y, y2)) {
+                    pre = V_NO_POINT;
+                } else if (gtab && rows.aux && (rows.aux[i] & 0xFFu) == HD_FAST_LIVE) {
+                    ge R;
+                    R.x = x;
+                    R.y = y;
+                    if (fe_is_odd(y) != ((v & 1u) != 0)) fe_neg(R.y, y);
+                    sc m;   // (s is sig_prefix's; m as k_fast_prep left it)
+                    soa_load(m.v, rows.u1, b.n, i);
+                    if (fb_is_infinity<HD_FB_WG>(m, s, R, GpTab{gtab})) pre = V_INFINITY;
+                }
             }
             keep = pre == V_VALID;
             if (!keep) {
@@ -1455,15 +1472,24 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         // k_fast_cmp wrote the valid bitmap; the slow path sets the bits of
         // its VALID messages
         const uint32_t full = std::min(blocks, (uint32_t)std::max(ctx->n_cu, 1) * 4u);
-        const uint32_t lift_blocks = fallback_blocks(f->est_host[0], full);
-        k_slow_lift<<<lift_blocks, 256, 0, s>>>(b, sc.slow, sc.count, d_verdict, d_rec32, d_signer, sc.slow2,
-                                                sc.count + 1, ctx->var[HD_VAR_WAVE_PRIO], f->est_dev);
-        FBCHK(hipGetLastError(), "k_slow_lift");
-        const SlowCtl ctl{sc.slow2, sc.count + 1, f->adm_slot, f->state, f->pub, d_bitmap, f->est_dev + 1,
-                          ctx->var[HD_VAR_WAVE_PRIO], f->fcap ? f->fdict : nullptr, f->fnext, f->fbase, f->fcap,
-                          f->fpend_dev};
+        // HD_VAR_SLOW_LIFT: the lift kernel first (its NO_POINT verdicts leave
+        // the list), or k_verify over the whole leftover list (it lifts too).
+        // A leftover list is usually under one wave per SIMD, so k_verify's
+        // time is one recovery's latency whatever the list length, and the
+        // separate lift only adds its own chain in series.
+        const bool lift = ctx->var[HD_VAR_SLOW_LIFT] != 0;
+        if (lift) {
+            const uint32_t lift_blocks = fallback_blocks(f->est_host[0], full);
+            k_slow_lift<<<lift_blocks, 256, 0, s>>>(b, sc.slow, sc.count, d_verdict, d_rec32, d_signer, sc.slow2,
+                                                    sc.count + 1, ctx->var[HD_VAR_WAVE_PRIO], f->est_dev, rows,
+                                                    f->gtab);
+            FBCHK(hipGetLastError(), "k_slow_lift");
+        }
+        const SlowCtl ctl{lift ? sc.slow2 : sc.slow, lift ? sc.count + 1 : sc.count, f->adm_slot, f->state, f->pub,
+                          d_bitmap, lift ? f->est_dev + 1 : f->est_dev, ctx->var[HD_VAR_WAVE_PRIO],
+                          f->fcap ? f->fdict : nullptr, f->fnext, f->fbase, f->fcap, f->fpend_dev};
         rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl,
-                            fallback_blocks(f->est_host[1], full), s);
+                            fallback_blocks(f->est_host[lift ? 1 : 0], full), s);
         if (rc) return rc;
         return fb_learn(ctx, s);
     }
@@ -1481,8 +1507,9 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         // device): a grid of 4 blocks per CU walks it, instead of one block
         // per 256 messages that would mostly start and exit
         const uint32_t slow_blocks = std::min(blocks, (uint32_t)std::max(ctx->n_cu, 1) * 4u);
+        SplitRows none{};
         k_slow_lift<<<slow_blocks, 256, 0, s>>>(b, sc.slow, sc.count, d_verdict, d_rec32, d_signer, sc.slow2,
-                                                sc.count + 1, ctx->var[HD_VAR_WAVE_PRIO], nullptr);
+                                                sc.count + 1, ctx->var[HD_VAR_WAVE_PRIO], nullptr, none, nullptr);
         FBCHK(hipGetLastError(), "k_slow_lift");
         const SlowCtl ctl{sc.slow2, sc.count + 1, f->adm_slot, f->state, f->pub, nullptr, nullptr,
                           ctx->var[HD_VAR_WAVE_PRIO], nullptr, nullptr, 0, 0, nullptr};

@@ -519,6 +519,43 @@ HD void verify_fast2(uint8_t out[2], const FastIn in[2], GT gtab, PT ptab0, PT p
     out[1] = ok1 ? fast_final(acc1, zib, x1, in[1].v) : o1;
 }
 
+// ---- the INFINITY verdict from the fixed-base G table ------------------------
+// The recovery returns the point at infinity (V_INFINITY, nothing recovered)
+// iff u2 R = -u1' G for its u1' = -m / r, u2 = s / r, i.e. iff s R = m G, i.e.
+// iff R == u1 G with u1 = m / s (n is prime, s != 0).  For a leftover of the
+// known-key check (m and s at hand) that is one scalar inversion and the
+// fixed-base G sum -- no doublings -- instead of the full recovery.  R is the
+// lifted point (y of the parity v & 1).  Returns true only when the sum is
+// exactly R; a degenerate partial sum (ZZ = 0) answers false, and the full
+// recovery then decides as before.
+template <int W, typename Tab>
+HD bool fb_is_infinity(const sc& m, const sc& s, const ge& R, Tab gtab) {
+    sc sinv, u1;
+    sc_inv_divsteps(sinv, s);
+    sc_mul(u1, m, sinv);
+    gxz acc;
+    bool started = false;
+    HD_NOUNROLL for (int j = 0; j < FbL<W>::NWIN; j++) {
+        const int d = fb_digit<W>(u1, j);
+        if (d == 0) continue;
+        ge t = gtab[(size_t)j * FbL<W>::N + (uint32_t)((d < 0 ? -d : d) - 1)];
+        if (d < 0) fe_neg(t.y, t.y);
+        if (!started) {
+            fe_norm_weak(t.y);
+            gxz_set_ge(acc, t);
+            started = true;
+        } else {
+            gxz_add_ge_nx(acc, acc, t);
+        }
+    }
+    if (!started || gxz_is_inf(acc)) return false;   // u1 G = infinity, or a degenerate sum
+    fe t;
+    fe_mul(t, R.x, acc.zz);                          // x: X == x_R ZZ
+    if (!fe_eq(acc.x, t)) return false;
+    fe_mul(t, R.y, acc.zzz);                         // y: Y == y_R ZZZ
+    return fe_eq(acc.y, t);
+}
+
 // ---- the full recovery's multiplication over the fixed-base G table --------
 // Q = u1 G + u2 R as ecmult_glv computes it, with u1 G taken out of the
 // ladder: the ladder keeps u2 R (GLV halves, 4-bit windows, 128 doublings on

@@ -359,8 +359,9 @@ int hd_verify_submit_compact(hd_ctx* ctx, const hd_batch_compact* batch, uint8_t
         if (max_u16(batch->value_idx, n) >= batch->n_values) return HD_EINVAL;
     }
     const CompactInfo ci{ctx->n_sig_caller, batch->n_escape};
-    // (an empty escape list still gets a device row: the kernel's pointer is never NULL)
-    static const uint8_t zero32[32] = {0};
+    // (no escape rows: no upload -- a tiny copy would run as a blit kernel
+    // queued behind another pipeline's kernels -- and the expansion, whose
+    // indices were checked above, never reads the table)
     const Col cols[HC_N] = {{batch->type, n},
                             {batch->height, 8 * (size_t)n},
                             {batch->round, 8 * (size_t)n},
@@ -370,8 +371,7 @@ int hd_verify_submit_compact(hd_ctx* ctx, const hd_batch_compact* batch, uint8_t
                             {batch->sig65, 65 * (size_t)n},
                             {batch->from_idx, 2 * (size_t)n},
                             {batch->value_idx, 2 * (size_t)n},
-                            {batch->n_escape ? (const void*)batch->escape32 : (const void*)zero32,
-                             32 * (size_t)std::max(batch->n_escape, 1u)},
+                            {batch->n_escape ? (const void*)batch->escape32 : nullptr, 32 * (size_t)batch->n_escape},
                             {batch->values32, 32 * (size_t)batch->n_values}};
     return submit_impl(ctx, n, cols, &ci, verdict, recovered32, valid_bitmap, ticket);
 }

@@ -36,7 +36,7 @@ struct hd_ctx {
     int device = 0;
     int n_cu = 256;
     int verify_waves = 3;   // register budget of k_verify (waves per SIMD)
-    int var[HD_VAR__COUNT] = {3, 0, 1, 0, -1, 0, 2, 0, 0, 0, 16};   // hd_ctx_set_variant (var[0] mirrors verify_waves)
+    int var[HD_VAR__COUNT] = {3, 0, 1, 0, -1, 0, 2, 0, 0, 0, 16, 1};   // hd_ctx_set_variant (var[0] mirrors verify_waves)
     hipStream_t stream = nullptr;
     int pkfmt = HD_PUBKEY_COMPRESSED;   // id.NewSignatory's pubkey encoding (hd_ctx_set_pubkey_format)
     hd::ge* d_gtab = nullptr;
@@ -70,6 +70,10 @@ int hd_dev_grow(hd_ctx* ctx, void** p, size_t* cap, size_t need);
 int hd_upload_batch(hd_ctx* ctx, const hd_batch* hb, hd_batch* db);
 int hd_verify_uploaded(hd_ctx* ctx, const hd_batch* db, uint8_t* verdict, uint8_t* recovered32, uint32_t* valid_bitmap);
 void hd_tally_release(hd_ctx* ctx);
+// hd_tally_routed_device with the per-row classification scattered on the
+// device to dup_global[global index] (hd_multi's owners; hd_tally.hip)
+int hd_tally_routed_dup_device(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* d_gidx, hd_tally_out* out,
+                               uint8_t* dup_global, hipStream_t s);
 void hd_host_release(hd_ctx* ctx);
 
 // known-key fast path (hd_fastverify.hip)

@@ -4,22 +4,28 @@
 // One context per device, one host thread per device while the devices work,
 // and one RCCL communicator over the devices (ncclCommInitAll: the
 // single-process, multi-device form a cgo caller -- one Go Replica -- needs).
-// Per hd_multi_verify_batch:
+// Per hd_multi_verify_batch, everything of a device on its context's stream:
 //   1. device k uploads its contiguous, 32-aligned shard only (every column:
-//      146 B per message, 1/G of the batch per device over PCIe);
-//   2. device k verifies it (the known-key check / full recovery of
-//      hd_verify_batch_device): verdicts, signatories, its bitmap words;
-//   3. with a tally: device k routes its shard's candidates (VALID Prevotes /
+//      146 B per message, 1/G of the batch per device over PCIe), verifies it
+//      (the known-key check / full recovery of hd_verify_batch_device) and
+//      queues the download of its verdicts, signatories and bitmap words --
+//      no host wait;
+//   2. with a tally: device k routes its shard's candidates (VALID Prevotes /
 //      Precommits) to the owners of their rounds (hd_route_candidates_device,
-//      64-byte rows); one grouped ncclSend / ncclRecv moves every group over
-//      xGMI (the only collective on the data path); device o rebuilds a batch
-//      from what it received, in global index order, and tallies it
-//      (hd_unroute_device + hd_tally_routed_device);
-//   4. the host merges the owners' disjoint tables in first-batch-index order
-//      -- the single-device output -- and scatters their per-row dup
-//      classification to the global indices (3 for non-candidates).
+//      64-byte rows; its one host read is the group sizes); one grouped
+//      ncclSend / ncclRecv moves every group over xGMI (the only collective
+//      on the data path);
+//   3. device o rebuilds a batch from what it received, in global index order,
+//      tallies it (hd_unroute_device + the routed tally) and scatters the
+//      per-row duplicate classification to the global indices of an n-byte
+//      array of its own, on the device (3 = not a candidate / not owned);
+//   4. the classifications merge by minimum on the devices (ncclReduce with
+//      ncclMin into device 0: an owner reports 0/1/2 for its rows and 3 for
+//      the rest), one download; the owners' small tables -- each already in
+//      first-batch-index order -- merge on the host by a k-way merge (no sort).
 // RCCL takes one rank per device; when a device is listed twice (e.g. two
-// contexts on one GPU in a test) step 3 moves the groups with device copies.
+// contexts on one GPU in a test) steps 2 and 4 use device copies ordered by
+// events.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -40,15 +46,18 @@ struct Dev {
     hd_ctx* ctx = nullptr;
     int device = 0;
     hipStream_t stream = nullptr;   // the ctx's stream
+    hipEvent_t routed = nullptr;    // after this device's route rows (copy exchange)
+    hipEvent_t owned = nullptr;     // after this device's dup classification (copy exchange)
     DevBuf verdict, rec, bitmap;
     DevBuf rows, recv, gidx, rb[5];  // route rows out / in, global indices, the rebuilt batch (type h r value from)
+    DevBuf dupg, dupx;              // classification at global indices (n); device 0: the other owners' (copy exchange)
     uint32_t lo = 0, hi = 0;        // shard
     std::vector<uint32_t> counts;   // route rows per owner
     uint32_t m = 0;                 // rows received
-    // this device's tally of the rounds it owns (host)
+    // this device's tally of the rounds it owns (host; grown, never shrunk)
     std::vector<int64_t> ch, cr, hh, hr;
-    std::vector<uint8_t> ct, dup;
-    std::vector<uint32_t> crep, cn, hprev, hprec, hany, hrep, gidx_h;
+    std::vector<uint8_t> ct;
+    std::vector<uint32_t> crep, cn, hprev, hprec, hany, hrep;
     uint32_t n_counts = 0, n_hr = 0;
     int rc = HD_OK;
 };
@@ -80,8 +89,11 @@ void shard(uint32_t n, int G, int k, uint32_t* lo, uint32_t* hi, uint32_t* per) 
     *hi = std::min<uint64_t>(n, (uint64_t)*lo + p);
 }
 
-// steps 1-2 on device d: its shard only
-int verify_shard(Dev& d, const hd_batch* hb, bool want_rec, hd_batch* dshard) {
+// step 1 on device d: its shard only, outputs queued for download into the
+// caller's arrays (no host wait)
+int verify_shard(Dev& d, const hd_batch* hb, uint8_t* verdict, uint8_t* recovered32, uint32_t* valid_bitmap,
+                 hd_batch* dshard) {
+    const bool want_rec = recovered32 != nullptr;
     (void)hipSetDevice(d.device);
     const uint32_t m = d.hi - d.lo;
     dshard->n = 0;
@@ -103,7 +115,15 @@ int verify_shard(Dev& d, const hd_batch* hb, bool want_rec, hd_batch* dshard) {
     rc = hd_verify_batch_device(d.ctx, dshard, (uint8_t*)d.verdict.p, want_rec ? (uint8_t*)d.rec.p : nullptr, nullptr,
                                 (uint32_t*)d.bitmap.p, d.stream);
     if (rc) return rc;
-    MCHK(hipStreamSynchronize(d.stream), "verify sync");
+    // the bitmap words of a shard are its own: shards are whole words except the last
+    MCHK(hipMemcpyAsync(verdict + d.lo, d.verdict.p, m, hipMemcpyDeviceToHost, d.stream), "verdict download");
+    if (recovered32)
+        MCHK(hipMemcpyAsync(recovered32 + 32 * lo, d.rec.p, 32 * (size_t)m, hipMemcpyDeviceToHost, d.stream),
+             "recovered download");
+    if (valid_bitmap)
+        MCHK(hipMemcpyAsync(valid_bitmap + d.lo / 32, d.bitmap.p, 4 * (size_t)((m + 31) / 32), hipMemcpyDeviceToHost,
+                            d.stream),
+             "bitmap download");
     return HD_OK;
 }
 
@@ -115,16 +135,26 @@ int route_shard(Dev& d, const hd_batch* dshard, int G) {
     if (m == 0) return HD_OK;
     int rc = hd_dev_grow(d.ctx, &d.rows.p, &d.rows.cap, (size_t)HD_ROUTE_ROW_BYTES * m);
     if (rc) return rc;
-    return hd_route_candidates_device(d.ctx, dshard, (const uint32_t*)d.bitmap.p, d.lo, (uint32_t)G,
-                                      (uint8_t*)d.rows.p, m, d.counts.data(), d.stream);
+    rc = hd_route_candidates_device(d.ctx, dshard, (const uint32_t*)d.bitmap.p, d.lo, (uint32_t)G,
+                                    (uint8_t*)d.rows.p, m, d.counts.data(), d.stream);
+    if (rc) return rc;
+    // (the rows are written by a kernel still in flight: a copy exchange on
+    // another stream waits for this event)
+    MCHK(hipEventRecord(d.routed, d.stream), "route event");
+    return HD_OK;
 }
 
 // step 3c on device d: the received rows -> a batch -> the tally of its
 // rounds (host vectors sized by what it received)
-int tally_owned(Dev& d, bool want_dup) {
+int tally_owned(Dev& d, uint32_t n, bool want_dup) {
     (void)hipSetDevice(d.device);
     const uint32_t m = d.m;
     d.n_counts = d.n_hr = 0;
+    if (want_dup) {
+        int rc = hd_dev_grow(d.ctx, &d.dupg.p, &d.dupg.cap, n);
+        if (rc) return rc;
+        MCHK(hipMemsetAsync(d.dupg.p, 3, n, d.stream), "dup clear");
+    }
     if (m == 0) return HD_OK;
     const size_t sz[5] = {m, 8 * (size_t)m, 8 * (size_t)m, 32 * (size_t)m, 32 * (size_t)m};
     for (int k = 0; k < 5; k++) {
@@ -138,9 +168,11 @@ int tally_owned(Dev& d, bool want_dup) {
     rc = hd_unroute_device(d.ctx, (const uint8_t*)d.recv.p, m, &o, (uint32_t*)d.gidx.p, d.stream);
     if (rc) return rc;
     hd_batch b{m, o.type, o.height, o.round, nullptr, o.value32, o.from32, nullptr};
-    d.ch.resize(m); d.cr.resize(m); d.ct.resize(m); d.crep.resize(m); d.cn.resize(m);
-    d.hh.resize(m); d.hr.resize(m); d.hprev.resize(m); d.hprec.resize(m); d.hany.resize(m); d.hrep.resize(m);
-    d.dup.resize(want_dup ? m : 0);
+    if (d.ch.size() < m) {   // host rows: grown, never shrunk (no per-call reallocation)
+        const size_t c = m + m / 4;
+        d.ch.resize(c); d.cr.resize(c); d.ct.resize(c); d.crep.resize(c); d.cn.resize(c);
+        d.hh.resize(c); d.hr.resize(c); d.hprev.resize(c); d.hprec.resize(c); d.hany.resize(c); d.hrep.resize(c);
+    }
     hd_tally_out t{};
     t.cap_counts = m;
     t.count_height = d.ch.data(); t.count_round = d.cr.data(); t.count_type = d.ct.data();
@@ -148,15 +180,12 @@ int tally_owned(Dev& d, bool want_dup) {
     t.cap_hr = m;
     t.hr_height = d.hh.data(); t.hr_round = d.hr.data(); t.hr_prevotes = d.hprev.data();
     t.hr_precommits = d.hprec.data(); t.hr_any = d.hany.data(); t.hr_rep = d.hrep.data();
-    t.dup = want_dup ? d.dup.data() : nullptr;
-    rc = hd_tally_routed_device(d.ctx, &b, (const uint32_t*)d.gidx.p, &t, d.stream);
+    // the classification stays on the device, scattered to global indices
+    rc = want_dup ? hd_tally_routed_dup_device(d.ctx, &b, (const uint32_t*)d.gidx.p, &t, (uint8_t*)d.dupg.p, d.stream)
+                  : hd_tally_routed_device(d.ctx, &b, (const uint32_t*)d.gidx.p, &t, d.stream);
     d.n_counts = t.n_counts;
     d.n_hr = t.n_hr;
-    if (rc || !want_dup) return rc;
-    d.gidx_h.resize(m);
-    MCHK(hipMemcpyAsync(d.gidx_h.data(), d.gidx.p, 4 * (size_t)m, hipMemcpyDeviceToHost, d.stream), "gidx download");
-    MCHK(hipStreamSynchronize(d.stream), "gidx download");
-    return HD_OK;
+    return rc;
 }
 
 template <typename F>
@@ -170,33 +199,42 @@ int on_all_devices(hd_multi* m, F f) {
     return HD_OK;
 }
 
-// the merged tally into the caller's arrays (HD_ECAP when they are too small)
-int merge_tally(hd_multi* m, uint32_t n, hd_tally_out* out) {
-    struct Ref { uint32_t rep; int dev; uint32_t row; };
-    std::vector<Ref> cr, hr;
-    for (int k = 0; k < (int)m->dev.size(); k++) {
-        const Dev& d = m->dev[k];
-        for (uint32_t j = 0; j < d.n_counts; j++) cr.push_back({d.crep[j], k, j});
-        for (uint32_t j = 0; j < d.n_hr; j++) hr.push_back({d.hrep[j], k, j});
+// The merged tally into the caller's arrays (HD_ECAP when they are too
+// small).  Each owner's rows are in first-batch-index order already (the
+// routed tally emits them by rep) and the owners' rep sets are disjoint, so a
+// k-way merge by rep gives the single-device order without sorting.
+int merge_tally(hd_multi* m, hd_tally_out* out) {
+    const int G = (int)m->dev.size();
+    uint32_t nc = 0, nh = 0;
+    for (const Dev& d : m->dev) {
+        nc += d.n_counts;
+        nh += d.n_hr;
     }
-    auto by_rep = [](const Ref& a, const Ref& b) { return a.rep < b.rep; };
-    std::sort(cr.begin(), cr.end(), by_rep);
-    std::sort(hr.begin(), hr.end(), by_rep);
-    out->n_counts = (uint32_t)cr.size();
-    out->n_hr = (uint32_t)hr.size();
-    if (out->n_counts > out->cap_counts || out->n_hr > out->cap_hr) return HD_ECAP;
-    for (size_t j = 0; j < cr.size(); j++) {
-        const Dev& d = m->dev[cr[j].dev];
-        const uint32_t r = cr[j].row;
+    out->n_counts = nc;
+    out->n_hr = nh;
+    if (nc > out->cap_counts || nh > out->cap_hr) return HD_ECAP;
+    std::vector<uint32_t> pos(G);
+    std::fill(pos.begin(), pos.end(), 0u);
+    for (uint32_t j = 0; j < nc; j++) {
+        int best = -1;
+        for (int k = 0; k < G; k++)
+            if (pos[k] < m->dev[k].n_counts && (best < 0 || m->dev[k].crep[pos[k]] < m->dev[best].crep[pos[best]]))
+                best = k;
+        const Dev& d = m->dev[best];
+        const uint32_t r = pos[best]++;
         out->count_height[j] = d.ch[r];
         out->count_round[j] = d.cr[r];
         out->count_type[j] = d.ct[r];
         out->count_rep[j] = d.crep[r];
         out->count_n[j] = d.cn[r];
     }
-    for (size_t j = 0; j < hr.size(); j++) {
-        const Dev& d = m->dev[hr[j].dev];
-        const uint32_t r = hr[j].row;
+    std::fill(pos.begin(), pos.end(), 0u);
+    for (uint32_t j = 0; j < nh; j++) {
+        int best = -1;
+        for (int k = 0; k < G; k++)
+            if (pos[k] < m->dev[k].n_hr && (best < 0 || m->dev[k].hrep[pos[k]] < m->dev[best].hrep[pos[best]])) best = k;
+        const Dev& d = m->dev[best];
+        const uint32_t r = pos[best]++;
         out->hr_height[j] = d.hh[r];
         out->hr_round[j] = d.hr[r];
         out->hr_prevotes[j] = d.hprev[r];
@@ -204,12 +242,45 @@ int merge_tally(hd_multi* m, uint32_t n, hd_tally_out* out) {
         out->hr_any[j] = d.hany[r];
         if (out->hr_rep) out->hr_rep[j] = d.hrep[r];
     }
-    if (out->dup) {
-        // non-candidates 3; each owner's rows at their global indices
-        memset(out->dup, 3, n);
-        for (const Dev& d : m->dev)
-            for (size_t j = 0; j < d.dup.size(); j++) out->dup[d.gidx_h[j]] = d.dup[j];
+    return HD_OK;
+}
+
+// k_dup_min: a[i] = min(a[i], b[i]) (the copy exchange's merge on device 0)
+__global__ __launch_bounds__(256) void k_dup_min(uint32_t n, uint8_t* __restrict__ a, const uint8_t* __restrict__ b) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) a[i] = b[i] < a[i] ? b[i] : a[i];
+}
+
+// Step 4's classification: every owner's n-byte array merged by minimum into
+// device 0's, then one download into `dup`.
+int merge_dup(hd_multi* m, uint32_t n, uint8_t* dup) {
+    Dev& d = m->dev[0];
+    const int G = (int)m->dev.size();
+    if (!m->comm.empty()) {
+        if (ncclGroupStart() != ncclSuccess) return HD_EDEVICE;
+        for (int k = 0; k < G; k++) {
+            Dev& e = m->dev[k];
+            if (ncclReduce(e.dupg.p, e.dupg.p, n, ncclUint8, ncclMin, 0, m->comm[k], e.stream) != ncclSuccess) {
+                (void)ncclGroupEnd();
+                return HD_EDEVICE;
+            }
+        }
+        if (ncclGroupEnd() != ncclSuccess) return HD_EDEVICE;
+    } else {
+        (void)hipSetDevice(d.device);
+        int rc = hd_dev_grow(d.ctx, &d.dupx.p, &d.dupx.cap, n);
+        if (rc) return rc;
+        for (int k = 1; k < G; k++) {
+            Dev& e = m->dev[k];
+            MCHK(hipStreamWaitEvent(d.stream, e.owned, 0), "dup order");
+            MCHK(hipMemcpyPeerAsync(d.dupx.p, d.device, e.dupg.p, e.device, n, d.stream), "dup gather");
+            k_dup_min<<<(n + 255) / 256, 256, 0, d.stream>>>(n, (uint8_t*)d.dupg.p, (const uint8_t*)d.dupx.p);
+            MCHK(hipGetLastError(), "k_dup_min");
+        }
     }
+    (void)hipSetDevice(d.device);
+    MCHK(hipMemcpyAsync(dup, d.dupg.p, n, hipMemcpyDeviceToHost, d.stream), "dup download");
+    MCHK(hipStreamSynchronize(d.stream), "dup download");
     return HD_OK;
 }
 
@@ -239,6 +310,12 @@ int hd_multi_create(int ngpus, const int* devices, hd_multi** out) {
             return rc;
         }
         d.stream = d.ctx->stream;
+        (void)hipSetDevice(d.device);
+        if (hipEventCreateWithFlags(&d.routed, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&d.owned, hipEventDisableTiming) != hipSuccess) {
+            hd_multi_destroy(m);
+            return HD_EDEVICE;
+        }
     }
     if (std::set<int>(list.begin(), list.end()).size() == list.size()) {
         m->comm.resize(ngpus);
@@ -259,8 +336,10 @@ int hd_multi_destroy(hd_multi* m) {
         if (!d.ctx) continue;
         (void)hipSetDevice(d.device);
         (void)hipStreamSynchronize(d.stream);
-        for (DevBuf* b : {&d.verdict, &d.rec, &d.bitmap, &d.rows, &d.recv, &d.gidx})
+        for (DevBuf* b : {&d.verdict, &d.rec, &d.bitmap, &d.rows, &d.recv, &d.gidx, &d.dupg, &d.dupx})
             if (b->p) (void)hipFree(b->p);
+        if (d.routed) (void)hipEventDestroy(d.routed);
+        if (d.owned) (void)hipEventDestroy(d.owned);
         for (DevBuf& b : d.rb)
             if (b.p) (void)hipFree(b.p);
         hd_ctx_destroy(d.ctx);
@@ -311,35 +390,24 @@ int hd_multi_verify_batch(hd_multi* m, const hd_batch* batch, uint8_t* verdict, 
     uint32_t per = 0;
     for (int k = 0; k < G; k++) shard(n, G, k, &m->dev[k].lo, &m->dev[k].hi, &per);
     std::vector<hd_batch> dshard(G);
-    // 1-2: every shard uploaded to and verified on its device
-    int rc = on_all_devices(m, [&](Dev& d, int k) { return verify_shard(d, batch, recovered32 != nullptr, &dshard[k]); });
+    // 1: every shard uploaded to, verified on and downloaded from its device,
+    // queued on the device's stream
+    int rc = on_all_devices(m, [&](Dev& d, int k) {
+        return verify_shard(d, batch, verdict, recovered32, valid_bitmap, &dshard[k]);
+    });
     if (rc) return rc;
-    // outputs of the shards (the bitmap words of a shard are its own: shards
-    // are whole words except the last)
-    for (int k = 0; k < G; k++) {
-        Dev& d = m->dev[k];
-        const uint32_t len = d.hi - d.lo;
-        if (!len) continue;
-        (void)hipSetDevice(d.device);
-        MCHK(hipMemcpyAsync(verdict + d.lo, d.verdict.p, len, hipMemcpyDeviceToHost, d.stream), "verdict download");
-        if (recovered32)
-            MCHK(hipMemcpyAsync(recovered32 + 32 * (size_t)d.lo, d.rec.p, 32 * (size_t)len, hipMemcpyDeviceToHost,
-                                d.stream),
-                 "recovered download");
-        if (valid_bitmap)
-            MCHK(hipMemcpyAsync(valid_bitmap + d.lo / 32, d.bitmap.p, 4 * (size_t)((len + 31) / 32),
-                                hipMemcpyDeviceToHost, d.stream),
-                 "bitmap download");
+    if (!tally) {
+        for (Dev& d : m->dev) {
+            (void)hipSetDevice(d.device);
+            MCHK(hipStreamSynchronize(d.stream), "output download");
+        }
+        return HD_OK;
     }
-    for (Dev& d : m->dev) {
-        (void)hipSetDevice(d.device);
-        MCHK(hipStreamSynchronize(d.stream), "output download");
-    }
-    if (!tally) return HD_OK;
-    // 3a: candidates -> route rows grouped by owner
+    // 2: candidates -> route rows grouped by owner (each device's one host
+    // read: its group sizes, after its verification)
     rc = on_all_devices(m, [&](Dev& d, int k) { return route_shard(d, &dshard[k], G); });
     if (rc) return rc;
-    // 3b: the groups to their owners, source-rank order (= global index order)
+    // the groups to their owners, source-rank order (= global index order)
     std::vector<std::vector<size_t>> soff(G, std::vector<size_t>(G + 1, 0)), roff(G, std::vector<size_t>(G + 1, 0));
     for (int k = 0; k < G; k++)
         for (int o = 0; o < G; o++) {
@@ -374,26 +442,39 @@ int hd_multi_verify_batch(hd_multi* m, const hd_batch* batch, uint8_t* verdict, 
         }
         if (ncclGroupEnd() != ncclSuccess) return HD_EDEVICE;
     } else {
+        // copies on the owner's stream, after the source's route kernel
         for (int k = 0; k < G; k++)
             for (int o = 0; o < G; o++) {
                 const size_t c = m->dev[k].counts[o];
                 if (!c) continue;
                 Dev& d = m->dev[o];
                 (void)hipSetDevice(d.device);
+                MCHK(hipStreamWaitEvent(d.stream, m->dev[k].routed, 0), "route order");
                 MCHK(hipMemcpyPeerAsync((char*)d.recv.p + RB * roff[o][k], d.device,
                                         (const char*)m->dev[k].rows.p + RB * soff[k][o], m->dev[k].device, RB * c,
                                         d.stream),
                      "route exchange");
             }
     }
-    for (Dev& d : m->dev) {
-        (void)hipSetDevice(d.device);
-        MCHK(hipStreamSynchronize(d.stream), "route exchange sync");
-    }
-    // 3c-4: each owner tallies its rounds; merged on the host
-    rc = on_all_devices(m, [&](Dev& d, int) { return tally_owned(d, tally->dup != nullptr); });
+    // 3: each owner tallies its rounds (its one host read: its table), the
+    // classification scattered to global indices on the device
+    const bool want_dup = tally->dup != nullptr;
+    rc = on_all_devices(m, [&](Dev& d, int) {
+        const int r = tally_owned(d, n, want_dup);
+        if (r || !want_dup) return r;
+        MCHK(hipEventRecord(d.owned, d.stream), "owner event");
+        return HD_OK;
+    });
     if (rc) return rc;
-    return merge_tally(m, n, tally);
+    // 4: classifications merged by minimum on the devices; tables on the host
+    if (want_dup && (rc = merge_dup(m, n, tally->dup))) return rc;
+    rc = merge_tally(m, tally);
+    if (rc) return rc;
+    for (Dev& d : m->dev) {   // the shards' output downloads
+        (void)hipSetDevice(d.device);
+        MCHK(hipStreamSynchronize(d.stream), "output download");
+    }
+    return HD_OK;
 }
 
 }  // extern "C"

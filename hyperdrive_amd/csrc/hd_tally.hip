@@ -648,10 +648,21 @@ static int table_order(hd_ctx* ctx, uint32_t n, uint32_t cap, const uint32_t* cl
 // candidate (e.g. a batch of a million single-message rounds)
 #define HD_TALLY_DENSE_MAX (64ull << 20)
 
+// dup_global[gidx[j]] = dup[j] (a routed batch's classification at its
+// global indices, in the owner's device memory: hd_multi)
+__global__ __launch_bounds__(256) void k_dup_scatter(uint32_t n, const uint8_t* __restrict__ dup,
+                                                     const uint32_t* __restrict__ gidx, uint8_t* __restrict__ dup_global) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) dup_global[gidx[j]] = dup[j];
+}
+
 // gidx (optional): the batch's messages' global indices -- the rep outputs
-// are mapped through it (a routed batch, hd_tally_routed_device)
+// are mapped through it (a routed batch, hd_tally_routed_device); with
+// dup_global the per-message classification is scattered there through gidx
+// on the device instead of being downloaded (out->dup unused)
 static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdict, const uint32_t* d_bitmap,
-                        Part part, hd_tally_out* out, hipStream_t s, const uint32_t* gidx = nullptr) {
+                        Part part, hd_tally_out* out, hipStream_t s, const uint32_t* gidx = nullptr,
+                        uint8_t* dup_global = nullptr) {
     const uint32_t n = hb->n;
     if (!ctx->tally) ctx->tally = new TallyWork();
     DevBatch b{n, hb->type, hb->height, hb->round, hb->valid_round, hb->value32, hb->from32, hb->sig65};
@@ -664,14 +675,15 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     // call's counts plus a margin; a batch with more groups than that emits and
     // downloads its rows a second time (the counts are known by then).
     TallyWork* tw = ctx->tally;
-    const size_t dup_off = 64, rows_off = dup_off + (((out->dup ? (size_t)n : 0) + 63) & ~(size_t)63);
+    const bool want_dup = out->dup || dup_global;
+    const size_t dup_off = 64, rows_off = dup_off + (((want_dup ? (size_t)n : 0) + 63) & ~(size_t)63);
     uint32_t H = tw->guess_hr, Cg = tw->guess_cnt;
     auto stage_bytes = [&](uint32_t h, uint32_t c) { return rows_off + 32 * (size_t)h + 25 * (size_t)c + 64; };
     char* st = (char*)tbuf(ctx, T_SEL, stage_bytes(H, Cg), &rc);
     uint32_t* at = (uint32_t*)tbuf(ctx, T_SORTK, 8 * (size_t)n, &rc);   // candidate flags; then at_g | at_c
     uint32_t* ccnt = (uint32_t*)tbuf(ctx, T_TMP, 4 * ((size_t)(n + HD_CHUNK - 1) / HD_CHUNK + 2), &rc);
     if (rc) return rc;
-    uint8_t* d_dup = out->dup ? (uint8_t*)(st + dup_off) : nullptr;
+    uint8_t* d_dup = want_dup ? (uint8_t*)(st + dup_off) : nullptr;
     // Items: the whole batch, or a partition's candidates compacted in batch
     // order (the rest of the tally then scales with the partition, not with
     // the replicated batch).
@@ -737,6 +749,7 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     k_tally_logs<<<grid, 256, adm_lds, s>>>(b, cand, m, gslot, rank_of, ctx->d_adm, S, ctx->adm_steps, Dd, tot, dcap, d,
                                             mask, ref, adm_lds > 0);
     k_tally_values<<<grid, 256, 0, s>>>(b, cand, m, Dd, S, d, G, C, mask, gslot, ref, d_dup);
+    if (dup_global && gidx) k_dup_scatter<<<nblk(n), 256, 0, s>>>(n, d_dup, gidx, dup_global);
     TCHK(hipGetLastError(), "tally kernels");
     rc = table_order(ctx, m, cap, C.claim, at + m, ccnt, ord + m, nullptr, tot + 1, s);
     if (rc) return rc;
@@ -771,6 +784,8 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     };
     TCHK(emit(st + rows_off, H, Cg), "tally emit");
     TCHK(hipMemcpyAsync(st, tot, 8, hipMemcpyDeviceToDevice, s), "tally counts stage");
+    // (the stage is downloaded whole; with dup_global the classification part
+    // is skipped: it starts at rows_off only when out->dup asked for it)
     const size_t total = stage_bytes(H, Cg);
     if (tw->host_cap < total) {
         if (tw->host) (void)hipHostFree(tw->host);
@@ -824,6 +839,20 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     put(out->count_rep, x.c_rep, 4 * (size_t)n_cnt);
     put(out->count_n, x.c_n, 4 * (size_t)n_cnt);
     return HD_OK;
+}
+
+// hd_tally_routed_device with the classification scattered, on the device,
+// to dup_global[global index] (n_global bytes the caller set to 3) instead of
+// being downloaded (hd_multi.hip)
+int hd_tally_routed_dup_device(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* d_gidx, hd_tally_out* out,
+                               uint8_t* dup_global, hipStream_t s) {
+    out->n_counts = out->n_hr = 0;
+    if (dbatch->n == 0) return HD_OK;
+    uint8_t* keep = out->dup;
+    out->dup = nullptr;
+    const int rc = tally_device(ctx, dbatch, nullptr, nullptr, Part{0, 1}, out, s, d_gidx, dup_global);
+    out->dup = keep;
+    return rc;
 }
 
 static bool tally_out_ok(const hd_tally_out* o) {

@@ -172,7 +172,10 @@ int hd_ctx_profile(hd_ctx* ctx, int enable);
                                    recovery's); applies from the next hd_set_signatories (reserved once per
                                    context, when the table budget allows; a later 0 stops using the block); 16 (default),
                                    0 = off [HD_FOREIGN_KEYS] */
-#define HD_VAR__COUNT 11
+#define HD_VAR_SLOW_LIFT 11     /* the known-key check's leftovers: 1 (default) a lift kernel first (x^3 + 7 a
+                                   square, else NO_POINT), then the full recovery over the rest; 0 the full
+                                   recovery over every leftover (it checks the lift itself) [HD_SLOW_LIFT] */
+#define HD_VAR__COUNT 12
 int hd_ctx_set_variant(hd_ctx* ctx, int which, int value);
 int hd_ctx_get_variant(hd_ctx* ctx, int which, int* value);
 int hd_ctx_profile_read(hd_ctx* ctx, uint32_t* calls, double* verify_ms, uint32_t* sums_launches, double* sums_ms);
@@ -223,8 +226,10 @@ int hd_authenticate_batch_device(hd_ctx* ctx, const hd_batch* dbatch, uint8_t* d
  * stay unchanged, and the output buffers valid, until the ticket's wait
  * returns.  A submit that reuses a pipeline first completes its previous
  * ticket.  Tickets start at 1; waiting on a completed ticket returns at once. */
-#define HD_HOST_SLOTS 4   /* a caller keeps up to 3 in flight: upload, verify and output store of three
-                             batches overlap (2 in flight serialise upload + verify + store) */
+#define HD_HOST_SLOTS 3   /* a caller keeps up to 3 in flight: upload, verify and output store of three
+                             batches overlap (2 in flight serialise upload + verify + store); more
+                             pipelines than the device's 4 hardware queues (with the context's own
+                             stream) would share queues and serialise behind each other */
 int hd_verify_submit(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8_t* recovered32,
                      uint32_t* valid_bitmap, uint64_t* ticket);
 int hd_verify_wait(hd_ctx* ctx, uint64_t ticket);

@@ -15,7 +15,6 @@ run() {  # name seconds cmd...
 : > gpurun_out/session.log
 for step in "$@"; do
   case $step in
-    light) run first_light 600 python scripts/first_light.py ;;
     probe) run w4_probe 240 python -u scripts/w4_probe.py base ;;
     gtest1) run pytest_gpu1 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "golden or c1 or host_pipeline or routed or multi" ;;
     bench_vs1) HD_BENCH_VSTREAMS=1 run bench_vs1 300 python bench.py --no-cpu --no-aux ;;
@@ -58,6 +57,13 @@ for step in "$@"; do
     gtest_fk) HD_FOREIGN_KEYS=16 run pytest_gpu_fk 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     bench_fk) HD_FOREIGN_KEYS=16 run bench_fk 600 python bench.py ;;
     abxyzz) run ab_xyzz 900 python -u scripts/ab_fast.py "HD_LIB=hyperdrive_amd/_lib/var/libhd_base.so" "HD_SUM_WAVES=3" "HD_SUM_WAVES=2" "HD_LIB=hyperdrive_amd/_lib/var/libhd_base.so" "HD_SUM_WAVES=3" "HD_SUM_WAVES=2" "HD_LIB=hyperdrive_amd/_lib/var/libhd_base.so AB_ADV=30" "HD_SUM_WAVES=3 AB_ADV=30" "HD_SUM_WAVES=2 AB_ADV=30" ;;
+    abprof) run ab_prof 900 bash scripts/gpu_ab_prof.sh "base:HD_LIB=hyperdrive_amd/_lib/var/libhd_base.so" "xyzz:HD_SUM_WAVES=0" "base5:HD_LIB=hyperdrive_amd/_lib/var/libhd_base.so AB_ADV=30" "xyzz5:AB_ADV=30" ;;
+    abc5) AB_VARS="sum_waves=0,2;verify_waves=3,4" AB_STREAMS=2 AB_ROUNDS=3 run ab_c5 900 python -u scripts/ab_prio.py C5 C2 ;;
+    hostpipe) run pytest_host 300 python -u -m pytest tests/test_host_pipeline.py -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread ;;
+    abc5b) AB_VARS="slow_lift=1,0;sum_waves=0,2" AB_STREAMS=2 AB_ROUNDS=3 run ab_c5b 900 python -u scripts/ab_prio.py C5 ;;
+    host_trace) run host_trace 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/host_trace -o run -- python3 scripts/host_probe.py ;;
+    swappc_bisect) run swappc_nolaunder 120 scripts/swappc_repro_nolaunder ; run swappc_nomacc 120 scripts/swappc_repro_nomacc ; run swappc_noasm 120 scripts/swappc_repro_noasm ;;
+    multitest) run pytest_multi 300 python -u -m pytest tests/test_multi_gpu.py tests/test_gpu_tally.py -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     gtest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     gputest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     gputest_all) run pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
@@ -67,7 +73,6 @@ for step in "$@"; do
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-aux --no-sub ;;
     pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 0 --no-cpu --no-aux --no-sub ;;
     pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 3 --warmup 0 --no-cpu --no-aux --no-sub ;;
-    abw) run ab_waves 600 python scripts/ab_waves.py ;;
     listc) run list_counters 120 rocprofv3 -L ;;
     pmc_stall) run pmc_stall 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_IFETCH SQ_INSTS_SMEM --output-format csv -d gpurun_out/pmc_stall -o run -- python3 bench.py --steps 3 --warmup 0 --no-cpu --no-aux --no-sub ;;
     pmc_icache) run pmc_icache 600 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQC_DCACHE_HITS SQC_DCACHE_MISSES --output-format csv -d gpurun_out/pmc_icache -o run -- python3 bench.py --steps 3 --warmup 0 --no-cpu --no-aux --no-sub ;;

@@ -606,3 +606,21 @@ extern "C" int hdh_ecmult_glv_fbg8(const uint8_t* rx, const uint8_t* ry, const u
     fe_out(out + 32, y);
     return 0;
 }
+
+// fb_is_infinity (hd_fixedbase.h) over the host's 12-bit G table: R and the
+// scalars m, s as 32-byte big-endian values; 1 iff R == (m / s) G
+extern "C" int hdh_fb_is_infinity(const uint8_t* rx, const uint8_t* ry, const uint8_t* m32, const uint8_t* s32) {
+    if (fb_gt.empty()) {   // the G table cache hdh_fb_verify uses
+        ge g;
+        g.x = gtab()[0].x;
+        g.y = gtab()[0].y;
+        fb_gt = fb_tables<HD_FB_WG>(g);
+    }
+    ge R;
+    fe_in(R.x, rx);
+    fe_in(R.y, ry);
+    sc m, s;
+    le_in(m.v, m32);
+    le_in(s.v, s32);
+    return fb_is_infinity<HD_FB_WG>(m, s, R, fb_gt.data()) ? 1 : 0;
+}

@@ -396,3 +396,30 @@ def test_misaligned_records_equal_aligned(gpu, off):
     assert torch.equal(rec_flat[off:off + 32 * n].view(n, 32), ref[2])
     assert int((ref[0] == 0).sum()) > 0 and v.fastpath_stats()[1] <= int((ref[0] != 0).sum())
     v.close()
+
+
+def test_infinity_from_the_g_table(fb, oracle):
+    """fb_is_infinity (k_slow_lift's early INFINITY verdict for leftovers of
+    the known-key check): true exactly when R == (m / s) G, i.e. when the
+    reference's recovery returns the point at infinity (s R = m G); false for
+    -R, for other R, and for m = 0; and the oracle's recovery agrees."""
+    O = oracle
+    fb.hdh_fb_is_infinity.argtypes = [ctypes.c_char_p] * 4
+    fb.hdh_fb_is_infinity.restype = ctypes.c_int
+    b32 = lambda v: v.to_bytes(32, "big")
+    rng = random.Random(31)
+    G = (O.GX, O.GY)
+    for t in range(12):
+        k = rng.randrange(1, O.N)
+        R = O.point_mul(k, G)
+        m = rng.randrange(1, O.N) if t else 0
+        s = m * pow(k, -1, O.N) % O.N if m else rng.randrange(1, O.N)
+        want = m != 0   # s R = m G by construction (m = 0: s R = 0 G impossible)
+        assert fb.hdh_fb_is_infinity(b32(R[0]), b32(R[1]), b32(m), b32(s)) == int(want), t
+        nR = O.point_neg(R)
+        assert fb.hdh_fb_is_infinity(b32(nR[0]), b32(nR[1]), b32(m), b32(s)) == 0
+        other = rng.randrange(1, O.N)
+        assert fb.hdh_fb_is_infinity(b32(R[0]), b32(R[1]), b32(m), b32(other)) == int(other == s)
+        if m and R[0] < O.N:        # the reference's recovery of (m, r = x_R, s, v = parity): infinity
+            v, _ = O.recover(b32(m), b32(R[0]) + b32(s) + bytes([R[1] & 1]))
+            assert v == O.INFINITY

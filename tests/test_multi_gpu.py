@@ -73,6 +73,10 @@ def test_routed_kernels_match_restatement(gpu, world):
     from hyperdrive_amd.shard import (merge_tally_parts, route_candidates, shard_range, tally_out,
                                       tally_routed_device, unroute)
     v = gpu.Verifier(0)
+    # the library's kernels on torch's current stream: the rows it writes are
+    # read by torch copies, and the received rows torch.cat builds are read
+    # by the library (on the context's own stream they would race)
+    cs = torch.cuda.current_stream().cuda_stream
     try:
         S, n = 50, 20_000 + 13
         ks = v.gen_keys(S)
@@ -89,7 +93,7 @@ def test_routed_kernels_match_restatement(gpu, world):
             lo, hi = shard_range(n, k, world)
             sub = DeviceBatch(hi - lo, db.type[lo:hi], db.height[lo:hi], db.round[lo:hi], db.valid_round[lo:hi],
                               db.value[lo:hi], db.frm[lo:hi], db.sig[lo:hi])
-            rows, counts = route_candidates(v, sub.c_struct(), bits.data_ptr() + 4 * (lo // 32), lo, world, 0)
+            rows, counts = route_candidates(v, sub.c_struct(), bits.data_ptr() + 4 * (lo // 32), lo, world, cs)
             want, want_counts = route_rows_np(ob, verdicts, lo, hi, world, adm)
             assert counts == want_counts
             got = rows[: sum(counts)].cpu().numpy()
@@ -100,8 +104,8 @@ def test_routed_kernels_match_restatement(gpu, world):
         parts = []
         for o in range(world):
             recv = torch.cat([sent[(k, o)] for k in range(world)]).contiguous()
-            rb, gidx = unroute(v, recv, 0)
-            local = tally_routed_device(v, rb, gidx, 0, tally_out(v, n, pinned=True), "cpu")
+            rb, gidx = unroute(v, recv, cs)
+            local = tally_routed_device(v, rb, gidx, cs, tally_out(v, n, pinned=True), "cpu")
             want = routed_tally_rows(recv.cpu().numpy(), adm)
             assert local["counts"].tolist() == want["counts"].tolist()
             assert local["hr"].tolist() == want["hr"].tolist()
@@ -111,5 +115,35 @@ def test_routed_kernels_match_restatement(gpu, world):
         assert merged["counts"].tolist() == single["counts"].tolist()
         assert merged["hr"].tolist() == single["hr"].tolist()
         assert sum(merged["counts"][:, 4].tolist()) == sum(whole.count.values())
+    finally:
+        v.close()
+
+
+def test_route_refuses_candidates_outside_the_set(gpu):
+    """A VALID candidate whose From left the admitted set after verification
+    cannot be named by a route row (rows carry the admitted index), so
+    hd_route_candidates_device refuses the batch (HD_EINVAL, with the count in
+    the context's last error) instead of tallying it under a synthetic From;
+    with the set restored the same call routes every candidate."""
+    import torch
+    from hyperdrive_amd import _lib
+    from hyperdrive_amd.device import generate
+    from hyperdrive_amd.shard import route_candidates
+    v = gpu.Verifier(0)
+    try:
+        S, n = 20, 4096
+        ks = v.gen_keys(S)
+        v.set_signatories(ks[0])
+        db, _, _ = generate(v, 0, n, S, 0, keys=ks)
+        res = v.verify_batch(db.to_host())
+        bits = torch.from_numpy(res.valid_bitmap.view(np.int32).copy()).cuda()
+        cs = torch.cuda.current_stream().cuda_stream   # ordered after the bitmap's upload
+        v.set_signatories(ks[0][: S // 2])          # half the signers leave
+        with pytest.raises(_lib.HDError) as e:
+            route_candidates(v, db.c_struct(), bits.data_ptr(), 0, 3, cs)
+        assert e.value.code == _lib.HD_EINVAL and "not in the current admitted set" in str(e.value)
+        v.set_signatories(ks[0])
+        _, counts = route_candidates(v, db.c_struct(), bits.data_ptr(), 0, 3, cs)
+        assert sum(counts) == int((res.verdict == 0).sum())
     finally:
         v.close()

@@ -663,20 +663,16 @@ HD void fast_rx(fe& x, const sc& r, uint32_t v) {
     fe_from_le(x, xw);
 }
 
-// One message per lane over a grid of whole wavefronts: the comparison of a
-// live message, the outputs of every message that has its final verdict, the
-// fallback list, and the valid bitmap -- a wavefront covers 64 consecutive
-// messages, two bitmap words written from one ballot.  Messages handed to the
-// full recovery get bit 0 here; k_verify sets theirs.
-__global__ __launch_bounds__(256) void k_fast_cmp(DevBatch b, SplitRows rows, const int32_t* __restrict__ adm_perm,
-                                                  uint8_t* __restrict__ verdict, uint8_t* __restrict__ rec32,
-                                                  int32_t* __restrict__ signer, uint32_t* __restrict__ slow,
-                                                  uint32_t* __restrict__ n_slow, uint32_t* __restrict__ bitmap,
-                                                  bool auth) {
-    wave_prio(rows.prio);
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+// The comparison of message i (zi: the inverse of its stored ZZ ZZZ, read
+// from the rows when null), its outputs when its verdict is final, its
+// place on the fallback list, and its bit of the valid bitmap.  Every lane
+// of the wavefront calls it together (ballots) for 64 consecutive, 64-aligned
+// message indices; `present` is false past the batch.
+__device__ __forceinline__ void cmp_one(const DevBatch& b, const SplitRows& rows, const int32_t* __restrict__ adm_perm,
+                       uint8_t* __restrict__ verdict, uint8_t* __restrict__ rec32, int32_t* __restrict__ signer,
+                       uint32_t* __restrict__ slow, uint32_t* __restrict__ n_slow, uint32_t* __restrict__ bitmap,
+                       bool auth, uint32_t i, bool present, const fe* zi) {
     const uint32_t n = b.n;
-    const bool present = i < n;
     uint8_t v = HD_NEEDS_SLOW;
     if (present) {
         v = (uint8_t)(rows.aux[i] & 0xFFu);
@@ -684,7 +680,8 @@ __global__ __launch_bounds__(256) void k_fast_cmp(DevBatch b, SplitRows rows, co
             fe xn, yn, w, x;
             soa_load(xn.n, rows.xyz, n, i);
             soa_load(yn.n, rows.xyz + 9 * (size_t)n, n, i);
-            soa_load(w.n, rows.pre, n, i);
+            if (zi) w = *zi;
+            else soa_load(w.n, rows.pre, n, i);
             sc r;
             soa_load(r.v, rows.u2, n, i);
             const uint32_t sv = b.sig65[65 * (size_t)i + 64];
@@ -724,6 +721,79 @@ __global__ __launch_bounds__(256) void k_fast_cmp(DevBatch b, SplitRows rows, co
             if (i0 + 32 < n) bitmap[(i0 >> 5) + 1] = (uint32_t)(ok >> 32);
         }
     }
+}
+
+// One message per lane over a grid of whole wavefronts: the comparison of a
+// live message, the outputs of every message that has its final verdict, the
+// fallback list, and the valid bitmap -- a wavefront covers 64 consecutive
+// messages, two bitmap words written from one ballot.  Messages handed to the
+// full recovery get bit 0 here; k_verify sets theirs.
+__global__ __launch_bounds__(256) void k_fast_cmp(DevBatch b, SplitRows rows, const int32_t* __restrict__ adm_perm,
+                                                  uint8_t* __restrict__ verdict, uint8_t* __restrict__ rec32,
+                                                  int32_t* __restrict__ signer, uint32_t* __restrict__ slow,
+                                                  uint32_t* __restrict__ n_slow, uint32_t* __restrict__ bitmap,
+                                                  bool auth) {
+    wave_prio(rows.prio);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    cmp_one(b, rows, adm_perm, verdict, rec32, signer, slow, n_slow, bitmap, auth, i, i < b.n, nullptr);
+}
+
+// k_fast_zinv and k_fast_cmp in one kernel (HD_VAR_FUSED_CMP): the lane that
+// inverts the ZZ ZZZ of its K messages compares them too, walking j = 0..K-1
+// (message j T + t: for each j a wavefront covers 64 consecutive, 64-aligned
+// messages, so the ballots of cmp_one hold).  No Z^-1 rows are written and
+// read back, and the comparison's 1M lanes of launch and loads disappear; the
+// inversion kernel's chain grows by K comparisons.
+template <int K>
+__global__ __launch_bounds__(256) void k_fast_zinv_cmp(DevBatch b, uint32_t T, SplitRows rows,
+                                                       const int32_t* __restrict__ adm_perm,
+                                                       uint8_t* __restrict__ verdict, uint8_t* __restrict__ rec32,
+                                                       int32_t* __restrict__ signer, uint32_t* __restrict__ slow,
+                                                       uint32_t* __restrict__ n_slow, uint32_t* __restrict__ bitmap,
+                                                       bool auth) {
+    static_assert(K >= 2 && (K & (K - 1)) == 0, "K: a power of two");
+    wave_prio(rows.prio);
+    const uint32_t n = b.n;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool lane_on = t < T;
+    const uint32_t* zrow = rows.xyz + 18 * (size_t)n;
+    fe node[2 * K];
+    uint32_t live = 0;
+    static_for<K>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        const uint32_t i = (uint32_t)j * T + t;
+        const bool in = lane_on && i < n;
+        const uint32_t ic = in ? i : 0;
+        const uint32_t a = rows.aux[ic];
+        fe z;
+        soa_load(z.n, zrow, n, ic);
+        const bool on = in && (a & 0xFFu) == HD_FAST_LIVE;
+        live |= on ? 1u << j : 0u;
+        HD_UNROLL for (int k = 1; k < 9; k++) z.n[k] = on ? z.n[k] : 0u;
+        z.n[0] = on ? z.n[0] : 1u;
+        node[K + j] = z;
+    });
+    if (__ballot(live != 0) != 0ull) {   // (a lane without live messages inverts ones)
+        static_for<K - 1>([&](auto ic) {
+            constexpr int i = K - 1 - decltype(ic)::value;
+            fe_mul(node[i], node[2 * i], node[2 * i + 1]);
+        });
+        fe_inv_divsteps(node[1], node[1]);   // a product of non-zero ZZ ZZZ (and ones): never 0
+        static_for<K - 1>([&](auto ic) {
+            constexpr int i = 1 + decltype(ic)::value;
+            fe a, c;
+            fe_mul(a, node[i], node[2 * i + 1]);
+            fe_mul(c, node[i], node[2 * i]);
+            node[2 * i] = a;
+            node[2 * i + 1] = c;
+        });
+    }
+    static_for<K>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        const uint32_t i = (uint32_t)j * T + t;
+        cmp_one(b, rows, adm_perm, verdict, rec32, signer, slow, n_slow, bitmap, auth, i, lane_on && i < n,
+                &node[K + j]);
+    });
 }
 
 // Before the full recovery of the leftovers: the reference's first checks
@@ -1377,6 +1447,12 @@ static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest
     if (dl) launch_sums<WP, true>(ctx, nb, s, n, f->gtab, f->tabs, rows);
     else launch_sums<WP, false>(ctx, nb, s, n, f->gtab, f->tabs, rows);
     if (pe) (void)hipEventRecord(pe[1], s);
+    if (ctx->var[HD_VAR_FUSED_CMP]) {
+        // T is a multiple of 64: each j step of a wavefront is one bitmap word pair
+        k_fast_zinv_cmp<K><<<tb, 256, 0, s>>>(b, T, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer, sc.slow,
+                                              sc.count, d_bitmap, auth);
+        return;
+    }
     k_fast_zinv<K><<<tb, 256, 0, s>>>(n, T, rows);
     // whole blocks of 256: every wavefront's 64 messages are one bitmap word pair
     k_fast_cmp<<<nb, 256, 0, s>>>(b, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer, sc.slow, sc.count,

@@ -175,7 +175,10 @@ int hd_ctx_profile(hd_ctx* ctx, int enable);
 #define HD_VAR_SLOW_LIFT 11     /* the known-key check's leftovers: 1 (default) a lift kernel first (x^3 + 7 a
                                    square, else NO_POINT), then the full recovery over the rest; 0 the full
                                    recovery over every leftover (it checks the lift itself) [HD_SLOW_LIFT] */
-#define HD_VAR__COUNT 12
+#define HD_VAR_FUSED_CMP 12     /* the known-key check's last step: 0 (default) an inversion kernel then a
+                                   comparison kernel, 1 one kernel whose lanes compare the K messages whose
+                                   ZZ ZZZ they inverted [HD_FUSED_CMP] */
+#define HD_VAR__COUNT 13
 int hd_ctx_set_variant(hd_ctx* ctx, int which, int value);
 int hd_ctx_get_variant(hd_ctx* ctx, int which, int* value);
 int hd_ctx_profile_read(hd_ctx* ctx, uint32_t* calls, double* verify_ms, uint32_t* sums_launches, double* sums_ms);

@@ -92,7 +92,7 @@ def parse():
                     help="priority of the tally stream")
     ap.add_argument("--no-aux", action="store_true", help="skip the SURVEY §8(f) side measurements")
     ap.add_argument("--no-sub", action="store_true", help="skip the C3 / C5 sub-benchmarks")
-    ap.add_argument("--sub-steps", type=int, default=8)
+    ap.add_argument("--sub-steps", type=int, default=20)
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank) or gloo: a rehearsal of the N > 1 path with ranks "
                          "sharing the visible GPUs and host-side collectives")

@@ -65,6 +65,7 @@ for step in "$@"; do
     swappc_bisect) run swappc_nolaunder 120 scripts/swappc_repro_nolaunder ; run swappc_nomacc 120 scripts/swappc_repro_nomacc ; run swappc_noasm 120 scripts/swappc_repro_noasm ;;
     multitest) run pytest_multi 300 python -u -m pytest tests/test_multi_gpu.py tests/test_gpu_tally.py -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     abfused) AB_VARS="fused_cmp=0,1" AB_STREAMS=1,2 AB_ROUNDS=3 run ab_fused 900 python -u scripts/ab_prio.py C2 C5 ;;
+    abg26) run ab_g26 900 bash scripts/gpu_ab_prof.sh "g24a:HD_SUM_WAVES=0" "g26a:HD_LIB=hyperdrive_amd/_lib/var/libhd_g26.so" "g24b:HD_SUM_WAVES=0" "g26b:HD_LIB=hyperdrive_amd/_lib/var/libhd_g26.so" ;;
     gtest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     gputest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     gputest_all) run pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;

@@ -179,9 +179,29 @@ int complete(hd_ctx* ctx, HostSlot& s) {
     return HD_OK;
 }
 
+// Each pipeline's stream gets a hardware queue of its own: a stream created
+// with a CU mask (here every CU) is given a dedicated queue, while ordinary
+// streams share the device's GPU_MAX_HW_QUEUES (4).  Two pipelines on one
+// shared queue run in FIFO order, so one pipeline's output-store kernel
+// (~0.7 ms of PCIe writes per 1M) held back the other's expansion and
+// verification (rocprofv3 trace, round 4).  HD_HOST_CUMASK=0 uses ordinary
+// streams (A/B).
+bool host_cumask_streams() {
+    static const bool on = !(getenv("HD_HOST_CUMASK") && strcmp(getenv("HD_HOST_CUMASK"), "0") == 0);
+    return on;
+}
+
 int slot_init(hd_ctx* ctx, HostSlot& s) {
     if (s.stream) return HD_OK;
-    HCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "host pipeline stream");
+    bool made = false;
+    if (host_cumask_streams()) {
+        const int ncu = std::max(ctx->n_cu, 1);
+        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0xFFFFFFFFu);
+        if (ncu % 32) mask.back() = (1u << (ncu % 32)) - 1u;
+        made = hipExtStreamCreateWithCUMask(&s.stream, (uint32_t)mask.size(), mask.data()) == hipSuccess;
+        if (!made) (void)hipGetLastError();
+    }
+    if (!made) HCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "host pipeline stream");
     HCHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "host pipeline event");
     return HD_OK;
 }

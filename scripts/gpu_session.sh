@@ -66,7 +66,6 @@ for step in "$@"; do
     multitest) run pytest_multi 300 python -u -m pytest tests/test_multi_gpu.py tests/test_gpu_tally.py -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     abfused) AB_VARS="fused_cmp=0,1" AB_STREAMS=1,2 AB_ROUNDS=3 run ab_fused 900 python -u scripts/ab_prio.py C2 C5 ;;
     abg26) run ab_g26 900 bash scripts/gpu_ab_prof.sh "g24a:HD_SUM_WAVES=0" "g26a:HD_LIB=hyperdrive_amd/_lib/var/libhd_g26.so" "g24b:HD_SUM_WAVES=0" "g26b:HD_LIB=hyperdrive_amd/_lib/var/libhd_g26.so" ;;
-    abg26k22) run ab_g26k22 900 bash scripts/gpu_ab_prof.sh "w2420a:HD_SUM_WAVES=0" "w2622a:HD_LIB=hyperdrive_amd/_lib/var/libhd_g26k22.so HD_FB_MAX_BYTES=200000000000" "w2420b:HD_SUM_WAVES=0" "w2622b:HD_LIB=hyperdrive_amd/_lib/var/libhd_g26k22.so HD_FB_MAX_BYTES=200000000000" ;;
     gtest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     gputest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     gputest_all) run pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;

@@ -109,6 +109,13 @@ struct FbWork {
     hipStream_t last = nullptr;
     bool any = false;
     bool steady = false;          // the previous call ran with nothing to learn
+    // HD_VAR_SUM_CHAIN: k_fast_sums of consecutive calls run one after the
+    // other whatever their streams (a call's sums waits for the previous
+    // call's), so that only one call's sums holds the SIMDs at a time and the
+    // other calls' short kernels run beside it instead of in lockstep
+    hipEvent_t sums_done = nullptr;
+    hipStream_t sums_last = nullptr;
+    bool sums_any = false;
     // hd_ctx_profile: event pairs around whole calls and around k_fast_sums
     bool prof = false;
     std::vector<hipEvent_t> ev_call, ev_sums;
@@ -648,6 +655,155 @@ __global__ __launch_bounds__(256) void k_fast_zinv(uint32_t n, uint32_t T, Split
         constexpr int j = decltype(jc)::value;
         if ((live >> j) & 1u) soa_store(rows.pre, n, (uint32_t)j * T + t, node[K + j].n);
     });
+}
+
+// Lean forms of the two inversion kernels (HD_VAR_LEAN_INV): the same
+// inverses from one inversion per lane, but a linear walk whose prefix
+// products go to the pre row of each message (which later receives that
+// message's inverse), with each step's inputs loaded one live message ahead,
+// instead of K inputs and K prefixes (or a product tree) in registers.  Far
+// fewer VGPRs than 368 / 397: a running k_fast_sums held at two waves per
+// SIMD (HD_VAR_SUM_CAP) leaves room for them, so with HD_VAR_SUM_CHAIN one
+// call's inversions run beside another call's sums.
+HD uint32_t live_mask(const SplitRows& rows, uint32_t n, uint32_t T, uint32_t t, int K) {
+    uint32_t live = 0;
+    for (int j = 0; j < K; j++) {
+        const uint32_t i = (uint32_t)j * T + t;
+        if (i < n && (rows.aux[i] & 0xFFu) == HD_FAST_LIVE) live |= 1u << j;
+    }
+    return live;
+}
+HD int hi_bit(uint32_t m) { return 31 - __builtin_clz(m); }
+
+template <int K>
+__global__ __launch_bounds__(256) void k_fast_sinv_lean(uint32_t n, uint32_t T, SplitRows rows) {
+    wave_prio(rows.prio);
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const uint32_t live = live_mask(rows, n, T, t, K);
+    if (!live) return;
+    // forward: acc = the product of the live messages up to j, into pre[j]
+    sm acc;
+    sc nx;
+    uint32_t m = live;
+    soa_load(nx.v, rows.s, n, (uint32_t)(__ffs(m) - 1) * T + t);
+    bool first = true;
+    HD_NOUNROLL while (m) {
+        const uint32_t j = (uint32_t)(__ffs(m) - 1);
+        m &= m - 1;
+        const sc cur = nx;
+        if (m) soa_load(nx.v, rows.s, n, (uint32_t)(__ffs(m) - 1) * T + t);
+        sm ss;
+        sm_from_sc(ss, cur);
+        if (first) acc = ss;
+        else sm_mul(acc, acc, ss);
+        first = false;
+        soa_store(rows.pre, n, j * T + t, acc.n);
+    }
+    sm inv;
+    {
+        sc p, pinv;
+        sm_to_sc(p, acc);
+        sc_inv_divsteps(pinv, p);   // a product of scalars in [1, n) times R^-k: never 0
+        sm_from_sc(inv, pinv);
+        sm r2;
+        sm_r2(r2);
+        sm_mul(inv, inv, r2);
+    }
+    // backward: s_j^-1 = inv * pre[previous live], then inv *= s_j
+    m = live;
+    sm prev;
+    sc sj;
+    {
+        const int j = hi_bit(m);
+        const uint32_t below = m & ((1u << j) - 1u);
+        if (below) {
+            soa_load(prev.n, rows.pre, n, (uint32_t)hi_bit(below) * T + t);
+            soa_load(sj.v, rows.s, n, (uint32_t)j * T + t);
+        }
+    }
+    HD_NOUNROLL while (m) {
+        const int j = hi_bit(m);
+        m &= ~(1u << j);
+        const uint32_t i = (uint32_t)j * T + t;
+        if (!m) {
+            soa_store(rows.pre, n, i, inv.n);
+            break;
+        }
+        const sm pv = prev;
+        const sc sv = sj;
+        {   // the next step's inputs, loaded ahead
+            const int jn = hi_bit(m);
+            const uint32_t below = m & ((1u << jn) - 1u);
+            if (below) {
+                soa_load(prev.n, rows.pre, n, (uint32_t)hi_bit(below) * T + t);
+                soa_load(sj.v, rows.s, n, (uint32_t)jn * T + t);
+            }
+        }
+        sm sinv, ss;
+        sm_mul(sinv, inv, pv);
+        sm_from_sc(ss, sv);
+        sm_mul(inv, inv, ss);
+        soa_store(rows.pre, n, i, sinv.n);
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_fast_zinv_lean(uint32_t n, uint32_t T, SplitRows rows) {
+    wave_prio(rows.prio);
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const uint32_t* zrow = rows.xyz + 18 * (size_t)n;
+    const uint32_t live = live_mask(rows, n, T, t, K);
+    if (!live) return;
+    fe acc, nx;
+    uint32_t m = live;
+    soa_load(nx.n, zrow, n, (uint32_t)(__ffs(m) - 1) * T + t);
+    bool first = true;
+    HD_NOUNROLL while (m) {
+        const uint32_t j = (uint32_t)(__ffs(m) - 1);
+        m &= m - 1;
+        const fe cur = nx;
+        if (m) soa_load(nx.n, zrow, n, (uint32_t)(__ffs(m) - 1) * T + t);
+        if (first) acc = cur;
+        else fe_mul(acc, acc, cur);
+        first = false;
+        soa_store(rows.pre, n, j * T + t, acc.n);
+    }
+    fe inv;
+    fe_inv_divsteps(inv, acc);   // a product of non-zero Z: never 0
+    m = live;
+    fe prev, zj;
+    {
+        const int j = hi_bit(m);
+        const uint32_t below = m & ((1u << j) - 1u);
+        if (below) {
+            soa_load(prev.n, rows.pre, n, (uint32_t)hi_bit(below) * T + t);
+            soa_load(zj.n, zrow, n, (uint32_t)j * T + t);
+        }
+    }
+    HD_NOUNROLL while (m) {
+        const int j = hi_bit(m);
+        m &= ~(1u << j);
+        const uint32_t i = (uint32_t)j * T + t;
+        if (!m) {
+            soa_store(rows.pre, n, i, inv.n);
+            break;
+        }
+        const fe pv = prev, zv = zj;
+        {
+            const int jn = hi_bit(m);
+            const uint32_t below = m & ((1u << jn) - 1u);
+            if (below) {
+                soa_load(prev.n, rows.pre, n, (uint32_t)hi_bit(below) * T + t);
+                soa_load(zj.n, zrow, n, (uint32_t)jn * T + t);
+            }
+        }
+        fe zi;
+        fe_mul(zi, inv, pv);
+        fe_mul(inv, inv, zv);
+        soa_store(rows.pre, n, i, zi.n);
+    }
 }
 
 // x = r (+ n when v & 2) as a field element: the x coordinate of R (the range
@@ -1205,6 +1361,7 @@ void hd_fb_release(hd_ctx* ctx) {
     FbWork* f = ctx->fb;
     fb_free_tables(ctx);
     if (f->done) (void)hipEventDestroy(f->done);
+    if (f->sums_done) (void)hipEventDestroy(f->sums_done);
     for (hipEvent_t e : f->ev_call) (void)hipEventDestroy(e);
     for (hipEvent_t e : f->ev_sums) (void)hipEventDestroy(e);
     for (auto& sc : f->sc) {
@@ -1439,21 +1596,34 @@ static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest
     const size_t adm_lds = adm_lds_bytes(ctx->n_adm);
     k_fast_prep<<<nb, 256, adm_lds, s>>>(b, d_digest, f->state, f->adm_slot, ctx->d_adm, ctx->n_adm, ctx->adm_steps,
                                          rows, adm_lds > 0, f->fcap ? f->fdict : nullptr);
-    k_fast_sinv<K><<<tb, 256, 0, s>>>(n, T, rows);
+    const bool lean = ctx->var[HD_VAR_LEAN_INV] != 0;
+    if (lean) k_fast_sinv_lean<K><<<tb, 256, 0, s>>>(n, T, rows);
+    else k_fast_sinv<K><<<tb, 256, 0, s>>>(n, T, rows);
     const bool dl = sums_digits_lds(ctx);
     if (!dl) k_fast_digits<WP><<<nb, 256, 0, s>>>(n, rows);
+    const bool chain = ctx->var[HD_VAR_SUM_CHAIN] != 0;
+    if (chain) {
+        if (!f->sums_done) (void)hipEventCreateWithFlags(&f->sums_done, hipEventDisableTiming);
+        if (f->sums_any && f->sums_last != s) (void)hipStreamWaitEvent(s, f->sums_done, 0);
+    }
     hipEvent_t* pe = fb_prof_pair(f->ev_sums, f->n_sums, f->prof);
     if (pe) (void)hipEventRecord(pe[0], s);
     if (dl) launch_sums<WP, true>(ctx, nb, s, n, f->gtab, f->tabs, rows);
     else launch_sums<WP, false>(ctx, nb, s, n, f->gtab, f->tabs, rows);
     if (pe) (void)hipEventRecord(pe[1], s);
+    if (chain && f->sums_done) {
+        (void)hipEventRecord(f->sums_done, s);
+        f->sums_last = s;
+        f->sums_any = true;
+    }
     if (ctx->var[HD_VAR_FUSED_CMP]) {
         // T is a multiple of 64: each j step of a wavefront is one bitmap word pair
         k_fast_zinv_cmp<K><<<tb, 256, 0, s>>>(b, T, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer, sc.slow,
                                               sc.count, d_bitmap, auth);
         return;
     }
-    k_fast_zinv<K><<<tb, 256, 0, s>>>(n, T, rows);
+    if (lean) k_fast_zinv_lean<K><<<tb, 256, 0, s>>>(n, T, rows);
+    else k_fast_zinv<K><<<tb, 256, 0, s>>>(n, T, rows);
     // whole blocks of 256: every wavefront's 64 messages are one bitmap word pair
     k_fast_cmp<<<nb, 256, 0, s>>>(b, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer, sc.slow, sc.count,
                                   d_bitmap, auth);

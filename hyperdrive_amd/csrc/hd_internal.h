@@ -36,7 +36,7 @@ struct hd_ctx {
     int device = 0;
     int n_cu = 256;
     int verify_waves = 3;   // register budget of k_verify (waves per SIMD)
-    int var[HD_VAR__COUNT] = {3, 0, 1, 0, -1, 0, 2, 0, 0, 0, 16, 1, 0};   // hd_ctx_set_variant (var[0] mirrors verify_waves)
+    int var[HD_VAR__COUNT] = {3, 0, 1, 0, -1, 0, 2, 0, 0, 0, 16, 1, 0, 0, 0};   // hd_ctx_set_variant (var[0] mirrors verify_waves)
     hipStream_t stream = nullptr;
     int pkfmt = HD_PUBKEY_COMPRESSED;   // id.NewSignatory's pubkey encoding (hd_ctx_set_pubkey_format)
     hd::ge* d_gtab = nullptr;

@@ -205,7 +205,8 @@ int hd_ctx_create(int device, hd_ctx** out) {
         {HD_VAR_FAST_WAVES, "HD_FAST_WAVES"},     {HD_VAR_KEY_WIDTH, "HD_FB_PW"},
         {HD_VAR_WAVE_PRIO, "HD_WAVE_PRIO"},       {HD_VAR_SUM_CAP, "HD_SUM_CAP"},
         {HD_VAR_FOREIGN_KEYS, "HD_FOREIGN_KEYS"}, {HD_VAR_SLOW_LIFT, "HD_SLOW_LIFT"},
-        {HD_VAR_FUSED_CMP, "HD_FUSED_CMP"},
+        {HD_VAR_FUSED_CMP, "HD_FUSED_CMP"},       {HD_VAR_LEAN_INV, "HD_LEAN_INV"},
+        {HD_VAR_SUM_CHAIN, "HD_SUM_CHAIN"},
     };
     for (auto& ev : envs)
         if (const char* e = getenv(ev.env)) (void)hd_ctx_set_variant(ctx, ev.key, atoi(e));
@@ -268,7 +269,7 @@ int hd_ctx_set_variant(hd_ctx* ctx, int which, int value) {
         case HD_VAR_WAVE_PRIO: ok = value >= 0 && value <= 3; break;
         case HD_VAR_SUM_CAP: ok = value == 0 || value == 2; break;
         case HD_VAR_FOREIGN_KEYS: ok = value >= 0 && value <= 64; break;
-        case HD_VAR_SLOW_LIFT: case HD_VAR_FUSED_CMP: ok = value == 0 || value == 1; break;
+        case HD_VAR_SLOW_LIFT: case HD_VAR_FUSED_CMP: case HD_VAR_LEAN_INV: case HD_VAR_SUM_CHAIN: ok = value == 0 || value == 1; break;
     }
     if (!ok) return HD_EINVAL;
     ctx->var[which] = value;

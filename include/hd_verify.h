@@ -178,7 +178,14 @@ int hd_ctx_profile(hd_ctx* ctx, int enable);
 #define HD_VAR_FUSED_CMP 12     /* the known-key check's last step: 0 (default) an inversion kernel then a
                                    comparison kernel, 1 one kernel whose lanes compare the K messages whose
                                    ZZ ZZZ they inverted [HD_FUSED_CMP] */
-#define HD_VAR__COUNT 13
+#define HD_VAR_LEAN_INV 13      /* the known-key check's inversion kernels: 0 (default) the lane's K inputs and
+                                   prefixes in registers, 1 the lean forms (prefixes in the rows, inputs
+                                   loaded one step ahead; few VGPRs, so they fit beside a running
+                                   k_fast_sums held at two waves per SIMD) [HD_LEAN_INV] */
+#define HD_VAR_SUM_CHAIN 14     /* 1: the k_fast_sums of consecutive verify calls run one after the other,
+                                   whatever their streams, so that the short kernels of one call run beside
+                                   the sums of another; 0 (default) no such order [HD_SUM_CHAIN] */
+#define HD_VAR__COUNT 15
 int hd_ctx_set_variant(hd_ctx* ctx, int which, int value);
 int hd_ctx_get_variant(hd_ctx* ctx, int which, int* value);
 int hd_ctx_profile_read(hd_ctx* ctx, uint32_t* calls, double* verify_ms, uint32_t* sums_launches, double* sums_ms);

@@ -66,6 +66,9 @@ for step in "$@"; do
     multitest) run pytest_multi 300 python -u -m pytest tests/test_multi_gpu.py tests/test_gpu_tally.py -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     abfused) AB_VARS="fused_cmp=0,1" AB_STREAMS=1,2 AB_ROUNDS=3 run ab_fused 900 python -u scripts/ab_prio.py C2 C5 ;;
     abg26) run ab_g26 900 bash scripts/gpu_ab_prof.sh "g24a:HD_SUM_WAVES=0" "g26a:HD_LIB=hyperdrive_amd/_lib/var/libhd_g26.so" "g24b:HD_SUM_WAVES=0" "g26b:HD_LIB=hyperdrive_amd/_lib/var/libhd_g26.so" ;;
+    goldlean) run pytest_goldlean 600 python -u -m pytest tests/test_golden.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "lean" ;;
+    abchain) AB_VARS="sum_chain=0,1;sum_cap=0,2;lean_inv=0,1" AB_STREAMS=2,3 AB_ROUNDS=2 run ab_chain 900 python -u scripts/ab_prio.py C2 C5 ;;
+    trace_chain) HD_SUM_CHAIN=1 HD_SUM_CAP=2 HD_LEAN_INV=1 run trace_chain 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_chain -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub ;;
     gtest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     gputest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     gputest_all) run pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;

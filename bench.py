@@ -137,7 +137,7 @@ class Pipeline:
     each owner tallies what it received (hd_tally_routed_device) and the
     owners' small tables are all-gathered and merged (gather_tally_device)."""
     NBUF = int(os.environ.get("HD_BENCH_NBUF", 4))
-    VSTREAMS = int(os.environ.get("HD_BENCH_VSTREAMS", 2))
+    VSTREAMS = int(os.environ.get("HD_BENCH_VSTREAMS", 3))
 
     def __init__(self, v, db, total, lo, rank, world, dist, ws, ts, tally=True):
         import torch

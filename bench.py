@@ -119,6 +119,22 @@ def glv_port():
     return GlvPort(os.path.join(ROOT, "oracle", "_build", "libglvport.so"))
 
 
+_EXTRA = {}
+
+
+def _extra_streams(dev, priority, k):
+    """The extra verify streams, created once per device and shared by every
+    Pipeline of the process: the runtime maps streams onto the device's few
+    hardware queues (GPU_MAX_HW_QUEUES, 4) round robin, so streams created per
+    Pipeline would end up sharing a queue with the headline's or the tally's
+    and serialise behind its kernels."""
+    import torch
+    have = _EXTRA.setdefault((str(dev), priority), [])
+    while len(have) < k:
+        have.append(torch.cuda.Stream(device=dev, priority=priority))
+    return have[:k]
+
+
 class Pipeline:
     """verify (library streams `ws`, alternating) -> tally (stream `ts`) for
     one batch shape, with NBUF output buffers: the tally of step k runs on its
@@ -148,7 +164,7 @@ class Pipeline:
         self.dev = dev
         B = db.n
         assert B % 32 == 0
-        self.wss = [ws] + [torch.cuda.Stream(device=dev, priority=ws.priority) for _ in range(self.VSTREAMS - 1)]
+        self.wss = [ws] + _extra_streams(dev, ws.priority, self.VSTREAMS - 1)
         self.shard = db.c_struct()
         self.verdicts = [torch.empty(B, dtype=torch.uint8, device=dev) for _ in range(self.NBUF)]
         self.recovered = [torch.empty((B, 32), dtype=torch.uint8, device=dev) for _ in range(self.NBUF)]
@@ -505,7 +521,7 @@ def sub_benchmarks(args, v, sigs, foreign, dev, ws, ts):
     B = args.batch
     db5, _, _ = generate(v, 0, B, args.signers, 30, keys=(sigs, foreign), device=str(dev))
     p5 = Pipeline(v, db5, B, 0, 0, 1, None, ws, ts)
-    p5.run(2)
+    p5.run(4)
     el = timed(p5, args.sub_steps, None, dev)
     vd, rec5, _ = p5.last(args.sub_steps)
     out["C5_adversarial_30pct"] = {"oracle_sample_check": oracle_sample_check(db5, vd, rec5, sigs),

@@ -9,6 +9,7 @@
 #include <cstdlib>
 
 #include "../hyperdrive_amd/csrc/hd_group.h"
+#include "fe8_proto.h"
 
 using namespace hd;
 
@@ -166,6 +167,18 @@ __global__ __launch_bounds__(256, 3) void k_bench(uint32_t iters, uint32_t* out)
         if (OP == 5) fe_normalize(a);
         if (OP == 6) { fe x = a; fe_inv_divsteps(a, x); }
     }
+    if (OP == 8 || OP == 9) {   // 8 x 32-bit words with carry-out mads (hd_fe8.h)
+        fe8 x, y;
+        fe_normalize(a);
+        fe_normalize(b);
+        fe_to_le(x.w, a);
+        fe_to_le(y.w, b);
+        for (uint32_t it = 0; it < iters; it++) {
+            if (OP == 8) fe8_mul(x, x, y);
+            else fe8_sqr(x, x);
+        }
+        fe_from_fe8(a, x);
+    }
     if (OP == 7) {   // the FP64 product chain (its own loop: f5 state)
         f5 x, y;
         f5_from_fe(x, a);
@@ -179,8 +192,8 @@ __global__ __launch_bounds__(256, 3) void k_bench(uint32_t iters, uint32_t* out)
 }
 
 static const char* NAMES[] = {"fe_mul", "fe_sqr", "gej_dbl", "gej_add_ge", "gej_add", "fe_normalize", "fe_inv_divsteps",
-                              "f5_mul (FP64 FMA)"};
-#define NOPS 8
+                              "f5_mul (FP64 FMA)", "fe8_mul", "fe8_sqr"};
+#define NOPS 10
 
 // f5_mul against fe_mul: a chain of `iters` products from the same seeds,
 // canonical results compared per lane (count of mismatching lanes)
@@ -206,6 +219,49 @@ __global__ __launch_bounds__(256) void k_f5_check(uint32_t iters, uint32_t* bad)
     fe_normalize(a);
     uint32_t d = 0;
     for (int i = 0; i < 9; i++) d |= a.n[i] ^ c.n[i];
+    if (d) atomicAdd(bad, 1u);
+}
+
+// fe8_mul / fe8_sqr against fe_mul / fe_sqr: chains of `iters` steps from the
+// same seeds (extremes on lane 0: p - 1), canonical results compared per lane
+__global__ __launch_bounds__(256) void k_fe8_check(uint32_t iters, uint32_t* bad) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    fe a, b;
+    seed_fe(a, t * 7 + 1);
+    seed_fe(b, t * 13 + 5);
+    if (t == 0) {
+        for (int i = 0; i < 9; i++) a.n[i] = b.n[i] = fe_p_limb(i);
+        a.n[0] -= 1;
+        b.n[0] -= 1;
+    }
+    fe_normalize(a);
+    fe_normalize(b);
+    fe8 x, y, z;
+    fe_to_le(x.w, a);
+    fe_to_le(y.w, b);
+    z = x;
+    fe c = a;
+    for (uint32_t it = 0; it < iters; it++) {
+        fe_mul(a, a, b);
+        fe8_mul(x, x, y);
+        fe_sqr(c, c);
+        fe8_sqr(z, z);
+        fe8 d;   // sums and differences along the way: (x - y) + y == x
+        fe8_sub(d, x, y);
+        fe8_add(d, d, y);
+        fe8_sub(d, d, x);
+        fe8_canon(d);
+        uint32_t nz = 0;
+        for (int i = 0; i < 8; i++) nz |= d.w[i];
+        if (nz) atomicAdd(bad + 1, 1u);
+    }
+    fe u, v;
+    fe_from_fe8(u, x);
+    fe_from_fe8(v, z);
+    fe_normalize(a);
+    fe_normalize(c);
+    uint32_t d = 0;
+    for (int i = 0; i < 9; i++) d |= (a.n[i] ^ u.n[i]) | (c.n[i] ^ v.n[i]);
     if (d) atomicAdd(bad, 1u);
 }
 
@@ -244,12 +300,18 @@ int main(int argc, char** argv) {
     (void)hipMalloc(&d, 4u * 256 * ncu * 8);
     printf("%d CUs, %d waves/SIMD\n", ncu, wps);
     uint32_t* bad;
-    (void)hipMalloc(&bad, 4);
+    (void)hipMalloc(&bad, 8);
     (void)hipMemset(bad, 0, 4);
     k_f5_check<<<ncu * 4, 256>>>(64, bad);
     uint32_t hb = 0;
     (void)hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost);
     printf("f5_mul vs fe_mul: %u of %d lanes differ after 64 chained products\n", hb, ncu * 4 * 256);
+    (void)hipMemset(bad, 0, 8);
+    k_fe8_check<<<ncu * 4, 256>>>(64, bad);
+    uint32_t hb8[2] = {0, 0};
+    (void)hipMemcpy(hb8, bad, 8, hipMemcpyDeviceToHost);
+    printf("fe8 vs fe: %u of %d lanes differ after 64 chained products and squares; add/sub identity failures %u\n",
+           hb8[0], ncu * 4 * 256, hb8[1]);
     run_all<0>(ncu * wps, d, ncu);
     return 0;
 }

@@ -53,6 +53,7 @@ for step in "$@"; do
     trace_prio) HD_WAVE_PRIO=3 run trace_prio 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_prio -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub ;;
     pcie) run pcie 120 scripts/pcie_probe && HSA_ENABLE_SDMA=0 run pcie_nosdma 120 scripts/pcie_probe ;;
     fieldbench) run fieldbench 120 scripts/fieldbench 3 ;;
+    fieldbench2) run fieldbench2 120 scripts/fieldbench 2 ;;
     swappc) run swappc 120 scripts/swappc_repro ;;
     gtest_fk) HD_FOREIGN_KEYS=16 run pytest_gpu_fk 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     bench_fk) HD_FOREIGN_KEYS=16 run bench_fk 600 python bench.py ;;

@@ -22,6 +22,8 @@ for step in "$@"; do
     bench_vs3) run bench_vs3 300 python bench.py --no-cpu --no-aux ;;
     c5probe) run c5probe 300 python -u scripts/c5_probe.py 5 20 && HD_FOREIGN_KEYS=0 run c5probe_fk0 300 python -u scripts/c5_probe.py 3 20 ;;
     trace_c5) run trace_c5 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_c5 -o run -- python3 scripts/c5_probe.py 2 10 ;;
+    bench_thi) run bench_thi 300 python bench.py --no-cpu --no-aux --tally-priority high ;;
+    abthi) run bench_thi_a 300 python bench.py --no-cpu --no-aux --tally-priority high && run bench_tlo_a 300 python bench.py --no-cpu --no-aux && run bench_thi_b 300 python bench.py --no-cpu --no-aux --tally-priority high && run bench_tlo_b 300 python bench.py --no-cpu --no-aux ;;
     bench_fast) run bench_fast 300 python bench.py --no-cpu --no-aux ;;
     pipe) run pipe_c3 300 python scripts/pipe_probe.py C3 40 && run pipe_c2 300 python scripts/pipe_probe.py C2 30 && run pipe_c5 300 python scripts/pipe_probe.py C5 20 ;;
     tally) run tally_c2 200 python scripts/tally_probe.py C2 && run tally_c3 200 python scripts/tally_probe.py C3 ;;

@@ -1596,8 +1596,10 @@ static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest
     const size_t adm_lds = adm_lds_bytes(ctx->n_adm);
     k_fast_prep<<<nb, 256, adm_lds, s>>>(b, d_digest, f->state, f->adm_slot, ctx->d_adm, ctx->n_adm, ctx->adm_steps,
                                          rows, adm_lds > 0, f->fcap ? f->fdict : nullptr);
-    const bool lean = ctx->var[HD_VAR_LEAN_INV] != 0;
-    if (lean) k_fast_sinv_lean<K><<<tb, 256, 0, s>>>(n, T, rows);
+    // K > 16 exists only in the lean forms (the register forms would not fit)
+    const bool lean = K > 16 || ctx->var[HD_VAR_LEAN_INV] != 0;
+    if constexpr (K > 16) k_fast_sinv_lean<K><<<tb, 256, 0, s>>>(n, T, rows);
+    else if (lean) k_fast_sinv_lean<K><<<tb, 256, 0, s>>>(n, T, rows);
     else k_fast_sinv<K><<<tb, 256, 0, s>>>(n, T, rows);
     const bool dl = sums_digits_lds(ctx);
     if (!dl) k_fast_digits<WP><<<nb, 256, 0, s>>>(n, rows);
@@ -1616,13 +1618,16 @@ static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest
         f->sums_last = s;
         f->sums_any = true;
     }
-    if (ctx->var[HD_VAR_FUSED_CMP]) {
-        // T is a multiple of 64: each j step of a wavefront is one bitmap word pair
-        k_fast_zinv_cmp<K><<<tb, 256, 0, s>>>(b, T, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer, sc.slow,
-                                              sc.count, d_bitmap, auth);
-        return;
+    if constexpr (K <= 16) {
+        if (ctx->var[HD_VAR_FUSED_CMP]) {
+            // T is a multiple of 64: each j step of a wavefront is one bitmap word pair
+            k_fast_zinv_cmp<K><<<tb, 256, 0, s>>>(b, T, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer,
+                                                  sc.slow, sc.count, d_bitmap, auth);
+            return;
+        }
     }
-    if (lean) k_fast_zinv_lean<K><<<tb, 256, 0, s>>>(n, T, rows);
+    if constexpr (K > 16) k_fast_zinv_lean<K><<<tb, 256, 0, s>>>(n, T, rows);
+    else if (lean) k_fast_zinv_lean<K><<<tb, 256, 0, s>>>(n, T, rows);
     else k_fast_zinv<K><<<tb, 256, 0, s>>>(n, T, rows);
     // whole blocks of 256: every wavefront's 64 messages are one bitmap word pair
     k_fast_cmp<<<nb, 256, 0, s>>>(b, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer, sc.slow, sc.count,
@@ -1706,10 +1711,12 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
 #define HD_SPLIT(K, WP) launch_split<K, WP>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, sc, s, auth)
         if (f->wp == HD_FB_WW) {
             if (k == 16) HD_SPLIT(16, HD_FB_WW);
+            else if (k == 32) HD_SPLIT(32, HD_FB_WW);
             else if (k == 4) HD_SPLIT(4, HD_FB_WW);
             else HD_SPLIT(8, HD_FB_WW);
         } else {
             if (k == 16) HD_SPLIT(16, HD_FB_W);
+            else if (k == 32) HD_SPLIT(32, HD_FB_W);
             else if (k == 4) HD_SPLIT(4, HD_FB_W);
             else HD_SPLIT(8, HD_FB_W);
         }

@@ -264,7 +264,7 @@ int hd_ctx_set_variant(hd_ctx* ctx, int which, int value) {
         case HD_VAR_FAST_WAVES: ok = value == 2 || value == 3; break;
         case HD_VAR_SUM_PREFETCH: ok = value == 1 || value == 2; break;
         case HD_VAR_SUM_DIGITS: case HD_VAR_RECOVER_G: ok = value == 0 || value == 1; break;
-        case HD_VAR_SPLIT_K: ok = value == -1 || value == 0 || value == 4 || value == 8 || value == 16; break;
+        case HD_VAR_SPLIT_K: ok = value == -1 || value == 0 || value == 4 || value == 8 || value == 16 || value == 32; break;
         case HD_VAR_KEY_WIDTH: ok = value == 0 || value == HD_FB_W || value == HD_FB_WW; break;
         case HD_VAR_WAVE_PRIO: ok = value >= 0 && value <= 3; break;
         case HD_VAR_SUM_CAP: ok = value == 0 || value == 2; break;

@@ -151,7 +151,8 @@ int hd_ctx_profile(hd_ctx* ctx, int enable);
 #define HD_VAR_SUM_DIGITS 3     /* window digits: 0 in k_fast_sums' LDS (default), 1 a k_fast_digits pass
                                    [HD_SUM_DIGITS=rows] */
 #define HD_VAR_SPLIT_K 4        /* messages per inversion of the known-key check: -1 by batch size (default),
-                                   0 the paired kernel k_verify_fast, 4, 8 or 16 [HD_FAST_K] */
+                                   0 the paired kernel k_verify_fast, 4, 8, 16 or 32 (32 always with the lean
+                                   inversion kernels, HD_VAR_LEAN_INV) [HD_FAST_K] */
 #define HD_VAR_RECOVER_G 5      /* the full recovery's u1 G: 0 from the fixed-base G table (default), 1 from the
                                    GLV ladder's own 12-bit table [HD_RECOVER_GLV_G] */
 #define HD_VAR_FAST_WAVES 6     /* k_verify_fast (split K = 0): 2 (default) or 3 [HD_FAST_WAVES] */

@@ -24,6 +24,8 @@ for step in "$@"; do
     trace_c5) run trace_c5 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_c5 -o run -- python3 scripts/c5_probe.py 2 10 ;;
     bench_thi) run bench_thi 300 python bench.py --no-cpu --no-aux --tally-priority high ;;
     abthi) run bench_thi_a 300 python bench.py --no-cpu --no-aux --tally-priority high && run bench_tlo_a 300 python bench.py --no-cpu --no-aux && run bench_thi_b 300 python bench.py --no-cpu --no-aux --tally-priority high && run bench_tlo_b 300 python bench.py --no-cpu --no-aux ;;
+    abk32) AB_VARS="split_k=-1,32;lean_inv=0,1" AB_STREAMS=3 AB_ROUNDS=3 run ab_k32 900 python -u scripts/ab_prio.py C2 C5 C3 ;;
+    goldk32) run pytest_goldk32 600 python -u -m pytest tests/test_golden.py tests/test_gpu_verify.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "lean or split_k_32 or adversarial_full" ;;
     bench_fast) run bench_fast 300 python bench.py --no-cpu --no-aux ;;
     pipe) run pipe_c3 300 python scripts/pipe_probe.py C3 40 && run pipe_c2 300 python scripts/pipe_probe.py C2 30 && run pipe_c5 300 python scripts/pipe_probe.py C5 20 ;;
     tally) run tally_c2 200 python scripts/tally_probe.py C2 && run tally_c3 200 python scripts/tally_probe.py C3 ;;

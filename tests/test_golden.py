@@ -184,7 +184,7 @@ VARIANTS = [("default", None, None), ("verify_waves_2", "verify_waves", 2), ("ve
             ("recover_glv_g", "recover_g", 1), ("key_width_16", "key_width", 16), ("key_width_20", "key_width", 20),
             ("wave_prio_2", "wave_prio", 2), ("sum_cap_2", "sum_cap", 2), ("foreign_keys_0", "foreign_keys", 0),
             ("slow_lift_0", "slow_lift", 0), ("fused_cmp_1", "fused_cmp", 1),
-            ("lean_inv_1", "lean_inv", 1)]
+            ("lean_inv_1", "lean_inv", 1), ("split_k_32", "split_k", 32)]
 
 
 @pytest.mark.gpu

@@ -122,15 +122,15 @@ def test_full_size_c2_properties(verifier, oracle, coracle):
     assert crec.tobytes() == rec.cpu().numpy()[pick].tobytes()
 
 
-@pytest.mark.parametrize("variants", [{}, {"lean_inv": 1, "split_k": 16}, {"lean_inv": 1, "split_k": 8}],
-                         ids=["default", "lean_k16", "lean_k8"])
+@pytest.mark.parametrize("variants", [{}, {"lean_inv": 1, "split_k": 16}, {"lean_inv": 1, "split_k": 8},
+                                      {"split_k": 32}], ids=["default", "lean_k16", "lean_k8", "lean_k32"])
 def test_adversarial_full_mix_vs_c_oracle(gpu, oracle, coracle, variants):
     """C5-style mix: 30 % adversarial across all classes, 64k messages, checked
     message by message against the C oracle on a context of its own: pass 1
     (no key known: the full recovery) teaches it the 100 keys, pass 2 runs the
     known-key check for the honest messages (its fallback list is only the
     adversarial share); both passes equal the oracle.  Also with the lean
-    inversion kernels (HD_VAR_LEAN_INV) at 16 and 8 messages per inversion."""
+    inversion kernels (HD_VAR_LEAN_INV) at 16, 8 and 32 messages per inversion."""
     from hyperdrive_amd.device import generate
     N, S = 65536, 100
     v = gpu.Verifier(0)

@@ -180,6 +180,13 @@ class Pipeline:
             self.t_part = tally_out(v, total, pinned=True)
         self.tally_info = {}
         self.last_tally = None
+        # single GPU: the tally is queued without a host wait
+        # (hd_tally_device_bitmap_async) and collected NBUF - 1 steps later
+        self.async_tally = world == 1 and not os.environ.get("HD_BENCH_SYNC_TALLY")
+        self.tickets = [None] * self.NBUF
+        self.t_events = [None] * self.NBUF
+        self.stages = [None] * self.NBUF
+        self.tally_retries = 0
         self.tally_group = None   # set by main() for RCCL ranks
         self.host_trace = [] if os.environ.get("HD_BENCH_HOSTTRACE") else None
 
@@ -192,6 +199,65 @@ class Pipeline:
         done = torch.cuda.Event()
         done.record(ws)
         return self.bitmaps[buf], done
+
+    def _stage(self, j, need):
+        from hyperdrive_amd import _lib
+        lib = _lib.load()
+        cur = self.stages[j]
+        if cur is not None and cur[1] >= need:
+            return cur
+        if cur is not None:
+            lib.hd_host_free(cur[0])
+        ptr = ctypes.c_void_p()
+        cap = need + need // 2
+        rc = lib.hd_host_alloc(cap, ctypes.byref(ptr))
+        if rc != 0:
+            raise _lib.HDError(rc, "hd_host_alloc", "")
+        self.stages[j] = (ptr.value, cap)
+        return self.stages[j]
+
+    def tally_submit(self, k, pending):
+        """Queue tally k on the tally stream (after verification k, a device
+        wait) with its results downloaded into stage k % NBUF; no host wait."""
+        from hyperdrive_amd import _lib
+        bitmap, done = pending
+        self.ts.wait_event(done)
+        lib = _lib.load()
+        j = k % self.NBUF
+        dup = 1 if self.t_out.dup else 0
+        t = _lib.HdTallyTicket()
+        for _ in range(2):
+            stage, cap = self._stage(j, lib.hd_tally_stage_bytes(self.v.handle, self.B, dup))
+            t.stage, t.stage_cap, t.dup = stage, cap, dup
+            rc = lib.hd_tally_device_bitmap_async(self.v.handle, ctypes.byref(self.shard), bitmap.data_ptr(),
+                                                  ctypes.byref(t), self.ts.cuda_stream)
+            if rc != _lib.HD_ECAP:
+                break
+        if rc != 0:
+            raise _lib.HDError(rc, "hd_tally_device_bitmap_async", lib.hd_ctx_last_error(self.v.handle).decode())
+        import torch
+        ev = torch.cuda.Event()
+        ev.record(self.ts)
+        self.tickets[j], self.t_events[j] = (t, bitmap), ev
+
+    def tally_collect(self, k):
+        """Wait for tally k's download and unpack it (HD_EAGAIN: more groups
+        than staged -- tally the same inputs synchronously)."""
+        from hyperdrive_amd import _lib
+        j = k % self.NBUF
+        (t, bitmap), ev = self.tickets[j], self.t_events[j]
+        ev.synchronize()
+        lib = _lib.load()
+        rc = lib.hd_tally_collect(self.v.handle, ctypes.byref(t), ctypes.byref(self.t_out))
+        if rc == _lib.HD_EAGAIN:
+            self.tally_retries += 1
+            rc = lib.hd_tally_device_bitmap(self.v.handle, ctypes.byref(self.shard), bitmap.data_ptr(),
+                                            ctypes.byref(self.t_out), self.ts.cuda_stream)
+        if rc != 0:
+            raise _lib.HDError(rc, "hd_tally_collect", lib.hd_ctx_last_error(self.v.handle).decode())
+        self.tally_info = {"n_hr": self.t_out.n_hr, "n_counts": self.t_out.n_counts}
+        self.last_tally = (self.t_out, self.t_arr)
+        self.tickets[j] = self.t_events[j] = None
 
     def tally(self, pending):
         import torch
@@ -235,6 +301,23 @@ class Pipeline:
         rewritten by verify(k + NBUF), issued only after tally(k) returned.
         The library calls release the GIL; verification and tally touch
         disjoint state of the context."""
+        if self.async_tally:
+            # one host thread: verification k, then tally k queued behind it on
+            # the tally stream, then tally k - NBUF + 1 collected -- which frees
+            # buffer (k + 1) % NBUF before verification k + 1 rewrites it
+            tr = self.host_trace
+            for k in range(steps):
+                if tr is not None:
+                    tr.append(("v", k, time.perf_counter()))
+                pending = self.verify(k)
+                if self.do_tally:
+                    self.tally_submit(k, pending)
+                    if k - self.NBUF + 1 >= 0:
+                        self.tally_collect(k - self.NBUF + 1)
+            if self.do_tally:
+                for k in range(max(0, steps - self.NBUF + 1), steps):
+                    self.tally_collect(k)
+            return
         import queue
         import threading
         tr = self.host_trace

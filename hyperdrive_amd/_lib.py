@@ -18,6 +18,7 @@ HD_EINVAL = -1
 HD_ENOMEM = -2
 HD_EDEVICE = -3
 HD_ECAP = -4
+HD_EAGAIN = -5
 
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
 c_i8p = ctypes.POINTER(ctypes.c_int8)
@@ -90,6 +91,12 @@ class HdTallyOut(ctypes.Structure):
     ]
 
 
+class HdTallyTicket(ctypes.Structure):
+    """include/hd_verify.h hd_tally_ticket (hd_tally_device_bitmap_async / hd_tally_collect)."""
+    _fields_ = [("stage", ctypes.c_void_p), ("stage_cap", ctypes.c_size_t), ("dup", ctypes.c_int),
+                ("n", ctypes.c_uint32), ("H", ctypes.c_uint32), ("Cg", ctypes.c_uint32), ("need", ctypes.c_size_t)]
+
+
 # every symbol include/*.h declares, with its ctypes signature
 SIGNATURES = {
     "hd_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
@@ -130,6 +137,10 @@ SIGNATURES = {
     "hd_tally_partition_of": (ctypes.c_uint32, [ctypes.c_int64, ctypes.c_int64, ctypes.c_uint32]),
     "hd_tally_device_bitmap": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                               ctypes.POINTER(HdTallyOut), ctypes.c_void_p]),
+    "hd_tally_device_bitmap_async": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
+                                                    ctypes.POINTER(HdTallyTicket), ctypes.c_void_p]),
+    "hd_tally_collect": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdTallyTicket), ctypes.POINTER(HdTallyOut)]),
+    "hd_tally_stage_bytes": (ctypes.c_size_t, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int]),
     "hd_process_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(HdTallyOut)]),
     "hd_multi_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),

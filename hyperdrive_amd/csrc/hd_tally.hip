@@ -656,13 +656,51 @@ __global__ __launch_bounds__(256) void k_dup_scatter(uint32_t n, const uint8_t* 
     if (j < n) dup_global[gidx[j]] = dup[j];
 }
 
+// The staged rows (column arrays at capacities h, c) into out's arrays.
+static void tally_unpack(const char* base, uint32_t h, uint32_t c, uint32_t n_hr, uint32_t n_cnt, hd_tally_out* out) {
+    const int64_t* o_h = reinterpret_cast<const int64_t*>(base);
+    const int64_t* o_r = o_h + h;
+    const uint32_t* o_prev = reinterpret_cast<const uint32_t*>(o_r + h);
+    const uint32_t* o_prec = o_prev + h;
+    const uint32_t* o_any = o_prec + h;
+    const uint32_t* o_rep = o_any + h;
+    const int64_t* c_h = reinterpret_cast<const int64_t*>(base + 32 * (size_t)h);
+    const int64_t* c_r = c_h + c;
+    const uint32_t* c_rep = reinterpret_cast<const uint32_t*>(c_r + c);
+    const uint32_t* c_n = c_rep + c;
+    const uint8_t* c_t = reinterpret_cast<const uint8_t*>(c_n + c);
+    auto put = [&](void* dst, const void* src, size_t sz) {
+        if (dst && sz) memcpy(dst, src, sz);
+    };
+    put(out->hr_height, o_h, 8 * (size_t)n_hr);
+    put(out->hr_round, o_r, 8 * (size_t)n_hr);
+    put(out->hr_prevotes, o_prev, 4 * (size_t)n_hr);
+    put(out->hr_precommits, o_prec, 4 * (size_t)n_hr);
+    put(out->hr_any, o_any, 4 * (size_t)n_hr);
+    put(out->hr_rep, o_rep, 4 * (size_t)n_hr);
+    put(out->count_height, c_h, 8 * (size_t)n_cnt);
+    put(out->count_round, c_r, 8 * (size_t)n_cnt);
+    put(out->count_type, c_t, (size_t)n_cnt);
+    put(out->count_rep, c_rep, 4 * (size_t)n_cnt);
+    put(out->count_n, c_n, 4 * (size_t)n_cnt);
+}
+
+// the stage layout: [n_hr, n_cnt | classification (n bytes, when staged) |
+// per-round rows (32 B each, capacity h) | per-value rows (25 B each, capacity c)]
+static size_t tally_rows_off(uint32_t n, bool dup) { return 64 + (((dup ? (size_t)n : 0) + 63) & ~(size_t)63); }
+static size_t tally_stage_bytes(uint32_t n, bool dup, uint32_t h, uint32_t c) {
+    return tally_rows_off(n, dup) + 32 * (size_t)h + 25 * (size_t)c + 64;
+}
+
 // gidx (optional): the batch's messages' global indices -- the rep outputs
 // are mapped through it (a routed batch, hd_tally_routed_device); with
 // dup_global the per-message classification is scattered there through gidx
-// on the device instead of being downloaded (out->dup unused)
+// on the device instead of being downloaded (out->dup unused).  With `tk`
+// (hd_tally_device_bitmap_async) nothing is waited for: the stage goes to the
+// ticket's pinned buffer and hd_tally_collect unpacks it later.
 static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdict, const uint32_t* d_bitmap,
                         Part part, hd_tally_out* out, hipStream_t s, const uint32_t* gidx = nullptr,
-                        uint8_t* dup_global = nullptr) {
+                        uint8_t* dup_global = nullptr, hd_tally_ticket* tk = nullptr) {
     const uint32_t n = hb->n;
     if (!ctx->tally) ctx->tally = new TallyWork();
     DevBatch b{n, hb->type, hb->height, hb->round, hb->valid_round, hb->value32, hb->from32, hb->sig65};
@@ -675,10 +713,18 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     // call's counts plus a margin; a batch with more groups than that emits and
     // downloads its rows a second time (the counts are known by then).
     TallyWork* tw = ctx->tally;
-    const bool want_dup = out->dup || dup_global;
-    const size_t dup_off = 64, rows_off = dup_off + (((want_dup ? (size_t)n : 0) + 63) & ~(size_t)63);
+    const bool want_dup = tk ? tk->dup != 0 : (out->dup || dup_global);
+    const size_t dup_off = 64, rows_off = tally_rows_off(n, want_dup);
     uint32_t H = tw->guess_hr, Cg = tw->guess_cnt;
-    auto stage_bytes = [&](uint32_t h, uint32_t c) { return rows_off + 32 * (size_t)h + 25 * (size_t)c + 64; };
+    auto stage_bytes = [&](uint32_t h, uint32_t c) { return tally_stage_bytes(n, want_dup, h, c); };
+    if (tk) {
+        if (part.nparts != 1 || gidx || dup_global) return HD_EINVAL;
+        tk->n = n;
+        tk->H = H;
+        tk->Cg = Cg;
+        tk->need = stage_bytes(H, Cg);
+        if (!tk->stage || tk->stage_cap < tk->need) return HD_ECAP;
+    }
     char* st = (char*)tbuf(ctx, T_SEL, stage_bytes(H, Cg), &rc);
     uint32_t* at = (uint32_t*)tbuf(ctx, T_SORTK, 8 * (size_t)n, &rc);   // candidate flags; then at_g | at_c
     uint32_t* ccnt = (uint32_t*)tbuf(ctx, T_TMP, 4 * ((size_t)(n + HD_CHUNK - 1) / HD_CHUNK + 2), &rc);
@@ -787,6 +833,10 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     // (the stage is downloaded whole; with dup_global the classification part
     // is skipped: it starts at rows_off only when out->dup asked for it)
     const size_t total = stage_bytes(H, Cg);
+    if (tk) {   // queued; hd_tally_collect reads the stage once the stream is past this point
+        TCHK(hipMemcpyAsync(tk->stage, st, total, hipMemcpyDeviceToHost, s), "tally download");
+        return HD_OK;
+    }
     if (tw->host_cap < total) {
         if (tw->host) (void)hipHostFree(tw->host);
         tw->host = nullptr;
@@ -823,21 +873,7 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
         TCHK(hipStreamSynchronize(s), "tally sync");
         hrows = (const char*)tw->host;
     }
-    const Cols x = cols(const_cast<char*>(hrows), H, Cg);
-    auto put = [&](void* dst, const void* src, size_t sz) {
-        if (dst && sz) memcpy(dst, src, sz);
-    };
-    put(out->hr_height, x.o_h, 8 * (size_t)n_hr);
-    put(out->hr_round, x.o_r, 8 * (size_t)n_hr);
-    put(out->hr_prevotes, x.o_prev, 4 * (size_t)n_hr);
-    put(out->hr_precommits, x.o_prec, 4 * (size_t)n_hr);
-    put(out->hr_any, x.o_any, 4 * (size_t)n_hr);
-    put(out->hr_rep, x.o_rep, 4 * (size_t)n_hr);
-    put(out->count_height, x.c_h, 8 * (size_t)n_cnt);
-    put(out->count_round, x.c_r, 8 * (size_t)n_cnt);
-    put(out->count_type, x.c_t, (size_t)n_cnt);
-    put(out->count_rep, x.c_rep, 4 * (size_t)n_cnt);
-    put(out->count_n, x.c_n, 4 * (size_t)n_cnt);
+    tally_unpack(hrows, H, Cg, n_hr, n_cnt, out);
     return HD_OK;
 }
 
@@ -893,6 +929,50 @@ int hd_tally_device(hd_ctx* ctx, const hd_batch* dbatch, const uint8_t* d_verdic
 int hd_tally_device_bitmap(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* d_valid_bitmap, hd_tally_out* out,
                            void* stream) {
     return hd_tally_device_bitmap_part(ctx, dbatch, d_valid_bitmap, 0, 1, out, stream);
+}
+
+int hd_tally_device_bitmap_async(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* d_valid_bitmap,
+                                 hd_tally_ticket* ticket, void* stream) {
+    if (!ctx || !dbatch || !ticket) return HD_EINVAL;
+    if (dbatch->n && !d_valid_bitmap) return HD_EINVAL;
+    ticket->n = dbatch->n;
+    ticket->H = ticket->Cg = 0;
+    ticket->need = 0;
+    if (dbatch->n == 0) return HD_OK;
+    (void)hipSetDevice(ctx->device);
+    hd_tally_out dummy{};
+    return tally_device(ctx, dbatch, nullptr, d_valid_bitmap, Part{0, 1}, &dummy,
+                        stream ? (hipStream_t)stream : ctx->stream, nullptr, nullptr, ticket);
+}
+
+size_t hd_tally_stage_bytes(hd_ctx* ctx, uint32_t n, int dup) {
+    if (!ctx) return 0;
+    const uint32_t h = ctx->tally ? ctx->tally->guess_hr : 1024u, c = ctx->tally ? ctx->tally->guess_cnt : 1024u;
+    return tally_stage_bytes(n, dup != 0, h, c);
+}
+
+int hd_tally_collect(hd_ctx* ctx, const hd_tally_ticket* ticket, hd_tally_out* out) {
+    if (!ctx || !ticket || !tally_out_ok(out)) return HD_EINVAL;
+    out->n_counts = out->n_hr = 0;
+    if (ticket->n == 0) return HD_OK;
+    if (!ticket->stage || ticket->need == 0) return HD_EINVAL;
+    const char* st = (const char*)ticket->stage;
+    const uint32_t n_hr = reinterpret_cast<const uint32_t*>(st)[0];
+    const uint32_t n_cnt = reinterpret_cast<const uint32_t*>(st)[1];
+    out->n_hr = n_hr;
+    out->n_counts = n_cnt;
+    if (!ctx->tally) ctx->tally = new TallyWork();
+    TallyWork* tw = ctx->tally;
+    tw->guess_hr = std::max<uint32_t>(tw->guess_hr, std::max<uint32_t>(1024u, n_hr + n_hr / 4));
+    tw->guess_cnt = std::max<uint32_t>(tw->guess_cnt, std::max<uint32_t>(1024u, n_cnt + n_cnt / 4));
+    if (n_hr > out->cap_hr || n_cnt > out->cap_counts) return HD_ECAP;
+    if (n_hr > ticket->H || n_cnt > ticket->Cg) return HD_EAGAIN;   // more groups than staged
+    if (out->dup) {
+        if (!ticket->dup) return HD_EINVAL;
+        memcpy(out->dup, st + 64, (size_t)ticket->n);
+    }
+    tally_unpack(st + tally_rows_off(ticket->n, ticket->dup != 0), ticket->H, ticket->Cg, n_hr, n_cnt, out);
+    return HD_OK;
 }
 
 int hd_tally_device_bitmap_part(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* d_valid_bitmap, uint32_t part,

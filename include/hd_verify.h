@@ -49,6 +49,8 @@ extern "C" {
 #define HD_ENOMEM (-2)   /* host or device allocation failed                 */
 #define HD_EDEVICE (-3)  /* HIP runtime / kernel failure                     */
 #define HD_ECAP (-4)     /* hd_tally_out capacity too small (n_* hold need)  */
+#define HD_EAGAIN (-5)   /* hd_tally_collect: more groups than were staged;
+                            run hd_tally_device_bitmap on the same inputs   */
 
 /* ---- message types (process/message.go:11-22) ------------------------ */
 #define HD_TYPE_PROPOSE 1
@@ -327,6 +329,36 @@ int hd_tally_device(hd_ctx* ctx, const hd_batch* dbatch, const uint8_t* d_verdic
  * (e.g. after an all-gather of per-GPU bitmaps over RCCL). */
 int hd_tally_device_bitmap(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* d_valid_bitmap, hd_tally_out* out,
                            void* stream);
+
+/* Asynchronous form of hd_tally_device_bitmap, for a caller that pipelines
+ * batches (the cgo binding's VerifyBatchAsync, bench.py): the tally's kernels
+ * and ONE download of its results into the ticket's pinned stage are queued on
+ * `stream`, and nothing is waited for.  Once the stream has passed that point
+ * (an event recorded after this call, or a stream sync), hd_tally_collect
+ * fills `out` exactly as hd_tally_device_bitmap would.  The inputs must stay
+ * unchanged until then.  The tallies of one context share device scratch, so
+ * issue them all on ONE stream (they then run in its order).
+ *  - The rows are staged at capacities guessed from earlier tallies (the
+ *    largest counts seen + 1/4).  A batch with more groups makes collect return
+ *    HD_EAGAIN with nothing written; run hd_tally_device_bitmap on the same
+ *    inputs instead.  Collect raises the guesses, so the next submit stages more.
+ *  - stage / stage_cap: pinned host memory (hd_host_alloc) of at least
+ *    hd_tally_stage_bytes(ctx, n, dup) bytes; a smaller stage makes the
+ *    submit return HD_ECAP with `need` set.
+ *  - dup != 0 stages the per-message classification too (out->dup of collect).
+ * The partitioned and routed tallies (several GPUs) stay synchronous. */
+typedef struct {
+    void* stage;        /* caller: pinned host buffer                          */
+    size_t stage_cap;   /* caller: its size in bytes                           */
+    int dup;            /* caller: stage the classification                    */
+    uint32_t n;         /* set by the submit: the batch size                   */
+    uint32_t H, Cg;     /* set by the submit: staged row capacities            */
+    size_t need;        /* set by the submit: stage bytes this submit needed   */
+} hd_tally_ticket;
+int hd_tally_device_bitmap_async(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* d_valid_bitmap,
+                                 hd_tally_ticket* ticket, void* stream);
+int hd_tally_collect(hd_ctx* ctx, const hd_tally_ticket* ticket, hd_tally_out* out);
+size_t hd_tally_stage_bytes(hd_ctx* ctx, uint32_t n, int dup);
 
 /* Partitioned tally for G GPUs: only candidates with
  * hd_tally_partition_of(height, round, nparts) == part are tallied.

@@ -187,3 +187,69 @@ def test_partitioned_tally_merges_to_the_whole(verifier, kind, n, S, adv):
         assert np.array_equal(merged["hr"], whole["hr"]), nparts
         assert np.array_equal(dup, whole_dup), nparts
         assert sum(len(p["hr"]) for p in parts) == len(whole["hr"])
+
+
+@pytest.mark.parametrize("kind,n,S,adv", [(0, 65536, 100, 30), (1, 128064, 1000, 10)])
+def test_async_tally_equals_sync(gpu, kind, n, S, adv):
+    """hd_tally_device_bitmap_async + hd_tally_collect give exactly what
+    hd_tally_device_bitmap gives (rows, counts, classification), including the
+    first submit on a fresh context, whose staged capacity is too small for
+    these batches: collect returns HD_EAGAIN and raises the guess, and the
+    next submit fits.  A stage smaller than hd_tally_stage_bytes is refused
+    with HD_ECAP before anything is queued."""
+    import ctypes
+
+    import torch
+    from hyperdrive_amd import _lib
+    from hyperdrive_amd.device import generate
+    lib = _lib.load()
+    v = gpu.Verifier(0)
+    stage = ctypes.c_void_p()
+    try:
+        ks = v.gen_keys(S)
+        v.set_signatories(ks[0])
+        db, _, _ = generate(v, kind, n, S, adv, keys=ks)
+        nn = db.n
+        shard = db.c_struct()
+        verdict = torch.empty(nn, dtype=torch.uint8, device="cuda")
+        bitmap = torch.zeros((nn + 31) // 32, dtype=torch.int32, device="cuda")
+        s = torch.cuda.current_stream().cuda_stream
+        for _ in range(2):
+            v.verify_batch_device(shard, verdict.data_ptr(), None, None, bitmap.data_ptr(), s)
+        torch.cuda.synchronize()
+        ref, ra = v._tally_struct(nn, pinned=False)
+        assert lib.hd_tally_device_bitmap(v.handle, ctypes.byref(shard), bitmap.data_ptr(), ctypes.byref(ref), s) == 0
+        # a fresh context's guesses (1024 groups) are below these batches' counts
+        v2 = gpu.Verifier(0)
+        try:
+            v2.set_signatories(ks[0])
+            cap = 64 << 20
+            assert lib.hd_host_alloc(cap, ctypes.byref(stage)) == 0
+            t = _lib.HdTallyTicket()
+            t.stage, t.stage_cap, t.dup = stage.value, 16, 1
+            assert lib.hd_tally_device_bitmap_async(v2.handle, ctypes.byref(shard), bitmap.data_ptr(),
+                                                    ctypes.byref(t), s) == _lib.HD_ECAP
+            assert t.need == lib.hd_tally_stage_bytes(v2.handle, nn, 1) > 16
+            rcs = []
+            for _ in range(2):
+                t.stage_cap = cap
+                assert lib.hd_tally_device_bitmap_async(v2.handle, ctypes.byref(shard), bitmap.data_ptr(),
+                                                        ctypes.byref(t), s) == 0
+                torch.cuda.synchronize()
+                got, ga = v2._tally_struct(nn, pinned=False)
+                rcs.append(lib.hd_tally_collect(v2.handle, ctypes.byref(t), ctypes.byref(got)))
+            assert rcs[0] in (0, _lib.HD_EAGAIN) and rcs[1] == 0, rcs
+            if ref.n_counts > 1024:
+                assert rcs[0] == _lib.HD_EAGAIN
+            assert (got.n_hr, got.n_counts) == (ref.n_hr, ref.n_counts)
+            for k in ("count_height", "count_round", "count_type", "count_rep", "count_n"):
+                assert ga[k][:ref.n_counts].tolist() == ra[k][:ref.n_counts].tolist(), k
+            for k in ("hr_height", "hr_round", "hr_prevotes", "hr_precommits", "hr_any", "hr_rep"):
+                assert ga[k][:ref.n_hr].tolist() == ra[k][:ref.n_hr].tolist(), k
+            assert ga["dup"][:nn].tolist() == ra["dup"][:nn].tolist()
+        finally:
+            v2.close()
+    finally:
+        if stage.value:
+            lib.hd_host_free(stage)
+        v.close()

@@ -187,6 +187,8 @@ class Pipeline:
         self.t_events = [None] * self.NBUF
         self.stages = [None] * self.NBUF
         self.tally_retries = 0
+        import threading
+        self.tally_lock = threading.Lock()   # submit (this thread) and collect (the collector) share tally state
         self.tally_group = None   # set by main() for RCCL ranks
         self.host_trace = [] if os.environ.get("HD_BENCH_HOSTTRACE") else None
 
@@ -226,6 +228,18 @@ class Pipeline:
         j = k % self.NBUF
         dup = 1 if self.t_out.dup else 0
         t = _lib.HdTallyTicket()
+        with self.tally_lock:
+            rc = self._submit_locked(lib, j, dup, t, bitmap)
+        if rc != 0:
+            raise _lib.HDError(rc, "hd_tally_device_bitmap_async", lib.hd_ctx_last_error(self.v.handle).decode())
+        import torch
+        ev = torch.cuda.Event()
+        ev.record(self.ts)
+        self.tickets[j], self.t_events[j] = (t, bitmap), ev
+
+    def _submit_locked(self, lib, j, dup, t, bitmap):
+        from hyperdrive_amd import _lib
+        rc = 0
         for _ in range(2):
             stage, cap = self._stage(j, lib.hd_tally_stage_bytes(self.v.handle, self.B, dup))
             t.stage, t.stage_cap, t.dup = stage, cap, dup
@@ -233,12 +247,7 @@ class Pipeline:
                                                   ctypes.byref(t), self.ts.cuda_stream)
             if rc != _lib.HD_ECAP:
                 break
-        if rc != 0:
-            raise _lib.HDError(rc, "hd_tally_device_bitmap_async", lib.hd_ctx_last_error(self.v.handle).decode())
-        import torch
-        ev = torch.cuda.Event()
-        ev.record(self.ts)
-        self.tickets[j], self.t_events[j] = (t, bitmap), ev
+        return rc
 
     def tally_collect(self, k):
         """Wait for tally k's download and unpack it (HD_EAGAIN: more groups
@@ -248,11 +257,12 @@ class Pipeline:
         (t, bitmap), ev = self.tickets[j], self.t_events[j]
         ev.synchronize()
         lib = _lib.load()
-        rc = lib.hd_tally_collect(self.v.handle, ctypes.byref(t), ctypes.byref(self.t_out))
-        if rc == _lib.HD_EAGAIN:
-            self.tally_retries += 1
-            rc = lib.hd_tally_device_bitmap(self.v.handle, ctypes.byref(self.shard), bitmap.data_ptr(),
-                                            ctypes.byref(self.t_out), self.ts.cuda_stream)
+        with self.tally_lock:
+            rc = lib.hd_tally_collect(self.v.handle, ctypes.byref(t), ctypes.byref(self.t_out))
+            if rc == _lib.HD_EAGAIN:
+                self.tally_retries += 1
+                rc = lib.hd_tally_device_bitmap(self.v.handle, ctypes.byref(self.shard), bitmap.data_ptr(),
+                                                ctypes.byref(self.t_out), self.ts.cuda_stream)
         if rc != 0:
             raise _lib.HDError(rc, "hd_tally_collect", lib.hd_ctx_last_error(self.v.handle).decode())
         self.tally_info = {"n_hr": self.t_out.n_hr, "n_counts": self.t_out.n_counts}
@@ -302,21 +312,50 @@ class Pipeline:
         The library calls release the GIL; verification and tally touch
         disjoint state of the context."""
         if self.async_tally:
-            # one host thread: verification k, then tally k queued behind it on
-            # the tally stream, then tally k - NBUF + 1 collected -- which frees
-            # buffer (k + 1) % NBUF before verification k + 1 rewrites it
+            # verification k and tally k are queued by this thread without a
+            # host wait (hd_tally_device_bitmap_async); a collector thread waits
+            # for each tally's download in order and unpacks it, which frees
+            # buffer k % NBUF for verification k + NBUF
+            import queue
+            import threading
             tr = self.host_trace
-            for k in range(steps):
-                if tr is not None:
-                    tr.append(("v", k, time.perf_counter()))
-                pending = self.verify(k)
-                if self.do_tally:
-                    self.tally_submit(k, pending)
-                    if k - self.NBUF + 1 >= 0:
-                        self.tally_collect(k - self.NBUF + 1)
-            if self.do_tally:
-                for k in range(max(0, steps - self.NBUF + 1), steps):
-                    self.tally_collect(k)
+            free = threading.Semaphore(self.NBUF)
+            work = queue.Queue()
+            errors = []
+
+            def collector():
+                while True:
+                    k = work.get()
+                    if k is None:
+                        return
+                    try:
+                        if not errors:
+                            self.tally_collect(k)
+                    except Exception as e:          # re-raised by run()
+                        errors.append(e)
+                    finally:
+                        free.release()
+
+            th = threading.Thread(target=collector, daemon=True)
+            th.start()
+            try:
+                for k in range(steps):
+                    free.acquire()
+                    if errors:
+                        break
+                    if tr is not None:
+                        tr.append(("v", k, time.perf_counter()))
+                    pending = self.verify(k)
+                    if self.do_tally:
+                        self.tally_submit(k, pending)
+                        work.put(k)
+                    else:
+                        free.release()
+            finally:
+                work.put(None)
+                th.join()
+            if errors:
+                raise errors[0]
             return
         import queue
         import threading
@@ -547,6 +586,7 @@ def main():
             "gen_s": gen_s,
             "one_stream_msgs_per_s": total * args.steps / prof_s,
             "verify_streams": len(all_streams),
+            "tally_mode": "async" if pipe.async_tally else "thread", "tally_retries": pipe.tally_retries,
         }
         if world == 1:
             out["oracle_sample_check"] = oracle_sample_check(db, verdict, recovered, sigs)

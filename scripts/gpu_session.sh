@@ -28,6 +28,7 @@ for step in "$@"; do
     goldk32) run pytest_goldk32 600 python -u -m pytest tests/test_golden.py tests/test_gpu_verify.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "lean or split_k_32 or adversarial_full" ;;
     c3host) run c3host 300 python -u scripts/c3_host_probe.py 40 && HD_BENCH_VSTREAMS=2 run c3host_vs2 300 python -u scripts/c3_host_probe.py 40 ;;
     abasync) run bench_async_a 300 python bench.py --no-cpu --no-aux && HD_BENCH_SYNC_TALLY=1 run bench_sync_a 300 python bench.py --no-cpu --no-aux && run bench_async_b 300 python bench.py --no-cpu --no-aux && HD_BENCH_SYNC_TALLY=1 run bench_sync_b 300 python bench.py --no-cpu --no-aux ;;
+    abasync2) run bench_async_thi 300 python bench.py --no-cpu --no-aux --tally-priority high && HD_BENCH_NBUF=8 run bench_async_nb8 300 python bench.py --no-cpu --no-aux && HD_BENCH_NBUF=8 run bench_async_nb8_thi 300 python bench.py --no-cpu --no-aux --tally-priority high ;;
     bench_fast) run bench_fast 300 python bench.py --no-cpu --no-aux ;;
     pipe) run pipe_c3 300 python scripts/pipe_probe.py C3 40 && run pipe_c2 300 python scripts/pipe_probe.py C2 30 && run pipe_c5 300 python scripts/pipe_probe.py C5 20 ;;
     tally) run tally_c2 200 python scripts/tally_probe.py C2 && run tally_c3 200 python scripts/tally_probe.py C3 ;;

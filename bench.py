@@ -184,7 +184,7 @@ class Pipeline:
         # (hd_tally_device_bitmap_async) and collected NBUF - 1 steps later
         self.async_tally = world == 1 and not os.environ.get("HD_BENCH_SYNC_TALLY")
         self.tickets = [None] * self.NBUF
-        self.t_events = [None] * self.NBUF
+        self.ticket_objs = [None] * self.NBUF   # hd_tally_ticket per slot (its event is reused)
         self.stages = [None] * self.NBUF
         self.tally_retries = 0
         import threading
@@ -227,15 +227,14 @@ class Pipeline:
         lib = _lib.load()
         j = k % self.NBUF
         dup = 1 if self.t_out.dup else 0
-        t = _lib.HdTallyTicket()
+        if self.ticket_objs[j] is None:
+            self.ticket_objs[j] = _lib.HdTallyTicket()
+        t = self.ticket_objs[j]
         with self.tally_lock:
             rc = self._submit_locked(lib, j, dup, t, bitmap)
         if rc != 0:
             raise _lib.HDError(rc, "hd_tally_device_bitmap_async", lib.hd_ctx_last_error(self.v.handle).decode())
-        import torch
-        ev = torch.cuda.Event()
-        ev.record(self.ts)
-        self.tickets[j], self.t_events[j] = (t, bitmap), ev
+        self.tickets[j] = (t, bitmap)
 
     def _submit_locked(self, lib, j, dup, t, bitmap):
         from hyperdrive_amd import _lib
@@ -254,11 +253,11 @@ class Pipeline:
         than staged -- tally the same inputs synchronously)."""
         from hyperdrive_amd import _lib
         j = k % self.NBUF
-        (t, bitmap), ev = self.tickets[j], self.t_events[j]
-        ev.synchronize()
+        t, bitmap = self.tickets[j]
         lib = _lib.load()
+        # the wait for the download happens inside the foreign call (no GIL)
+        rc = lib.hd_tally_collect(self.v.handle, ctypes.byref(t), ctypes.byref(self.t_out))
         with self.tally_lock:
-            rc = lib.hd_tally_collect(self.v.handle, ctypes.byref(t), ctypes.byref(self.t_out))
             if rc == _lib.HD_EAGAIN:
                 self.tally_retries += 1
                 rc = lib.hd_tally_device_bitmap(self.v.handle, ctypes.byref(self.shard), bitmap.data_ptr(),
@@ -267,7 +266,7 @@ class Pipeline:
             raise _lib.HDError(rc, "hd_tally_collect", lib.hd_ctx_last_error(self.v.handle).decode())
         self.tally_info = {"n_hr": self.t_out.n_hr, "n_counts": self.t_out.n_counts}
         self.last_tally = (self.t_out, self.t_arr)
-        self.tickets[j] = self.t_events[j] = None
+        self.tickets[j] = None
 
     def tally(self, pending):
         import torch

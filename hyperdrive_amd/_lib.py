@@ -94,7 +94,8 @@ class HdTallyOut(ctypes.Structure):
 class HdTallyTicket(ctypes.Structure):
     """include/hd_verify.h hd_tally_ticket (hd_tally_device_bitmap_async / hd_tally_collect)."""
     _fields_ = [("stage", ctypes.c_void_p), ("stage_cap", ctypes.c_size_t), ("dup", ctypes.c_int),
-                ("n", ctypes.c_uint32), ("H", ctypes.c_uint32), ("Cg", ctypes.c_uint32), ("need", ctypes.c_size_t)]
+                ("n", ctypes.c_uint32), ("H", ctypes.c_uint32), ("Cg", ctypes.c_uint32), ("need", ctypes.c_size_t),
+                ("done", ctypes.c_void_p)]
 
 
 # every symbol include/*.h declares, with its ctypes signature
@@ -141,6 +142,7 @@ SIGNATURES = {
                                                     ctypes.POINTER(HdTallyTicket), ctypes.c_void_p]),
     "hd_tally_collect": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdTallyTicket), ctypes.POINTER(HdTallyOut)]),
     "hd_tally_stage_bytes": (ctypes.c_size_t, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int]),
+    "hd_tally_ticket_release": (ctypes.c_int, [ctypes.POINTER(HdTallyTicket)]),
     "hd_process_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(HdTallyOut)]),
     "hd_multi_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),

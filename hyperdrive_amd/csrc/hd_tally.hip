@@ -35,6 +35,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <atomic>
 #include <vector>
 
 #include "hd_internal.h"
@@ -49,7 +50,9 @@ struct TallyWork {
     void* host = nullptr;   // pinned download stage (hipHostMalloc)
     size_t host_cap = 0;
     uint32_t* scalar = nullptr;   // pinned word (a partition's candidate count)
-    uint32_t guess_hr = 1024, guess_cnt = 1024;   // staged row capacities (the last call's counts + 1/4)
+    // staged row capacities (the last call's counts + 1/4); atomic: an async
+    // collect may raise them while another thread submits
+    std::atomic<uint32_t> guess_hr{1024}, guess_cnt{1024};
 };
 // T_G: the hash tables; T_C: the dense log cells; T_D: a partition's candidates;
 // T_SEL: the output stage;
@@ -833,8 +836,10 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     // (the stage is downloaded whole; with dup_global the classification part
     // is skipped: it starts at rows_off only when out->dup asked for it)
     const size_t total = stage_bytes(H, Cg);
-    if (tk) {   // queued; hd_tally_collect reads the stage once the stream is past this point
+    if (tk) {   // queued; hd_tally_collect waits for tk->done, then reads the stage
         TCHK(hipMemcpyAsync(tk->stage, st, total, hipMemcpyDeviceToHost, s), "tally download");
+        if (!tk->done) TCHK(hipEventCreateWithFlags((hipEvent_t*)&tk->done, hipEventDisableTiming), "tally event");
+        TCHK(hipEventRecord((hipEvent_t)tk->done, s), "tally event record");
         return HD_OK;
     }
     if (tw->host_cap < total) {
@@ -945,9 +950,16 @@ int hd_tally_device_bitmap_async(hd_ctx* ctx, const hd_batch* dbatch, const uint
                         stream ? (hipStream_t)stream : ctx->stream, nullptr, nullptr, ticket);
 }
 
+int hd_tally_ticket_release(hd_tally_ticket* ticket) {
+    if (!ticket) return HD_EINVAL;
+    if (ticket->done) (void)hipEventDestroy((hipEvent_t)ticket->done);
+    ticket->done = nullptr;
+    return HD_OK;
+}
+
 size_t hd_tally_stage_bytes(hd_ctx* ctx, uint32_t n, int dup) {
     if (!ctx) return 0;
-    const uint32_t h = ctx->tally ? ctx->tally->guess_hr : 1024u, c = ctx->tally ? ctx->tally->guess_cnt : 1024u;
+    const uint32_t h = ctx->tally ? ctx->tally->guess_hr.load() : 1024u, c = ctx->tally ? ctx->tally->guess_cnt.load() : 1024u;
     return tally_stage_bytes(n, dup != 0, h, c);
 }
 
@@ -955,7 +967,9 @@ int hd_tally_collect(hd_ctx* ctx, const hd_tally_ticket* ticket, hd_tally_out* o
     if (!ctx || !ticket || !tally_out_ok(out)) return HD_EINVAL;
     out->n_counts = out->n_hr = 0;
     if (ticket->n == 0) return HD_OK;
-    if (!ticket->stage || ticket->need == 0) return HD_EINVAL;
+    if (!ticket->stage || ticket->need == 0 || !ticket->done) return HD_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    TCHK(hipEventSynchronize((hipEvent_t)ticket->done), "tally collect wait");
     const char* st = (const char*)ticket->stage;
     const uint32_t n_hr = reinterpret_cast<const uint32_t*>(st)[0];
     const uint32_t n_cnt = reinterpret_cast<const uint32_t*>(st)[1];
@@ -963,8 +977,8 @@ int hd_tally_collect(hd_ctx* ctx, const hd_tally_ticket* ticket, hd_tally_out* o
     out->n_counts = n_cnt;
     if (!ctx->tally) ctx->tally = new TallyWork();
     TallyWork* tw = ctx->tally;
-    tw->guess_hr = std::max<uint32_t>(tw->guess_hr, std::max<uint32_t>(1024u, n_hr + n_hr / 4));
-    tw->guess_cnt = std::max<uint32_t>(tw->guess_cnt, std::max<uint32_t>(1024u, n_cnt + n_cnt / 4));
+    tw->guess_hr = std::max<uint32_t>(tw->guess_hr.load(), std::max<uint32_t>(1024u, n_hr + n_hr / 4));
+    tw->guess_cnt = std::max<uint32_t>(tw->guess_cnt.load(), std::max<uint32_t>(1024u, n_cnt + n_cnt / 4));
     if (n_hr > out->cap_hr || n_cnt > out->cap_counts) return HD_ECAP;
     if (n_hr > ticket->H || n_cnt > ticket->Cg) return HD_EAGAIN;   // more groups than staged
     if (out->dup) {

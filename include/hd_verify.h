@@ -337,7 +337,8 @@ int hd_tally_device_bitmap(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* 
  * (an event recorded after this call, or a stream sync), hd_tally_collect
  * fills `out` exactly as hd_tally_device_bitmap would.  The inputs must stay
  * unchanged until then.  The tallies of one context share device scratch, so
- * issue them all on ONE stream (they then run in its order).
+ * issue them all on ONE stream (they then run in its order).  Collect waits
+ * (on the host, for the ticket's event) until the download has landed.
  *  - The rows are staged at capacities guessed from earlier tallies (the
  *    largest counts seen + 1/4).  A batch with more groups makes collect return
  *    HD_EAGAIN with nothing written; run hd_tally_device_bitmap on the same
@@ -354,10 +355,13 @@ typedef struct {
     uint32_t n;         /* set by the submit: the batch size                   */
     uint32_t H, Cg;     /* set by the submit: staged row capacities            */
     size_t need;        /* set by the submit: stage bytes this submit needed   */
+    void* done;         /* library: an event recorded after the download
+                           (created by the first submit; hd_tally_ticket_release) */
 } hd_tally_ticket;
 int hd_tally_device_bitmap_async(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* d_valid_bitmap,
                                  hd_tally_ticket* ticket, void* stream);
-int hd_tally_collect(hd_ctx* ctx, const hd_tally_ticket* ticket, hd_tally_out* out);
+int hd_tally_collect(hd_ctx* ctx, const hd_tally_ticket* ticket, hd_tally_out* out);   /* waits for `done` */
+int hd_tally_ticket_release(hd_tally_ticket* ticket);
 size_t hd_tally_stage_bytes(hd_ctx* ctx, uint32_t n, int dup);
 
 /* Partitioned tally for G GPUs: only candidates with

@@ -247,6 +247,7 @@ def test_async_tally_equals_sync(gpu, kind, n, S, adv):
             for k in ("hr_height", "hr_round", "hr_prevotes", "hr_precommits", "hr_any", "hr_rep"):
                 assert ga[k][:ref.n_hr].tolist() == ra[k][:ref.n_hr].tolist(), k
             assert ga["dup"][:nn].tolist() == ra["dup"][:nn].tolist()
+            assert lib.hd_tally_ticket_release(ctypes.byref(t)) == 0 and not t.done
         finally:
             v2.close()
     finally:

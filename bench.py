@@ -180,9 +180,12 @@ class Pipeline:
             self.t_part = tally_out(v, total, pinned=True)
         self.tally_info = {}
         self.last_tally = None
-        # single GPU: the tally is queued without a host wait
-        # (hd_tally_device_bitmap_async) and collected NBUF - 1 steps later
-        self.async_tally = world == 1 and not os.environ.get("HD_BENCH_SYNC_TALLY")
+        # HD_BENCH_ASYNC_TALLY=1 (single GPU): the tally is queued without a
+        # host wait (hd_tally_device_bitmap_async) and a collector thread
+        # unpacks it.  Off by default: measured +3-5 % on C3 but the headline
+        # C2 pipeline stalled for ~6 ms every few steps inside the submit
+        # (DESIGN.md §4), so the tally thread with the synchronous call stays.
+        self.async_tally = world == 1 and bool(os.environ.get("HD_BENCH_ASYNC_TALLY"))
         self.tickets = [None] * self.NBUF
         self.ticket_objs = [None] * self.NBUF   # hd_tally_ticket per slot (its event is reused)
         self.stages = [None] * self.NBUF
@@ -255,8 +258,13 @@ class Pipeline:
         j = k % self.NBUF
         t, bitmap = self.tickets[j]
         lib = _lib.load()
+        tr = self.host_trace
+        if tr is not None:
+            tr.append(("c0", k, time.perf_counter()))
         # the wait for the download happens inside the foreign call (no GIL)
         rc = lib.hd_tally_collect(self.v.handle, ctypes.byref(t), ctypes.byref(self.t_out))
+        if tr is not None:
+            tr.append(("c1", k, time.perf_counter()))
         with self.tally_lock:
             if rc == _lib.HD_EAGAIN:
                 self.tally_retries += 1
@@ -347,6 +355,8 @@ class Pipeline:
                     pending = self.verify(k)
                     if self.do_tally:
                         self.tally_submit(k, pending)
+                        if tr is not None:
+                            tr.append(("s", k, time.perf_counter()))
                         work.put(k)
                     else:
                         free.release()
@@ -461,6 +471,12 @@ def main():
 
     torch.cuda.set_stream(ws)          # torch ops (RCCL all-gather included) share the library's stream
     ts = torch.cuda.Stream(device=dev, priority=-1 if args.tally_priority == "high" else 0)
+    if os.environ.get("HD_BENCH_DEDICATED_TS"):
+        # the tally stream on a hardware queue of its own (hd_stream_create_dedicated)
+        from hyperdrive_amd import _lib
+        sp = ctypes.c_void_p()
+        if _lib.load().hd_stream_create_dedicated(v.handle, ctypes.byref(sp)) == 0:
+            ts = torch.cuda.ExternalStream(sp.value, device=dev)
     pipe = Pipeline(v, db, total, lo, rank, world, dist, ws, ts, tally=not args.no_tally)
     if dist is not None and args.dist_backend == "nccl":
         pipe.tally_group = dist.new_group(backend="nccl")

@@ -128,6 +128,8 @@ SIGNATURES = {
     "hd_verify_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
     "hd_host_alloc": (ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
     "hd_host_free": (ctypes.c_int, [ctypes.c_void_p]),
+    "hd_stream_create_dedicated": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "hd_stream_destroy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "hd_tally": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                 ctypes.POINTER(HdTallyOut)]),
     "hd_tally_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,

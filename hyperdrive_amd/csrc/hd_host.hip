@@ -345,6 +345,34 @@ int submit_impl(hd_ctx* ctx, uint32_t n, const Col (&cols)[HC_N], const CompactI
 
 extern "C" {
 
+// A stream on a hardware queue of its own: a CU-mask stream with every CU set
+// (ordinary streams share the device's GPU_MAX_HW_QUEUES queues round robin,
+// and a cross-stream wait queued in a shared queue holds back every stream
+// mapped to it).  Falls back to an ordinary non-blocking stream.
+int hd_stream_create_dedicated(hd_ctx* ctx, void** stream) {
+    if (!ctx || !stream) return HD_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    hipStream_t st = nullptr;
+    const int ncu = std::max(ctx->n_cu, 1);
+    std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0xFFFFFFFFu);
+    if (ncu % 32) mask.back() = (1u << (ncu % 32)) - 1u;
+    if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+        (void)hipGetLastError();
+        const hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+        if (e != hipSuccess) return hd_ctx_fail(ctx, e, "hd_stream_create_dedicated");
+    }
+    *stream = st;
+    return HD_OK;
+}
+
+int hd_stream_destroy(hd_ctx* ctx, void* stream) {
+    if (!ctx || !stream) return HD_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    const hipError_t e = hipStreamDestroy((hipStream_t)stream);
+    return e == hipSuccess ? HD_OK : hd_ctx_fail(ctx, e, "hd_stream_destroy");
+}
+
+
 int hd_verify_submit(hd_ctx* ctx, const hd_batch* batch, uint8_t* verdict, uint8_t* recovered32,
                      uint32_t* valid_bitmap, uint64_t* ticket) {
     if (!ctx || !batch || !verdict || !ticket) return HD_EINVAL;

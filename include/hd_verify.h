@@ -281,6 +281,14 @@ int hd_verify_submit_compact(hd_ctx* ctx, const hd_batch_compact* batch, uint8_t
 int hd_host_alloc(size_t bytes, void** out);
 int hd_host_free(void* p);
 
+/* A stream on a hardware queue of its own (a CU-mask stream with every CU
+ * set), for a caller's verify or tally streams.  Ordinary streams share the
+ * device's few hardware queues (GPU_MAX_HW_QUEUES, 4) round robin, and a
+ * cross-stream wait queued in a shared queue holds back the other streams
+ * mapped to it.  Destroy with hd_stream_destroy. */
+int hd_stream_create_dedicated(hd_ctx* ctx, void** stream);
+int hd_stream_destroy(hd_ctx* ctx, void* stream);
+
 /* ---- tally --------------------------------------------------------------
  * Input: a batch and its verdicts.  Candidates are VALID Prevotes and
  * Precommits.  Per (height, round, type, signer) the lowest batch index wins

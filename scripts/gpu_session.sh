@@ -27,8 +27,10 @@ for step in "$@"; do
     abk32) AB_VARS="split_k=-1,32;lean_inv=0,1" AB_STREAMS=3 AB_ROUNDS=3 run ab_k32 900 python -u scripts/ab_prio.py C2 C5 C3 ;;
     goldk32) run pytest_goldk32 600 python -u -m pytest tests/test_golden.py tests/test_gpu_verify.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "lean or split_k_32 or adversarial_full" ;;
     c3host) run c3host 300 python -u scripts/c3_host_probe.py 40 && HD_BENCH_VSTREAMS=2 run c3host_vs2 300 python -u scripts/c3_host_probe.py 40 ;;
-    abasync) run bench_async_a 300 python bench.py --no-cpu --no-aux && HD_BENCH_SYNC_TALLY=1 run bench_sync_a 300 python bench.py --no-cpu --no-aux && run bench_async_b 300 python bench.py --no-cpu --no-aux && HD_BENCH_SYNC_TALLY=1 run bench_sync_b 300 python bench.py --no-cpu --no-aux ;;
+    abasync) HD_BENCH_ASYNC_TALLY=1 run bench_async_a 300 python bench.py --no-cpu --no-aux && run bench_sync_a 300 python bench.py --no-cpu --no-aux && HD_BENCH_ASYNC_TALLY=1 run bench_async_b 300 python bench.py --no-cpu --no-aux && run bench_sync_b 300 python bench.py --no-cpu --no-aux ;;
     abasync2) run bench_async_thi 300 python bench.py --no-cpu --no-aux --tally-priority high && HD_BENCH_NBUF=8 run bench_async_nb8 300 python bench.py --no-cpu --no-aux && HD_BENCH_NBUF=8 run bench_async_nb8_thi 300 python bench.py --no-cpu --no-aux --tally-priority high ;;
+    hosttrace_async) HD_BENCH_ASYNC_TALLY=1 HD_BENCH_HOSTTRACE=1 run hosttrace_async 300 python bench.py --no-cpu --no-aux --no-sub ;;
+    abdts) HD_BENCH_ASYNC_TALLY=1 HD_BENCH_DEDICATED_TS=1 run bench_async_dts_a 300 python bench.py --no-cpu --no-aux && HD_BENCH_DEDICATED_TS=1 run bench_thread_dts_a 300 python bench.py --no-cpu --no-aux && run bench_thread_a 300 python bench.py --no-cpu --no-aux && HD_BENCH_ASYNC_TALLY=1 HD_BENCH_DEDICATED_TS=1 run bench_async_dts_b 300 python bench.py --no-cpu --no-aux && HD_BENCH_DEDICATED_TS=1 run bench_thread_dts_b 300 python bench.py --no-cpu --no-aux && run bench_thread_b 300 python bench.py --no-cpu --no-aux ;;
     bench_fast) run bench_fast 300 python bench.py --no-cpu --no-aux ;;
     pipe) run pipe_c3 300 python scripts/pipe_probe.py C3 40 && run pipe_c2 300 python scripts/pipe_probe.py C2 30 && run pipe_c5 300 python scripts/pipe_probe.py C5 20 ;;
     tally) run tally_c2 200 python scripts/tally_probe.py C2 && run tally_c3 200 python scripts/tally_probe.py C3 ;;

@@ -227,6 +227,8 @@ class Pipeline:
         from hyperdrive_amd import _lib
         bitmap, done = pending
         self.ts.wait_event(done)
+        if self.host_trace is not None:
+            self.host_trace.append(("w", k, time.perf_counter()))
         lib = _lib.load()
         j = k % self.NBUF
         dup = 1 if self.t_out.dup else 0

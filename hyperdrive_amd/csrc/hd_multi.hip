@@ -331,11 +331,18 @@ int hd_multi_create(int ngpus, const int* devices, hd_multi** out) {
 
 int hd_multi_destroy(hd_multi* m) {
     if (!m) return HD_EINVAL;
-    for (ncclComm_t c : m->comm) (void)ncclCommDestroy(c);
+    // every device's stream first: a device's buffers receive copies queued
+    // on the other devices' streams (the copy exchange), so none is freed
+    // before all of them have drained
     for (Dev& d : m->dev) {
         if (!d.ctx) continue;
         (void)hipSetDevice(d.device);
         (void)hipStreamSynchronize(d.stream);
+    }
+    for (ncclComm_t c : m->comm) (void)ncclCommDestroy(c);
+    for (Dev& d : m->dev) {
+        if (!d.ctx) continue;
+        (void)hipSetDevice(d.device);
         for (DevBuf* b : {&d.verdict, &d.rec, &d.bitmap, &d.rows, &d.recv, &d.gidx, &d.dupg, &d.dupx})
             if (b->p) (void)hipFree(b->p);
         if (d.routed) (void)hipEventDestroy(d.routed);

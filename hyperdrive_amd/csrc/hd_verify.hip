@@ -241,6 +241,10 @@ int hd_ctx_destroy(hd_ctx* ctx) {
     if (!ctx) return HD_EINVAL;
     (void)hipSetDevice(ctx->device);
     (void)hd_ctx_quiesce(ctx);
+    // work the caller queued on its own streams may still read or write this
+    // context's scratch (a route's k_route_write, an async tally): nothing is
+    // freed before the whole device has drained
+    (void)hipDeviceSynchronize();
     if (ctx->ev_slow) (void)hipEventDestroy(ctx->ev_slow);
     void* ptrs[] = {ctx->d_gtab, ctx->d_adm, ctx->d_adm_perm, ctx->d_sig_caller};
     for (void* p : ptrs)

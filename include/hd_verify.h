@@ -91,6 +91,8 @@ typedef struct {
 
 /* ---- context --------------------------------------------------------- */
 int hd_ctx_create(int device, hd_ctx** out);
+/* Destroy waits for the whole device to drain first (work a caller queued on
+ * its own streams may still use the context's scratch). */
 int hd_ctx_destroy(hd_ctx* ctx);
 /* The pubkey encoding id.NewSignatory hashes [renproject/id v0.4.2; not
  * confirmable in this container, SURVEY §8(c)]:

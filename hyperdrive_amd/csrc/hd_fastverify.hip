@@ -345,22 +345,6 @@ __global__ __launch_bounds__(256) void k_fast_prep(DevBatch b, const uint8_t* __
     } else {
         uint32_t from_be[8];
         src.from_words(from_be);
-        // the message's other fields do not depend on the lookup below: their
-        // loads issue now and land while the lookup's dependent reads run (a
-        // message whose key is not ready wastes them; in the steady state
-        // almost none is)
-        FastIn in;
-        uint32_t value_be[8];
-        int64_t h = 0, r = 0, vr = -1;
-        if (digest_in) {
-            load_row32_be(in.digest_be, digest_in, i);
-        } else {
-            src.value_words(value_be);
-            h = b.height[i];
-            r = b.round[i];
-            if (type == T_PROPOSE && b.valid_round) vr = b.valid_round[i];
-        }
-        src.sig(in.r_be, in.s_be, in.v);
         idx = adm_in_lds ? admitted_find(sh_adm, n_adm, adm_steps, from_be) : admitted_find(adm, n_adm, adm_steps, from_be);
         int32_t sl = idx >= 0 ? adm_slot[idx] : -1;
         if (idx < 0 && fdict) {
@@ -371,10 +355,19 @@ __global__ __launch_bounds__(256) void k_fast_prep(DevBatch b, const uint8_t* __
         }
         if (sl >= 0 && state[sl] == HD_FB_READY) {
             slot = (uint32_t)sl;
-            if (!digest_in) {
-                if (type == T_PROPOSE) sha256_propose(in.digest_be, h, r, vr, value_be);
-                else sha256_vote(in.digest_be, h, r, value_be);
+            FastIn in;
+            if (digest_in) {
+                load_row32_be(in.digest_be, digest_in, i);
+            } else {
+                uint32_t value_be[8];
+                src.value_words(value_be);
+                if (type == T_PROPOSE)
+                    sha256_propose(in.digest_be, b.height[i], b.round[i], b.valid_round ? b.valid_round[i] : -1,
+                                   value_be);
+                else
+                    sha256_vote(in.digest_be, b.height[i], b.round[i], value_be);
             }
+            src.sig(in.r_be, in.s_be, in.v);
             in.ready = true;
             sc r, s, m;
             fe x;

@@ -33,7 +33,6 @@ for step in "$@"; do
     abdts) HD_BENCH_ASYNC_TALLY=1 HD_BENCH_DEDICATED_TS=1 run bench_async_dts_a 300 python bench.py --no-cpu --no-aux && HD_BENCH_DEDICATED_TS=1 run bench_thread_dts_a 300 python bench.py --no-cpu --no-aux && run bench_thread_a 300 python bench.py --no-cpu --no-aux && HD_BENCH_ASYNC_TALLY=1 HD_BENCH_DEDICATED_TS=1 run bench_async_dts_b 300 python bench.py --no-cpu --no-aux && HD_BENCH_DEDICATED_TS=1 run bench_thread_dts_b 300 python bench.py --no-cpu --no-aux && run bench_thread_b 300 python bench.py --no-cpu --no-aux ;;
     routedflake) run routed_flake 300 python -u tests/routed_flake_probe.py 6 ;;
     abasync3) HD_BENCH_ASYNC_TALLY=1 HD_BENCH_NBUF=2 run bench_async_nb2 300 python bench.py --no-cpu --no-aux && HD_BENCH_ASYNC_TALLY=1 HD_BENCH_NBUF=3 run bench_async_nb3 300 python bench.py --no-cpu --no-aux && HD_BENCH_ASYNC_TALLY=1 HD_BENCH_NBUF=2 HD_BENCH_HOSTTRACE=1 run hosttrace_async_nb2 300 python bench.py --no-cpu --no-aux --no-sub ;;
-    abprep) run ab_prep 900 bash scripts/gpu_ab_prof.sh "base:HD_LIB=hyperdrive_amd/_lib/var/libhd_base.so" "hoist:AB_ADV=0" "base2:HD_LIB=hyperdrive_amd/_lib/var/libhd_base.so" "hoist2:AB_ADV=0" "base5:HD_LIB=hyperdrive_amd/_lib/var/libhd_base.so AB_ADV=30" "hoist5:AB_ADV=30" && run goldadv 600 python -u -m pytest tests/test_golden.py tests/test_gpu_verify.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "matches_golden or default or adversarial_full or foreign" ;;
     bench_fast) run bench_fast 300 python bench.py --no-cpu --no-aux ;;
     pipe) run pipe_c3 300 python scripts/pipe_probe.py C3 40 && run pipe_c2 300 python scripts/pipe_probe.py C2 30 && run pipe_c5 300 python scripts/pipe_probe.py C5 20 ;;
     tally) run tally_c2 200 python scripts/tally_probe.py C2 && run tally_c3 200 python scripts/tally_probe.py C3 ;;

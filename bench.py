@@ -185,7 +185,9 @@ class Pipeline:
         # unpacks it.  Off by default: measured +3-5 % on C3 but the headline
         # C2 pipeline stalled for ~6 ms every few steps inside the submit
         # (DESIGN.md §4), so the tally thread with the synchronous call stays.
+        # (=2: the collector thread also submits, one tally ahead of the one it collects)
         self.async_tally = world == 1 and bool(os.environ.get("HD_BENCH_ASYNC_TALLY"))
+        self.async_mode = int(os.environ.get("HD_BENCH_ASYNC_TALLY", "0") or 0)
         self.tickets = [None] * self.NBUF
         self.ticket_objs = [None] * self.NBUF   # hd_tally_ticket per slot (its event is reused)
         self.stages = [None] * self.NBUF
@@ -345,7 +347,26 @@ class Pipeline:
                     finally:
                         free.release()
 
-            th = threading.Thread(target=collector, daemon=True)
+            def submit_collector():
+                # mode 2: submit tally k, then collect tally k - 1
+                prev = None
+                while True:
+                    item = work.get()
+                    try:
+                        if item is not None and not errors:
+                            self.tally_submit(item[0], item[1])
+                        if prev is not None and not errors:
+                            self.tally_collect(prev)
+                    except Exception as e:          # re-raised by run()
+                        errors.append(e)
+                    finally:
+                        if prev is not None:
+                            free.release()
+                    if item is None:
+                        return
+                    prev = item[0]
+
+            th = threading.Thread(target=submit_collector if self.async_mode == 2 else collector, daemon=True)
             th.start()
             try:
                 for k in range(steps):
@@ -355,13 +376,15 @@ class Pipeline:
                     if tr is not None:
                         tr.append(("v", k, time.perf_counter()))
                     pending = self.verify(k)
-                    if self.do_tally:
+                    if not self.do_tally:
+                        free.release()
+                    elif self.async_mode == 2:
+                        work.put((k, pending))
+                    else:
                         self.tally_submit(k, pending)
                         if tr is not None:
                             tr.append(("s", k, time.perf_counter()))
                         work.put(k)
-                    else:
-                        free.release()
             finally:
                 work.put(None)
                 th.join()

@@ -35,6 +35,7 @@ for step in "$@"; do
     abasync3) HD_BENCH_ASYNC_TALLY=1 HD_BENCH_NBUF=2 run bench_async_nb2 300 python bench.py --no-cpu --no-aux && HD_BENCH_ASYNC_TALLY=1 HD_BENCH_NBUF=3 run bench_async_nb3 300 python bench.py --no-cpu --no-aux && HD_BENCH_ASYNC_TALLY=1 HD_BENCH_NBUF=2 HD_BENCH_HOSTTRACE=1 run hosttrace_async_nb2 300 python bench.py --no-cpu --no-aux --no-sub ;;
     abwarm) run bench_w5a 300 python bench.py --no-cpu --no-aux && run bench_w15 300 python bench.py --no-cpu --no-aux --warmup 15 && run bench_w5b 300 python bench.py --no-cpu --no-aux ;;
     ablean3) AB_VARS="lean_inv=0,1" AB_STREAMS=3 AB_ROUNDS=5 run ab_lean3 900 python -u scripts/ab_prio.py C3 C5 ;;
+    abasync4) HD_BENCH_ASYNC_TALLY=2 run bench_async2_a 300 python bench.py --no-cpu --no-aux && run bench_thr_a 300 python bench.py --no-cpu --no-aux && HD_BENCH_ASYNC_TALLY=2 run bench_async2_b 300 python bench.py --no-cpu --no-aux && run bench_thr_b 300 python bench.py --no-cpu --no-aux ;;
     bench_fast) run bench_fast 300 python bench.py --no-cpu --no-aux ;;
     pipe) run pipe_c3 300 python scripts/pipe_probe.py C3 40 && run pipe_c2 300 python scripts/pipe_probe.py C2 30 && run pipe_c5 300 python scripts/pipe_probe.py C5 20 ;;
     tally) run tally_c2 200 python scripts/tally_probe.py C2 && run tally_c3 200 python scripts/tally_probe.py C3 ;;

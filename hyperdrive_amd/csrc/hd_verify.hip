@@ -145,7 +145,8 @@ __global__ __launch_bounds__(256, WAVES) void k_verify(DevBatch b, const ge* __r
 
 // ---------------------------------------------------------------- host side
 namespace {
-const char* const kErr[] = {"ok", "invalid argument", "out of memory", "device error", "tally capacity too small"};
+const char* const kErr[] = {"ok", "invalid argument", "out of memory", "device error", "tally capacity too small",
+                            "more tally groups than staged (run the synchronous tally)"};
 }
 
 int hd_ctx_fail(hd_ctx* ctx, hipError_t e, const char* what) {
@@ -175,7 +176,7 @@ int hd_abi_version(void) { return 2; }
 
 const char* hd_strerror(int code) {
     int k = -code;
-    if (k < 0 || k > 4) return "unknown error";
+    if (k < 0 || k > 5) return "unknown error";
     return kErr[k];
 }
 

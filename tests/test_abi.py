@@ -61,3 +61,36 @@ def test_strerror_without_gpu():
     assert lib.hd_ctx_create(0, None) == -1
     assert lib.hd_verify_batch(None, None, None, None, None) == -1
     assert lib.hd_tally(None, None, None, None) == -1
+
+
+def test_struct_layouts_match_the_header(tmp_path):
+    """The ctypes mirrors of the ABI structs have the C compiler's sizes and
+    field offsets (gcc on include/hd_verify.h; no GPU)."""
+    import shutil
+
+    import pytest
+    from hyperdrive_amd import _lib
+    if not shutil.which("gcc"):
+        pytest.skip("gcc absent")
+    structs = {"hd_batch": _lib.HdBatch, "hd_batch_compact": _lib.HdBatchCompact, "hd_batch_out": _lib.HdBatchOut,
+               "hd_tally_out": _lib.HdTallyOut, "hd_tally_ticket": _lib.HdTallyTicket}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "hd_verify.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for fname, _ in py._fields_:
+            lines.append(f'printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    got = {}
+    for line in out:
+        if line:
+            parts = line.split()
+            got[(parts[0], parts[1])] = int(parts[2])
+    for cname, py in structs.items():
+        assert got[(cname, "size")] == ctypes.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert got[(cname, fname)] == getattr(py, fname).offset, (cname, fname)

@@ -83,7 +83,7 @@ int hd_gen_batch_device(hd_ctx* ctx, uint32_t kind, uint64_t start, uint32_t n, 
     k_gen<<<blocks, 256, 0, s>>>(kind, start, n, S, adv_pct, ctx->d_gtab, d_signatories32, d_foreign32, *d_out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hd_ctx_fail(ctx, e, "k_gen launch");
-    return HD_OK;
+    return hd_ctx_note_stream(ctx, s);   // k_gen reads the context's G table
 }
 
 }  // extern "C"

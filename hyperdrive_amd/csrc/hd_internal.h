@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "../../include/hd_verify.h"
 #include "hd_fixedbase.h"
@@ -56,8 +58,17 @@ struct hd_ctx {
     bool fastpath = true;   // known-key fast path (HD_VERIFY_FASTPATH=0 disables)
     hipEvent_t ev_slow = nullptr;   // after the last full-recovery-only verify call (fast path off)
     HostPipe* host = nullptr;
+    // caller streams that ran work reading this context's scratch or tables
+    // (route, unroute, async tallies, the generator), each with an event
+    // recorded after its last such work: hd_ctx_destroy waits for these
+    // instead of for the whole device
+    std::vector<std::pair<hipStream_t, hipEvent_t>> caller_ev;
     std::string last_error;
 };
+
+// Record (after work just queued on s) that s uses this context; a no-op for
+// the context's own stream, which destroy synchronises anyway.
+int hd_ctx_note_stream(hd_ctx* ctx, hipStream_t s);
 
 // Wait (host) for every kernel this context queued: its own stream and the
 // verify calls on caller streams.  Replaces device-wide synchronisation, so a

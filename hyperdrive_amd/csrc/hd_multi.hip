@@ -381,9 +381,12 @@ int hd_multi_set_pubkey_format(hd_multi* m, int format) {
     return HD_OK;
 }
 
-int hd_multi_verify_batch(hd_multi* m, const hd_batch* batch, uint8_t* verdict, uint8_t* recovered32,
-                          uint32_t* valid_bitmap, hd_tally_out* tally) {
-    if (!m || !batch || !verdict) return HD_EINVAL;
+}  // extern "C"
+
+namespace {
+
+int multi_verify(hd_multi* m, const hd_batch* batch, uint8_t* verdict, uint8_t* recovered32, uint32_t* valid_bitmap,
+                 hd_tally_out* tally) {
     const uint32_t n = batch->n;
     if (tally) tally->n_counts = tally->n_hr = 0;
     if (n == 0) return HD_OK;
@@ -482,6 +485,26 @@ int hd_multi_verify_batch(hd_multi* m, const hd_batch* batch, uint8_t* verdict, 
         MCHK(hipStreamSynchronize(d.stream), "output download");
     }
     return HD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hd_multi_verify_batch(hd_multi* m, const hd_batch* batch, uint8_t* verdict, uint8_t* recovered32,
+                          uint32_t* valid_bitmap, hd_tally_out* tally) {
+    if (!m || !batch || !verdict) return HD_EINVAL;
+    const int rc = multi_verify(m, batch, verdict, recovered32, valid_bitmap, tally);
+    if (rc) {
+        // step 1 queues the output downloads into the caller's arrays without
+        // waiting, and a later step may fail (a device error, HD_ECAP from the
+        // merge): drain every device before handing the arrays back
+        for (Dev& d : m->dev) {
+            (void)hipSetDevice(d.device);
+            (void)hipStreamSynchronize(d.stream);
+        }
+    }
+    return rc;
 }
 
 }  // extern "C"

@@ -55,9 +55,10 @@ struct TallyWork {
     std::atomic<uint32_t> guess_hr{1024}, guess_cnt{1024};
 };
 // T_G: the hash tables; T_C: the dense log cells; T_D: a partition's candidates;
-// T_SEL: the output stage;
+// T_SEL: the output stage; T_DUP: a routed batch's classification when it is
+// scattered on the device instead of staged; T_CHECK: HD_TALLY_CHECK's counters;
 // T_SORTK / T_SORTV: order marks / compacted order
-enum TSlot { T_G, T_D, T_C, T_GSLOT, T_DSLOT, T_NSEL, T_SEL, T_SORTK, T_SORTV, T_TMP, T_DUP, T_ROUTE };
+enum TSlot { T_G, T_D, T_C, T_GSLOT, T_DSLOT, T_NSEL, T_SEL, T_SORTK, T_SORTV, T_TMP, T_DUP, T_ROUTE, T_CHECK };
 
 // table layouts (structure of arrays inside one allocation, capacity cap)
 struct GTab {   // (h, r)
@@ -279,6 +280,12 @@ __global__ void k_tally_logs(DevBatch b, const uint32_t* __restrict__ cand, uint
     }
 }
 
+// the C table's key hash: (G slot, type, value)
+__device__ __forceinline__ uint64_t hash_count(const uint8_t* value, uint32_t g, uint8_t t) {
+    const uint64_t hv = *reinterpret_cast<const uint64_t*>(value) ^ *reinterpret_cast<const uint64_t*>(value + 8);
+    return mix64(hv ^ ((uint64_t)g << 1 | (t & 1u)));
+}
+
 // Per-value counts of a wavefront's winners: the distinct (round, type,
 // value) keys among the active lanes are handled one at a time -- the lowest
 // lane holding a key (the lowest item, so first-wins of the claim word stays
@@ -313,9 +320,8 @@ __device__ __forceinline__ void count_value(CTab C, uint32_t mask, const DevBatc
     // the keys' lowest lanes probe C together (their keys differ), instead of
     // one after another inside the loop above
     if (mine) {
-        const uint64_t hv = *reinterpret_cast<const uint64_t*>(value) ^ *reinterpret_cast<const uint64_t*>(value + 8);
         bool created;
-        const uint32_t c = probe(C.claim, mask, mix64(hv ^ ((uint64_t)g << 1 | (t & 1u))), q,
+        const uint32_t c = probe(C.claim, mask, hash_count(value, g, t), q,
                                  [&](uint32_t o) {
                                      const uint32_t io = msg_of(cand, o);
                                      return gslot[o] == g && b.type[io] == t && eq32(b.value32 + 32 * (size_t)io, value);
@@ -367,6 +373,98 @@ __global__ void k_tally_values(DevBatch b, const uint32_t* __restrict__ cand, ui
         }
         wave_add(G.nboth, g, both);
         count_value(C, mask, b, cand, gslot, g, t, q, value);
+    }
+}
+
+// ------------------------------------------------- consistency check (debug)
+// HD_TALLY_CHECK=1 in the environment: after k_tally_values, three kernels
+// re-derive the tables' invariants and the host compares them (a violation is
+// HD_EDEVICE with the counters in the context's last error, and the first
+// offending slot printed by the device):
+//   * every candidate's log cell holds an item of the same cell, no later than
+//     itself (a stale or foreign cell would silently drop a winner);
+//   * every non-empty dense cell / hashed D slot holds an item that maps to it;
+//   * no two C (or D) slots hold the same key: the probe from the key of a
+//     slot's claimer finds that slot first;
+//   * every C claimer is a winner;
+//   * winners == sum over G of (prevotes + precommits) == sum over C of n
+//     == non-empty dense cells + D claims.
+struct TallyCheck {
+    uint32_t winners, cells, d_claims, sum_g, sum_c, stale, bad_cell, dup_key, bad_claim, pad[7];
+};
+
+__device__ __forceinline__ uint32_t cell_value(const uint32_t* Dd, const uint32_t* D, uint32_t rf) {
+    return (rf & HD_REF_HASHED) ? D[rf & ~HD_REF_HASHED] : Dd[rf];
+}
+
+__global__ void k_tally_check_items(uint32_t m, const uint32_t* __restrict__ gslot, const uint32_t* __restrict__ ref,
+                                    const uint32_t* __restrict__ Dd, const uint32_t* __restrict__ D,
+                                    TallyCheck* chk) {
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < m; q += gridDim.x * blockDim.x) {
+        if (gslot[q] == kEmpty) continue;
+        const uint32_t rf = ref[q], w = cell_value(Dd, D, rf);
+        if (w == q) {
+            atomicAdd(&chk->winners, 1u);
+        } else if (w == kEmpty || w > q || gslot[w] == kEmpty || ref[w] != rf) {
+            if (atomicAdd(&chk->stale, 1u) == 0)
+                printf("hd tally check: item %u ref %08x holds %u (ref %08x)\n", q, rf, w,
+                       w < m ? ref[w] : 0xFFFFFFFFu);
+        }
+    }
+}
+
+__global__ void k_tally_check_cells(const uint32_t* __restrict__ Dd, const uint32_t* __restrict__ n_hr, uint32_t per,
+                                    size_t dcap, uint32_t m, const uint32_t* __restrict__ ref, TallyCheck* chk) {
+    const size_t cells = (size_t)*n_hr * per;
+    if (!Dd || cells > dcap) return;   // k_tally_logs hashed every candidate
+    for (size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x; c < cells; c += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t w = Dd[c];
+        if (w == kEmpty) continue;
+        atomicAdd(&chk->cells, 1u);
+        if (w >= m || ref[w] != (uint32_t)c)
+            if (atomicAdd(&chk->bad_cell, 1u) == 0) printf("hd tally check: dense cell %lu holds item %u\n", (unsigned long)c, w);
+    }
+}
+
+__global__ void k_tally_check_slots(DevBatch b, const uint32_t* __restrict__ cand, uint32_t m, uint32_t cap,
+                                    GTab G, CTab C, const uint32_t* __restrict__ D, const uint32_t* __restrict__ Dd,
+                                    const uint32_t* __restrict__ gslot, const uint32_t* __restrict__ ref,
+                                    TallyCheck* chk) {
+    const uint32_t mask = cap - 1;
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += gridDim.x * blockDim.x) {
+        if (G.claim[s] != kEmpty) atomicAdd(&chk->sum_g, G.nprev[s] + G.nprec[s]);
+        const uint32_t c = C.claim[s];
+        if (c != kEmpty) {
+            atomicAdd(&chk->sum_c, C.n[s]);
+            const uint32_t ic = msg_of(cand, c), g = gslot[c];
+            const uint8_t t = b.type[ic];
+            const uint8_t* value = b.value32 + 32 * (size_t)ic;
+            if (c >= m || g == kEmpty || cell_value(Dd, D, ref[c]) != c)
+                if (atomicAdd(&chk->bad_claim, 1u) == 0) printf("hd tally check: C slot %u claimer %u\n", s, c);
+            const uint32_t f = find(C.claim, mask, hash_count(value, g, t), [&](uint32_t o) {
+                const uint32_t io = msg_of(cand, o);
+                return gslot[o] == g && b.type[io] == t && eq32(b.value32 + 32 * (size_t)io, value);
+            });
+            if (f != s)
+                if (atomicAdd(&chk->dup_key, 1u) == 0)
+                    printf("hd tally check: C slots %u and %u hold one key (claimers %u, %u)\n", f, s,
+                           f == kEmpty ? kEmpty : C.claim[f], c);
+        }
+        const uint32_t d = D[s];
+        if (d != kEmpty) {
+            atomicAdd(&chk->d_claims, 1u);
+            const uint32_t id = msg_of(cand, d);
+            const uint8_t t = b.type[id];
+            const int64_t h = b.height[id], r = b.round[id];
+            const uint8_t* from = b.from32 + 32 * (size_t)id;
+            const uint32_t f = find(D, mask, hash_log(hash_hr(h, r), from, t), [&](uint32_t o) {
+                const uint32_t io = msg_of(cand, o);
+                return b.type[io] == t && b.height[io] == h && b.round[io] == r &&
+                       eq32(b.from32 + 32 * (size_t)io, from);
+            });
+            if (f != s)
+                if (atomicAdd(&chk->dup_key, 1u) == 0) printf("hd tally check: D slots %u and %u hold one key\n", f, s);
+        }
     }
 }
 
@@ -695,6 +793,35 @@ static size_t tally_stage_bytes(uint32_t n, bool dup, uint32_t h, uint32_t c) {
     return tally_rows_off(n, dup) + 32 * (size_t)h + 25 * (size_t)c + 64;
 }
 
+// HD_TALLY_CHECK: the invariants of the tables just built (k_tally_check_*),
+// read back at once (a synchronisation: debug only)
+static int tally_check(hd_ctx* ctx, const DevBatch& b, const uint32_t* cand, uint32_t m, uint32_t cap, GTab G,
+                       CTab C, const uint32_t* D, const uint32_t* Dd, const uint32_t* n_hr, uint32_t per, size_t dcap,
+                       const uint32_t* gslot, const uint32_t* ref, hipStream_t s) {
+    int rc = 0;
+    TallyCheck* chk = (TallyCheck*)tbuf(ctx, T_CHECK, sizeof(TallyCheck), &rc);
+    if (rc) return rc;
+    TCHK(hipMemsetAsync(chk, 0, sizeof(TallyCheck), s), "tally check clear");
+    const uint32_t grid = std::min<uint32_t>(nblk(std::max(m, cap)), (uint32_t)ctx->n_cu * 8u);
+    k_tally_check_items<<<grid, 256, 0, s>>>(m, gslot, ref, Dd, D, chk);
+    k_tally_check_cells<<<grid, 256, 0, s>>>(Dd, n_hr, per, dcap, m, ref, chk);
+    k_tally_check_slots<<<grid, 256, 0, s>>>(b, cand, m, cap, G, C, D, Dd, gslot, ref, chk);
+    TCHK(hipGetLastError(), "tally check kernels");
+    TallyCheck h{};
+    TCHK(hipMemcpyAsync(&h, chk, sizeof h, hipMemcpyDeviceToHost, s), "tally check download");
+    TCHK(hipStreamSynchronize(s), "tally check sync");
+    const bool ok = h.stale == 0 && h.bad_cell == 0 && h.dup_key == 0 && h.bad_claim == 0 && h.winners == h.sum_g &&
+                    h.winners == h.sum_c && h.winners == h.cells + h.d_claims;
+    if (ok) return HD_OK;
+    char buf[320];
+    snprintf(buf, sizeof buf,
+             "tally check failed: winners %u, sum G %u, sum C %u, dense cells %u + D claims %u, stale %u, "
+             "bad cells %u, duplicate keys %u, bad C claimers %u (m %u, cap %u)",
+             h.winners, h.sum_g, h.sum_c, h.cells, h.d_claims, h.stale, h.bad_cell, h.dup_key, h.bad_claim, m, cap);
+    ctx->last_error = buf;
+    return HD_EDEVICE;
+}
+
 // gidx (optional): the batch's messages' global indices -- the rep outputs
 // are mapped through it (a routed batch, hd_tally_routed_device); with
 // dup_global the per-message classification is scattered there through gidx
@@ -716,10 +843,13 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     // call's counts plus a margin; a batch with more groups than that emits and
     // downloads its rows a second time (the counts are known by then).
     TallyWork* tw = ctx->tally;
-    const bool want_dup = tk ? tk->dup != 0 : (out->dup || dup_global);
-    const size_t dup_off = 64, rows_off = tally_rows_off(n, want_dup);
+    // the classification is staged for download only when the caller reads it
+    // (out->dup, or the ticket's dup); a routed owner's scatter (dup_global)
+    // keeps it in device scratch of its own
+    const bool stage_dup = tk ? tk->dup != 0 : out->dup != nullptr;
+    const size_t dup_off = 64, rows_off = tally_rows_off(n, stage_dup);
     uint32_t H = tw->guess_hr, Cg = tw->guess_cnt;
-    auto stage_bytes = [&](uint32_t h, uint32_t c) { return tally_stage_bytes(n, want_dup, h, c); };
+    auto stage_bytes = [&](uint32_t h, uint32_t c) { return tally_stage_bytes(n, stage_dup, h, c); };
     if (tk) {
         if (part.nparts != 1 || gidx || dup_global) return HD_EINVAL;
         tk->n = n;
@@ -731,8 +861,9 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     char* st = (char*)tbuf(ctx, T_SEL, stage_bytes(H, Cg), &rc);
     uint32_t* at = (uint32_t*)tbuf(ctx, T_SORTK, 8 * (size_t)n, &rc);   // candidate flags; then at_g | at_c
     uint32_t* ccnt = (uint32_t*)tbuf(ctx, T_TMP, 4 * ((size_t)(n + HD_CHUNK - 1) / HD_CHUNK + 2), &rc);
+    uint8_t* d_dup = stage_dup ? (uint8_t*)(st + dup_off) : nullptr;
+    if (!stage_dup && dup_global) d_dup = (uint8_t*)tbuf(ctx, T_DUP, n, &rc);
     if (rc) return rc;
-    uint8_t* d_dup = want_dup ? (uint8_t*)(st + dup_off) : nullptr;
     // Items: the whole batch, or a partition's candidates compacted in batch
     // order (the rest of the tally then scales with the partition, not with
     // the replicated batch).
@@ -800,6 +931,10 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     k_tally_values<<<grid, 256, 0, s>>>(b, cand, m, Dd, S, d, G, C, mask, gslot, ref, d_dup);
     if (dup_global && gidx) k_dup_scatter<<<nblk(n), 256, 0, s>>>(n, d_dup, gidx, dup_global);
     TCHK(hipGetLastError(), "tally kernels");
+    if (const char* e = getenv("HD_TALLY_CHECK"); e && atoi(e)) {
+        rc = tally_check(ctx, b, cand, m, cap, G, C, d, Dd, tot, 2 * S, dcap, gslot, ref, s);
+        if (rc) return rc;
+    }
     rc = table_order(ctx, m, cap, C.claim, at + m, ccnt, ord + m, nullptr, tot + 1, s);
     if (rc) return rc;
     // rows at capacity (H, Cg) in column arrays
@@ -833,14 +968,13 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     };
     TCHK(emit(st + rows_off, H, Cg), "tally emit");
     TCHK(hipMemcpyAsync(st, tot, 8, hipMemcpyDeviceToDevice, s), "tally counts stage");
-    // (the stage is downloaded whole; with dup_global the classification part
-    // is skipped: it starts at rows_off only when out->dup asked for it)
+    // (the stage is downloaded whole: the classification only when staged)
     const size_t total = stage_bytes(H, Cg);
     if (tk) {   // queued; hd_tally_collect waits for tk->done, then reads the stage
         TCHK(hipMemcpyAsync(tk->stage, st, total, hipMemcpyDeviceToHost, s), "tally download");
         if (!tk->done) TCHK(hipEventCreateWithFlags((hipEvent_t*)&tk->done, hipEventDisableTiming), "tally event");
         TCHK(hipEventRecord((hipEvent_t)tk->done, s), "tally event record");
-        return HD_OK;
+        return hd_ctx_note_stream(ctx, s);
     }
     if (tw->host_cap < total) {
         if (tw->host) (void)hipHostFree(tw->host);
@@ -1057,7 +1191,7 @@ int hd_route_candidates_device(hd_ctx* ctx, const hd_batch* dshard, const uint32
     k_route_write<<<nb, 256, adm_lds, s>>>(b, d_valid_bitmap, nparts, base_index, off, ctx->d_adm, ctx->n_adm,
                                            ctx->adm_steps, adm_lds > 0, reinterpret_cast<RouteRow*>(d_rows));
     TCHK(hipGetLastError(), "k_route_write");
-    return HD_OK;
+    return hd_ctx_note_stream(ctx, s);
 }
 
 int hd_unroute_device(hd_ctx* ctx, const uint8_t* d_rows, uint32_t n, const hd_batch_out* d_out, uint32_t* d_gidx,
@@ -1072,7 +1206,7 @@ int hd_unroute_device(hd_ctx* ctx, const uint8_t* d_rows, uint32_t n, const hd_b
     k_unroute<<<nblk(n), 256, 0, s>>>(reinterpret_cast<const RouteRow*>(d_rows), n, ctx->d_adm, ctx->n_adm, *d_out,
                                       d_gidx);
     TCHK(hipGetLastError(), "k_unroute");
-    return HD_OK;
+    return hd_ctx_note_stream(ctx, s);
 }
 
 int hd_tally_routed_device(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* d_gidx, hd_tally_out* out,

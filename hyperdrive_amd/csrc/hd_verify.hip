@@ -158,6 +158,20 @@ int hd_ctx_fail(hd_ctx* ctx, hipError_t e, const char* what) {
     return e == hipErrorOutOfMemory ? HD_ENOMEM : HD_EDEVICE;
 }
 
+int hd_ctx_note_stream(hd_ctx* ctx, hipStream_t s) {
+    if (!s || s == ctx->stream) return HD_OK;
+    hipEvent_t ev = nullptr;
+    for (auto& se : ctx->caller_ev)
+        if (se.first == s) ev = se.second;
+    if (!ev) {
+        hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e != hipSuccess) return hd_ctx_fail(ctx, e, "caller stream event");
+        ctx->caller_ev.emplace_back(s, ev);
+    }
+    hipError_t e = hipEventRecord(ev, s);
+    return e == hipSuccess ? HD_OK : hd_ctx_fail(ctx, e, "caller stream event record");
+}
+
 int hd_dev_grow(hd_ctx* ctx, void** p, size_t* cap, size_t need) {
     if (need <= *cap) return HD_OK;
     if (*p) (void)hipFree(*p);
@@ -244,8 +258,13 @@ int hd_ctx_destroy(hd_ctx* ctx) {
     (void)hd_ctx_quiesce(ctx);
     // work the caller queued on its own streams may still read or write this
     // context's scratch (a route's k_route_write, an async tally): nothing is
-    // freed before the whole device has drained
-    (void)hipDeviceSynchronize();
+    // freed before the last such work of every stream has finished (other
+    // contexts' and streams' work is not waited for)
+    for (auto& se : ctx->caller_ev) {
+        (void)hipEventSynchronize(se.second);
+        (void)hipEventDestroy(se.second);
+    }
+    ctx->caller_ev.clear();
     if (ctx->ev_slow) (void)hipEventDestroy(ctx->ev_slow);
     void* ptrs[] = {ctx->d_gtab, ctx->d_adm, ctx->d_adm_perm, ctx->d_sig_caller};
     for (void* p : ptrs)

@@ -91,8 +91,14 @@ typedef struct {
 
 /* ---- context --------------------------------------------------------- */
 int hd_ctx_create(int device, hd_ctx** out);
-/* Destroy waits for the whole device to drain first (work a caller queued on
- * its own streams may still use the context's scratch). */
+/* Destroy first waits for the context's own stream, its verify calls, and the
+ * last work of every caller stream that used its scratch or tables (routes,
+ * tallies, digests, codec, generator); other work on the device is not waited
+ * for.
+ * Streams: a `stream` argument of NULL means the context's own stream, which
+ * is created non-blocking: it is NOT ordered after work on the legacy NULL
+ * stream (e.g. torch's default stream).  Device inputs produced on another
+ * stream must be ordered by the caller (pass that stream, or an event). */
 int hd_ctx_destroy(hd_ctx* ctx);
 /* The pubkey encoding id.NewSignatory hashes [renproject/id v0.4.2; not
  * confirmable in this container, SURVEY §8(c)]:

@@ -31,7 +31,7 @@ for step in "$@"; do
     abasync2) run bench_async_thi 300 python bench.py --no-cpu --no-aux --tally-priority high && HD_BENCH_NBUF=8 run bench_async_nb8 300 python bench.py --no-cpu --no-aux && HD_BENCH_NBUF=8 run bench_async_nb8_thi 300 python bench.py --no-cpu --no-aux --tally-priority high ;;
     hosttrace_async) HD_BENCH_ASYNC_TALLY=1 HD_BENCH_HOSTTRACE=1 run hosttrace_async 300 python bench.py --no-cpu --no-aux --no-sub ;;
     abdts) HD_BENCH_ASYNC_TALLY=1 HD_BENCH_DEDICATED_TS=1 run bench_async_dts_a 300 python bench.py --no-cpu --no-aux && HD_BENCH_DEDICATED_TS=1 run bench_thread_dts_a 300 python bench.py --no-cpu --no-aux && run bench_thread_a 300 python bench.py --no-cpu --no-aux && HD_BENCH_ASYNC_TALLY=1 HD_BENCH_DEDICATED_TS=1 run bench_async_dts_b 300 python bench.py --no-cpu --no-aux && HD_BENCH_DEDICATED_TS=1 run bench_thread_dts_b 300 python bench.py --no-cpu --no-aux && run bench_thread_b 300 python bench.py --no-cpu --no-aux ;;
-    routedflake) run routed_flake 300 python -u tests/routed_flake_probe.py 6 ;;
+    nullrace) run null_stream_race 300 python -u scripts/null_stream_race.py ;;
     abasync3) HD_BENCH_ASYNC_TALLY=1 HD_BENCH_NBUF=2 run bench_async_nb2 300 python bench.py --no-cpu --no-aux && HD_BENCH_ASYNC_TALLY=1 HD_BENCH_NBUF=3 run bench_async_nb3 300 python bench.py --no-cpu --no-aux && HD_BENCH_ASYNC_TALLY=1 HD_BENCH_NBUF=2 HD_BENCH_HOSTTRACE=1 run hosttrace_async_nb2 300 python bench.py --no-cpu --no-aux --no-sub ;;
     abwarm) run bench_w5a 300 python bench.py --no-cpu --no-aux && run bench_w15 300 python bench.py --no-cpu --no-aux --warmup 15 && run bench_w5b 300 python bench.py --no-cpu --no-aux ;;
     ablean3) AB_VARS="lean_inv=0,1" AB_STREAMS=3 AB_ROUNDS=5 run ab_lean3 900 python -u scripts/ab_prio.py C3 C5 ;;
@@ -101,5 +101,7 @@ for step in "$@"; do
     pmc_stall) run pmc_stall 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_IFETCH SQ_INSTS_SMEM --output-format csv -d gpurun_out/pmc_stall -o run -- python3 bench.py --steps 3 --warmup 0 --no-cpu --no-aux --no-sub ;;
     pmc_icache) run pmc_icache 600 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQC_DCACHE_HITS SQC_DCACHE_MISSES --output-format csv -d gpurun_out/pmc_icache -o run -- python3 bench.py --steps 3 --warmup 0 --no-cpu --no-aux --no-sub ;;
     pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_sq -o run -- python3 bench.py --steps 3 --warmup 0 --no-cpu --no-aux --no-sub ;;
+    hiptrace_async) HD_BENCH_ASYNC_TALLY=1 run hiptrace_async 300 rocprofv3 --hip-trace --kernel-trace --output-format csv -d gpurun_out/hiptrace_async -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-aux --no-sub ;;
+    routedtest) HD_TALLY_CHECK=1 run pytest_routed 400 python -u -m pytest tests/test_multi_gpu.py tests/test_gpu_tally.py -m gpu -x -v -p no:cacheprovider --timeout 200 --timeout-method thread ;;
   esac
 done

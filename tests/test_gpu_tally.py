@@ -201,7 +201,7 @@ def test_async_tally_equals_sync(gpu, kind, n, S, adv):
 
     import torch
     from hyperdrive_amd import _lib
-    from hyperdrive_amd.device import generate
+    from hyperdrive_amd.device import generate, work_stream
     lib = _lib.load()
     v = gpu.Verifier(0)
     stage = ctypes.c_void_p()
@@ -211,9 +211,11 @@ def test_async_tally_equals_sync(gpu, kind, n, S, adv):
         db, _, _ = generate(v, kind, n, S, adv, keys=ks)
         nn = db.n
         shard = db.c_struct()
-        verdict = torch.empty(nn, dtype=torch.uint8, device="cuda")
-        bitmap = torch.zeros((nn + 31) // 32, dtype=torch.int32, device="cuda")
-        s = torch.cuda.current_stream().cuda_stream
+        ws = work_stream()
+        with torch.cuda.stream(ws):    # the bitmap's fill ordered before the library's kernels
+            verdict = torch.empty(nn, dtype=torch.uint8, device="cuda")
+            bitmap = torch.zeros((nn + 31) // 32, dtype=torch.int32, device="cuda")
+        s = ws.cuda_stream
         for _ in range(2):
             v.verify_batch_device(shard, verdict.data_ptr(), None, None, bitmap.data_ptr(), s)
         torch.cuda.synchronize()

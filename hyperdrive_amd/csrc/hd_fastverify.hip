@@ -457,21 +457,27 @@ __global__ __launch_bounds__(256) void k_fast_sinv(uint32_t n, uint32_t T, Split
 // addition.  (Sending such messages to the full recovery instead costs a
 // whole recovery's latency per verify call: measured 1.95 -> 3.0 ms per 1M.)
 // The sums are XYZZ (gxz, hd_fixedbase.h: 8M + 2S per addition).
-HD void sum_step_sel(gxz& acc, bool& started, const ge& cur, bool nz) {
-    gxz s;
-    gxz_add_ge_nx(s, acc, cur);
-    gxz first;
-    gxz_set_ge(first, cur);
-    fe_norm_weak(first.y);
-    gxz_cmov(s, first, !started);
-    gxz_cmov(acc, s, nz);
-    started = started || nz;
-}
+// One addition of window point cur (digit flags ec) to acc.  The common step
+// is the bare in-place addition; a wavefront holding a zero digit or a
+// not-yet-started sum (rare: ~2^-W per window) also keeps the old sum for
+// its zero-digit lanes and starts the sum at cur where it had not started.
+// (The addition always runs in place, so no path leaves the accumulator in
+// other registers: the loop carries no copies of it.)
 HD void sum_step(gxz& acc, bool& started, ge cur, uint32_t ec) {
     if (ec & HD_REF_NEG) fe_neg(cur.y, cur.y);
     const bool nz = !(ec & HD_REF_ZERO);
-    if (__ballot(!(started && nz)) == 0ull) gxz_add_ge_nx(acc, acc, cur);
-    else sum_step_sel(acc, started, cur, nz);
+    const bool rare = __ballot(!(started && nz)) != 0ull;
+    gxz keep;
+    if (rare) keep = acc;
+    gxz_add_ge_nx(acc, acc, cur);
+    if (rare) {
+        gxz first;
+        gxz_set_ge(first, cur);
+        fe_norm_weak(first.y);
+        gxz_cmov(acc, first, !started);
+        gxz_cmov(acc, keep, !nz);
+        started = started || nz;
+    }
 }
 
 // the first addition: the accumulator is still the first window's affine
@@ -479,8 +485,18 @@ HD void sum_step(gxz& acc, bool& started, ge cur, uint32_t ec) {
 HD void sum_first(gxz& acc, bool& started, const ge& p0, ge cur, uint32_t ec) {
     if (ec & HD_REF_NEG) fe_neg(cur.y, cur.y);
     const bool nz = !(ec & HD_REF_ZERO);
-    if (__ballot(!(started && nz)) == 0ull) gxz_add_ge_z1(acc, p0, cur);
-    else sum_step_sel(acc, started, cur, nz);
+    const bool rare = __ballot(!(started && nz)) != 0ull;
+    gxz keep;
+    if (rare) keep = acc;
+    gxz_add_ge_z1(acc, p0, cur);
+    if (rare) {
+        gxz first;
+        gxz_set_ge(first, cur);
+        fe_norm_weak(first.y);
+        gxz_cmov(acc, first, !started);
+        gxz_cmov(acc, keep, !nz);
+        started = started || nz;
+    }
 }
 
 // the window digits of u1 = m / s and u2 = r / s (Montgomery products with
@@ -513,6 +529,13 @@ __global__ __launch_bounds__(256) void k_fast_digits(uint32_t n, SplitRows rows)
     fast_digit_refs<WP>(rows.dig + i, n, rows, n, i);
 }
 
+// a table point read through a global (address space 1) pointer (k_fast_sums)
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __attribute__((address_space(1))) const gp gp_global;
+#else
+typedef const gp gp_global;
+#endif
+
 // DL: the digits are computed here, into this lane's column of an LDS array
 // (no k_fast_digits pass, no digit rows in HBM); else read from the rows.
 template <int WAVES, int WP, int PF, bool DL>
@@ -525,7 +548,13 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
     if (i >= n) return;
     const uint32_t a = rows.aux[i];
     if ((a & 0xFFu) != HD_FAST_LIVE) return;
-    const gp* __restrict__ ptab = tabs[a >> 8];
+    // The table pointers as global (address space 1) pointers: the loads
+    // are then global_load (counted in vmcnt only).  A flat load -- what a
+    // pointer read from memory (tabs[]) compiles to -- also counts in
+    // lgkmcnt, so the wait for the next digit's LDS read would wait for the
+    // point prefetched one addition ahead as well, exposing its latency.
+    const gp_global* gt = (const gp_global*)gtab;
+    const gp_global* pt = (const gp_global*)tabs[a >> 8];
     // a lane reads back only its own column: no barrier
     const size_t dstride = DL ? 256 : n;
     const uint32_t* dp = DL ? sdig + threadIdx.x : rows.dig + i;
@@ -533,28 +562,32 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
     uint32_t e = dp[0];
     gxz acc;
     ge p0;
-    gp_unpack(p0, gtab[e & HD_REF_IDX]);
+    gp_unpack(p0, gt[e & HD_REF_IDX]);
     if (e & HD_REF_NEG) fe_neg(p0.y, p0.y);
     fe_norm_weak(p0.y);
     gxz_set_ge(acc, p0);
     bool started = !(e & HD_REF_ZERO);   // (while not started, acc is never read)
     // The next PF windows' points, packed (16 words each) until used; the
     // digit of the window after those is read one addition earlier still, so
-    // no load waits on another load inside an addition.
-    uint32_t c1 = dp[dstride], c2 = 0, dn = 0;
+    // no load waits on another load inside an addition.  Window indices past
+    // the last are clamped to it (a wasted but valid load), so every load is
+    // unconditional and lands straight in the registers that carry it.
+    auto tab = [&](int w) { return w < NG ? gt : pt; };
+    auto dig = [&](int w) { return dp[(size_t)(w < NT - 1 ? w : NT - 1) * dstride]; };
+    uint32_t c1 = dig(1), c2 = 0, dn = 0;
     gp q1, q2;
-    if (PF > 0) q1 = gtab[c1 & HD_REF_IDX];
+    if (PF > 0) q1 = gt[c1 & HD_REF_IDX];
     if (PF == 2) {
-        c2 = dp[2 * dstride];
-        q2 = (2 < NG ? gtab : ptab)[c2 & HD_REF_IDX];
+        c2 = dig(2);
+        q2 = tab(2)[c2 & HD_REF_IDX];
     }
-    if (PF > 0 && PF + 1 < NT) dn = dp[(size_t)(PF + 1) * dstride];
+    if (PF > 0) dn = dig(PF + 1);
     // window j's point and digit reference, advancing the prefetch queue
     // (PF = 0: loaded when used; the other waves of the SIMD cover the wait)
     auto advance = [&](int j, gp& cur, uint32_t& ec) {
         if (PF == 0) {
-            ec = j == 1 ? c1 : dp[(size_t)j * dstride];
-            cur = (j < NG ? gtab : ptab)[ec & HD_REF_IDX];
+            ec = j == 1 ? c1 : dig(j);
+            cur = tab(j)[ec & HD_REF_IDX];
             return;
         }
         cur = q1;
@@ -562,15 +595,13 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
         if (PF == 2) {
             q1 = q2;
             c1 = c2;
-            if (j + 2 < NT) {
-                c2 = dn;
-                q2 = (j + 2 < NG ? gtab : ptab)[c2 & HD_REF_IDX];
-            }
-        } else if (j + 1 < NT) {
+            c2 = dn;
+            q2 = tab(j + 2 < NT ? j + 2 : NT - 1)[c2 & HD_REF_IDX];
+        } else {
             c1 = dn;
-            q1 = (j + 1 < NG ? gtab : ptab)[c1 & HD_REF_IDX];
+            q1 = tab(j + 1 < NT ? j + 1 : NT - 1)[c1 & HD_REF_IDX];
         }
-        if (j + PF + 1 < NT) dn = dp[(size_t)(j + PF + 1) * dstride];
+        dn = dig(j + PF + 1);
     };
     {
         gp cur;

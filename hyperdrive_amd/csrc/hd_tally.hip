@@ -24,8 +24,8 @@
 // The distinct signers of a round over both types (TraceLogs[r] restricted to
 // votes, process.go:744-754) are prevotes + precommits - signers with both.
 // Counts are integer atomics, hence deterministic; outputs are ordered by the
-// batch index of each group's first message (an index-addressed scatter and
-// an ordered compaction, no sort).
+// batch index of each group's first message (first-item bitmaps and their
+// popcount prefixes, no sort).
 // Non-winners compare their value with the winner's: identical -> dropped
 // silently, different -> the double vote handed to Catcher.CatchDouble*
 // (process.go:838-843, 875-880).
@@ -46,19 +46,27 @@ using namespace hd;
 static const uint32_t kEmpty = 0xFFFFFFFFu;
 
 struct TallyWork {
-    DevBuf b[13];
+    DevBuf b[15];
     void* host = nullptr;   // pinned download stage (hipHostMalloc)
     size_t host_cap = 0;
     uint32_t* scalar = nullptr;   // pinned word (a partition's candidate count)
     // staged row capacities (the last call's counts + 1/4); atomic: an async
     // collect may raise them while another thread submits
     std::atomic<uint32_t> guess_hr{1024}, guess_cnt{1024};
+    // the tables clean themselves (k_tally_emit): cleared only when their
+    // allocation or capacity changes, or a call did not queue all its launches
+    bool dirty = false;
+    const void* tab_p = nullptr;
+    uint32_t tab_k = 0;
 };
-// T_G: the hash tables; T_C: the dense log cells; T_D: a partition's candidates;
-// T_SEL: the output stage; T_DUP: a routed batch's classification when it is
-// scattered on the device instead of staged; T_CHECK: HD_TALLY_CHECK's counters;
-// T_SORTK / T_SORTV: order marks / compacted order
-enum TSlot { T_G, T_D, T_C, T_GSLOT, T_DSLOT, T_NSEL, T_SEL, T_SORTK, T_SORTV, T_TMP, T_DUP, T_ROUTE, T_CHECK };
+// T_G: the hash tables and call counters; T_C: the dense log cells; T_D /
+// T_SORTK / T_TMP: a partition's candidate compaction; T_GSLOT / T_DSLOT /
+// T_CSLOT: per-item round slot, log reference and count slot; T_BITS: the
+// first-item bitmaps and their prefixes; T_SEL: the output stage; T_NSEL: the
+// overflow rows; T_DUP: a routed batch's classification when it is scattered
+// on the device instead of staged; T_CHECK: HD_TALLY_CHECK's counters
+enum TSlot { T_G, T_D, T_C, T_GSLOT, T_DSLOT, T_NSEL, T_SEL, T_SORTK, T_SORTV, T_TMP, T_DUP, T_ROUTE, T_CHECK,
+             T_CSLOT, T_BITS };
 
 // table layouts (structure of arrays inside one allocation, capacity cap)
 struct GTab {   // (h, r)
@@ -66,11 +74,18 @@ struct GTab {   // (h, r)
     uint32_t* nprev;
     uint32_t* nprec;
     uint32_t* nboth;
+    uint32_t* gid;   // the round's number (creation order): its dense log cells
 };
 struct CTab {   // (G slot, type, value)
     uint32_t* claim;
     uint32_t* n;
 };
+struct TallyCtr {   // 64 B, zero between calls (the last block of k_tally_firsts resets it)
+    uint32_t n_rounds;   // rounds numbered so far (k_tally_rounds)
+    uint32_t done;       // k_tally_firsts' finished blocks
+    uint32_t pad[14];
+};
+
 
 HD uint64_t mix64(uint64_t x) {
     x ^= x >> 30;
@@ -200,53 +215,77 @@ __global__ __launch_bounds__(256) void k_tally_flag(DevBatch b, const uint8_t* _
 }
 
 // pass 1: every candidate -> its round (G slot).  Lanes of a wavefront
-// usually share their round, so the first active lane probes for all lanes
-// with its (h, r) (first_active_lane / shfl64).  Without cand[] the pass
-// also filters the candidates.
+// usually share their round, so the first candidate lane probes for all lanes
+// with its (h, r) (shfl64).  Without cand[] the pass also filters the
+// candidates.  The lane that creates a round's slot numbers the round
+// (gid, in creation order) and its wavefront clears the round's 2S dense log
+// cells, so the cells need no clearing pass.  The loop is wavefront-uniform
+// (every lane reaches the ballots).
 __global__ void k_tally_rounds(DevBatch b, const uint32_t* __restrict__ cand, uint32_t m,
                                const uint8_t* __restrict__ verdict, const uint32_t* __restrict__ bitmap, Part p,
-                               GTab G, uint32_t mask, uint32_t* __restrict__ gslot, uint8_t* __restrict__ dup) {
+                               GTab G, uint32_t mask, uint32_t* __restrict__ gslot, uint8_t* __restrict__ dup,
+                               TallyCtr* ctr, uint32_t* __restrict__ Dd, uint32_t per, uint32_t nd) {
     const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < m; q += stride) {
-        const uint32_t i = msg_of(cand, q);
-        if (!cand && !candidate(b, verdict, bitmap, i, p)) {
+    const int lane = threadIdx.x & 63;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < m; base += stride) {
+        const uint32_t q = base + threadIdx.x;
+        bool c = q < m;
+        const uint32_t i = c ? msg_of(cand, q) : 0u;
+        if (c && !cand && !candidate(b, verdict, bitmap, i, p)) {
             if (dup) dup[i] = 3;
             gslot[q] = kEmpty;
-            continue;
+            c = false;
         }
-        const int64_t h = b.height[i], r = b.round[i];
-        const int lead = first_active_lane();
-        const bool follower = shfl64(h, lead) == h && shfl64(r, lead) == r && (int)(threadIdx.x & 63) != lead;
-        uint32_t g = kEmpty;
-        bool created;
-        if (!follower)
+        const unsigned long long act = __ballot(c);
+        if (!act) continue;
+        const int lead = __ffsll((long long)act) - 1;
+        const int64_t h = c ? b.height[i] : 0, r = c ? b.round[i] : 0;
+        const int64_t hl = shfl64(h, lead), rl = shfl64(r, lead);   // every lane takes part in the shuffles
+        const bool follower = c && lane != lead && hl == h && rl == r;
+        uint32_t g = kEmpty, id = kEmpty;
+        bool created = false;
+        if (c && !follower) {
             g = probe(G.claim, mask, hash_hr(h, r), q,
-                      [&](uint32_t c) {
-                          const uint32_t ic = msg_of(cand, c);
-                          return b.height[ic] == h && b.round[ic] == r;
+                      [&](uint32_t o) {
+                          const uint32_t io = msg_of(cand, o);
+                          return b.height[io] == h && b.round[io] == r;
                       },
                       created);
+            if (created) {
+                id = atomicAdd(&ctr->n_rounds, 1u);
+                G.gid[g] = id;
+            }
+        }
         const uint32_t gl = (uint32_t)__shfl((int)g, lead, 64);
-        gslot[q] = follower ? gl : g;
+        if (c) gslot[q] = follower ? gl : g;
+        // the new rounds' dense cells, one round at a time by the whole wavefront
+        unsigned long long cr = __ballot(created && id < nd);
+        while (cr) {
+            const int l = __ffsll((long long)cr) - 1;
+            const uint32_t idl = (uint32_t)__shfl((int)id, l, 64);
+            uint32_t* cells = Dd + (size_t)idl * per;
+            for (uint32_t k = lane; k < per; k += 64) cells[k] = kEmpty;
+            cr &= cr - 1;
+        }
     }
 }
 
 // Dense vote logs.  A candidate's log key (h, r, type, From) is, for an
-// admitted From, the cell (round rank, type, admitted index) of an array of
-// n_rounds x 2 x S words -- a few MB, L2-resident -- and first-wins is one
+// admitted From, the cell (round number, type, admitted index) of an array of
+// nd x 2 x S words -- a few MB, L2-resident -- and first-wins is one
 // atomicMin of the item number into that cell: no hashing, no key compares
 // against the batch.  A From outside the context's admitted set (possible
-// when the caller's verdicts predate a set change) takes the hashed table D
-// instead; a signatory's prevote and precommit always take the same path.
-// ref[q]: the cell index, or HD_REF_HASHED | the D slot.
+// when the caller's verdicts predate a set change), or a round numbered past
+// the dense cells (a batch of very many rounds), takes the hashed table D
+// instead; a signatory's prevote and precommit of a round always take the
+// same path.  ref[q]: the cell index, or HD_REF_HASHED | the D slot.
 #define HD_REF_HASHED 0x80000000u
 __global__ void k_tally_logs(DevBatch b, const uint32_t* __restrict__ cand, uint32_t m,
-                             const uint32_t* __restrict__ gslot, const uint32_t* __restrict__ rank_of,
+                             const uint32_t* __restrict__ gslot, const uint32_t* __restrict__ gid,
                              const uint32_t* __restrict__ adm, uint32_t S, int adm_steps, uint32_t* __restrict__ Dd,
-                             const uint32_t* __restrict__ n_hr, size_t dcap, uint32_t* __restrict__ D, uint32_t mask,
-                             uint32_t* __restrict__ ref, int adm_in_lds) {
+                             uint32_t nd, uint32_t* __restrict__ D, uint32_t mask, uint32_t* __restrict__ ref,
+                             int adm_in_lds) {
     extern __shared__ uint32_t sh_adm[];
-    if (Dd && (size_t)*n_hr * 2 * S > dcap) Dd = nullptr;   // more rounds than dense cells: all hashed
     if (adm_in_lds) adm_stage(sh_adm, adm, S);
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < m; q += stride) {
@@ -255,24 +294,25 @@ __global__ void k_tally_logs(DevBatch b, const uint32_t* __restrict__ cand, uint
         const uint32_t i = msg_of(cand, q);
         const uint8_t t = b.type[i];
         const uint8_t* from = b.from32 + 32 * (size_t)i;
+        const uint32_t rid = gid[g];
         int32_t signer = -1;
-        if (Dd) {
+        if (rid < nd) {
             uint32_t from_be[8];
             load_row32_be(from_be, b.from32, i);
             signer = adm_in_lds ? admitted_find(sh_adm, S, adm_steps, from_be) : admitted_find(adm, S, adm_steps, from_be);
         }
         if (signer >= 0) {
-            const uint32_t cell = (rank_of[g] * 2u + (t == T_PRECOMMIT ? 1u : 0u)) * S + (uint32_t)signer;
+            const uint32_t cell = (rid * 2u + (t == T_PRECOMMIT ? 1u : 0u)) * S + (uint32_t)signer;
             atomicMin(&Dd[cell], q);
             ref[q] = cell;
         } else {
             const int64_t h = b.height[i], r = b.round[i];
             bool created;
             const uint32_t d = probe(D, mask, hash_log(hash_hr(h, r), from, t), q,
-                                     [&](uint32_t c) {
-                                         const uint32_t ic = msg_of(cand, c);
-                                         return b.type[ic] == t && b.height[ic] == h && b.round[ic] == r &&
-                                                eq32(b.from32 + 32 * (size_t)ic, from);
+                                     [&](uint32_t o) {
+                                         const uint32_t io = msg_of(cand, o);
+                                         return b.type[io] == t && b.height[io] == h && b.round[io] == r &&
+                                                eq32(b.from32 + 32 * (size_t)io, from);
                                      },
                                      created);
             ref[q] = HD_REF_HASHED | d;
@@ -292,15 +332,16 @@ __device__ __forceinline__ uint64_t hash_count(const uint8_t* value, uint32_t g,
 // exact) probes C once and adds the number of lanes with that key in one
 // atomic.  A batch's votes repeat few values per round, so this is a few
 // probes and atomics per wavefront instead of one per lane on a handful of
-// hot words.
-__device__ __forceinline__ void count_value(CTab C, uint32_t mask, const DevBatch& b, const uint32_t* cand,
-                                            const uint32_t* gslot, uint32_t g, uint8_t t, uint32_t q,
-                                            const uint8_t* value) {
+// hot words.  Returns the C slot of this lane's key.
+__device__ __forceinline__ uint32_t count_value(CTab C, uint32_t mask, const DevBatch& b, const uint32_t* cand,
+                                                const uint32_t* gslot, uint32_t g, uint8_t t, uint32_t q,
+                                                const uint8_t* value) {
     const uint4* vw = reinterpret_cast<const uint4*>(value);
     const uint4 v0 = vw[0], v1 = vw[1];
     const int lane = threadIdx.x & 63;
     unsigned long long pending = __ballot(true);
     uint32_t mine = 0;   // on a key's lowest lane: the number of lanes with the key
+    int my_lead = lane;  // the lowest lane with this lane's key
     while (pending) {
         const int lead = __ffsll((long long)pending) - 1;
         uint32_t diff = (uint32_t)__shfl((int)g, lead, 64) ^ g;
@@ -314,31 +355,36 @@ __device__ __forceinline__ void count_value(CTab C, uint32_t mask, const DevBatc
         diff |= (uint32_t)__shfl((int)v1.z, lead, 64) ^ v1.z;
         diff |= (uint32_t)__shfl((int)v1.w, lead, 64) ^ v1.w;
         const unsigned long long same = __ballot(diff == 0 && ((pending >> lane) & 1ull));
+        if ((same >> lane) & 1ull) my_lead = lead;
         if (lane == lead) mine = (uint32_t)__popcll(same);
         pending &= ~same;
     }
     // the keys' lowest lanes probe C together (their keys differ), instead of
     // one after another inside the loop above
+    uint32_t c = kEmpty;
     if (mine) {
         bool created;
-        const uint32_t c = probe(C.claim, mask, hash_count(value, g, t), q,
-                                 [&](uint32_t o) {
-                                     const uint32_t io = msg_of(cand, o);
-                                     return gslot[o] == g && b.type[io] == t && eq32(b.value32 + 32 * (size_t)io, value);
-                                 },
-                                 created);
+        c = probe(C.claim, mask, hash_count(value, g, t), q,
+                  [&](uint32_t o) {
+                      const uint32_t io = msg_of(cand, o);
+                      return gslot[o] == g && b.type[io] == t && eq32(b.value32 + 32 * (size_t)io, value);
+                  },
+                  created);
         atomicAdd(&C.n[c], mine);
     }
+    return (uint32_t)__shfl((int)c, my_lead, 64);
 }
 
 // pass 3: each log entry's winner (the lowest item of its key) counts as a
 // distinct signer of its type in the round and counts its value (C); a
 // prevote winner whose signer also has a precommit log in the round counts
 // in nboth.  The other candidates are classified against the winner's value.
+// cslot[q]: a winner's C slot, kEmpty for the other candidates.
 __global__ void k_tally_values(DevBatch b, const uint32_t* __restrict__ cand, uint32_t m,
                                const uint32_t* __restrict__ Dd, uint32_t S, const uint32_t* __restrict__ D,
                                GTab G, CTab C, uint32_t mask, const uint32_t* __restrict__ gslot,
-                               const uint32_t* __restrict__ ref, uint8_t* __restrict__ dup) {
+                               const uint32_t* __restrict__ ref, uint32_t* __restrict__ cslot,
+                               uint8_t* __restrict__ dup) {
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < m; q += stride) {
         const uint32_t g = gslot[q];
@@ -350,6 +396,7 @@ __global__ void k_tally_values(DevBatch b, const uint32_t* __restrict__ cand, ui
         const uint8_t* value = b.value32 + 32 * (size_t)i;
         if (w != q) {
             if (dup) dup[i] = eq32(b.value32 + 32 * (size_t)msg_of(cand, w), value) ? 1 : 2;
+            cslot[q] = kEmpty;
             continue;
         }
         if (dup) dup[i] = 0;
@@ -372,8 +419,198 @@ __global__ void k_tally_values(DevBatch b, const uint32_t* __restrict__ cand, ui
             }
         }
         wave_add(G.nboth, g, both);
-        count_value(C, mask, b, cand, gslot, g, t, q, value);
+        cslot[q] = count_value(C, mask, b, cand, gslot, g, t, q, value);
     }
+}
+
+// Output order: the groups of each table by their first item.  A group's
+// first item is the one its slot's claim word holds; the per-item flags
+// "first of its round" / "first of its (round, type, value)" are bitmaps
+// Bg / Bc, one bit per item, and an item's output position is the number of
+// flags before it.  Both passes below give each block HD_TALLY_IPB
+// consecutive items (HD_TALLY_IPB / 32 bitmap words it alone writes):
+//   k_tally_firsts  the block's flags as whole words (two ballots per
+//                   wavefront: no atomics, nothing to clear), their popcount
+//                   prefix within the block, and the block's totals; the
+//                   last block to finish (a ticket counter) scans the totals
+//                   into block offsets and writes the group counts into the
+//                   stage header;
+//   k_tally_emit    every first item writes its group's row at its position
+//                   (rows past the staged capacity go to the overflow
+//                   columns), then resets its table slots, so the tables are
+//                   clean for the next call without a clearing pass.
+#define HD_TALLY_IPB 2048u   // items per block (8 per thread)
+
+__global__ __launch_bounds__(256) void k_tally_firsts(uint32_t m, const uint32_t* __restrict__ gslot,
+                                                      const uint32_t* __restrict__ cslot, const uint32_t* G_claim,
+                                                      const uint32_t* C_claim, uint32_t* __restrict__ Bg,
+                                                      uint32_t* __restrict__ Bc, uint32_t* __restrict__ pre_g,
+                                                      uint32_t* __restrict__ pre_c, uint32_t* blk, TallyCtr* ctr,
+                                                      uint32_t* stage_hdr) {
+    constexpr uint32_t W = HD_TALLY_IPB / 32;   // words per block
+    __shared__ uint32_t wg[W], wc[W];
+    __shared__ bool last;
+    const uint32_t nb = gridDim.x;
+    const uint32_t lo = blockIdx.x * HD_TALLY_IPB;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t k = 0; k < HD_TALLY_IPB / 256; k++) {
+        const uint32_t q = lo + k * 256 + threadIdx.x;
+        bool fg = false, fc = false;
+        if (q < m) {
+            const uint32_t g = gslot[q];
+            if (g != kEmpty) {
+                fg = G_claim[g] == q;
+                const uint32_t c = cslot[q];
+                fc = c != kEmpty && C_claim[c] == q;
+            }
+        }
+        const unsigned long long bg = __ballot(fg), bc = __ballot(fc);
+        if (lane == 0) {
+            const uint32_t w = k * 8 + wave * 2;
+            wg[w] = (uint32_t)bg;
+            wg[w + 1] = (uint32_t)(bg >> 32);
+            wc[w] = (uint32_t)bc;
+            wc[w + 1] = (uint32_t)(bc >> 32);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < W) {   // one lane per word (W == 64: wavefront 0)
+        const uint32_t t = threadIdx.x, gw = wg[t], cw = wc[t];
+        uint32_t ig = (uint32_t)__popc(gw), ic = (uint32_t)__popc(cw);
+        for (int d = 1; d < 64; d <<= 1) {   // inclusive scan across the wavefront
+            const uint32_t yg = (uint32_t)__shfl_up((int)ig, d, 64), yc = (uint32_t)__shfl_up((int)ic, d, 64);
+            if ((int)t >= d) {
+                ig += yg;
+                ic += yc;
+            }
+        }
+        const size_t wi = (size_t)blockIdx.x * W + t;
+        Bg[wi] = gw;
+        Bc[wi] = cw;
+        pre_g[wi] = ig - (uint32_t)__popc(gw);
+        pre_c[wi] = ic - (uint32_t)__popc(cw);
+        if (t == W - 1) {
+            blk[blockIdx.x] = ig;
+            blk[nb + blockIdx.x] = ic;
+        }
+    }
+    // the last block to finish scans the block totals
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(&ctr->done, 1u) == nb - 1;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    typedef hipcub::BlockScan<uint32_t, 256> Scan;
+    __shared__ typename Scan::TempStorage ts;
+    __shared__ uint32_t carry[2];
+    for (int j = 0; j < 2; j++) {
+        if (threadIdx.x == 0) carry[j] = 0;
+        __syncthreads();
+        const uint32_t* tot = blk + (size_t)j * nb;
+        uint32_t* off = blk + (size_t)(2 + j) * nb;
+        for (uint32_t base = 0; base < nb; base += 256) {
+            const uint32_t k = base + threadIdx.x;
+            // written by other blocks of this launch: read through L2
+            const uint32_t v = k < nb ? __hip_atomic_load(tot + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            uint32_t ex, agg;
+            Scan(ts).ExclusiveSum(v, ex, agg);
+            if (k < nb) off[k] = carry[j] + ex;
+            __syncthreads();
+            if (threadIdx.x == 0) carry[j] += agg;
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x == 0) {
+        stage_hdr[0] = carry[0];   // rounds (hr rows)
+        stage_hdr[1] = carry[1];   // (round, type, value) groups
+        ctr->n_rounds = 0;
+        ctr->done = 0;
+    }
+}
+
+// the output rows of one call, column arrays at capacities (H, Cg) in the
+// stage and (m - H, m - Cg) in the overflow
+struct TallyCols {
+    int64_t *o_h, *o_r, *c_h, *c_r;
+    uint32_t *o_prev, *o_prec, *o_any, *o_rep, *c_rep, *c_n;
+    uint8_t* c_t;
+};
+HD_HOSTONLY TallyCols tally_cols(char* base, uint32_t h, uint32_t c) {
+    TallyCols x;
+    x.o_h = reinterpret_cast<int64_t*>(base);
+    x.o_r = x.o_h + h;
+    x.o_prev = reinterpret_cast<uint32_t*>(x.o_r + h);
+    x.o_prec = x.o_prev + h;
+    x.o_any = x.o_prec + h;
+    x.o_rep = x.o_any + h;
+    x.c_h = reinterpret_cast<int64_t*>(base + 32 * (size_t)h);
+    x.c_r = x.c_h + c;
+    x.c_rep = reinterpret_cast<uint32_t*>(x.c_r + c);
+    x.c_n = x.c_rep + c;
+    x.c_t = reinterpret_cast<uint8_t*>(x.c_n + c);
+    return x;
+}
+
+__global__ __launch_bounds__(256) void k_tally_emit(DevBatch b, const uint32_t* __restrict__ cand, uint32_t m,
+                                                    const uint32_t* __restrict__ gidx, const uint32_t* __restrict__ gslot,
+                                                    const uint32_t* __restrict__ cslot, const uint32_t* __restrict__ ref,
+                                                    GTab G, CTab C, uint32_t* __restrict__ D,
+                                                    const uint32_t* __restrict__ Bg, const uint32_t* __restrict__ Bc,
+                                                    const uint32_t* __restrict__ pre_g, const uint32_t* __restrict__ pre_c,
+                                                    const uint32_t* __restrict__ blk, TallyCols st, uint32_t H,
+                                                    uint32_t Cg, TallyCols ov) {
+    const uint32_t nb = gridDim.x;
+    const uint32_t og = blk[2 * nb + blockIdx.x], oc = blk[3 * nb + blockIdx.x];
+    const uint32_t lo = blockIdx.x * HD_TALLY_IPB;
+    for (uint32_t k = 0; k < HD_TALLY_IPB / 256; k++) {
+        const uint32_t q = lo + k * 256 + threadIdx.x;
+        if (q >= m) break;
+        const uint32_t g = gslot[q];
+        if (g == kEmpty) continue;
+        const uint32_t i = msg_of(cand, q), w = q >> 5, below = (1u << (q & 31)) - 1u;
+        const uint32_t gw = Bg[w], cw = Bc[w];
+        if ((gw >> (q & 31)) & 1u) {   // the round's first candidate: its hr row
+            const uint32_t pos = og + pre_g[w] + (uint32_t)__popc(gw & below);
+            const TallyCols& x = pos < H ? st : ov;
+            const uint32_t j = pos < H ? pos : pos - H;
+            const uint32_t np = G.nprev[g], nc = G.nprec[g], nbo = G.nboth[g];
+            x.o_h[j] = b.height[i];
+            x.o_r[j] = b.round[i];
+            x.o_prev[j] = np;
+            x.o_prec[j] = nc;
+            x.o_any[j] = np + nc - nbo;
+            x.o_rep[j] = gidx ? gidx[i] : i;
+            G.claim[g] = kEmpty;
+            G.nprev[g] = G.nprec[g] = G.nboth[g] = 0;
+        }
+        if ((cw >> (q & 31)) & 1u) {   // the (round, type, value) group's first winner: its count row
+            const uint32_t c = cslot[q];
+            const uint32_t pos = oc + pre_c[w] + (uint32_t)__popc(cw & below);
+            const TallyCols& x = pos < Cg ? st : ov;
+            const uint32_t j = pos < Cg ? pos : pos - Cg;
+            x.c_h[j] = b.height[i];
+            x.c_r[j] = b.round[i];
+            x.c_t[j] = b.type[i];
+            x.c_rep[j] = gidx ? gidx[i] : i;
+            x.c_n[j] = C.n[c];
+            C.claim[c] = kEmpty;
+            C.n[c] = 0;
+        }
+        const uint32_t rf = ref[q];
+        if ((rf & HD_REF_HASHED) && D[rf & ~HD_REF_HASHED] == q) D[rf & ~HD_REF_HASHED] = kEmpty;   // the log's winner
+    }
+}
+
+// HD_TALLY_CHECK after k_tally_emit: the tables are clean again
+__global__ void k_tally_check_clean(uint32_t cap, const uint32_t* __restrict__ tabs, TallyCtr* ctr, uint32_t* bad) {
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += gridDim.x * blockDim.x) {
+        bool ok = true;
+        for (int k = 0; k < 3; k++) ok &= tabs[(size_t)k * cap + s] == kEmpty;
+        for (int k = 3; k < 7; k++) ok &= tabs[(size_t)k * cap + s] == 0u;
+        if (!ok && atomicAdd(bad, 1u) == 0) printf("hd tally check: slot %u not clean after the emit\n", s);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (ctr->n_rounds | ctr->done)) atomicAdd(bad, 1u);
 }
 
 // ------------------------------------------------- consistency check (debug)
@@ -413,16 +650,17 @@ __global__ void k_tally_check_items(uint32_t m, const uint32_t* __restrict__ gsl
     }
 }
 
-__global__ void k_tally_check_cells(const uint32_t* __restrict__ Dd, const uint32_t* __restrict__ n_hr, uint32_t per,
-                                    size_t dcap, uint32_t m, const uint32_t* __restrict__ ref, TallyCheck* chk) {
-    const size_t cells = (size_t)*n_hr * per;
-    if (!Dd || cells > dcap) return;   // k_tally_logs hashed every candidate
+__global__ void k_tally_check_cells(const uint32_t* __restrict__ Dd, const TallyCtr* ctr, uint32_t per, uint32_t nd,
+                                    uint32_t m, const uint32_t* __restrict__ ref, TallyCheck* chk) {
+    if (!Dd) return;
+    const size_t cells = (size_t)min(ctr->n_rounds, nd) * per;   // the rounds numbered into dense cells
     for (size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x; c < cells; c += (size_t)gridDim.x * blockDim.x) {
         const uint32_t w = Dd[c];
         if (w == kEmpty) continue;
         atomicAdd(&chk->cells, 1u);
         if (w >= m || ref[w] != (uint32_t)c)
-            if (atomicAdd(&chk->bad_cell, 1u) == 0) printf("hd tally check: dense cell %lu holds item %u\n", (unsigned long)c, w);
+            if (atomicAdd(&chk->bad_cell, 1u) == 0)
+                printf("hd tally check: dense cell %lu holds item %u\n", (unsigned long)c, w);
     }
 }
 
@@ -468,21 +706,9 @@ __global__ void k_tally_check_slots(DevBatch b, const uint32_t* __restrict__ can
     }
 }
 
-// Output order: the groups of a table sorted by their first batch index.
-// Each occupied slot's claim word IS that index (unique per table), so the
-// sort is a scatter into an index-addressed array (at[claim] = slot) and an
-// ordered compaction of it -- no radix sort.
-__global__ __launch_bounds__(256) void k_tally_mark(uint32_t cap, const uint32_t* __restrict__ claim,
-                                                    uint32_t* __restrict__ at) {
-    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += gridDim.x * blockDim.x) {
-        const uint32_t c = claim[s];
-        if (c != kEmpty) at[c] = s;
-    }
-}
-
-// ordered compaction of at (n entries) in chunks of HD_CHUNK: per-chunk
-// counts, then each chunk writes from the sum of the counts before it (a
-// block reads at most n / HD_CHUNK words); rank_of[slot] = output position
+// ordered compaction of at (n entries) in chunks of HD_CHUNK (a partition's
+// candidates, in batch order): per-chunk counts, then each chunk writes from
+// the sum of the counts before it (a block reads at most n / HD_CHUNK words)
 #define HD_CHUNK 8192
 __global__ __launch_bounds__(256) void k_tally_chunk_counts(uint32_t n, const uint32_t* __restrict__ at,
                                                             uint32_t* __restrict__ cnt) {
@@ -531,54 +757,6 @@ __global__ __launch_bounds__(256) void k_tally_chunk_write(uint32_t n, const uin
                 o++;
             }
         }
-    }
-}
-
-// the dense log cells of the rounds found (n_hr x per words, n_hr on the
-// device), left alone when they exceed the allocation (k_tally_logs then
-// hashes every candidate)
-__global__ __launch_bounds__(256) void k_tally_dense_clear(uint32_t* __restrict__ Dd, const uint32_t* __restrict__ n_hr,
-                                                           uint32_t per, size_t cap) {
-    const size_t cells = (size_t)*n_hr * per;
-    if (cells > cap) return;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < cells; i += (size_t)gridDim.x * blockDim.x)
-        Dd[i] = kEmpty;
-}
-
-// Emit kernels: the first min(count, cap) groups in output order (count on
-// the device, cap the stage's capacity)
-__global__ void k_tally_emit_hr(const uint32_t* __restrict__ d_n, uint32_t cap, const uint32_t* __restrict__ slot,
-                                const uint32_t* __restrict__ cand,
-                                const uint32_t* __restrict__ gidx, GTab G, const int64_t* __restrict__ h,
-                                const int64_t* __restrict__ r, int64_t* __restrict__ oh, int64_t* __restrict__ orr,
-                                uint32_t* __restrict__ oprev, uint32_t* __restrict__ oprec, uint32_t* __restrict__ oany,
-                                uint32_t* __restrict__ orep) {
-    const uint32_t n = min(*d_n, cap);
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-        const uint32_t s = slot[k], i = msg_of(cand, G.claim[s]);
-        orep[k] = gidx ? gidx[i] : i;
-        oh[k] = h[i];
-        orr[k] = r[i];
-        oprev[k] = G.nprev[s];
-        oprec[k] = G.nprec[s];
-        oany[k] = G.nprev[s] + G.nprec[s] - G.nboth[s];
-    }
-}
-
-__global__ void k_tally_emit_counts(const uint32_t* __restrict__ d_n, uint32_t cap, const uint32_t* __restrict__ slot,
-                                    const uint32_t* __restrict__ cand,
-                                    const uint32_t* __restrict__ gidx, CTab C, const int64_t* __restrict__ h,
-                                    const int64_t* __restrict__ r, const uint8_t* __restrict__ type,
-                                    int64_t* __restrict__ oh, int64_t* __restrict__ orr, uint8_t* __restrict__ ot,
-                                    uint32_t* __restrict__ orep, uint32_t* __restrict__ on) {
-    const uint32_t n = min(*d_n, cap);
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-        const uint32_t s = slot[k], i = msg_of(cand, C.claim[s]);
-        oh[k] = h[i];
-        orr[k] = r[i];
-        ot[k] = type[i];
-        orep[k] = gidx ? gidx[i] : i;
-        on[k] = C.n[s];
     }
 }
 
@@ -732,21 +910,8 @@ void hd_tally_release(hd_ctx* ctx) {
 
 static inline uint32_t nblk(uint32_t n) { return (n + 255) / 256; }
 
-// the groups of one table (claim words, capacity cap) in first-index order:
-// order[0 .. total), rank_of[slot] (optional); the count lands in *d_total.
-// `at` (n words) must be all-empty on entry.
-static int table_order(hd_ctx* ctx, uint32_t n, uint32_t cap, const uint32_t* claim, uint32_t* at, uint32_t* cnt,
-                       uint32_t* order, uint32_t* rank_of, uint32_t* d_total, hipStream_t s) {
-    const uint32_t nch = (n + HD_CHUNK - 1) / HD_CHUNK;
-    k_tally_mark<<<std::min<uint32_t>(nblk(cap), (uint32_t)ctx->n_cu * 8u), 256, 0, s>>>(cap, claim, at);
-    k_tally_chunk_counts<<<nch, 256, 0, s>>>(n, at, cnt);
-    k_tally_chunk_write<<<nch, 256, 0, s>>>(n, at, cnt, order, rank_of, d_total);
-    TCHK(hipGetLastError(), "tally order kernels");
-    return HD_OK;
-}
-
-// dense log cells allowed (words): beyond this the hashed table takes every
-// candidate (e.g. a batch of a million single-message rounds)
+// dense log cells allowed (words): rounds numbered past nd = this / 2S take
+// the hashed table (e.g. a batch of a million single-message rounds)
 #define HD_TALLY_DENSE_MAX (64ull << 20)
 
 // dup_global[gidx[j]] = dup[j] (a routed batch's classification at its
@@ -757,33 +922,25 @@ __global__ __launch_bounds__(256) void k_dup_scatter(uint32_t n, const uint8_t* 
     if (j < n) dup_global[gidx[j]] = dup[j];
 }
 
-// The staged rows (column arrays at capacities h, c) into out's arrays.
-static void tally_unpack(const char* base, uint32_t h, uint32_t c, uint32_t n_hr, uint32_t n_cnt, hd_tally_out* out) {
-    const int64_t* o_h = reinterpret_cast<const int64_t*>(base);
-    const int64_t* o_r = o_h + h;
-    const uint32_t* o_prev = reinterpret_cast<const uint32_t*>(o_r + h);
-    const uint32_t* o_prec = o_prev + h;
-    const uint32_t* o_any = o_prec + h;
-    const uint32_t* o_rep = o_any + h;
-    const int64_t* c_h = reinterpret_cast<const int64_t*>(base + 32 * (size_t)h);
-    const int64_t* c_r = c_h + c;
-    const uint32_t* c_rep = reinterpret_cast<const uint32_t*>(c_r + c);
-    const uint32_t* c_n = c_rep + c;
-    const uint8_t* c_t = reinterpret_cast<const uint8_t*>(c_n + c);
-    auto put = [&](void* dst, const void* src, size_t sz) {
-        if (dst && sz) memcpy(dst, src, sz);
+// The first rows (at most capacities h, c of the column arrays at base) into
+// out's arrays, starting at row (o_hr, o_cnt).
+static void tally_unpack(const char* base, uint32_t h, uint32_t c, uint32_t n_hr, uint32_t n_cnt, hd_tally_out* out,
+                         uint32_t o_hr = 0, uint32_t o_cnt = 0) {
+    const TallyCols x = tally_cols(const_cast<char*>(base), h, c);
+    auto put = [&](void* dst, size_t at, const void* src, size_t sz) {
+        if (dst && sz) memcpy((char*)dst + at, src, sz);
     };
-    put(out->hr_height, o_h, 8 * (size_t)n_hr);
-    put(out->hr_round, o_r, 8 * (size_t)n_hr);
-    put(out->hr_prevotes, o_prev, 4 * (size_t)n_hr);
-    put(out->hr_precommits, o_prec, 4 * (size_t)n_hr);
-    put(out->hr_any, o_any, 4 * (size_t)n_hr);
-    put(out->hr_rep, o_rep, 4 * (size_t)n_hr);
-    put(out->count_height, c_h, 8 * (size_t)n_cnt);
-    put(out->count_round, c_r, 8 * (size_t)n_cnt);
-    put(out->count_type, c_t, (size_t)n_cnt);
-    put(out->count_rep, c_rep, 4 * (size_t)n_cnt);
-    put(out->count_n, c_n, 4 * (size_t)n_cnt);
+    put(out->hr_height, 8 * (size_t)o_hr, x.o_h, 8 * (size_t)n_hr);
+    put(out->hr_round, 8 * (size_t)o_hr, x.o_r, 8 * (size_t)n_hr);
+    put(out->hr_prevotes, 4 * (size_t)o_hr, x.o_prev, 4 * (size_t)n_hr);
+    put(out->hr_precommits, 4 * (size_t)o_hr, x.o_prec, 4 * (size_t)n_hr);
+    put(out->hr_any, 4 * (size_t)o_hr, x.o_any, 4 * (size_t)n_hr);
+    put(out->hr_rep, 4 * (size_t)o_hr, x.o_rep, 4 * (size_t)n_hr);
+    put(out->count_height, 8 * (size_t)o_cnt, x.c_h, 8 * (size_t)n_cnt);
+    put(out->count_round, 8 * (size_t)o_cnt, x.c_r, 8 * (size_t)n_cnt);
+    put(out->count_type, (size_t)o_cnt, x.c_t, (size_t)n_cnt);
+    put(out->count_rep, 4 * (size_t)o_cnt, x.c_rep, 4 * (size_t)n_cnt);
+    put(out->count_n, 4 * (size_t)o_cnt, x.c_n, 4 * (size_t)n_cnt);
 }
 
 // the stage layout: [n_hr, n_cnt | classification (n bytes, when staged) |
@@ -796,7 +953,7 @@ static size_t tally_stage_bytes(uint32_t n, bool dup, uint32_t h, uint32_t c) {
 // HD_TALLY_CHECK: the invariants of the tables just built (k_tally_check_*),
 // read back at once (a synchronisation: debug only)
 static int tally_check(hd_ctx* ctx, const DevBatch& b, const uint32_t* cand, uint32_t m, uint32_t cap, GTab G,
-                       CTab C, const uint32_t* D, const uint32_t* Dd, const uint32_t* n_hr, uint32_t per, size_t dcap,
+                       CTab C, const uint32_t* D, const uint32_t* Dd, const TallyCtr* ctr, uint32_t per, uint32_t nd,
                        const uint32_t* gslot, const uint32_t* ref, hipStream_t s) {
     int rc = 0;
     TallyCheck* chk = (TallyCheck*)tbuf(ctx, T_CHECK, sizeof(TallyCheck), &rc);
@@ -804,7 +961,7 @@ static int tally_check(hd_ctx* ctx, const DevBatch& b, const uint32_t* cand, uin
     TCHK(hipMemsetAsync(chk, 0, sizeof(TallyCheck), s), "tally check clear");
     const uint32_t grid = std::min<uint32_t>(nblk(std::max(m, cap)), (uint32_t)ctx->n_cu * 8u);
     k_tally_check_items<<<grid, 256, 0, s>>>(m, gslot, ref, Dd, D, chk);
-    k_tally_check_cells<<<grid, 256, 0, s>>>(Dd, n_hr, per, dcap, m, ref, chk);
+    k_tally_check_cells<<<grid, 256, 0, s>>>(Dd, ctr, per, nd, m, ref, chk);
     k_tally_check_slots<<<grid, 256, 0, s>>>(b, cand, m, cap, G, C, D, Dd, gslot, ref, chk);
     TCHK(hipGetLastError(), "tally check kernels");
     TallyCheck h{};
@@ -822,12 +979,35 @@ static int tally_check(hd_ctx* ctx, const DevBatch& b, const uint32_t* cand, uin
     return HD_EDEVICE;
 }
 
+// HD_TALLY_CHECK after the emit: every table slot and the counters are clean
+static int tally_check_clean(hd_ctx* ctx, uint32_t cap, const uint32_t* tabs, TallyCtr* ctr, hipStream_t s) {
+    int rc = 0;
+    uint32_t* bad = (uint32_t*)tbuf(ctx, T_CHECK, sizeof(TallyCheck), &rc);
+    if (rc) return rc;
+    TCHK(hipMemsetAsync(bad, 0, 4, s), "tally clean check clear");
+    k_tally_check_clean<<<std::min<uint32_t>(nblk(cap), (uint32_t)ctx->n_cu * 8u), 256, 0, s>>>(cap, tabs, ctr, bad);
+    uint32_t h = 0;
+    TCHK(hipMemcpyAsync(&h, bad, 4, hipMemcpyDeviceToHost, s), "tally clean check download");
+    TCHK(hipStreamSynchronize(s), "tally clean check sync");
+    if (h == 0) return HD_OK;
+    ctx->last_error = "tally check failed: " + std::to_string(h) + " table slots not clean after the emit";
+    return HD_EDEVICE;
+}
+
 // gidx (optional): the batch's messages' global indices -- the rep outputs
 // are mapped through it (a routed batch, hd_tally_routed_device); with
 // dup_global the per-message classification is scattered there through gidx
 // on the device instead of being downloaded (out->dup unused).  With `tk`
 // (hd_tally_device_bitmap_async) nothing is waited for: the stage goes to the
 // ticket's pinned buffer and hd_tally_collect unpacks it later.
+//
+// Launches per call: k_tally_rounds, k_tally_logs, k_tally_values,
+// k_tally_firsts, k_tally_emit and one download (a partition adds its
+// candidate compaction and one host read; a routed owner's scatter one
+// kernel).  The hash tables and counters clean themselves (k_tally_emit), the
+// dense cells are cleared by the round that takes them (k_tally_rounds), and
+// the bitmaps are written whole: nothing is cleared per call unless the
+// table capacity changed or an earlier call did not finish its launches.
 static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdict, const uint32_t* d_bitmap,
                         Part part, hd_tally_out* out, hipStream_t s, const uint32_t* gidx = nullptr,
                         uint8_t* dup_global = nullptr, hd_tally_ticket* tk = nullptr) {
@@ -837,11 +1017,15 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     int rc = 0;
     // blocks per CU of the probe passes (HD_TALLY_BPC, default 16)
     static const uint32_t bpc = getenv("HD_TALLY_BPC") ? (uint32_t)std::max(1, atoi(getenv("HD_TALLY_BPC"))) : 16u;
+    const bool check = [] {
+        const char* e = getenv("HD_TALLY_CHECK");
+        return e && atoi(e) != 0;
+    }();
     // The output stage: [n_hr, n_cnt | per-message classification | per-round
     // rows (32 B each, capacity H) | per-value rows (25 B each, capacity Cg)],
     // downloaded with ONE copy after ONE host sync.  H and Cg are the previous
-    // call's counts plus a margin; a batch with more groups than that emits and
-    // downloads its rows a second time (the counts are known by then).
+    // call's counts plus a margin; rows past them land in overflow columns on
+    // the device, downloaded by a second round of copies when needed.
     TallyWork* tw = ctx->tally;
     // the classification is staged for download only when the caller reads it
     // (out->dup, or the ticket's dup); a routed owner's scatter (dup_global)
@@ -859,8 +1043,6 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
         if (!tk->stage || tk->stage_cap < tk->need) return HD_ECAP;
     }
     char* st = (char*)tbuf(ctx, T_SEL, stage_bytes(H, Cg), &rc);
-    uint32_t* at = (uint32_t*)tbuf(ctx, T_SORTK, 8 * (size_t)n, &rc);   // candidate flags; then at_g | at_c
-    uint32_t* ccnt = (uint32_t*)tbuf(ctx, T_TMP, 4 * ((size_t)(n + HD_CHUNK - 1) / HD_CHUNK + 2), &rc);
     uint8_t* d_dup = stage_dup ? (uint8_t*)(st + dup_off) : nullptr;
     if (!stage_dup && dup_global) d_dup = (uint8_t*)tbuf(ctx, T_DUP, n, &rc);
     if (rc) return rc;
@@ -870,6 +1052,8 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     uint32_t m = n;
     const uint32_t* cand = nullptr;
     if (part.nparts > 1) {
+        uint32_t* at = (uint32_t*)tbuf(ctx, T_SORTK, 4 * (size_t)n, &rc);
+        uint32_t* ccnt = (uint32_t*)tbuf(ctx, T_TMP, 4 * ((size_t)(n + HD_CHUNK - 1) / HD_CHUNK + 2), &rc);
         uint32_t* cl = (uint32_t*)tbuf(ctx, T_D, 4 * (size_t)n, &rc);
         if (rc) return rc;
         const uint32_t nch = (n + HD_CHUNK - 1) / HD_CHUNK;
@@ -895,80 +1079,66 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     uint32_t cap = 1024;
     while (cap < 2 * m) cap <<= 1;
     const uint32_t mask = cap - 1;
-    const uint32_t nch = (m + HD_CHUNK - 1) / HD_CHUNK;
-    // one allocation for the tables: the claim words (G, C, D; := empty by one
-    // memset), then the counters (G x 3, C; := 0 by one memset), then rank_of
-    uint32_t* tabs = (uint32_t*)tbuf(ctx, T_G, 4 * 8 * (size_t)cap, &rc);
+    const uint32_t nbo = (m + HD_TALLY_IPB - 1) / HD_TALLY_IPB;   // blocks of the order passes
+    const size_t nw = (size_t)nbo * (HD_TALLY_IPB / 32);
+    // one allocation for the tables: the claim words (G, C, D: empty), the
+    // counters (G x 3, C: zero), the round numbers (gid); then the call
+    // counters (TallyCtr)
+    const size_t K = cap;
+    char* tb = (char*)tbuf(ctx, T_G, 4 * 8 * K + sizeof(TallyCtr), &rc);
     uint32_t* gslot = (uint32_t*)tbuf(ctx, T_GSLOT, 4 * (size_t)m, &rc);
     uint32_t* ref = (uint32_t*)tbuf(ctx, T_DSLOT, 4 * (size_t)m, &rc);
-    uint32_t* ord = (uint32_t*)tbuf(ctx, T_SORTV, 8 * (size_t)m, &rc);     // order_g | order_c
-    // dense log cells (n_hr x 2 x S, n_hr known on the device only) for
-    // admitted signatories, the hashed D table for the rest: room for every
-    // item's round up to HD_TALLY_DENSE_MAX words; the logs pass checks n_hr
+    uint32_t* cslot = (uint32_t*)tbuf(ctx, T_CSLOT, 4 * (size_t)m, &rc);
+    // Bg | Bc | pre_g | pre_c (nw words each) | block totals and offsets (4 nbo)
+    uint32_t* bits = (uint32_t*)tbuf(ctx, T_BITS, 4 * (4 * nw + 4 * (size_t)nbo), &rc);
+    // dense log cells (nd rounds x 2 x S) for admitted signatories, the hashed
+    // D table for the rest: room for every item's round up to HD_TALLY_DENSE_MAX words
     const uint32_t S = ctx->n_adm;
     const size_t dcap = S > 0 ? std::min<size_t>(HD_TALLY_DENSE_MAX, (size_t)m * 2 * S) : 0;
+    const uint32_t nd = S > 0 ? (uint32_t)(dcap / (2 * (size_t)S)) : 0u;
     uint32_t* Dd = dcap ? (uint32_t*)tbuf(ctx, T_C, 4 * dcap, &rc) : nullptr;
     if (rc) return rc;
-    const size_t K = cap;
-    GTab G{tabs, tabs + 3 * K, tabs + 4 * K, tabs + 5 * K};
+    uint32_t* tabs = (uint32_t*)tb;
+    GTab G{tabs, tabs + 3 * K, tabs + 4 * K, tabs + 5 * K, tabs + 7 * K};
     CTab C{tabs + K, tabs + 6 * K};
     uint32_t* d = tabs + 2 * K;
-    uint32_t* rank_of = tabs + 7 * K;
-    uint32_t* tot = ccnt + nch;
-    TCHK(hipMemsetAsync(tabs, 0xFF, 4 * 3 * K, s), "clear claims");
-    TCHK(hipMemsetAsync(tabs + 3 * K, 0, 4 * 4 * K, s), "clear counters");
-    TCHK(hipMemsetAsync(at, 0xFF, 8 * (size_t)m, s), "clear order marks");
-    // rounds, then their first-item order (the output order and the dense rank)
-    k_tally_rounds<<<grid, 256, 0, s>>>(b, cand, m, d_verdict, d_bitmap, part, G, mask, gslot, d_dup);
-    rc = table_order(ctx, m, cap, G.claim, at, ccnt, ord, rank_of, tot, s);
-    if (rc) return rc;
-    if (Dd)
-        k_tally_dense_clear<<<std::min<uint32_t>(nblk((uint32_t)dcap), (uint32_t)ctx->n_cu * 4u), 256, 0, s>>>(
-            Dd, tot, 2 * S, dcap);
-    const size_t adm_lds = Dd ? adm_lds_bytes(S) : 0;
-    k_tally_logs<<<grid, 256, adm_lds, s>>>(b, cand, m, gslot, rank_of, ctx->d_adm, S, ctx->adm_steps, Dd, tot, dcap, d,
-                                            mask, ref, adm_lds > 0);
-    k_tally_values<<<grid, 256, 0, s>>>(b, cand, m, Dd, S, d, G, C, mask, gslot, ref, d_dup);
+    TallyCtr* ctr = reinterpret_cast<TallyCtr*>(tb + 4 * 8 * K);
+    if (tw->dirty || tw->tab_p != tb || tw->tab_k != cap) {   // first use, new capacity, or an unfinished call
+        TCHK(hipMemsetAsync(tabs, 0xFF, 4 * 3 * K, s), "clear claims");
+        TCHK(hipMemsetAsync(tabs + 3 * K, 0, 4 * 4 * K, s), "clear counters");
+        TCHK(hipMemsetAsync(ctr, 0, sizeof(TallyCtr), s), "clear call counters");
+        tw->tab_p = tb;
+        tw->tab_k = cap;
+    }
+    tw->dirty = true;   // until every launch below is queued
+    k_tally_rounds<<<grid, 256, 0, s>>>(b, cand, m, d_verdict, d_bitmap, part, G, mask, gslot, d_dup, ctr, Dd, 2 * S,
+                                        nd);
+    const size_t adm_lds = nd ? adm_lds_bytes(S) : 0;
+    k_tally_logs<<<grid, 256, adm_lds, s>>>(b, cand, m, gslot, G.gid, ctx->d_adm, S, ctx->adm_steps, Dd, nd, d, mask,
+                                            ref, adm_lds > 0);
+    k_tally_values<<<grid, 256, 0, s>>>(b, cand, m, Dd, S, d, G, C, mask, gslot, ref, cslot, d_dup);
     if (dup_global && gidx) k_dup_scatter<<<nblk(n), 256, 0, s>>>(n, d_dup, gidx, dup_global);
     TCHK(hipGetLastError(), "tally kernels");
-    if (const char* e = getenv("HD_TALLY_CHECK"); e && atoi(e)) {
-        rc = tally_check(ctx, b, cand, m, cap, G, C, d, Dd, tot, 2 * S, dcap, gslot, ref, s);
+    if (check) {
+        rc = tally_check(ctx, b, cand, m, cap, G, C, d, Dd, ctr, 2 * S, nd, gslot, ref, s);
         if (rc) return rc;
     }
-    rc = table_order(ctx, m, cap, C.claim, at + m, ccnt, ord + m, nullptr, tot + 1, s);
+    uint32_t *Bg = bits, *Bc = bits + nw, *pre_g = bits + 2 * nw, *pre_c = bits + 3 * nw, *blk = bits + 4 * nw;
+    // rows at capacity (H, Cg) in the stage, the rest in the overflow columns
+    // (capacity m each: a batch has at most m groups of either kind)
+    char* ovf = (char*)tbuf(ctx, T_NSEL, 57 * (size_t)m + 64, &rc);
     if (rc) return rc;
-    // rows at capacity (H, Cg) in column arrays
-    struct Cols {
-        int64_t *o_h, *o_r, *c_h, *c_r;
-        uint32_t *o_prev, *o_prec, *o_any, *o_rep, *c_rep, *c_n;
-        uint8_t* c_t;
-    };
-    auto cols = [&](char* base, uint32_t h, uint32_t c) {
-        Cols x;
-        x.o_h = reinterpret_cast<int64_t*>(base);
-        x.o_r = x.o_h + h;
-        x.o_prev = reinterpret_cast<uint32_t*>(x.o_r + h);
-        x.o_prec = x.o_prev + h;
-        x.o_any = x.o_prec + h;
-        x.o_rep = x.o_any + h;
-        x.c_h = reinterpret_cast<int64_t*>(base + 32 * (size_t)h);
-        x.c_r = x.c_h + c;
-        x.c_rep = reinterpret_cast<uint32_t*>(x.c_r + c);
-        x.c_n = x.c_rep + c;
-        x.c_t = reinterpret_cast<uint8_t*>(x.c_n + c);
-        return x;
-    };
-    auto emit = [&](char* base, uint32_t h, uint32_t c) {
-        const Cols x = cols(base, h, c);
-        k_tally_emit_hr<<<std::min<uint32_t>(nblk(std::min(h, m)), (uint32_t)ctx->n_cu * 4u), 256, 0, s>>>(
-            tot, h, ord, cand, gidx, G, b.height, b.round, x.o_h, x.o_r, x.o_prev, x.o_prec, x.o_any, x.o_rep);
-        k_tally_emit_counts<<<std::min<uint32_t>(nblk(std::min(c, m)), (uint32_t)ctx->n_cu * 4u), 256, 0, s>>>(
-            tot + 1, c, ord + m, cand, gidx, C, b.height, b.round, b.type, x.c_h, x.c_r, x.c_t, x.c_rep, x.c_n);
-        return hipGetLastError();
-    };
-    TCHK(emit(st + rows_off, H, Cg), "tally emit");
-    TCHK(hipMemcpyAsync(st, tot, 8, hipMemcpyDeviceToDevice, s), "tally counts stage");
-    // (the stage is downloaded whole: the classification only when staged)
+    const TallyCols sc = tally_cols(st + rows_off, H, Cg), oc = tally_cols(ovf, m, m);
+    k_tally_firsts<<<nbo, 256, 0, s>>>(m, gslot, cslot, G.claim, C.claim, Bg, Bc, pre_g, pre_c, blk, ctr,
+                                       (uint32_t*)st);
+    k_tally_emit<<<nbo, 256, 0, s>>>(b, cand, m, gidx, gslot, cslot, ref, G, C, d, Bg, Bc, pre_g, pre_c, blk, sc, H,
+                                     Cg, oc);
+    TCHK(hipGetLastError(), "tally order kernels");
+    tw->dirty = false;
+    if (check) {
+        rc = tally_check_clean(ctx, cap, tabs, ctr, s);
+        if (rc) return rc;
+    }
     const size_t total = stage_bytes(H, Cg);
     if (tk) {   // queued; hd_tally_collect waits for tk->done, then reads the stage
         TCHK(hipMemcpyAsync(tk->stage, st, total, hipMemcpyDeviceToHost, s), "tally download");
@@ -993,26 +1163,30 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     tw->guess_cnt = std::max<uint32_t>(1024u, n_cnt + n_cnt / 4);
     if (n_hr > out->cap_hr || n_cnt > out->cap_counts) return HD_ECAP;
     if (out->dup) memcpy(out->dup, (const char*)tw->host + dup_off, (size_t)n);
-    const char* hrows = (const char*)tw->host + rows_off;
-    if (n_hr > H || n_cnt > Cg) {   // more groups than staged: emit and download the rows again
-        H = n_hr;
-        Cg = n_cnt;
-        const size_t rb = 32 * (size_t)H + 25 * (size_t)Cg;
-        char* st2 = (char*)tbuf(ctx, T_NSEL, rb + 64, &rc);
-        if (rc) return rc;
-        TCHK(emit(st2, H, Cg), "tally emit");
-        if (tw->host_cap < rb) {
-            (void)hipHostFree(tw->host);
-            tw->host = nullptr;
-            tw->host_cap = 0;
-            TCHK(hipHostMalloc(&tw->host, rb + (rb >> 2), hipHostMallocDefault), "tally host stage");
-            tw->host_cap = rb + (rb >> 2);
-        }
-        TCHK(hipMemcpyAsync(tw->host, st2, rb, hipMemcpyDeviceToHost, s), "tally download");
-        TCHK(hipStreamSynchronize(s), "tally sync");
-        hrows = (const char*)tw->host;
+    tally_unpack((const char*)tw->host + rows_off, H, Cg, std::min(n_hr, H), std::min(n_cnt, Cg), out);
+    if (n_hr > H || n_cnt > Cg) {   // more groups than staged: the overflow columns, straight into out
+        const uint32_t eh = n_hr > H ? n_hr - H : 0, ec = n_cnt > Cg ? n_cnt - Cg : 0;
+        struct Piece {
+            void* dst;
+            const void* src;
+            size_t sz;
+        } pieces[] = {
+            {out->hr_height ? out->hr_height + H : nullptr, oc.o_h, 8 * (size_t)eh},
+            {out->hr_round ? out->hr_round + H : nullptr, oc.o_r, 8 * (size_t)eh},
+            {out->hr_prevotes ? out->hr_prevotes + H : nullptr, oc.o_prev, 4 * (size_t)eh},
+            {out->hr_precommits ? out->hr_precommits + H : nullptr, oc.o_prec, 4 * (size_t)eh},
+            {out->hr_any ? out->hr_any + H : nullptr, oc.o_any, 4 * (size_t)eh},
+            {out->hr_rep ? out->hr_rep + H : nullptr, oc.o_rep, 4 * (size_t)eh},
+            {out->count_height ? out->count_height + Cg : nullptr, oc.c_h, 8 * (size_t)ec},
+            {out->count_round ? out->count_round + Cg : nullptr, oc.c_r, 8 * (size_t)ec},
+            {out->count_type ? out->count_type + Cg : nullptr, oc.c_t, (size_t)ec},
+            {out->count_rep ? out->count_rep + Cg : nullptr, oc.c_rep, 4 * (size_t)ec},
+            {out->count_n ? out->count_n + Cg : nullptr, oc.c_n, 4 * (size_t)ec},
+        };
+        for (const Piece& p : pieces)
+            if (p.dst && p.sz) TCHK(hipMemcpyAsync(p.dst, p.src, p.sz, hipMemcpyDeviceToHost, s), "tally overflow");
+        TCHK(hipStreamSynchronize(s), "tally overflow sync");
     }
-    tally_unpack(hrows, H, Cg, n_hr, n_cnt, out);
     return HD_OK;
 }
 

@@ -103,5 +103,8 @@ for step in "$@"; do
     pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_sq -o run -- python3 bench.py --steps 3 --warmup 0 --no-cpu --no-aux --no-sub ;;
     hiptrace_async) HD_BENCH_ASYNC_TALLY=1 run hiptrace_async 300 rocprofv3 --hip-trace --kernel-trace --output-format csv -d gpurun_out/hiptrace_async -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-aux --no-sub ;;
     routedtest) HD_TALLY_CHECK=1 run pytest_routed 400 python -u -m pytest tests/test_multi_gpu.py tests/test_gpu_tally.py -m gpu -x -v -p no:cacheprovider --timeout 200 --timeout-method thread ;;
+    tallycheck) HD_TALLY_CHECK=1 run pytest_tallycheck 600 python -u -m pytest tests/test_gpu_tally.py tests/test_golden.py tests/test_multi_gpu.py tests/test_ingress.py tests/test_c1_network.py -m gpu -x -v -p no:cacheprovider --timeout 200 --timeout-method thread ;;
+    goldsums) run pytest_goldsums 600 python -u -m pytest tests/test_golden.py tests/test_gpu_verify.py tests/test_fastpath.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    absums) run ab_sums 900 bash scripts/gpu_ab_prof.sh "base:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5base.so" "new:HD_SUM_WAVES=0" "base2:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5base.so" "new2:HD_SUM_WAVES=0" "base5:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5base.so AB_ADV=30" "new5:AB_ADV=30" ;;
   esac
 done

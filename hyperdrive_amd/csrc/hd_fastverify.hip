@@ -2,19 +2,16 @@
 // the tables it runs on (hd_fixedbase.h).
 //
 // Per batch, stream-ordered, no host synchronisation:
-//   k_fast_prep / k_fast_sinv / k_fast_digits / k_fast_sums / k_fast_zinv / k_fast_cmp
+//   k_fast_prep / k_fast_sinv / k_fast_sums / k_fast_zinv / k_fast_cmp
 //                   the split known-key check (the default, see "the split
 //                   check" below): a message whose claimed From is an
 //                   admitted signatory with a known key is checked with two
 //                   fixed-base multiplications (23 mixed additions, no
 //                   doublings, no square root); VALID / early exact verdicts
 //                   are final, everything else is appended to a list
-//   k_verify_fast   the older single-kernel form (two messages per lane,
-//                   HD_FAST_K=0), kept for A/B
 //   k_verify        (hd_verify.hip) the full libsecp256k1-semantics recovery
 //                   over that list only; VALID messages of signatories without
 //                   a known key publish the recovered key to their slot
-//   k_fb_bitmap     the valid bitmap from the final verdicts
 //   k_fb_list / k_fb_bases / k_fb_runs / k_fb_ready
 //                   build the tables of newly learned keys (window bases,
 //                   then the affine multiples by segments of consecutive
@@ -109,13 +106,6 @@ struct FbWork {
     hipStream_t last = nullptr;
     bool any = false;
     bool steady = false;          // the previous call ran with nothing to learn
-    // HD_VAR_SUM_CHAIN: k_fast_sums of consecutive calls run one after the
-    // other whatever their streams (a call's sums waits for the previous
-    // call's), so that only one call's sums holds the SIMDs at a time and the
-    // other calls' short kernels run beside it instead of in lockstep
-    hipEvent_t sums_done = nullptr;
-    hipStream_t sums_last = nullptr;
-    bool sums_any = false;
     // hd_ctx_profile: event pairs around whole calls and around k_fast_sums
     bool prof = false;
     std::vector<hipEvent_t> ev_call, ev_sums;
@@ -169,108 +159,17 @@ struct FastSrc {
     __device__ __forceinline__ void value_words(uint32_t w[8]) const { load_row32_be(w, b.value32, i); }
 };
 
-// Lane t checks messages 2t and 2t + 1 (verify_fast2: one inversion of each
-// kind for the pair).
-template <int WAVES>
-__global__ __launch_bounds__(256, WAVES) void k_verify_fast(DevBatch b, const uint8_t* __restrict__ digest_in,
-                                                     const gp* __restrict__ gtab, const gp* const* __restrict__ tabs, const uint32_t* __restrict__ state,
-                                                     const int32_t* __restrict__ adm_slot,
-                                                     const uint32_t* __restrict__ adm, const int32_t* __restrict__ adm_perm,
-                                                     uint32_t n_adm, int adm_steps, uint8_t* __restrict__ verdict,
-                                                     uint8_t* __restrict__ rec32, int32_t* __restrict__ signer,
-                                                     uint32_t* __restrict__ slow, uint32_t* __restrict__ n_slow) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    FastIn in[2];
-    int32_t idx[2], slot[2];
-    bool present[2], bad_type[2];
-    HD_UNROLL for (int k = 0; k < 2; k++) {
-        const uint32_t i = 2 * t + k;
-        present[k] = i < b.n;
-        bad_type[k] = false;
-        idx[k] = -1;
-        slot[k] = -1;
-        HD_UNROLL for (int w = 0; w < 8; w++) in[k].digest_be[w] = in[k].r_be[w] = in[k].s_be[w] = 0u;
-        in[k].v = 0;
-        in[k].ready = false;
-        if (!present[k]) continue;
-        FastSrc src{b, i, digest_in};
-        const uint32_t type = src.type();
-        if (type < 1 || type > 3) {
-            bad_type[k] = true;
-            continue;
-        }
-        uint32_t from_be[8];
-        HD_UNROLL for (int w = 0; w < 8; w++) from_be[w] = src.from(w);
-        idx[k] = admitted_find(adm, n_adm, adm_steps, from_be);
-        slot[k] = idx[k] >= 0 ? adm_slot[idx[k]] : -1;
-        in[k].ready = slot[k] >= 0 && state[slot[k]] == HD_FB_READY;
-        if (!in[k].ready) continue;
-        if (digest_in) {
-            HD_UNROLL for (int w = 0; w < 8; w++) in[k].digest_be[w] = load_be32(digest_in + 32 * (size_t)i + 4 * w);
-        } else {
-            uint32_t value_be[8];
-            HD_UNROLL for (int w = 0; w < 8; w++) value_be[w] = src.value(w);
-            if (type == T_PROPOSE)
-                sha256_propose(in[k].digest_be, b.height[i], b.round[i], b.valid_round ? b.valid_round[i] : -1,
-                               value_be);
-            else
-                sha256_vote(in[k].digest_be, b.height[i], b.round[i], value_be);
-        }
-        HD_UNROLL for (int w = 0; w < 8; w++) { in[k].r_be[w] = src.sig_r(w); in[k].s_be[w] = src.sig_s(w); }
-        in[k].v = src.sig_v();
-    }
-    uint8_t v[2];
-    __shared__ FastPark park[256];
-    verify_fast2(v, in, GpTab{gtab}, GpTab{slot[0] > 0 ? tabs[slot[0]] : gtab},
-                 GpTab{slot[1] > 0 ? tabs[slot[1]] : gtab}, &park[threadIdx.x]);
-    bool to_slow[2];
-    HD_UNROLL for (int k = 0; k < 2; k++) {
-        const uint32_t i = 2 * t + k;
-        to_slow[k] = false;
-        if (!present[k]) continue;
-        if (bad_type[k]) v[k] = V_BAD_TYPE;
-        if (v[k] == HD_NEEDS_SLOW) {
-            to_slow[k] = true;
-            continue;
-        }
-        // VALID: the recovered key is the signatory's, so the recovered
-        // signatory is From; early verdicts recover nothing
-        const bool ok = v[k] == V_VALID;
-        verdict[i] = v[k];
-        if (rec32) {
-            uint8_t* o = rec32 + 32 * (size_t)i;
-            const uint8_t* f = b.from32 + 32 * (size_t)i;
-            HD_UNROLL for (int w = 0; w < 8; w++) store_be32(o + 4 * w, ok ? load_be32(f + 4 * w) : 0u);
-        }
-        if (signer) signer[i] = ok ? adm_perm[idx[k]] : -1;
-    }
-    // wave-aggregated append of the slow-path indices (order is irrelevant:
-    // every message is verified on its own)
-    HD_UNROLL for (int k = 0; k < 2; k++) {
-        const unsigned long long bal = __ballot(to_slow[k]);
-        if (bal) {
-            const uint32_t lane = threadIdx.x & 63u;
-            const uint32_t leader = (uint32_t)__ffsll((long long)bal) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(n_slow, (uint32_t)__popcll(bal));
-            base = __shfl(base, (int)leader);
-            if (to_slow[k]) slow[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1))] = 2 * t + k;
-        }
-    }
-}
-
 // ---- the split check: K messages per lane share each inversion ----------
-// k_verify_fast inverts s and Z once per two messages.  The split form runs
-// the same check in six kernels: the two inversions (of s mod n, of Z mod p)
-// serve K messages of a lane each (Montgomery's trick over K), and everything
-// else runs one message per lane, so that only the inversion kernels have the
-// low occupancy of n / K lanes.  Per-message state sits in word-major HBM rows
+// The known-key check in five kernels: the two inversions (of s mod n, of Z
+// mod p) serve K messages of a lane each (Montgomery's trick over K), and
+// everything else runs one message per lane, so that only the inversion
+// kernels have the low occupancy of n / K lanes.  Per-message state sits in word-major HBM rows
 // between them (lane t reads word w of message i at w * n + i, coalesced):
 //   k_fast_prep     one per lane: lookup, digest, early checks; m, r, s
 //   k_fast_sinv     K per lane: prefix products of s, one inversion mod n,
 //                   s^-1 of each message
-//   k_fast_digits   one per lane: u1 = m / s, u2 = r / s as window digits
-//   k_fast_sums     one per lane: u1 G + u2 P (the first window's point
+//   k_fast_sums     one per lane: u1 = m / s, u2 = r / s as window digits
+//                   (into LDS), then u1 G + u2 P (the first window's point
 //                   loaded, one XYZZ mixed addition per further window)
 //   k_fast_zinv     K per lane: prefix products of Z, one inversion mod p,
 //                   Z^-1 of each message
@@ -278,8 +177,8 @@ __global__ __launch_bounds__(256, WAVES) void k_verify_fast(DevBatch b, const ui
 //                   bitmap and the fallback list
 // Message i of lane t of an inversion kernel is i = j T + t (j < K,
 // T = ceil(n / K)), so every step j of a wave touches consecutive messages.
-// The verdicts are the ones verify_fast2 gives: same early checks, same sums,
-// same comparison.
+// The verdicts are the ones verify_fast2 (hd_fixedbase.h, host-tested) gives:
+// same early checks, same sums, same comparison.
 #define HD_FAST_LIVE 0xFDu   // aux code: keep going (the rest are final verdicts or HD_NEEDS_SLOW)
 
 template <int NW>
@@ -299,7 +198,6 @@ struct SplitRows {
     uint32_t* s;     // 8n: s
     uint32_t* pre;   // 9n: prefix products of s, then s^-1 R (radix 2^29); later of Z, then Z^-1
     uint32_t* xyz;   // 27n: the XYZZ sum as (X ZZZ, Y ZZ, Z = ZZ ZZZ) (gxz_finish)
-    uint32_t* dig;   // (NWIN(WG) + NWIN(W)) n: window digits as table references (fb_ref)
     int prio;        // wave priority of the short kernels (HD_VAR_WAVE_PRIO)
 };
 
@@ -457,46 +355,14 @@ __global__ __launch_bounds__(256) void k_fast_sinv(uint32_t n, uint32_t T, Split
 // addition.  (Sending such messages to the full recovery instead costs a
 // whole recovery's latency per verify call: measured 1.95 -> 3.0 ms per 1M.)
 // The sums are XYZZ (gxz, hd_fixedbase.h: 8M + 2S per addition).
-// One addition of window point cur (digit flags ec) to acc.  The common step
-// is the bare in-place addition; a wavefront holding a zero digit or a
-// not-yet-started sum (rare: ~2^-W per window) also keeps the old sum for
-// its zero-digit lanes and starts the sum at cur where it had not started.
-// (The addition always runs in place, so no path leaves the accumulator in
-// other registers: the loop carries no copies of it.)
-HD void sum_step(gxz& acc, bool& started, ge cur, uint32_t ec) {
-    if (ec & HD_REF_NEG) fe_neg(cur.y, cur.y);
+// One window step (gxz_sum_step, hd_fixedbase.h): dst = src + the window's
+// point; the repair branch runs in a wavefront with a zero digit or a
+// not-yet-started sum.
+template <bool FIRST>
+HD void sum_add(gxz& dst, const gxz& src, bool& started, const ge& p0, const ge& g, uint32_t ec) {
     const bool nz = !(ec & HD_REF_ZERO);
     const bool rare = __ballot(!(started && nz)) != 0ull;
-    gxz keep;
-    if (rare) keep = acc;
-    gxz_add_ge_nx(acc, acc, cur);
-    if (rare) {
-        gxz first;
-        gxz_set_ge(first, cur);
-        fe_norm_weak(first.y);
-        gxz_cmov(acc, first, !started);
-        gxz_cmov(acc, keep, !nz);
-        started = started || nz;
-    }
-}
-
-// the first addition: the accumulator is still the first window's affine
-// point p0, so the cheaper affine + affine formula applies (4M + 2S)
-HD void sum_first(gxz& acc, bool& started, const ge& p0, ge cur, uint32_t ec) {
-    if (ec & HD_REF_NEG) fe_neg(cur.y, cur.y);
-    const bool nz = !(ec & HD_REF_ZERO);
-    const bool rare = __ballot(!(started && nz)) != 0ull;
-    gxz keep;
-    if (rare) keep = acc;
-    gxz_add_ge_z1(acc, p0, cur);
-    if (rare) {
-        gxz first;
-        gxz_set_ge(first, cur);
-        fe_norm_weak(first.y);
-        gxz_cmov(acc, first, !started);
-        gxz_cmov(acc, keep, !nz);
-        started = started || nz;
-    }
+    gxz_sum_step<FIRST>(dst, src, started, p0, g, (ec & HD_REF_NEG) != 0, nz, rare);
 }
 
 // the window digits of u1 = m / s and u2 = r / s (Montgomery products with
@@ -521,14 +387,6 @@ HD void fast_digit_refs(uint32_t* dst, size_t stride, const SplitRows& rows, uin
         dst[(size_t)(FbL<HD_FB_WG>::NWIN + w) * stride] = fb_ref<WP>(fb_digit<WP>(u, w), w);
 }
 
-// one message per lane: the digit rows of k_fast_sums<..., DL = false>
-template <int WP>
-__global__ __launch_bounds__(256) void k_fast_digits(uint32_t n, SplitRows rows) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || (rows.aux[i] & 0xFFu) != HD_FAST_LIVE) return;
-    fast_digit_refs<WP>(rows.dig + i, n, rows, n, i);
-}
-
 // a table point read through a global (address space 1) pointer (k_fast_sums)
 #if defined(__HIP_DEVICE_COMPILE__)
 typedef __attribute__((address_space(1))) const gp gp_global;
@@ -536,14 +394,14 @@ typedef __attribute__((address_space(1))) const gp gp_global;
 typedef const gp gp_global;
 #endif
 
-// DL: the digits are computed here, into this lane's column of an LDS array
-// (no k_fast_digits pass, no digit rows in HBM); else read from the rows.
-template <int WAVES, int WP, int PF, bool DL>
+// The digits are computed here, into this lane's column of an LDS array (no
+// digit pass, no digit rows in HBM).
+template <int WAVES, int WP, int PF>
 __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* __restrict__ gtab,
                                                           const gp* const* __restrict__ tabs, SplitRows rows) {
     constexpr int NG = FbL<HD_FB_WG>::NWIN, NT = NG + FbL<WP>::NWIN;
     static_assert(PF >= 0 && PF <= 2, "prefetch depth");
-    __shared__ uint32_t sdig[DL ? NT * 256 : 1];
+    __shared__ uint32_t sdig[NT * 256];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t a = rows.aux[i];
@@ -556,9 +414,9 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
     const gp_global* gt = (const gp_global*)gtab;
     const gp_global* pt = (const gp_global*)tabs[a >> 8];
     // a lane reads back only its own column: no barrier
-    const size_t dstride = DL ? 256 : n;
-    const uint32_t* dp = DL ? sdig + threadIdx.x : rows.dig + i;
-    if (DL) fast_digit_refs<WP>(sdig + threadIdx.x, 256, rows, n, i);
+    const size_t dstride = 256;
+    const uint32_t* dp = sdig + threadIdx.x;
+    fast_digit_refs<WP>(sdig + threadIdx.x, 256, rows, n, i);
     uint32_t e = dp[0];
     gxz acc;
     ge p0;
@@ -603,22 +461,24 @@ __global__ __launch_bounds__(256, WAVES) void k_fast_sums(uint32_t n, const gp* 
         }
         dn = dig(j + PF + 1);
     };
-    {
-        gp cur;
-        uint32_t ec;
-        advance(1, cur, ec);
-        ge g;
-        gp_unpack(g, cur);
-        sum_first(acc, started, p0, g, ec);
-    }
-    HD_NOUNROLL for (int j = 2; j < NT; j++) {
+    // two accumulators in turn (gxz_sum_step): window 1 into b, then a, b, ...
+    gxz b;
+    auto step = [&](int j, gxz& dst, const gxz& src) {
         gp cur;
         uint32_t ec;
         advance(j, cur, ec);
         ge g;
         gp_unpack(g, cur);
-        sum_step(acc, started, g, ec);
+        if (j == 1) sum_add<true>(dst, src, started, p0, g, ec);
+        else sum_add<false>(dst, src, started, p0, g, ec);
+    };
+    step(1, b, acc);
+    HD_NOUNROLL for (int j = 2; j + 1 < NT; j += 2) {
+        step(j, acc, b);
+        step(j + 1, b, acc);
     }
+    if constexpr ((NT - 2) % 2 == 1) step(NT - 1, acc, b);   // an odd number of windows after the first two
+    else acc = b;
     // infinity, or a degenerate addition on the way (ZZ = 0): full recovery
     if (!started || gxz_is_inf(acc)) {
         rows.aux[i] = (a & ~0xFFu) | HD_NEEDS_SLOW;
@@ -686,155 +546,6 @@ __global__ __launch_bounds__(256) void k_fast_zinv(uint32_t n, uint32_t T, Split
         constexpr int j = decltype(jc)::value;
         if ((live >> j) & 1u) soa_store(rows.pre, n, (uint32_t)j * T + t, node[K + j].n);
     });
-}
-
-// Lean forms of the two inversion kernels (HD_VAR_LEAN_INV): the same
-// inverses from one inversion per lane, but a linear walk whose prefix
-// products go to the pre row of each message (which later receives that
-// message's inverse), with each step's inputs loaded one live message ahead,
-// instead of K inputs and K prefixes (or a product tree) in registers.  Far
-// fewer VGPRs than 368 / 397: a running k_fast_sums held at two waves per
-// SIMD (HD_VAR_SUM_CAP) leaves room for them, so with HD_VAR_SUM_CHAIN one
-// call's inversions run beside another call's sums.
-HD uint32_t live_mask(const SplitRows& rows, uint32_t n, uint32_t T, uint32_t t, int K) {
-    uint32_t live = 0;
-    for (int j = 0; j < K; j++) {
-        const uint32_t i = (uint32_t)j * T + t;
-        if (i < n && (rows.aux[i] & 0xFFu) == HD_FAST_LIVE) live |= 1u << j;
-    }
-    return live;
-}
-HD int hi_bit(uint32_t m) { return 31 - __builtin_clz(m); }
-
-template <int K>
-__global__ __launch_bounds__(256) void k_fast_sinv_lean(uint32_t n, uint32_t T, SplitRows rows) {
-    wave_prio(rows.prio);
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= T) return;
-    const uint32_t live = live_mask(rows, n, T, t, K);
-    if (!live) return;
-    // forward: acc = the product of the live messages up to j, into pre[j]
-    sm acc;
-    sc nx;
-    uint32_t m = live;
-    soa_load(nx.v, rows.s, n, (uint32_t)(__ffs(m) - 1) * T + t);
-    bool first = true;
-    HD_NOUNROLL while (m) {
-        const uint32_t j = (uint32_t)(__ffs(m) - 1);
-        m &= m - 1;
-        const sc cur = nx;
-        if (m) soa_load(nx.v, rows.s, n, (uint32_t)(__ffs(m) - 1) * T + t);
-        sm ss;
-        sm_from_sc(ss, cur);
-        if (first) acc = ss;
-        else sm_mul(acc, acc, ss);
-        first = false;
-        soa_store(rows.pre, n, j * T + t, acc.n);
-    }
-    sm inv;
-    {
-        sc p, pinv;
-        sm_to_sc(p, acc);
-        sc_inv_divsteps(pinv, p);   // a product of scalars in [1, n) times R^-k: never 0
-        sm_from_sc(inv, pinv);
-        sm r2;
-        sm_r2(r2);
-        sm_mul(inv, inv, r2);
-    }
-    // backward: s_j^-1 = inv * pre[previous live], then inv *= s_j
-    m = live;
-    sm prev;
-    sc sj;
-    {
-        const int j = hi_bit(m);
-        const uint32_t below = m & ((1u << j) - 1u);
-        if (below) {
-            soa_load(prev.n, rows.pre, n, (uint32_t)hi_bit(below) * T + t);
-            soa_load(sj.v, rows.s, n, (uint32_t)j * T + t);
-        }
-    }
-    HD_NOUNROLL while (m) {
-        const int j = hi_bit(m);
-        m &= ~(1u << j);
-        const uint32_t i = (uint32_t)j * T + t;
-        if (!m) {
-            soa_store(rows.pre, n, i, inv.n);
-            break;
-        }
-        const sm pv = prev;
-        const sc sv = sj;
-        {   // the next step's inputs, loaded ahead
-            const int jn = hi_bit(m);
-            const uint32_t below = m & ((1u << jn) - 1u);
-            if (below) {
-                soa_load(prev.n, rows.pre, n, (uint32_t)hi_bit(below) * T + t);
-                soa_load(sj.v, rows.s, n, (uint32_t)jn * T + t);
-            }
-        }
-        sm sinv, ss;
-        sm_mul(sinv, inv, pv);
-        sm_from_sc(ss, sv);
-        sm_mul(inv, inv, ss);
-        soa_store(rows.pre, n, i, sinv.n);
-    }
-}
-
-template <int K>
-__global__ __launch_bounds__(256) void k_fast_zinv_lean(uint32_t n, uint32_t T, SplitRows rows) {
-    wave_prio(rows.prio);
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= T) return;
-    const uint32_t* zrow = rows.xyz + 18 * (size_t)n;
-    const uint32_t live = live_mask(rows, n, T, t, K);
-    if (!live) return;
-    fe acc, nx;
-    uint32_t m = live;
-    soa_load(nx.n, zrow, n, (uint32_t)(__ffs(m) - 1) * T + t);
-    bool first = true;
-    HD_NOUNROLL while (m) {
-        const uint32_t j = (uint32_t)(__ffs(m) - 1);
-        m &= m - 1;
-        const fe cur = nx;
-        if (m) soa_load(nx.n, zrow, n, (uint32_t)(__ffs(m) - 1) * T + t);
-        if (first) acc = cur;
-        else fe_mul(acc, acc, cur);
-        first = false;
-        soa_store(rows.pre, n, j * T + t, acc.n);
-    }
-    fe inv;
-    fe_inv_divsteps(inv, acc);   // a product of non-zero Z: never 0
-    m = live;
-    fe prev, zj;
-    {
-        const int j = hi_bit(m);
-        const uint32_t below = m & ((1u << j) - 1u);
-        if (below) {
-            soa_load(prev.n, rows.pre, n, (uint32_t)hi_bit(below) * T + t);
-            soa_load(zj.n, zrow, n, (uint32_t)j * T + t);
-        }
-    }
-    HD_NOUNROLL while (m) {
-        const int j = hi_bit(m);
-        m &= ~(1u << j);
-        const uint32_t i = (uint32_t)j * T + t;
-        if (!m) {
-            soa_store(rows.pre, n, i, inv.n);
-            break;
-        }
-        const fe pv = prev, zv = zj;
-        {
-            const int jn = hi_bit(m);
-            const uint32_t below = m & ((1u << jn) - 1u);
-            if (below) {
-                soa_load(prev.n, rows.pre, n, (uint32_t)hi_bit(below) * T + t);
-                soa_load(zj.n, zrow, n, (uint32_t)jn * T + t);
-            }
-        }
-        fe zi;
-        fe_mul(zi, inv, pv);
-        fe_mul(inv, inv, zv);
-        soa_store(rows.pre, n, i, zi.n);
-    }
 }
 
 // x = r (+ n when v & 2) as a field element: the x coordinate of R (the range
@@ -925,64 +636,6 @@ __global__ __launch_bounds__(256) void k_fast_cmp(DevBatch b, SplitRows rows, co
     cmp_one(b, rows, adm_perm, verdict, rec32, signer, slow, n_slow, bitmap, auth, i, i < b.n, nullptr);
 }
 
-// k_fast_zinv and k_fast_cmp in one kernel (HD_VAR_FUSED_CMP): the lane that
-// inverts the ZZ ZZZ of its K messages compares them too, walking j = 0..K-1
-// (message j T + t: for each j a wavefront covers 64 consecutive, 64-aligned
-// messages, so the ballots of cmp_one hold).  No Z^-1 rows are written and
-// read back, and the comparison's 1M lanes of launch and loads disappear; the
-// inversion kernel's chain grows by K comparisons.
-template <int K>
-__global__ __launch_bounds__(256) void k_fast_zinv_cmp(DevBatch b, uint32_t T, SplitRows rows,
-                                                       const int32_t* __restrict__ adm_perm,
-                                                       uint8_t* __restrict__ verdict, uint8_t* __restrict__ rec32,
-                                                       int32_t* __restrict__ signer, uint32_t* __restrict__ slow,
-                                                       uint32_t* __restrict__ n_slow, uint32_t* __restrict__ bitmap,
-                                                       bool auth) {
-    static_assert(K >= 2 && (K & (K - 1)) == 0, "K: a power of two");
-    wave_prio(rows.prio);
-    const uint32_t n = b.n;
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool lane_on = t < T;
-    const uint32_t* zrow = rows.xyz + 18 * (size_t)n;
-    fe node[2 * K];
-    uint32_t live = 0;
-    static_for<K>([&](auto jc) {
-        constexpr int j = decltype(jc)::value;
-        const uint32_t i = (uint32_t)j * T + t;
-        const bool in = lane_on && i < n;
-        const uint32_t ic = in ? i : 0;
-        const uint32_t a = rows.aux[ic];
-        fe z;
-        soa_load(z.n, zrow, n, ic);
-        const bool on = in && (a & 0xFFu) == HD_FAST_LIVE;
-        live |= on ? 1u << j : 0u;
-        HD_UNROLL for (int k = 1; k < 9; k++) z.n[k] = on ? z.n[k] : 0u;
-        z.n[0] = on ? z.n[0] : 1u;
-        node[K + j] = z;
-    });
-    if (__ballot(live != 0) != 0ull) {   // (a lane without live messages inverts ones)
-        static_for<K - 1>([&](auto ic) {
-            constexpr int i = K - 1 - decltype(ic)::value;
-            fe_mul(node[i], node[2 * i], node[2 * i + 1]);
-        });
-        fe_inv_divsteps(node[1], node[1]);   // a product of non-zero ZZ ZZZ (and ones): never 0
-        static_for<K - 1>([&](auto ic) {
-            constexpr int i = 1 + decltype(ic)::value;
-            fe a, c;
-            fe_mul(a, node[i], node[2 * i + 1]);
-            fe_mul(c, node[i], node[2 * i]);
-            node[2 * i] = a;
-            node[2 * i + 1] = c;
-        });
-    }
-    static_for<K>([&](auto jc) {
-        constexpr int j = decltype(jc)::value;
-        const uint32_t i = (uint32_t)j * T + t;
-        cmp_one(b, rows, adm_perm, verdict, rec32, signer, slow, n_slow, bitmap, auth, i, lane_on && i < n,
-                &node[K + j]);
-    });
-}
-
 // Before the full recovery of the leftovers: the reference's first checks
 // and the lift of R (V >= 4, r / s range,
 // r + n >= p, x^3 + 7 a square), in recover_m's order.  A message that fails
@@ -1056,15 +709,6 @@ __global__ __launch_bounds__(256) void k_slow_lift(DevBatch b, const uint32_t* _
             if (keep) out[o + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = i;
         }
     }
-}
-
-__global__ void k_fb_bitmap(uint32_t n, const uint8_t* __restrict__ verdict, uint32_t* __restrict__ bitmap) {
-    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (32 * w >= n) return;
-    uint32_t bits = 0;
-    const uint32_t lim = min(32u, n - 32 * w);
-    for (uint32_t k = 0; k < lim; k++) bits |= (uint32_t)(verdict[32 * w + k] == V_VALID) << k;
-    bitmap[w] = bits;
 }
 
 __global__ void k_fb_list(uint32_t nslots, const uint32_t* __restrict__ state, uint32_t* __restrict__ list,
@@ -1392,7 +1036,6 @@ void hd_fb_release(hd_ctx* ctx) {
     FbWork* f = ctx->fb;
     fb_free_tables(ctx);
     if (f->done) (void)hipEventDestroy(f->done);
-    if (f->sums_done) (void)hipEventDestroy(f->sums_done);
     for (hipEvent_t e : f->ev_call) (void)hipEventDestroy(e);
     for (hipEvent_t e : f->ev_sums) (void)hipEventDestroy(e);
     for (auto& sc : f->sc) {
@@ -1411,27 +1054,25 @@ void hd_fb_release(hd_ctx* ctx) {
     ctx->fb = nullptr;
 }
 
-// Messages per inversion of the split check (HD_VAR_SPLIT_K): 0 = the paired
-// kernel k_verify_fast, 4, 8 or 16; -1 (default) by batch size: 16 from
-// 2^20 - 2^16 messages up (65,536 lanes, one wave per SIMD), else 8.  The
-// inversion kernels are bound by their dependent ALU chains; halving the
-// inversions outweighs the lost second wave per SIMD (1M C2 messages, one
-// box, scalars and prefixes in registers: k_fast_sinv 102 -> 91 us,
-// k_fast_zinv 91 -> 76 us from K = 8 to 16; with the rows in HBM between
-// steps K = 4 / 8 / 16 gave 177 / 111 / 90 and 166 / 102 / 85 us)
+// Messages per inversion of the known-key check (HD_VAR_SPLIT_K): 8 or 16;
+// -1 (default) by batch size: 16 from 2^20 - 2^16 messages up (65,536 lanes,
+// one wave per SIMD), else 8.  The inversion kernels are bound by their
+// dependent ALU chains; halving the inversions outweighs the lost second wave
+// per SIMD (1M C2 messages, one box, scalars and prefixes in registers:
+// k_fast_sinv 102 -> 91 us, k_fast_zinv 91 -> 76 us from K = 8 to 16; with the
+// rows in HBM between steps K = 4 / 8 / 16 gave 177 / 111 / 90 and 166 / 102
+// / 85 us)
 static int split_k_for(const hd_ctx* ctx, uint32_t n) {
     const int k = ctx->var[HD_VAR_SPLIT_K];
-    if (k >= 0) return k;
+    if (k > 0) return k;
     return n >= (1u << 20) - (1u << 16) ? 16 : 8;
 }
 
 // Per-key window width for an admitted set of m: the wide tables
 // (HD_FB_WW, 13 additions for u2 instead of 16, 12x the bytes) when all m keys
 // fit the device's table budget next to what other contexts hold, else the
-// narrow ones.  HD_FB_PW=16|20 forces one; the paired check (HD_FAST_K=0)
-// only has the narrow form.
+// narrow ones.  HD_FB_PW=16|20 forces one.
 static int fb_pick_width(hd_ctx* ctx, uint32_t m) {
-    if (ctx->var[HD_VAR_SPLIT_K] == 0) return HD_FB_W;
     if (ctx->var[HD_VAR_KEY_WIDTH]) return ctx->var[HD_VAR_KEY_WIDTH];
     FbWork* f = ctx->fb;
     const double others = (double)(fb_device_bytes(ctx->device) - std::min(fb_device_bytes(ctx->device), f->bytes));
@@ -1581,19 +1222,8 @@ static uint32_t fallback_blocks(uint32_t est, uint32_t full) {
     return (uint32_t)std::min<uint64_t>(full, std::max<uint64_t>(want, std::min(64u, full)));
 }
 
-// Dynamic LDS that caps k_fast_sums at `cap` blocks per CU (HD_VAR_SUM_CAP):
-// with `stat` bytes of static LDS per block, a block reserves just over
-// 1 / (cap + 1) of the CU's 160 KiB.
-static size_t sums_cap_lds(int cap, size_t stat) {
-    if (cap <= 0) return 0;
-    const size_t per = ((160u * 1024u) / (size_t)(cap + 1) + 1 + 511) & ~(size_t)511;
-    return per > stat ? per - stat : 0;
-}
-
-// k_fast_sums occupancy (HD_VAR_SUM_WAVES), prefetch depth
-// (HD_VAR_SUM_PREFETCH) and where the window digits come from (DL:
-// HD_VAR_SUM_DIGITS 0 = computed into LDS, 1 = a k_fast_digits pass)
-template <int WP, bool DL>
+// k_fast_sums occupancy (HD_VAR_SUM_WAVES) and prefetch depth (HD_VAR_SUM_PREFETCH)
+template <int WP>
 static void launch_sums(const hd_ctx* ctx, uint32_t blocks, hipStream_t s, uint32_t n, const gp* gtab,
                         const gp* const* tab, const SplitRows& rows) {
     // 0 (the default): 4 waves per SIMD for a batch that fills fewer than two
@@ -1602,18 +1232,15 @@ static void launch_sums(const hd_ctx* ctx, uint32_t blocks, hipStream_t s, uint3
     int w = ctx->var[HD_VAR_SUM_WAVES];
     const int pf = ctx->var[HD_VAR_SUM_PREFETCH];
     if (w == 0) w = (uint64_t)n < 2ull * 3 * 4 * 64 * (uint64_t)std::max(ctx->n_cu, 1) ? 4 : 3;
-    constexpr size_t stat = DL ? 4 * 256 * (size_t)(FbL<HD_FB_WG>::NWIN + FbL<WP>::NWIN) : 4;
-    const size_t dyn = sums_cap_lds(ctx->var[HD_VAR_SUM_CAP], stat);
     if (pf == 2) {
-        if (w == 2) k_fast_sums<2, WP, 2, DL><<<blocks, 256, dyn, s>>>(n, gtab, tab, rows);
-        else k_fast_sums<3, WP, 2, DL><<<blocks, 256, dyn, s>>>(n, gtab, tab, rows);   // (no 4-wave form)
+        if (w == 2) k_fast_sums<2, WP, 2><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
+        else k_fast_sums<3, WP, 2><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);   // (no 4-wave form)
     } else {
-        if (w == 2) k_fast_sums<2, WP, 1, DL><<<blocks, 256, dyn, s>>>(n, gtab, tab, rows);
-        else if (w == 4) k_fast_sums<4, WP, 0, DL><<<blocks, 256, dyn, s>>>(n, gtab, tab, rows);
-        else k_fast_sums<3, WP, 1, DL><<<blocks, 256, dyn, s>>>(n, gtab, tab, rows);
+        if (w == 2) k_fast_sums<2, WP, 1><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
+        else if (w == 4) k_fast_sums<4, WP, 0><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
+        else k_fast_sums<3, WP, 1><<<blocks, 256, 0, s>>>(n, gtab, tab, rows);
     }
 }
-static bool sums_digits_lds(const hd_ctx* ctx) { return ctx->var[HD_VAR_SUM_DIGITS] == 0; }
 
 template <int K, int WP>
 static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict,
@@ -1627,39 +1254,12 @@ static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest
     const size_t adm_lds = adm_lds_bytes(ctx->n_adm);
     k_fast_prep<<<nb, 256, adm_lds, s>>>(b, d_digest, f->state, f->adm_slot, ctx->d_adm, ctx->n_adm, ctx->adm_steps,
                                          rows, adm_lds > 0, f->fcap ? f->fdict : nullptr);
-    // K > 16 exists only in the lean forms (the register forms would not fit)
-    const bool lean = K > 16 || ctx->var[HD_VAR_LEAN_INV] != 0;
-    if constexpr (K > 16) k_fast_sinv_lean<K><<<tb, 256, 0, s>>>(n, T, rows);
-    else if (lean) k_fast_sinv_lean<K><<<tb, 256, 0, s>>>(n, T, rows);
-    else k_fast_sinv<K><<<tb, 256, 0, s>>>(n, T, rows);
-    const bool dl = sums_digits_lds(ctx);
-    if (!dl) k_fast_digits<WP><<<nb, 256, 0, s>>>(n, rows);
-    const bool chain = ctx->var[HD_VAR_SUM_CHAIN] != 0;
-    if (chain) {
-        if (!f->sums_done) (void)hipEventCreateWithFlags(&f->sums_done, hipEventDisableTiming);
-        if (f->sums_any && f->sums_last != s) (void)hipStreamWaitEvent(s, f->sums_done, 0);
-    }
+    k_fast_sinv<K><<<tb, 256, 0, s>>>(n, T, rows);
     hipEvent_t* pe = fb_prof_pair(f->ev_sums, f->n_sums, f->prof);
     if (pe) (void)hipEventRecord(pe[0], s);
-    if (dl) launch_sums<WP, true>(ctx, nb, s, n, f->gtab, f->tabs, rows);
-    else launch_sums<WP, false>(ctx, nb, s, n, f->gtab, f->tabs, rows);
+    launch_sums<WP>(ctx, nb, s, n, f->gtab, f->tabs, rows);
     if (pe) (void)hipEventRecord(pe[1], s);
-    if (chain && f->sums_done) {
-        (void)hipEventRecord(f->sums_done, s);
-        f->sums_last = s;
-        f->sums_any = true;
-    }
-    if constexpr (K <= 16) {
-        if (ctx->var[HD_VAR_FUSED_CMP]) {
-            // T is a multiple of 64: each j step of a wavefront is one bitmap word pair
-            k_fast_zinv_cmp<K><<<tb, 256, 0, s>>>(b, T, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer,
-                                                  sc.slow, sc.count, d_bitmap, auth);
-            return;
-        }
-    }
-    if constexpr (K > 16) k_fast_zinv_lean<K><<<tb, 256, 0, s>>>(n, T, rows);
-    else if (lean) k_fast_zinv_lean<K><<<tb, 256, 0, s>>>(n, T, rows);
-    else k_fast_zinv<K><<<tb, 256, 0, s>>>(n, T, rows);
+    k_fast_zinv<K><<<tb, 256, 0, s>>>(n, T, rows);
     // whole blocks of 256: every wavefront's 64 messages are one bitmap word pair
     k_fast_cmp<<<nb, 256, 0, s>>>(b, rows, ctx->d_adm_perm, d_verdict, d_rec32, d_signer, sc.slow, sc.count,
                                   d_bitmap, auth);
@@ -1716,14 +1316,11 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
     int rc = hd_dev_grow(ctx, (void**)&sc.slow, &sc.cap_slow, 4 * (size_t)b.n);
     if (rc) return rc;
     const uint32_t blocks = (b.n + 255) / 256;
-    const uint32_t fast_blocks = ((b.n + 1) / 2 + 255) / 256;   // two messages per lane
     rc = hd_dev_grow(ctx, (void**)&sc.slow2, &sc.cap_slow2, 4 * (size_t)b.n);
     if (rc) return rc;
     FBCHK(hipMemsetAsync(sc.count, 0, 8, s), "fb count reset");
-    if (ctx->n_adm > 0 && f->adm_slot && split_k_for(ctx, b.n) > 0) {
-        // 62 words per message; the digit rows (the narrow width has more
-        // windows) only for the HD_SUM_DIGITS=rows A/B form
-        const size_t row_words = 62 + (sums_digits_lds(ctx) ? 0 : FbL<HD_FB_WG>::NWIN + FbL<HD_FB_W>::NWIN);
+    if (ctx->n_adm > 0 && f->adm_slot) {
+        const size_t row_words = 62;   // per message
         rc = hd_dev_grow(ctx, (void**)&sc.rows, &sc.cap_rows, 4 * row_words * (size_t)b.n);
         if (rc) return rc;
         const uint32_t n = b.n;
@@ -1735,20 +1332,15 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         rows.s = sc.rows + 18 * (size_t)n;
         rows.pre = sc.rows + 26 * (size_t)n;
         rows.xyz = sc.rows + 35 * (size_t)n;
-        rows.dig = sums_digits_lds(ctx) ? nullptr : sc.rows + 62 * (size_t)n;
         rows.prio = ctx->var[HD_VAR_WAVE_PRIO];
         const int k = split_k_for(ctx, n);
         f->last_k = k;
 #define HD_SPLIT(K, WP) launch_split<K, WP>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, sc, s, auth)
         if (f->wp == HD_FB_WW) {
             if (k == 16) HD_SPLIT(16, HD_FB_WW);
-            else if (k == 32) HD_SPLIT(32, HD_FB_WW);
-            else if (k == 4) HD_SPLIT(4, HD_FB_WW);
             else HD_SPLIT(8, HD_FB_WW);
         } else {
             if (k == 16) HD_SPLIT(16, HD_FB_W);
-            else if (k == 32) HD_SPLIT(32, HD_FB_W);
-            else if (k == 4) HD_SPLIT(4, HD_FB_W);
             else HD_SPLIT(8, HD_FB_W);
         }
 #undef HD_SPLIT
@@ -1775,34 +1367,6 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl,
                             fallback_blocks(f->est_host[lift ? 1 : 0], full), s);
         if (rc) return rc;
-        return fb_learn(ctx, s);
-    }
-    if (ctx->n_adm > 0 && f->adm_slot) {
-        const int fw = ctx->var[HD_VAR_FAST_WAVES];
-#define HD_LAUNCH_FAST(W)                                                                                        \
-    k_verify_fast<W><<<fast_blocks, 256, 0, s>>>(b, d_digest, f->gtab, f->tabs, f->state, f->adm_slot, ctx->d_adm, ctx->d_adm_perm, \
-                                            ctx->n_adm, ctx->adm_steps, d_verdict, d_rec32, d_signer, sc.slow,       \
-                                            sc.count)
-        if (fw == 2) HD_LAUNCH_FAST(2);
-        else HD_LAUNCH_FAST(3);   // (4 and 5 waves spill heavily; not offered)
-#undef HD_LAUNCH_FAST
-        FBCHK(hipGetLastError(), "k_verify_fast launch");
-        // the fallback list is usually short (its length is only known on the
-        // device): a grid of 4 blocks per CU walks it, instead of one block
-        // per 256 messages that would mostly start and exit
-        const uint32_t slow_blocks = std::min(blocks, (uint32_t)std::max(ctx->n_cu, 1) * 4u);
-        SplitRows none{};
-        k_slow_lift<<<slow_blocks, 256, 0, s>>>(b, sc.slow, sc.count, d_verdict, d_rec32, d_signer, sc.slow2,
-                                                sc.count + 1, ctx->var[HD_VAR_WAVE_PRIO], nullptr, none, nullptr);
-        FBCHK(hipGetLastError(), "k_slow_lift");
-        const SlowCtl ctl{sc.slow2, sc.count + 1, f->adm_slot, f->state, f->pub, nullptr, nullptr,
-                          ctx->var[HD_VAR_WAVE_PRIO], nullptr, nullptr, 0, 0, nullptr};
-        rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl, slow_blocks, s);
-        if (rc) return rc;
-        if (d_bitmap) {
-            k_fb_bitmap<<<((b.n + 31) / 32 + 255) / 256, 256, 0, s>>>(b.n, d_verdict, d_bitmap);
-            FBCHK(hipGetLastError(), "k_fb_bitmap launch");
-        }
         return fb_learn(ctx, s);
     }
     // no admitted set: every message takes the full recovery (it ends in

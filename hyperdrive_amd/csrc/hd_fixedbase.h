@@ -279,6 +279,45 @@ HD void gxz_add_ge_z1(gxz& r, const ge& a, const ge& b) {
     r = o;
 }
 
+// Keeps a wavefront-uniform branch a branch (the compiler would otherwise
+// turn a short guarded block into selects that every caller executes).
+HD void hd_branch_barrier() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" ::: "memory");
+#endif
+}
+
+// One window step of k_fast_sums (and of its host check,
+// tests/native/hd_host_check.cpp hdh_xyzz_sum): dst = src + the window's
+// table point g (negated when neg); FIRST: src is still the first window's
+// affine point p0, so the affine + affine formula applies.  The kernel
+// alternates two accumulators (dst and src swap roles every step), so the
+// addition never overwrites its own inputs: the compiler schedules it more
+// freely than an in-place update (measured ~2 % faster), and the old sum is
+// still at hand for the rare repair.  `rare` (the kernel: some lane of the
+// wavefront has a zero digit, nz false, or a sum not yet started) runs the
+// repair in a branch of its own:
+//  * a zero digit's lane keeps the old sum (it added the window's entry 0,
+//    read in its place);
+//  * a lane whose sum had not started starts it at the window's point.
+template <bool FIRST>
+HD void gxz_sum_step(gxz& dst, const gxz& src, bool& started, const ge& p0, const ge& g, bool neg, bool nz,
+                     bool rare) {
+    ge cur = g;
+    if (neg) fe_neg(cur.y, g.y);
+    if (FIRST) gxz_add_ge_z1(dst, p0, cur);
+    else gxz_add_ge_nx(dst, src, cur);
+    if (rare) {
+        hd_branch_barrier();
+        gxz first;
+        gxz_cmov(dst, src, !nz);
+        gxz_set_ge(first, cur);
+        fe_norm_weak(first.y);
+        gxz_cmov(dst, first, !started);
+        started = started || nz;
+    }
+}
+
 // the sum as k_fast_sums stores it: X ZZZ, Y ZZ and the value to invert, ZZ ZZZ
 HD void gxz_finish(fe& xn, fe& yn, fe& t, const gxz& a) {
     fe_mul(xn, a.x, a.zzz);

@@ -217,15 +217,11 @@ int hd_ctx_create(int device, hd_ctx** out) {
     struct { int key; const char* env; } envs[] = {
         {HD_VAR_VERIFY_WAVES, "HD_VERIFY_WAVES"}, {HD_VAR_SUM_WAVES, "HD_SUM_WAVES"},
         {HD_VAR_SUM_PREFETCH, "HD_SUM_PF"},       {HD_VAR_SPLIT_K, "HD_FAST_K"},
-        {HD_VAR_FAST_WAVES, "HD_FAST_WAVES"},     {HD_VAR_KEY_WIDTH, "HD_FB_PW"},
-        {HD_VAR_WAVE_PRIO, "HD_WAVE_PRIO"},       {HD_VAR_SUM_CAP, "HD_SUM_CAP"},
+        {HD_VAR_KEY_WIDTH, "HD_FB_PW"},           {HD_VAR_WAVE_PRIO, "HD_WAVE_PRIO"},
         {HD_VAR_FOREIGN_KEYS, "HD_FOREIGN_KEYS"}, {HD_VAR_SLOW_LIFT, "HD_SLOW_LIFT"},
-        {HD_VAR_FUSED_CMP, "HD_FUSED_CMP"},       {HD_VAR_LEAN_INV, "HD_LEAN_INV"},
-        {HD_VAR_SUM_CHAIN, "HD_SUM_CHAIN"},
     };
     for (auto& ev : envs)
         if (const char* e = getenv(ev.env)) (void)hd_ctx_set_variant(ctx, ev.key, atoi(e));
-    if (const char* e = getenv("HD_SUM_DIGITS")) (void)hd_ctx_set_variant(ctx, HD_VAR_SUM_DIGITS, strcmp(e, "rows") == 0);
     if (getenv("HD_RECOVER_GLV_G")) (void)hd_ctx_set_variant(ctx, HD_VAR_RECOVER_G, 1);
     if (const char* f = getenv("HD_VERIFY_FASTPATH")) ctx->fastpath = atoi(f) != 0;
     // G tables (1G..2048G and lambda*(1G..2048G), affine), built once on the
@@ -285,15 +281,13 @@ int hd_ctx_set_variant(hd_ctx* ctx, int which, int value) {
     switch (which) {
         case HD_VAR_VERIFY_WAVES: ok = value >= 2 && value <= 4; break;
         case HD_VAR_SUM_WAVES: ok = value == 0 || (value >= 2 && value <= 4); break;
-        case HD_VAR_FAST_WAVES: ok = value == 2 || value == 3; break;
         case HD_VAR_SUM_PREFETCH: ok = value == 1 || value == 2; break;
-        case HD_VAR_SUM_DIGITS: case HD_VAR_RECOVER_G: ok = value == 0 || value == 1; break;
-        case HD_VAR_SPLIT_K: ok = value == -1 || value == 0 || value == 4 || value == 8 || value == 16 || value == 32; break;
+        case HD_VAR_RECOVER_G: case HD_VAR_SLOW_LIFT: ok = value == 0 || value == 1; break;
+        case HD_VAR_SPLIT_K: ok = value == -1 || value == 8 || value == 16; break;
         case HD_VAR_KEY_WIDTH: ok = value == 0 || value == HD_FB_W || value == HD_FB_WW; break;
         case HD_VAR_WAVE_PRIO: ok = value >= 0 && value <= 3; break;
-        case HD_VAR_SUM_CAP: ok = value == 0 || value == 2; break;
         case HD_VAR_FOREIGN_KEYS: ok = value >= 0 && value <= 64; break;
-        case HD_VAR_SLOW_LIFT: case HD_VAR_FUSED_CMP: case HD_VAR_LEAN_INV: case HD_VAR_SUM_CHAIN: ok = value == 0 || value == 1; break;
+        default: ok = false;   // a key of a variant removed in round 5 (measured without gain)
     }
     if (!ok) return HD_EINVAL;
     ctx->var[which] = value;

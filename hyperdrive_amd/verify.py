@@ -214,10 +214,8 @@ class Verifier:
         self.n_signatories = len(arr)
 
     # include/hd_verify.h HD_VAR_*: kernel variants of this context
-    VARIANTS = {"verify_waves": 0, "sum_waves": 1, "sum_prefetch": 2, "sum_digits": 3, "split_k": 4,
-                "recover_g": 5, "fast_waves": 6, "key_width": 7, "wave_prio": 8, "sum_cap": 9,
-                "foreign_keys": 10, "slow_lift": 11, "fused_cmp": 12,
-                "lean_inv": 13, "sum_chain": 14}
+    VARIANTS = {"verify_waves": 0, "sum_waves": 1, "sum_prefetch": 2, "split_k": 4, "recover_g": 5,
+                "key_width": 7, "wave_prio": 8, "foreign_keys": 10, "slow_lift": 11}
 
     def set_variant(self, name: str, value: int) -> None:
         """Select a compiled kernel variant (A/B, variant tests); see

@@ -158,14 +158,10 @@ int hd_ctx_profile(hd_ctx* ctx, int enable);
 #define HD_VAR_SUM_WAVES 1      /* k_fast_sums waves per SIMD: 2, 3 or 4 (128 VGPRs, table points loaded when
                                    used); 0 (default) 4 for batches under two rounds at 3, else 3 [HD_SUM_WAVES] */
 #define HD_VAR_SUM_PREFETCH 2   /* k_fast_sums table-point prefetch depth: 1 (default) or 2 [HD_SUM_PF] */
-#define HD_VAR_SUM_DIGITS 3     /* window digits: 0 in k_fast_sums' LDS (default), 1 a k_fast_digits pass
-                                   [HD_SUM_DIGITS=rows] */
 #define HD_VAR_SPLIT_K 4        /* messages per inversion of the known-key check: -1 by batch size (default),
-                                   0 the paired kernel k_verify_fast, 4, 8, 16 or 32 (32 always with the lean
-                                   inversion kernels, HD_VAR_LEAN_INV) [HD_FAST_K] */
+                                   8 or 16 [HD_FAST_K] */
 #define HD_VAR_RECOVER_G 5      /* the full recovery's u1 G: 0 from the fixed-base G table (default), 1 from the
                                    GLV ladder's own 12-bit table [HD_RECOVER_GLV_G] */
-#define HD_VAR_FAST_WAVES 6     /* k_verify_fast (split K = 0): 2 (default) or 3 [HD_FAST_WAVES] */
 #define HD_VAR_KEY_WIDTH 7      /* per-key table windows: 0 by the table budget (default), 16 or 20; applies from
                                    the next hd_set_signatories [HD_FB_PW] */
 #define HD_VAR_WAVE_PRIO 8      /* wave issue priority (s_setprio 0..3) of the known-key check's short kernels
@@ -173,10 +169,6 @@ int hd_ctx_profile(hd_ctx* ctx, int enable);
                                    k_fast_sums' 0 they keep
                                    their SIMD share while the next call's sums waves share the SIMD
                                    [HD_WAVE_PRIO] */
-#define HD_VAR_SUM_CAP 9        /* k_fast_sums residency: 0 as registers allow (3 waves per SIMD, default), 2 at
-                                   most 2 blocks per CU (2 waves per SIMD, by an LDS reservation), leaving a
-                                   slot per SIMD to the short kernels of a concurrent call and the tally
-                                   [HD_SUM_CAP] */
 #define HD_VAR_FOREIGN_KEYS 10  /* table slots (0..64) reserved for authenticated Froms outside the admitted set:
                                    a NOT_ADMITTED recovery teaches the context its key, and later messages of
                                    that From take the known-key check (verdict NOT_ADMITTED, identical to the
@@ -186,16 +178,10 @@ int hd_ctx_profile(hd_ctx* ctx, int enable);
 #define HD_VAR_SLOW_LIFT 11     /* the known-key check's leftovers: 1 (default) a lift kernel first (x^3 + 7 a
                                    square, else NO_POINT), then the full recovery over the rest; 0 the full
                                    recovery over every leftover (it checks the lift itself) [HD_SLOW_LIFT] */
-#define HD_VAR_FUSED_CMP 12     /* the known-key check's last step: 0 (default) an inversion kernel then a
-                                   comparison kernel, 1 one kernel whose lanes compare the K messages whose
-                                   ZZ ZZZ they inverted [HD_FUSED_CMP] */
-#define HD_VAR_LEAN_INV 13      /* the known-key check's inversion kernels: 0 (default) the lane's K inputs and
-                                   prefixes in registers, 1 the lean forms (prefixes in the rows, inputs
-                                   loaded one step ahead; few VGPRs, so they fit beside a running
-                                   k_fast_sums held at two waves per SIMD) [HD_LEAN_INV] */
-#define HD_VAR_SUM_CHAIN 14     /* 1: the k_fast_sums of consecutive verify calls run one after the other,
-                                   whatever their streams, so that the short kernels of one call run beside
-                                   the sums of another; 0 (default) no such order [HD_SUM_CHAIN] */
+/* Keys 3, 6, 9, 12, 13 and 14 (the digit pass, the paired kernel's waves, the
+ * sums residency cap, the fused comparison, the lean inversions and the sums
+ * chain) were measured without gain and removed in round 5: set returns
+ * HD_EINVAL for them, get returns their fixed value. */
 #define HD_VAR__COUNT 15
 int hd_ctx_set_variant(hd_ctx* ctx, int which, int value);
 int hd_ctx_get_variant(hd_ctx* ctx, int which, int* value);

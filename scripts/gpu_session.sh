@@ -106,5 +106,7 @@ for step in "$@"; do
     tallycheck) HD_TALLY_CHECK=1 run pytest_tallycheck 600 python -u -m pytest tests/test_gpu_tally.py tests/test_golden.py tests/test_multi_gpu.py tests/test_ingress.py tests/test_c1_network.py -m gpu -x -v -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     goldsums) run pytest_goldsums 600 python -u -m pytest tests/test_golden.py tests/test_gpu_verify.py tests/test_fastpath.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     absums) run ab_sums 900 bash scripts/gpu_ab_prof.sh "base:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5base.so" "new:HD_SUM_WAVES=0" "base2:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5base.so" "new2:HD_SUM_WAVES=0" "base5:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5base.so AB_ADV=30" "new5:AB_ADV=30" ;;
+    absums2) run ab_sums2 900 bash scripts/gpu_ab_prof.sh "base:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5base.so" "p1:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5p1.so" "new:HD_SUM_WAVES=0" "base2:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5base.so" "p1b:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5p1.so" "new2:HD_SUM_WAVES=0" ;;
+    absums3) run ab_sums3 900 bash scripts/gpu_ab_prof.sh "p1:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5p1.so" "pp:HD_SUM_WAVES=0" "p1b:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5p1.so" "ppb:HD_SUM_WAVES=0" "pp_pf2:HD_SUM_PF=2" "p1_pf2:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5p1.so HD_SUM_PF=2" ;;
   esac
 done

@@ -488,41 +488,37 @@ extern "C" int hdh_add_affine(const uint8_t* ax, const uint8_t* ay, const uint8_
 
 // k_fast_sums' XYZZ accumulation on the host: n affine points (x || y
 // big-endian, 64 B each), point k negated when neg[k] and skipped when
-// skip[k] (a zero digit), summed the way the kernel does it (the first
-// non-skipped point starts the sum, the affine first addition when the
-// second window's digit is non-zero, then gxz_add_ge_nx); the result through
-// gxz_finish, one inversion and fast_final_xz's products.  Returns 1 for a
-// degenerate sum (ZZ = 0 or nothing started), else out = affine x || y.
-extern "C" int hdh_xyzz_sum(const uint8_t* pts, const int* neg, const int* skip, int n, uint8_t* out64) {
+// skip[k] (a zero digit), summed by the kernel's own window step
+// (gxz_sum_step: the first window's point starts the sum, the affine first
+// addition, then the general one, each into the other accumulator and
+// followed by the repair branch when `rare`).  force_rare runs the repair branch at every step (the kernel runs
+// it whenever any lane of the wavefront needs it), else only where this
+// lane needs it.  The result goes through gxz_finish, one inversion and
+// fast_final_xz's products.  Returns 1 for a degenerate sum (ZZ = 0 or
+// nothing started), else out = affine x || y.
+extern "C" int hdh_xyzz_sum(const uint8_t* pts, const int* neg, const int* skip, int n, uint8_t* out64,
+                            int force_rare) {
     gxz acc;
+    ge p0;
     bool started = false;
     for (int k = 0; k < n; k++) {
-        ge cur;
-        fe_in(cur.x, pts + 64 * k);
-        fe_in(cur.y, pts + 64 * k + 32);
-        if (neg[k]) fe_neg(cur.y, cur.y);
+        ge g;
+        fe_in(g.x, pts + 64 * k);
+        fe_in(g.y, pts + 64 * k + 32);
         const bool nz = !skip[k];
         if (k == 0) {
-            fe_norm_weak(cur.y);
-            gxz_set_ge(acc, cur);
+            p0 = g;
+            if (neg[k]) fe_neg(p0.y, p0.y);
+            fe_norm_weak(p0.y);
+            gxz_set_ge(acc, p0);
             started = nz;
             continue;
         }
-        if (k == 1 && started && nz) {
-            ge p0;
-            p0.x = acc.x;
-            p0.y = acc.y;
-            gxz_add_ge_z1(acc, p0, cur);
-            continue;
-        }
-        gxz s;
-        gxz_add_ge_nx(s, acc, cur);
-        gxz first;
-        gxz_set_ge(first, cur);
-        fe_norm_weak(first.y);
-        gxz_cmov(s, first, !started);
-        gxz_cmov(acc, s, nz);
-        started = started || nz;
+        const bool rare = force_rare || !(started && nz);
+        gxz next;   // the kernel's two accumulators in turn
+        if (k == 1) gxz_sum_step<true>(next, acc, started, p0, g, neg[k] != 0, nz, rare);
+        else gxz_sum_step<false>(next, acc, started, p0, g, neg[k] != 0, nz, rare);
+        acc = next;
     }
     if (!started || gxz_is_inf(acc)) return 1;
     fe xn, yn, t, w, ax, ay;

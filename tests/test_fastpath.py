@@ -95,14 +95,15 @@ def test_first_step_addition(fb, oracle):
     assert fb.hdh_add_affine(b32(a[0]), b32(a[1]), b32(a[0]), b32(a[1]), out) == 1
 
 
-def _xyzz_sum(fb, pts, neg, skip):
-    fb.hdh_xyzz_sum.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
+def _xyzz_sum(fb, pts, neg, skip, force_rare=0):
+    fb.hdh_xyzz_sum.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p,
+                                ctypes.c_int]
     fb.hdh_xyzz_sum.restype = ctypes.c_int
     n = len(pts)
     out = ctypes.create_string_buffer(64)
     ng = np.asarray(neg, np.int32)
     sk = np.asarray(skip, np.int32)
-    deg = fb.hdh_xyzz_sum(b"".join(_pub64(p) for p in pts), ng.ctypes.data, sk.ctypes.data, n, out)
+    deg = fb.hdh_xyzz_sum(b"".join(_pub64(p) for p in pts), ng.ctypes.data, sk.ctypes.data, n, out, force_rare)
     return None if deg else (int.from_bytes(out.raw[:32], "big"), int.from_bytes(out.raw[32:], "big"))
 
 
@@ -130,11 +131,12 @@ def test_xyzz_sums(fb, oracle):
                 continue
             q = O.point_neg(p) if ng else p
             want = q if want is None else O.point_add(want, q)
-        got = _xyzz_sum(fb, pts, [int(x) for x in neg], [int(x) for x in skip])
-        if want is None:
-            assert got is None
-        else:
-            assert got == want, t
+        for force in (0, 1):   # the repair branch where this lane needs it / at every step
+            got = _xyzz_sum(fb, pts, [int(x) for x in neg], [int(x) for x in skip], force)
+            if want is None:
+                assert got is None
+            else:
+                assert got == want, (t, force)
     # degenerate: the partial sum equals +-the next point (doubling / cancel)
     a = O.point_mul(12345, G)
     b = O.point_mul(777, G)
@@ -145,7 +147,12 @@ def test_xyzz_sums(fb, oracle):
     assert _xyzz_sum(fb, [a, a], [0, 1], [0, 0]) is None
     assert _xyzz_sum(fb, [a, a, b], [0, 0, 0], [0, 0, 0]) is None
     # a skipped second window, then the general addition from an affine start
-    assert _xyzz_sum(fb, [a, b, b], [0, 0, 1], [0, 1, 0]) == O.point_add(a, O.point_neg(b))
+    for force in (0, 1):
+        assert _xyzz_sum(fb, [a, b, b], [0, 0, 1], [0, 1, 0], force) == O.point_add(a, O.point_neg(b))
+    # a skipped window's point is never added: a sum equal to +-that point
+    # stays exact
+    for force in (0, 1):
+        assert _xyzz_sum(fb, [a, b, ab, b], [0, 0, 0, 0], [0, 0, 1, 0], force) == O.point_add(ab, b)
 
 
 def test_fast_path_agrees_with_recovery(fb, oracle):

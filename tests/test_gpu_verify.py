@@ -122,15 +122,14 @@ def test_full_size_c2_properties(verifier, oracle, coracle):
     assert crec.tobytes() == rec.cpu().numpy()[pick].tobytes()
 
 
-@pytest.mark.parametrize("variants", [{}, {"lean_inv": 1, "split_k": 16}, {"lean_inv": 1, "split_k": 8},
-                                      {"split_k": 32}], ids=["default", "lean_k16", "lean_k8", "lean_k32"])
+@pytest.mark.parametrize("variants", [{}, {"split_k": 16}], ids=["default", "k16"])
 def test_adversarial_full_mix_vs_c_oracle(gpu, oracle, coracle, variants):
     """C5-style mix: 30 % adversarial across all classes, 64k messages, checked
     message by message against the C oracle on a context of its own: pass 1
     (no key known: the full recovery) teaches it the 100 keys, pass 2 runs the
     known-key check for the honest messages (its fallback list is only the
-    adversarial share); both passes equal the oracle.  Also with the lean
-    inversion kernels (HD_VAR_LEAN_INV) at 16, 8 and 32 messages per inversion."""
+    adversarial share); both passes equal the oracle.  Also at 16 messages
+    per inversion (the default takes 8 below 2^20 - 2^16 messages, 16 above)."""
     from hyperdrive_amd.device import generate
     N, S = 65536, 100
     v = gpu.Verifier(0)
@@ -368,3 +367,93 @@ def test_c4_16m_sharded_emulation(verifier, coracle):
         m = t1.n_counts if k.startswith("count") else t1.n_hr
         assert np.array_equal(a1[k][:m], a2[k][:m]), k
     assert t1.n_hr == N // (2 * S) + (1 if N % (2 * S) else 0)
+
+
+def _zero_digit_rows(oracle, S):
+    """Signatures whose known-key check scalars u1 = m / s and u2 = r / s have
+    zero window digits (in the 24-bit G windows and the 16- and 20-bit key
+    windows), made by choosing u1, u2 first: k = u1 + u2 d, R = k G, r = R.x,
+    s = r / u2, m = u1 s (the digest is supplied, hd_verify_batch_digest_device).
+    Zero digits otherwise come up ~2^-W per window; here every message has
+    several, including a sum that starts late (u1's low windows zero, or u1 = 0)."""
+    import random
+    O = oracle
+    keys = O.KeyCache()
+    rng = random.Random(5)
+    ones = lambda lo, hi: ((1 << (hi - lo + 1)) - 1) << lo
+    pairs = [
+        (2 ** 100 + 2 ** 30 + 5, 2 ** 200 + 7),                   # sparse: most digits zero, any width
+        (0, rng.randrange(1, O.N)),                              # u1 = 0: the sum starts in the key windows
+        (rng.randrange(1, 2 ** 200) << 24, rng.randrange(1, O.N)),  # G window 0 zero: starts at window 1
+        (rng.randrange(1, 2 ** 180) << 48, rng.randrange(1, O.N)),  # G windows 0, 1 zero
+        (rng.randrange(1, O.N) | ones(71, 95), rng.randrange(1, O.N)),   # G window 3 all ones (Booth zero)
+        (rng.randrange(1, O.N), rng.randrange(1, 2 ** 239)),     # key top window zero (20-bit tables)
+        (rng.randrange(1, O.N), rng.randrange(1, O.N) | ones(99, 119)),  # 20-bit key window 5 all ones
+        (rng.randrange(1, O.N), rng.randrange(1, O.N) & ~ones(63, 79)),  # 16-bit key window 4 zero
+        (rng.randrange(1, O.N), 2 ** 128 + 1),                   # sparse u2
+        (rng.randrange(1, O.N), rng.randrange(1, O.N)),          # control
+    ]
+    rows, digests = [], []
+    for j, (u1, u2) in enumerate(pairs):
+        for signer, claimed in ((j % S, j % S), (j % S, (j + 1) % S)):   # honest, then a mismatching From
+            d = keys.sk(signer)
+            k = (u1 + u2 * d) % O.N
+            R = O.point_mul(k, O.G)
+            r = R[0] % O.N
+            v = (R[1] & 1) | (2 if R[0] >= O.N else 0)
+            s = r * pow(u2, -1, O.N) % O.N
+            m = u1 * s % O.N
+            sig = r.to_bytes(32, "big") + s.to_bytes(32, "big") + bytes([v])
+            val = bytes(rng.randrange(256) for _ in range(32))
+            rows.append((O.PREVOTE, 1 + j, 0, -1, val, keys.signatory(claimed), sig))
+            digests.append(m.to_bytes(32, "big"))
+    return rows, digests, keys
+
+
+@pytest.mark.parametrize("key_width", [16, 20])
+def test_zero_window_digits_vs_oracle(gpu, oracle, key_width):
+    """The known-key check's rare branch (k_fast_sums: a wavefront with a
+    zero window digit adds the window's entry 0 and takes it off again; a sum
+    that has not started starts at the first non-zero window) on messages
+    built to have zero digits: verdicts and recovered signatories equal the
+    oracle's recovery through the full recovery (pass 1) and the known-key
+    check (passes 2, 3), where only the mismatching Froms fall back."""
+    import torch
+    from hyperdrive_amd.device import DeviceBatch, work_stream
+    from hyperdrive_amd.digest import verify_digest_device
+    from hyperdrive_amd.verify import Batch
+    O = oracle
+    S = 4
+    rows, digests, keys = _zero_digit_rows(O, S)
+    want, wrec = [], []
+    for (t, h, r, vr, val, frm, sig), dg in zip(rows, digests):
+        verdict, Q = O.recover(dg, sig)
+        if verdict == O.VALID:
+            got = O.signatory_of_pub(Q, True)
+            verdict = O.VALID if got == frm else O.SIGNATORY_MISMATCH
+            wrec.append(got)
+        else:
+            wrec.append(bytes(32))
+        want.append(verdict)
+    assert want.count(O.VALID) == len(rows) // 2
+    v = gpu.Verifier(0)
+    try:
+        v.set_variant("key_width", key_width)
+        v.set_signatories(np.frombuffer(b"".join(keys.signatory(k) for k in range(S)), np.uint8).reshape(S, 32))
+        b = Batch.from_lists(*[[x[k] for x in rows] for k in range(7)])
+        ws = work_stream()
+        with torch.cuda.stream(ws):
+            db = DeviceBatch.from_host(b)
+            dg = torch.from_numpy(np.frombuffer(b"".join(digests), np.uint8).reshape(-1, 32).copy()).cuda()
+            n = len(rows)
+            for rnd in range(3):
+                vd = torch.full((n,), 9, dtype=torch.uint8, device="cuda")
+                rec = torch.zeros((n, 32), dtype=torch.uint8, device="cuda")
+                verify_digest_device(v, db, dg, vd.data_ptr(), rec.data_ptr(), stream=ws)
+                ws.synchronize()
+                assert vd.cpu().tolist() == want, rnd
+                assert rec.cpu().numpy().tobytes() == b"".join(wrec), rnd
+                if rnd > 0:
+                    assert v.fastpath_stats()[1] == n // 2, rnd   # only the mismatching Froms fall back
+    finally:
+        v.close()

@@ -12,10 +12,13 @@ rank's shard, the valid-bitmap all-gather over RCCL (N > 1), and the
 first-wins 2f+1 tally.  Inputs are resident in HBM when timing starts.
 
 Multi-GPU: one process per GPU (torch.distributed.run), weak scaling: rank k
-verifies messages [k*B, (k+1)*B) of the N*B-message stream (C4 generator);
-the batch metadata is replicated, the verdict bitmaps cross xGMI, every rank
-tallies only the rounds hd_tally_partition_of assigns it and the small count
-tables are all-gathered and merged (hyperdrive_amd/shard.py).
+generates and verifies only messages [k*B, (k+1)*B) of the N*B-message stream
+(C4 generator; --global-batch: one C4 batch split over the ranks).  Each rank
+tallies its own shard; the ranks all-gather their (height, round) sets, and
+only the candidates of rounds present in more than one shard (the rounds a
+shard boundary cuts) are routed to the round's owner over RCCL; the small
+count tables are then all-gathered and merged (hyperdrive_amd/shard.py).  The
+line reports routed_out per rank.
 
 Prints ONE JSON line on rank 0, with:
   roofline      the dominant kernel (k_fast_sums) timed live with HIP events
@@ -147,11 +150,15 @@ class Pipeline:
     complete inside the timed region.
 
     N > 1 (one process per GPU): `db` is this rank's shard only (global
-    indices lo .. lo + B - 1); the tally routes the shard's candidates to the
-    owners of their rounds over RCCL (shard.route_candidates /
-    exchange_routed: one all-to-all of the counts, one of the 64-byte rows),
-    each owner tallies what it received (hd_tally_routed_device) and the
-    owners' small tables are all-gathered and merged (gather_tally_device)."""
+    indices lo .. lo + B - 1).  The tally: the rank tallies its shard
+    (hd_tally_device_bitmap, reps + lo); the ranks all-gather their round sets
+    (shard.shared_rounds); the candidates of rounds present in more than one
+    shard go to the owners of those rounds over RCCL
+    (shard.route_candidates(rounds=...) / exchange_routed: one all-to-all of
+    the counts, one of the 64-byte rows), each owner tallies what it received
+    (hd_tally_routed_device); every rank keeps its local rows of the other
+    rounds (shard.drop_rounds) and the small tables are all-gathered and
+    merged (gather_tally_device)."""
     NBUF = int(os.environ.get("HD_BENCH_NBUF", 4))
     VSTREAMS = int(os.environ.get("HD_BENCH_VSTREAMS", 3))
 
@@ -176,8 +183,11 @@ class Pipeline:
         self.route_rows = None
         if world > 1:
             from hyperdrive_amd.shard import tally_out
-            # an owner receives about B candidates; sized for all of a skewed batch
-            self.t_part = tally_out(v, total, pinned=True)
+            # the shard's own tally, and the owner's tally of the shared rounds
+            # it received (separate pinned outputs: the first one's uploads may
+            # still be reading its stage); sized for a skewed batch
+            self.t_part = tally_out(v, B, pinned=True)
+            self.t_own = tally_out(v, total, pinned=True)
         self.tally_info = {}
         self.last_tally = None
         # HD_BENCH_ASYNC_TALLY=1 (single GPU): the tally is queued without a
@@ -296,20 +306,32 @@ class Pipeline:
             self.tally_info = {"n_hr": self.t_out.n_hr, "n_counts": self.t_out.n_counts}
             self.last_tally = (self.t_out, self.t_arr)
             return
-        from hyperdrive_amd.shard import (exchange_routed, gather_tally_device, route_candidates,
-                                          tally_routed_device, unroute)
+        from hyperdrive_amd.shard import (drop_rounds, exchange_routed, gather_tally_device, route_candidates,
+                                          shared_rounds, tally_part_device, tally_routed_device, unroute)
         s = self.ts.cuda_stream
+        g = self.tally_group
         with torch.cuda.stream(self.ts):
-            rows, counts = route_candidates(self.v, self.shard, bitmap.data_ptr(), self.lo, self.world, s,
-                                            rows=self.route_rows)
-            self.route_rows = rows
-            recv = exchange_routed(rows, counts, self.world, group=self.tally_group)
-            db, gidx = unroute(self.v, recv, s)
-            local = tally_routed_device(self.v, db, gidx, s, self.t_part, self.dev)
-            merged = gather_tally_device(local, self.world, group=self.tally_group)
+            local = tally_part_device(self.v, self.shard, bitmap.data_ptr(), 0, 1, s, self.t_part, self.dev)
+            local["counts"][:, 3] += self.lo           # reps -> global indices
+            local["hr"][:, 5] += self.lo
+            shared = shared_rounds(local["hr"][:, :2], self.world, group=g)
+            routed_out = routed_in = 0
+            mine = local
+            if shared.shape[0]:                        # (identical on every rank)
+                rows, counts = route_candidates(self.v, self.shard, bitmap.data_ptr(), self.lo, self.world, s,
+                                                rows=self.route_rows, rounds=shared)
+                self.route_rows = rows
+                recv = exchange_routed(rows, counts, self.world, group=g)
+                routed_out, routed_in = int(sum(counts)), int(recv.shape[0])
+                mine = {k: drop_rounds(t, shared) for k, t in local.items()}
+                if routed_in:
+                    db, gidx = unroute(self.v, recv, s)
+                    own = tally_routed_device(self.v, db, gidx, s, self.t_own, self.dev)
+                    mine = {k: torch.cat([mine[k], own[k]]) for k in mine}
+            merged = gather_tally_device(mine, self.world, group=g)
         self.tally_info = {"n_hr": len(merged["hr"]), "n_counts": len(merged["counts"]),
-                           "n_hr_this_rank": len(local["hr"]), "routed_in": int(recv.shape[0]),
-                           "routed_out": int(sum(counts))}
+                           "n_hr_this_rank": len(mine["hr"]), "shared_rounds": int(shared.shape[0]),
+                           "routed_in": routed_in, "routed_out": routed_out}
         self.last_tally = merged
 
     def run(self, steps):
@@ -432,6 +454,26 @@ class Pipeline:
     def last(self, steps):
         buf = (steps - 1) % self.NBUF
         return self.verdicts[buf], self.recovered[buf], self.bitmaps[buf]
+
+    def close(self):
+        """Release the asynchronous tally's tickets (their events) and pinned
+        stages (include/hd_verify.h hd_tally_ticket_release, hd_host_free)."""
+        from hyperdrive_amd import _lib
+        lib = _lib.load()
+        for j, t in enumerate(self.ticket_objs):
+            if t is not None:
+                lib.hd_tally_ticket_release(ctypes.byref(t))
+                self.ticket_objs[j] = None
+        for j, st in enumerate(self.stages):
+            if st is not None:
+                lib.hd_host_free(st[0])
+                self.stages[j] = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def timed(pipe, steps, dist, dev):

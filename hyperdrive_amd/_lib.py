@@ -158,6 +158,11 @@ SIGNATURES = {
     "hd_route_candidates_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
                                                   ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                                   ctypes.POINTER(ctypes.c_uint32), ctypes.c_void_p]),
+    "hd_route_candidates_listed_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,
+                                                         ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                                         ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                                         ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                                                         ctypes.c_void_p]),
     "hd_unroute_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                          ctypes.POINTER(HdBatchOut), ctypes.c_void_p, ctypes.c_void_p]),
     "hd_tally_routed_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HdBatch), ctypes.c_void_p,

@@ -781,6 +781,27 @@ struct RouteRow {          // 64 B
 static_assert(sizeof(RouteRow) == 64, "route row");
 #define HD_ROUTE_MAX_PARTS 64u
 
+// Optional round filter of the route kernels: only candidates whose (h, r)
+// is in a sorted list (lexicographic, signed) are routed -- the rounds that
+// appear in more than one shard (hd_route_candidates_listed_device); every
+// other round is tallied where it is.
+struct RoundList {
+    const int64_t* h;
+    const int64_t* r;
+    uint32_t n;
+};
+__device__ __forceinline__ bool round_listed(const RoundList& l, int64_t h, int64_t r) {
+    if (!l.h) return true;
+    uint32_t lo = 0, hi = l.n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const int64_t mh = l.h[mid], mr = l.r[mid];
+        if (mh < h || (mh == h && mr < r)) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < l.n && l.h[lo] == h && l.r[lo] == r;
+}
+
 // per block and owner: the number of candidates (o-major: cnt[o * nb + blk]);
 // *outside counts candidates whose From is not in the context's admitted set
 // (possible when the set changed since verification): a row carries the
@@ -788,14 +809,14 @@ static_assert(sizeof(RouteRow) == 64, "route row");
 __global__ __launch_bounds__(256) void k_route_count(DevBatch b, const uint32_t* __restrict__ bitmap, uint32_t nparts,
                                                      const uint32_t* __restrict__ adm, uint32_t n_adm, int adm_steps,
                                                      int adm_in_lds, uint32_t* __restrict__ cnt,
-                                                     uint32_t* __restrict__ outside) {
+                                                     uint32_t* __restrict__ outside, RoundList rl) {
     extern __shared__ uint32_t sh_adm[];
     __shared__ uint32_t c[HD_ROUTE_MAX_PARTS];
     if (adm_in_lds) adm_stage(sh_adm, adm, n_adm);
     if (threadIdx.x < nparts) c[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < b.n && candidate(b, nullptr, bitmap, i, Part{0, 1})) {
+    if (i < b.n && candidate(b, nullptr, bitmap, i, Part{0, 1}) && round_listed(rl, b.height[i], b.round[i])) {
         atomicAdd(&c[part_of(hash_hr(b.height[i], b.round[i]), nparts)], 1u);
         uint32_t from_be[8];
         load_row32_be(from_be, b.from32, i);
@@ -813,13 +834,13 @@ __global__ __launch_bounds__(256) void k_route_count(DevBatch b, const uint32_t*
 __global__ __launch_bounds__(256) void k_route_write(DevBatch b, const uint32_t* __restrict__ bitmap, uint32_t nparts,
                                                      uint32_t base, const uint32_t* __restrict__ off,
                                                      const uint32_t* __restrict__ adm, uint32_t n_adm, int adm_steps,
-                                                     int adm_in_lds, RouteRow* __restrict__ rows) {
+                                                     int adm_in_lds, RouteRow* __restrict__ rows, RoundList rl) {
     extern __shared__ uint32_t sh_adm[];
     __shared__ uint32_t wcnt[4][HD_ROUTE_MAX_PARTS];
     if (adm_in_lds) adm_stage(sh_adm, adm, n_adm);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const bool c = i < b.n && candidate(b, nullptr, bitmap, i, Part{0, 1});
+    const bool c = i < b.n && candidate(b, nullptr, bitmap, i, Part{0, 1}) && round_listed(rl, b.height[i], b.round[i]);
     const uint32_t o = c ? part_of(hash_hr(b.height[i], b.round[i]), nparts) : 0xFFFFFFFFu;
     uint32_t rank = 0;
     for (uint32_t k = 0; k < nparts; k++) {
@@ -1312,9 +1333,36 @@ uint32_t hd_tally_partition_of(int64_t height, int64_t round, uint32_t nparts) {
     return part_of(hash_hr(height, round), nparts);
 }
 
+static int route_candidates(hd_ctx* ctx, const hd_batch* dshard, const uint32_t* d_valid_bitmap,
+                            uint32_t base_index, uint32_t nparts, RoundList rl, uint8_t* d_rows, uint32_t cap_rows,
+                            uint32_t* counts, void* stream);
+
 int hd_route_candidates_device(hd_ctx* ctx, const hd_batch* dshard, const uint32_t* d_valid_bitmap,
                                uint32_t base_index, uint32_t nparts, uint8_t* d_rows, uint32_t cap_rows,
                                uint32_t* counts, void* stream) {
+    return route_candidates(ctx, dshard, d_valid_bitmap, base_index, nparts, RoundList{nullptr, nullptr, 0}, d_rows,
+                            cap_rows, counts, stream);
+}
+
+int hd_route_candidates_listed_device(hd_ctx* ctx, const hd_batch* dshard, const uint32_t* d_valid_bitmap,
+                                      uint32_t base_index, uint32_t nparts, const int64_t* d_round_h,
+                                      const int64_t* d_round_r, uint32_t n_rounds, uint8_t* d_rows,
+                                      uint32_t cap_rows, uint32_t* counts, void* stream) {
+    if (!ctx || !counts || nparts == 0 || nparts > HD_ROUTE_MAX_PARTS) return HD_EINVAL;
+    if (n_rounds == 0) {   // nothing is shared: nothing to route
+        for (uint32_t o = 0; o < nparts; o++) counts[o] = 0;
+        return HD_OK;
+    }
+    if (!d_round_h || !d_round_r) return HD_EINVAL;
+    return route_candidates(ctx, dshard, d_valid_bitmap, base_index, nparts, RoundList{d_round_h, d_round_r, n_rounds},
+                            d_rows, cap_rows, counts, stream);
+}
+
+}  // extern "C"
+
+static int route_candidates(hd_ctx* ctx, const hd_batch* dshard, const uint32_t* d_valid_bitmap,
+                            uint32_t base_index, uint32_t nparts, RoundList rl, uint8_t* d_rows, uint32_t cap_rows,
+                            uint32_t* counts, void* stream) {
     if (!ctx || !dshard || !counts || nparts == 0 || nparts > HD_ROUTE_MAX_PARTS) return HD_EINVAL;
     for (uint32_t o = 0; o < nparts; o++) counts[o] = 0;
     const uint32_t n = dshard->n;
@@ -1346,7 +1394,7 @@ int hd_route_candidates_device(hd_ctx* ctx, const hd_batch* dshard, const uint32
     const size_t adm_lds = adm_lds_bytes(ctx->n_adm);
     TCHK(hipMemsetAsync(starts + nparts + 1, 0, 4, s), "route outside count");
     k_route_count<<<nb, 256, adm_lds, s>>>(b, d_valid_bitmap, nparts, ctx->d_adm, ctx->n_adm, ctx->adm_steps,
-                                           adm_lds > 0, cnt, starts + nparts + 1);
+                                           adm_lds > 0, cnt, starts + nparts + 1, rl);
     TCHK(hipGetLastError(), "k_route_count");
     TCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, (int)cells, s), "route scan");
     k_route_starts<<<1, 64, 0, s>>>(off, cnt, nparts, nb, starts);
@@ -1363,10 +1411,12 @@ int hd_route_candidates_device(hd_ctx* ctx, const hd_batch* dshard, const uint32
     for (uint32_t o = 0; o < nparts; o++) counts[o] = st[o + 1] - st[o];
     if (st[nparts] > cap_rows) return HD_ECAP;
     k_route_write<<<nb, 256, adm_lds, s>>>(b, d_valid_bitmap, nparts, base_index, off, ctx->d_adm, ctx->n_adm,
-                                           ctx->adm_steps, adm_lds > 0, reinterpret_cast<RouteRow*>(d_rows));
+                                           ctx->adm_steps, adm_lds > 0, reinterpret_cast<RouteRow*>(d_rows), rl);
     TCHK(hipGetLastError(), "k_route_write");
     return hd_ctx_note_stream(ctx, s);
 }
+
+extern "C" {
 
 int hd_unroute_device(hd_ctx* ctx, const uint8_t* d_rows, uint32_t n, const hd_batch_out* d_out, uint32_t* d_gidx,
                       void* stream) {

@@ -7,13 +7,19 @@ batch whose metadata is replicated on every rank; the only exchange is an
 all-gather of the per-rank valid bitmaps (n/32 words in total, latency-bound
 over xGMI).
 
-The tally is partitioned too.  First-wins is per (height, round, type,
-signer), so the rank that owns an (height, round) -- ``partition_of`` -- sees
-every duplicate of its keys: rank k tallies only its rounds
-(hd_tally_device_bitmap_part) from the replicated metadata and the gathered
-bitmap, and the small per-rank count tables are all-gathered and merged in
-first-batch-index order (``gather_tally``), which is exactly the single-GPU
-tally's output order.
+The tally: first-wins is per (height, round, type, signer), so a round whose
+candidates all sit in one shard is complete there.  Each rank tallies its own
+shard; the ranks all-gather their round sets (``shared_rounds``: a few
+thousand (height, round) pairs) and only the candidates of rounds present in
+more than one shard -- the rounds straddling a shard boundary -- are routed
+to the owner of the round (``partition_of``) by one all-to-all
+(``route_candidates(rounds=...)`` / ``exchange_routed``).  Each rank keeps
+its local rows of the other rounds (``drop_rounds``) plus the rows of the
+shared rounds it owns, and the small tables are all-gathered and merged in
+first-batch-index order (``gather_tally_device``), which is exactly the
+single-GPU tally's output order.  (The older partitioned forms -- every rank
+tallying the rounds it owns from a replicated batch, or every candidate
+routed to its owner -- stay available.)
 """
 from __future__ import annotations
 
@@ -176,11 +182,14 @@ def gather_tally_device(local, world: int, group=None):
 ROUTE_ROW_BYTES = 64       # include/hd_verify.h HD_ROUTE_ROW_BYTES
 
 
-def route_candidates(v, dshard, d_bitmap: int, base_index: int, world: int, stream, rows=None):
+def route_candidates(v, dshard, d_bitmap: int, base_index: int, world: int, stream, rows=None, rounds=None):
     """This rank's candidates (VALID Prevotes / Precommits of its shard, global
     index base_index + i) as route rows grouped by the owner of their round
     (hd_route_candidates_device).  Returns (rows uint8 tensor [cap, 64], counts
-    list of `world` ints); rows may be passed in for reuse."""
+    list of `world` ints); rows may be passed in for reuse.  rounds: an int64
+    [k, 2] CUDA tensor of (height, round) pairs sorted lexicographically
+    (shared_rounds): only candidates of those rounds are routed
+    (hd_route_candidates_listed_device)."""
     import torch
     from . import _lib
     lib = _lib.load()
@@ -189,11 +198,66 @@ def route_candidates(v, dshard, d_bitmap: int, base_index: int, world: int, stre
     if rows is None or rows.shape[0] < max(n, 1):
         rows = torch.empty((max(n, 1), ROUTE_ROW_BYTES), dtype=torch.uint8, device=dev)
     counts = (ctypes.c_uint32 * world)()
-    rc = lib.hd_route_candidates_device(v.handle, ctypes.byref(dshard), d_bitmap, int(base_index), int(world),
-                                        rows.data_ptr(), rows.shape[0], counts, stream)
+    if rounds is None:
+        rc = lib.hd_route_candidates_device(v.handle, ctypes.byref(dshard), d_bitmap, int(base_index), int(world),
+                                            rows.data_ptr(), rows.shape[0], counts, stream)
+        where = "hd_route_candidates_device"
+    else:
+        rh = rounds[:, 0].contiguous()
+        rr = rounds[:, 1].contiguous()
+        k = int(rounds.shape[0])
+        rc = lib.hd_route_candidates_listed_device(v.handle, ctypes.byref(dshard), d_bitmap, int(base_index),
+                                                   int(world), rh.data_ptr() if k else None,
+                                                   rr.data_ptr() if k else None, k, rows.data_ptr(), rows.shape[0],
+                                                   counts, stream)
+        where = "hd_route_candidates_listed_device"
     if rc != 0:
-        raise _lib.HDError(rc, "hd_route_candidates_device", lib.hd_ctx_last_error(v.handle).decode())
+        raise _lib.HDError(rc, where, lib.hd_ctx_last_error(v.handle).decode())
     return rows, [int(c) for c in counts]
+
+
+def shared_rounds(local_rounds, world: int, group=None):
+    """The (height, round) pairs that occur in more than one rank's shard,
+    as an int64 [k, 2] tensor sorted lexicographically, identical on every
+    rank.  local_rounds: this rank's distinct rounds ([m, 2] int64, e.g. the
+    first two columns of its local tally's hr rows).  One all-gather of the
+    sizes and one of the pairs (padded to the largest); torch only, so it runs
+    over RCCL on the device and over gloo on the CPU."""
+    import torch
+    import torch.distributed as dist
+    dev = local_rounds.device
+    if local_rounds.is_cuda and dist.get_backend(group) == "gloo":
+        return shared_rounds(local_rounds.cpu(), world, group).to(dev)
+    pairs = local_rounds.to(torch.int64).reshape(-1, 2)
+    size = torch.tensor([pairs.shape[0]], dtype=torch.int64, device=dev)
+    sizes = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(sizes, size, group=group)
+    sizes = sizes.cpu().tolist()
+    width = max(1, max(sizes))
+    pad = torch.zeros((width, 2), dtype=torch.int64, device=dev)
+    pad[: pairs.shape[0]] = pairs
+    out = torch.empty((world * width, 2), dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(out, pad, group=group)
+    keep = (torch.arange(width, device=dev)[None, :] < torch.tensor(sizes, device=dev)[:, None]).reshape(-1)
+    allp = out[keep]
+    if allp.shape[0] == 0:
+        return allp
+    # a rank lists each of its rounds once, so a pair seen twice is shared
+    uniq, cnt = torch.unique(allp, dim=0, return_counts=True)   # rows sorted lexicographically
+    return uniq[cnt > 1].contiguous()
+
+
+def drop_rounds(rows, rounds):
+    """rows (an int64 [m, c] tensor whose first two columns are height and
+    round) without those of the given (height, round) pairs."""
+    import torch
+    if rows.shape[0] == 0 or rounds.shape[0] == 0:
+        return rows
+    both = torch.cat([rounds.to(rows.device), rows[:, :2]])
+    _, inv = torch.unique(both, dim=0, return_inverse=True)
+    shared_ids = inv[: rounds.shape[0]]
+    mask = ~torch.isin(inv[rounds.shape[0]:], shared_ids)
+    return rows[mask]
 
 
 def exchange_routed(rows, counts, world: int, group=None):

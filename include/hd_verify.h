@@ -454,6 +454,17 @@ int hd_gen_batch_device(hd_ctx* ctx, uint32_t kind, uint64_t start, uint32_t n, 
 int hd_route_candidates_device(hd_ctx* ctx, const hd_batch* dshard, const uint32_t* d_valid_bitmap,
                                uint32_t base_index, uint32_t nparts, uint8_t* d_rows, uint32_t cap_rows,
                                uint32_t* counts, void* stream);
+/* The same, routing only candidates whose (height, round) is one of the
+ * n_rounds pairs (d_round_h[k], d_round_r[k]), sorted lexicographically (as
+ * signed int64): the rounds that appear in more than one shard.  A round
+ * present in one shard only is complete there, so that shard tallies it
+ * itself (hd_tally_device_bitmap, reps + base_index) and keeps only those
+ * rows of its local tables; only the shared rounds cross xGMI, to their
+ * owners (hd_tally_partition_of).  n_rounds = 0 routes nothing. */
+int hd_route_candidates_listed_device(hd_ctx* ctx, const hd_batch* dshard, const uint32_t* d_valid_bitmap,
+                                      uint32_t base_index, uint32_t nparts, const int64_t* d_round_h,
+                                      const int64_t* d_round_r, uint32_t n_rounds, uint8_t* d_rows,
+                                      uint32_t cap_rows, uint32_t* counts, void* stream);
 int hd_unroute_device(hd_ctx* ctx, const uint8_t* d_rows, uint32_t n, const hd_batch_out* d_out, uint32_t* d_gidx,
                       void* stream);
 int hd_tally_routed_device(hd_ctx* ctx, const hd_batch* dbatch, const uint32_t* d_gidx, hd_tally_out* out,

@@ -256,3 +256,86 @@ def test_tally_check_runs_clean(gpu, monkeypatch):
         assert t2.count == t3.count and t2.dup.tolist() == t3.dup.tolist()
     finally:
         v.close()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_local_tally_plus_shared_rounds_match_restatement(gpu, world, monkeypatch):
+    """The default N > 1 tally (bench.Pipeline.tally, shard.py) on one GPU,
+    every rank's shard in turn: each shard's own tally equals its restatement
+    (reps + lo), the listed route (hd_route_candidates_listed_device: only the
+    rounds present in more than one shard) is byte-identical to
+    route_rows_np(rounds=...), the owners' tallies of what they received equal
+    theirs, and local rows without the shared rounds plus the owners' rows
+    merge to the single-context tally.  Heights run in index order (C2/C4),
+    so only the rounds a shard boundary cuts are routed."""
+    import torch
+    from test_multi_rank import local_tally_rows, route_rows_np, routed_tally_rows, tally_rows
+    from util import from_np
+    from hyperdrive_amd.device import DeviceBatch, generate, work_stream
+    from hyperdrive_amd.shard import (drop_rounds, merge_tally_parts, route_candidates, shard_range,
+                                      tally_out, tally_part_device, tally_routed_device, unroute)
+    monkeypatch.setenv("HD_TALLY_CHECK", "1")
+    v = gpu.Verifier(0)
+    ws = work_stream()
+    cs = ws.cuda_stream
+    try:
+        with torch.cuda.stream(ws):
+            S, n = 50, 20_000 + 13
+            ks = v.gen_keys(S)
+            v.set_signatories(ks[0])
+            db, _, _ = generate(v, 0, n, S, 30, keys=ks, start=99)
+            hb = db.to_host()
+            res, whole = v.process_batch(hb)
+            ob = from_np(hb)
+            verdicts = res.verdict.tolist()
+            adm = sorted(bytes(x) for x in ks[0])
+            bits = torch.from_numpy(res.valid_bitmap.view(np.int32).copy()).cuda()
+            subs, locals_ = [], []
+            for k in range(world):
+                lo, hi = shard_range(n, k, world)
+                sub = DeviceBatch(hi - lo, db.type[lo:hi], db.height[lo:hi], db.round[lo:hi], db.valid_round[lo:hi],
+                                  db.value[lo:hi], db.frm[lo:hi], db.sig[lo:hi])
+                local = tally_part_device(v, sub.c_struct(), bits.data_ptr() + 4 * (lo // 32), 0, 1, cs,
+                                          tally_out(v, hi - lo, pinned=True), "cpu")
+                local = {key: t.clone() for key, t in local.items()}
+                local["counts"][:, 3] += lo
+                local["hr"][:, 5] += lo
+                want = local_tally_rows(ob, verdicts, lo, hi)
+                assert local["counts"].tolist() == want["counts"].tolist()
+                assert local["hr"].tolist() == want["hr"].tolist()
+                subs.append((lo, hi, sub))
+                locals_.append(local)
+            seen = {}
+            for local in locals_:
+                for h, r in {(int(a), int(b)) for a, b in local["hr"][:, :2].tolist()}:
+                    seen[(h, r)] = seen.get((h, r), 0) + 1
+            shared_set = {key for key, c in seen.items() if c > 1}
+            assert 1 <= len(shared_set) <= 2 * (world - 1)
+            shared = torch.tensor(sorted(shared_set), dtype=torch.int64).reshape(-1, 2).cuda()
+            sent = {}
+            for k, (lo, hi, sub) in enumerate(subs):
+                rows, counts = route_candidates(v, sub.c_struct(), bits.data_ptr() + 4 * (lo // 32), lo, world, cs,
+                                                rounds=shared)
+                want_rows, want_counts = route_rows_np(ob, verdicts, lo, hi, world, adm, rounds=shared_set)
+                assert counts == want_counts
+                assert rows[: sum(counts)].cpu().numpy().tobytes() == want_rows.tobytes()
+                off = np.concatenate([[0], np.cumsum(counts)])
+                for o in range(world):
+                    sent[(k, o)] = rows[off[o]: off[o + 1]]
+            parts = []
+            for o in range(world):
+                recv = torch.cat([sent[(k, o)] for k in range(world)]).contiguous()
+                mine = {key: drop_rounds(t, shared.cpu()) for key, t in locals_[o].items()}
+                if recv.shape[0]:
+                    rb, gidx = unroute(v, recv, cs)
+                    own = tally_routed_device(v, rb, gidx, cs, tally_out(v, n, pinned=True), "cpu")
+                    want = routed_tally_rows(recv.cpu().numpy(), adm)
+                    assert own["counts"].tolist() == want["counts"].tolist()
+                    mine = {key: torch.cat([mine[key], own[key]]) for key in mine}
+                parts.append({key: t.numpy() for key, t in mine.items()})
+            merged = merge_tally_parts(parts)
+            single = tally_rows(ob, verdicts)
+            assert merged["counts"].tolist() == single["counts"].tolist()
+            assert merged["hr"].tolist() == single["hr"].tolist()
+    finally:
+        v.close()

@@ -179,16 +179,19 @@ def test_gloo_partitioned_tally_equals_single_rank(world):
 ROW = 64
 
 
-def route_rows_np(b, verdicts, lo, hi, nparts, adm_sorted):
+def route_rows_np(b, verdicts, lo, hi, nparts, adm_sorted, rounds=None):
     """Restatement of hd_route_candidates_device (include/hd_verify.h) for the
     shard [lo, hi) of an oracle batch: 64-byte rows (h, r: int64 LE; value:
     32 B; global index: u32 LE; admitted sorted index << 8 | type: u32 LE;
-    8 zero bytes), grouped by owner, index order inside a group."""
+    8 zero bytes), grouped by owner, index order inside a group.  rounds (a
+    set of (h, r)): hd_route_candidates_listed_device, only those rounds."""
     groups = [[] for _ in range(nparts)]
     index = {a: k for k, a in enumerate(adm_sorted)}
     for i in range(lo, hi):
         t = b.mtype[i]
         if verdicts[i] != 0 or t not in (2, 3):
+            continue
+        if rounds is not None and (b.height[i], b.round[i]) not in rounds:
             continue
         o = partition_of(b.height[i], b.round[i], nparts)
         row = (int(b.height[i]).to_bytes(8, "little", signed=True) + int(b.round[i]).to_bytes(8, "little", signed=True)
@@ -282,3 +285,107 @@ def test_gloo_routed_tally_equals_single_rank(world):
     assert sum(r[3] for r in res) == n_cand == sum(r[4] for r in res)   # every candidate reached one owner
     for rank, counts, hrs, n_in, n_out in res:
         assert counts == want["counts"].tolist() and hrs == want["hr"].tolist()
+
+
+# ---- local tallies + shared rounds only (the default N > 1 exchange) ------
+class _Shard:
+    """Rows lo .. hi - 1 of an oracle batch, indexed from 0."""
+
+    def __init__(self, b, lo, hi):
+        self.mtype, self.height, self.round = b.mtype[lo:hi], b.height[lo:hi], b.round[lo:hi]
+        self.value, self.frm = b.value[lo:hi], b.frm[lo:hi]
+
+    def __len__(self):
+        return len(self.mtype)
+
+
+def local_tally_rows(b, verdicts, lo, hi):
+    """A rank's tally of its own shard (hd_tally_device_bitmap on the shard),
+    reps moved to global indices."""
+    t = tally_rows(_Shard(b, lo, hi), verdicts[lo:hi])
+    for key, col in (("counts", 3), ("hr", 5)):
+        if len(t[key]):
+            t[key][:, col] += lo
+    return t
+
+
+def _case(name):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    if name == "random_mix":
+        from tally_cases import scenarios
+        sc = [s for s in scenarios() if s.name == "random_mix"][0]
+        return sc.b, [0 if i % 7 else 5 for i in range(len(sc.b))]
+    # heights in index order (the C2 / C4 stream): only rounds cut by a shard
+    # boundary are shared; a few duplicates and double votes straddle them
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import hashlib
+    import hd_pyoracle as O
+    S = 10                                      # the C2 layout (hd_gen.h kind 0), unsigned: the tally reads no signatures
+    b = O.Batch()
+    for i in range(600):
+        h = 1 + i // (2 * S)
+        b.append(2 + (i // S) % 2, h, 0, -1, O.canonical_value(h, 0),
+                 hashlib.sha256(b"signer" + bytes([i % S])).digest(), bytes(65))
+    # copies of earlier votes just past the shard boundaries (320 for two
+    # ranks, 224 and 448 for three), one with a conflicting value (a double
+    # vote), and one inside a shard
+    for dst, src in ((321, 318), (322, 316), (226, 219), (450, 445), (95, 88)):
+        for f in ("mtype", "height", "round", "value", "frm"):
+            getattr(b, f)[dst] = getattr(b, f)[src]
+    b.value[322] = bytes(32)
+    return b, [0 if i % 11 else 6 for i in range(len(b))]
+
+
+def _hybrid_worker(rank, world, port, name, out_q):
+    from hyperdrive_amd.shard import drop_rounds, exchange_routed, gather_tally_device, shared_rounds
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b, verdicts = _case(name)
+    adm = sorted(set(b.frm))
+    lo, hi = shard_range(len(b), rank, world)
+    local = local_tally_rows(b, verdicts, lo, hi)
+    shared = shared_rounds(torch.from_numpy(local["hr"][:, :2].copy()), world)
+    rows, counts = route_rows_np(b, verdicts, lo, hi, world, adm, rounds={tuple(x) for x in shared.tolist()})
+    recv = exchange_routed(torch.from_numpy(rows), counts, world)
+    own = routed_tally_rows(recv.numpy(), adm)
+    mine = {k: torch.cat([drop_rounds(torch.from_numpy(local[k]), shared), torch.from_numpy(own[k])])
+            for k in ("counts", "hr")}
+    merged = gather_tally_device(mine, world)
+    out_q.put((rank, merged["counts"].tolist(), merged["hr"].tolist(), sum(counts), len(shared)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["random_mix", "height_order"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_local_tally_plus_shared_rounds_equals_single_rank(world, name):
+    """The default N > 1 tally: each rank tallies its own shard, the ranks
+    all-gather their round sets (shard.shared_rounds), only the candidates of
+    rounds present in more than one shard are routed to their owners
+    (hd_route_candidates_listed_device, restated), each rank keeps its local
+    rows of the other rounds (shard.drop_rounds) plus the shared rounds it
+    owns, and the merged tables equal the single-rank tally row for row --
+    with duplicates and a double vote straddling shard boundaries.  In height
+    order only the boundary rounds move."""
+    b, verdicts = _case(name)
+    want = tally_rows(b, verdicts)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hybrid_worker, args=(r, world, port, name, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, counts, hrs, routed, n_shared in res:
+        assert counts == want["counts"].tolist() and hrs == want["hr"].tolist()
+    n_cand = sum(1 for i in range(len(b)) if verdicts[i] == 0 and b.mtype[i] in (2, 3))
+    routed = sum(r[3] for r in res)
+    assert res[0][4] >= 1 and 0 < routed
+    if name == "height_order":
+        # boundary rounds only: the one a boundary cuts, and one a copied vote reaches
+        assert res[0][4] <= 2 * (world - 1) and routed <= 21 * res[0][4] < n_cand

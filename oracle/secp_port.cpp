@@ -1,0 +1,1042 @@
+// secp_port.cpp -- CPU BASELINE ONLY (bench.py's cpu_baseline leg, kind
+// "port-secp-class"; tests).  Not the oracle and not a product path.
+//
+// The reference recovers signatories through go-ethereum's cgo binding of
+// libsecp256k1 (/root/reference/go.mod:6; /root/reference/process/
+// message_test.go:145-158).  Go and that library are absent here, so this is
+// a C++ restatement of the same ALGORITHM CLASS, written for x86-64 hosts:
+//   * field: 5 x 52-bit limbs, products in unsigned __int128, lazy reduction
+//     (magnitudes), the 2^260 fold of the high half;
+//   * scalars mod n: 4 x 64-bit limbs, three folds by 2^256 - n;
+//   * inversions (r^-1 mod n, Z^-1 mod p): Bernstein-Yang divsteps on signed
+//     62-bit limbs, 62-step jumps with an early exit once g = 0;
+//   * ecmult: the GLV split of both scalars, one Strauss ladder of ~129
+//     doublings over four 129-bit scalars, wNAF-5 digits for R and lambda R
+//     (8 odd multiples each, Jacobian), wNAF-15 digits for G and lambda G
+//     over a precomputed affine table of 8,192 odd multiples of G (lambda G
+//     by the endomorphism, beta x);
+//   * square root by the (p + 1) / 4 addition chain.
+// Semantics are the reference path's: V >= 4, r / s
+// range, r + n >= p, lift, u1 = -m / r, u2 = s / r, Q = u1 G + u2 R, the
+// point at infinity; signatory = SHA-256(pubkey); Equal(From); admitted
+// (process/message.go:53-78, 165-186, 263-284; mq/mq.go:49-51).  Digests and
+// the pubkey hash use the repository's host-compilable SHA-256 lanes.
+// It is checked verdict for verdict and byte for byte against the C oracle
+// (tests/test_secp_port.py) and against the GPU in bench.py.
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../hyperdrive_amd/csrc/hd_sha256.h"
+
+namespace sp {
+
+typedef unsigned __int128 u128;
+typedef __int128 i128;
+
+// ------------------------------------------------------------ field mod p
+// value = sum n[i] 2^(52 i).  Magnitude m: n[0..3] <= m (2^52 - 1) roughly,
+// n[4] <= m (2^48 - 1).  fmul / fsqr take magnitudes <= 8 and return <= 1.
+struct F {
+    uint64_t n[5];
+};
+constexpr uint64_t M52 = (1ULL << 52) - 1, M48 = (1ULL << 48) - 1;
+constexpr uint64_t FOLD260 = 0x1000003D10ULL;   // 2^260 mod p
+constexpr uint64_t FOLD256 = 0x1000003D1ULL;    // 2^256 mod p
+constexpr uint64_t P0 = 0xFFFFEFFFFFC2FULL;
+
+inline void fset(F& r, uint64_t v) {
+    r.n[0] = v;
+    r.n[1] = r.n[2] = r.n[3] = r.n[4] = 0;
+}
+inline void f_from_be(F& r, const uint8_t* b) {
+    uint64_t w[4];
+    for (int k = 0; k < 4; k++) {
+        uint64_t x = 0;
+        for (int j = 0; j < 8; j++) x = (x << 8) | b[8 * (3 - k) + j];
+        w[k] = x;
+    }
+    r.n[0] = w[0] & M52;
+    r.n[1] = ((w[0] >> 52) | (w[1] << 12)) & M52;
+    r.n[2] = ((w[1] >> 40) | (w[2] << 24)) & M52;
+    r.n[3] = ((w[2] >> 28) | (w[3] << 36)) & M52;
+    r.n[4] = w[3] >> 16;
+}
+inline void f_to_be(uint8_t* b, const F& a) {   // a fully normalised
+    const uint64_t w[4] = {a.n[0] | (a.n[1] << 52), (a.n[1] >> 12) | (a.n[2] << 40), (a.n[2] >> 24) | (a.n[3] << 28),
+                           (a.n[3] >> 36) | (a.n[4] << 16)};
+    for (int k = 0; k < 4; k++)
+        for (int j = 0; j < 8; j++) b[8 * (3 - k) + j] = (uint8_t)(w[k] >> (56 - 8 * j));
+}
+inline void fadd(F& r, const F& a, const F& b) {
+    for (int i = 0; i < 5; i++) r.n[i] = a.n[i] + b.n[i];
+}
+inline void fmul_int(F& r, uint64_t k) {
+    for (int i = 0; i < 5; i++) r.n[i] *= k;
+}
+// r = -a for a of magnitude <= m: 2 (m + 1) p - a (magnitude 2 (m + 1))
+inline void fneg(F& r, const F& a, uint64_t m) {
+    const uint64_t k = 2 * (m + 1);
+    r.n[0] = k * P0 - a.n[0];
+    r.n[1] = k * M52 - a.n[1];
+    r.n[2] = k * M52 - a.n[2];
+    r.n[3] = k * M52 - a.n[3];
+    r.n[4] = k * M48 - a.n[4];
+}
+// carries, the top fold: magnitude 1
+inline void fnorm_weak(F& r) {
+    uint64_t t0 = r.n[0], t1 = r.n[1], t2 = r.n[2], t3 = r.n[3], t4 = r.n[4];
+    const uint64_t x = t4 >> 48;
+    t4 &= M48;
+    t0 += x * FOLD256;
+    t1 += t0 >> 52;
+    t0 &= M52;
+    t2 += t1 >> 52;
+    t1 &= M52;
+    t3 += t2 >> 52;
+    t2 &= M52;
+    t4 += t3 >> 52;
+    t3 &= M52;
+    r.n[0] = t0;
+    r.n[1] = t1;
+    r.n[2] = t2;
+    r.n[3] = t3;
+    r.n[4] = t4;
+}
+// canonical, < p
+inline void fnorm(F& r) {
+    fnorm_weak(r);
+    fnorm_weak(r);   // n[4] <= 2^48: at most one more subtraction of p
+    uint64_t t0 = r.n[0], t1 = r.n[1], t2 = r.n[2], t3 = r.n[3], t4 = r.n[4];
+    const uint64_t over = (t4 >> 48) | (uint64_t)(t4 == M48 && (t3 & t2 & t1) == M52 && t0 >= P0);
+    t0 += over * FOLD256;
+    t1 += t0 >> 52;
+    t0 &= M52;
+    t2 += t1 >> 52;
+    t1 &= M52;
+    t3 += t2 >> 52;
+    t2 &= M52;
+    t4 += t3 >> 52;
+    t3 &= M52;
+    t4 &= M48;
+    r.n[0] = t0;
+    r.n[1] = t1;
+    r.n[2] = t2;
+    r.n[3] = t3;
+    r.n[4] = t4;
+}
+inline bool fis_zero(const F& a) {
+    F t = a;
+    fnorm(t);
+    return (t.n[0] | t.n[1] | t.n[2] | t.n[3] | t.n[4]) == 0;
+}
+// The 9 column sums fold: columns 5..8 (weight 2^260 times 2^(52 k)) become
+// 52-bit limbs h0..h4, which enter columns 0..4 times 2^260 mod p.
+inline void fold_columns(F& r, u128 c0, u128 c1, u128 c2, u128 c3, u128 c4, u128 c5, u128 c6, u128 c7, u128 c8) {
+    u128 t = c5;
+    const uint64_t h0 = (uint64_t)t & M52;
+    t = (t >> 52) + c6;
+    const uint64_t h1 = (uint64_t)t & M52;
+    t = (t >> 52) + c7;
+    const uint64_t h2 = (uint64_t)t & M52;
+    t = (t >> 52) + c8;
+    const uint64_t h3 = (uint64_t)t & M52;
+    const uint64_t h4 = (uint64_t)(t >> 52);
+    t = c0 + (u128)h0 * FOLD260;
+    uint64_t r0 = (uint64_t)t & M52;
+    t = (t >> 52) + c1 + (u128)h1 * FOLD260;
+    uint64_t r1 = (uint64_t)t & M52;
+    t = (t >> 52) + c2 + (u128)h2 * FOLD260;
+    const uint64_t r2 = (uint64_t)t & M52;
+    t = (t >> 52) + c3 + (u128)h3 * FOLD260;
+    const uint64_t r3 = (uint64_t)t & M52;
+    t = (t >> 52) + c4 + (u128)h4 * FOLD260;
+    const uint64_t r4 = (uint64_t)t & M48;
+    const u128 top = t >> 48;   // weight 2^256
+    const u128 z = (u128)r0 + top * FOLD256;
+    r0 = (uint64_t)z & M52;
+    r1 += (uint64_t)(z >> 52);
+    r.n[0] = r0;
+    r.n[1] = r1;
+    r.n[2] = r2;
+    r.n[3] = r3;
+    r.n[4] = r4;
+}
+inline void fmul(F& r, const F& a, const F& b) {
+    const uint64_t *x = a.n, *y = b.n;
+    const u128 c0 = (u128)x[0] * y[0];
+    const u128 c1 = (u128)x[0] * y[1] + (u128)x[1] * y[0];
+    const u128 c2 = (u128)x[0] * y[2] + (u128)x[1] * y[1] + (u128)x[2] * y[0];
+    const u128 c3 = (u128)x[0] * y[3] + (u128)x[1] * y[2] + (u128)x[2] * y[1] + (u128)x[3] * y[0];
+    const u128 c4 =
+        (u128)x[0] * y[4] + (u128)x[1] * y[3] + (u128)x[2] * y[2] + (u128)x[3] * y[1] + (u128)x[4] * y[0];
+    const u128 c5 = (u128)x[1] * y[4] + (u128)x[2] * y[3] + (u128)x[3] * y[2] + (u128)x[4] * y[1];
+    const u128 c6 = (u128)x[2] * y[4] + (u128)x[3] * y[3] + (u128)x[4] * y[2];
+    const u128 c7 = (u128)x[3] * y[4] + (u128)x[4] * y[3];
+    const u128 c8 = (u128)x[4] * y[4];
+    fold_columns(r, c0, c1, c2, c3, c4, c5, c6, c7, c8);
+}
+inline void fsqr(F& r, const F& a) {
+    const uint64_t* x = a.n;
+    const uint64_t d0 = 2 * x[0], d1 = 2 * x[1], d2 = 2 * x[2], d3 = 2 * x[3];
+    const u128 c0 = (u128)x[0] * x[0];
+    const u128 c1 = (u128)d0 * x[1];
+    const u128 c2 = (u128)d0 * x[2] + (u128)x[1] * x[1];
+    const u128 c3 = (u128)d0 * x[3] + (u128)d1 * x[2];
+    const u128 c4 = (u128)d0 * x[4] + (u128)d1 * x[3] + (u128)x[2] * x[2];
+    const u128 c5 = (u128)d1 * x[4] + (u128)d2 * x[3];
+    const u128 c6 = (u128)d2 * x[4] + (u128)x[3] * x[3];
+    const u128 c7 = (u128)d3 * x[4];
+    const u128 c8 = (u128)x[4] * x[4];
+    fold_columns(r, c0, c1, c2, c3, c4, c5, c6, c7, c8);
+}
+inline void fsqr_n(F& r, const F& a, int n) {
+    r = a;
+    for (int i = 0; i < n; i++) fsqr(r, r);
+}
+
+// ---------------------------------------------- divsteps inversion (62-bit)
+// Bernstein-Yang safegcd on signed 62-bit limbs (5 limbs; value = sum
+// v[i] 2^(62 i), limbs 0..3 in [0, 2^62) when normalised, limb 4 signed),
+// 62 divsteps per jump from the low bits of f and g, the (d, e) update kept
+// modulo m by adding the multiple of m that clears the low 62 bits.  Jumps
+// stop once g = 0 (variable time: a CPU baseline, not a product path).
+struct S62 {
+    int64_t v[5];
+};
+struct Mod62 {
+    S62 m;
+    uint64_t m_inv62;   // m^-1 mod 2^62
+};
+struct T2 {
+    int64_t u, v, q, r;
+};
+constexpr int64_t M62 = (int64_t)((1ULL << 62) - 1);
+
+inline int64_t divsteps62(int64_t zeta, uint64_t f0, uint64_t g0, T2& t) {
+    uint64_t u = 1, v = 0, q = 0, r = 1, f = f0, g = g0;
+    for (int i = 0; i < 62; i++) {
+        uint64_t c1 = (uint64_t)(zeta >> 63);   // zeta < 0: delta > 0
+        const uint64_t c2 = 0 - (g & 1);        // g odd
+        const uint64_t x = (f ^ c1) - c1, y = (u ^ c1) - c1, z = (v ^ c1) - c1;
+        g += x & c2;
+        q += y & c2;
+        r += z & c2;
+        c1 &= c2;
+        zeta = (int64_t)(((uint64_t)zeta ^ c1) - 1);
+        f += g & c1;
+        u += q & c1;
+        v += r & c1;
+        g >>= 1;
+        u <<= 1;
+        v <<= 1;
+    }
+    t.u = (int64_t)u;
+    t.v = (int64_t)v;
+    t.q = (int64_t)q;
+    t.r = (int64_t)r;
+    return zeta;
+}
+inline void update_de62(S62& d, S62& e, const T2& t, const Mod62& mi) {
+    const int64_t u = t.u, v = t.v, q = t.q, r = t.r;
+    const int64_t sd = d.v[4] >> 63, se = e.v[4] >> 63;
+    int64_t md = (u & sd) + (v & se), me = (q & sd) + (r & se);
+    i128 cd = (i128)u * d.v[0] + (i128)v * e.v[0];
+    i128 ce = (i128)q * d.v[0] + (i128)r * e.v[0];
+    md -= (int64_t)((mi.m_inv62 * (uint64_t)cd + (uint64_t)md) & (uint64_t)M62);
+    me -= (int64_t)((mi.m_inv62 * (uint64_t)ce + (uint64_t)me) & (uint64_t)M62);
+    cd += (i128)mi.m.v[0] * md;
+    ce += (i128)mi.m.v[0] * me;
+    cd >>= 62;
+    ce >>= 62;
+    for (int i = 1; i < 5; i++) {
+        cd += (i128)u * d.v[i] + (i128)v * e.v[i] + (i128)mi.m.v[i] * md;
+        ce += (i128)q * d.v[i] + (i128)r * e.v[i] + (i128)mi.m.v[i] * me;
+        d.v[i - 1] = (int64_t)cd & M62;
+        cd >>= 62;
+        e.v[i - 1] = (int64_t)ce & M62;
+        ce >>= 62;
+    }
+    d.v[4] = (int64_t)cd;
+    e.v[4] = (int64_t)ce;
+}
+inline void update_fg62(S62& f, S62& g, const T2& t) {
+    const int64_t u = t.u, v = t.v, q = t.q, r = t.r;
+    i128 cf = (i128)u * f.v[0] + (i128)v * g.v[0];
+    i128 cg = (i128)q * f.v[0] + (i128)r * g.v[0];
+    cf >>= 62;
+    cg >>= 62;
+    for (int i = 1; i < 5; i++) {
+        cf += (i128)u * f.v[i] + (i128)v * g.v[i];
+        cg += (i128)q * f.v[i] + (i128)r * g.v[i];
+        f.v[i - 1] = (int64_t)cf & M62;
+        cf >>= 62;
+        g.v[i - 1] = (int64_t)cg & M62;
+        cg >>= 62;
+    }
+    f.v[4] = (int64_t)cf;
+    g.v[4] = (int64_t)cg;
+}
+inline void normalize62(S62& d, int64_t sign, const Mod62& mi) {
+    int64_t add = d.v[4] >> 63;
+    for (int i = 0; i < 5; i++) d.v[i] += mi.m.v[i] & add;
+    const int64_t neg = sign >> 63;
+    for (int i = 0; i < 5; i++) d.v[i] = (d.v[i] ^ neg) - neg;
+    for (int i = 0; i < 4; i++) {
+        d.v[i + 1] += d.v[i] >> 62;
+        d.v[i] &= M62;
+    }
+    add = d.v[4] >> 63;
+    for (int i = 0; i < 5; i++) d.v[i] += mi.m.v[i] & add;
+    for (int i = 0; i < 4; i++) {
+        d.v[i + 1] += d.v[i] >> 62;
+        d.v[i] &= M62;
+    }
+}
+// x in [0, m) -> x^-1 mod m (0 -> 0)
+inline void modinv62(S62& x, const Mod62& mi) {
+    S62 d{}, e{}, f = mi.m, g = x;
+    e.v[0] = 1;
+    int64_t zeta = -1;
+    for (int it = 0; it < 10; it++) {   // 620 >= 590 divsteps
+        T2 t;
+        zeta = divsteps62(zeta, (uint64_t)f.v[0], (uint64_t)g.v[0], t);
+        update_de62(d, e, t, mi);
+        update_fg62(f, g, t);
+        if ((g.v[0] | g.v[1] | g.v[2] | g.v[3] | g.v[4]) == 0) break;
+    }
+    normalize62(d, f.v[4], mi);
+    x = d;
+}
+// 4 little-endian 64-bit words <-> signed-62 limbs
+inline void s62_from_u64(S62& r, const uint64_t w[4]) {
+    r.v[0] = (int64_t)(w[0] & (uint64_t)M62);
+    r.v[1] = (int64_t)(((w[0] >> 62) | (w[1] << 2)) & (uint64_t)M62);
+    r.v[2] = (int64_t)(((w[1] >> 60) | (w[2] << 4)) & (uint64_t)M62);
+    r.v[3] = (int64_t)(((w[2] >> 58) | (w[3] << 6)) & (uint64_t)M62);
+    r.v[4] = (int64_t)(w[3] >> 56);
+}
+inline void s62_to_u64(uint64_t w[4], const S62& a) {
+    w[0] = (uint64_t)a.v[0] | ((uint64_t)a.v[1] << 62);
+    w[1] = ((uint64_t)a.v[1] >> 2) | ((uint64_t)a.v[2] << 60);
+    w[2] = ((uint64_t)a.v[2] >> 4) | ((uint64_t)a.v[3] << 58);
+    w[3] = ((uint64_t)a.v[3] >> 6) | ((uint64_t)a.v[4] << 56);
+}
+inline uint64_t inv_mod_2_64(uint64_t m) {   // m odd: Newton on 2-adic inverse
+    uint64_t x = m;
+    for (int i = 0; i < 6; i++) x *= 2 - m * x;
+    return x;
+}
+inline Mod62 mod62_of(const uint64_t w[4]) {
+    Mod62 mi;
+    s62_from_u64(mi.m, w);
+    mi.m_inv62 = inv_mod_2_64(w[0]) & (uint64_t)M62;
+    return mi;
+}
+const uint64_t NW[4] = {0xBFD25E8CD0364141ULL, 0xBAAEDCE6AF48A03BULL, 0xFFFFFFFFFFFFFFFEULL, 0xFFFFFFFFFFFFFFFFULL};
+const uint64_t PW[4] = {0xFFFFFFFEFFFFFC2FULL, 0xFFFFFFFFFFFFFFFFULL, 0xFFFFFFFFFFFFFFFFULL, 0xFFFFFFFFFFFFFFFFULL};
+const Mod62& mod_n() {
+    static const Mod62 mi = mod62_of(NW);
+    return mi;
+}
+const Mod62& mod_p() {
+    static const Mod62 mi = mod62_of(PW);
+    return mi;
+}
+
+inline void finv(F& r, const F& a) {
+    F t = a;
+    fnorm(t);
+    uint64_t w[4] = {t.n[0] | (t.n[1] << 52), (t.n[1] >> 12) | (t.n[2] << 40), (t.n[2] >> 24) | (t.n[3] << 28),
+                     (t.n[3] >> 36) | (t.n[4] << 16)};
+    S62 x;
+    s62_from_u64(x, w);
+    modinv62(x, mod_p());
+    s62_to_u64(w, x);
+    r.n[0] = w[0] & M52;
+    r.n[1] = ((w[0] >> 52) | (w[1] << 12)) & M52;
+    r.n[2] = ((w[1] >> 40) | (w[2] << 24)) & M52;
+    r.n[3] = ((w[2] >> 28) | (w[3] << 36)) & M52;
+    r.n[4] = w[3] >> 16;
+}
+// r = a^((p+1)/4); true iff r^2 = a (the addition chain of x^(2^223 - 1))
+inline bool fsqrt(F& r, const F& a) {
+    F x2, x3, x6, x9, x11, x22, x44, x88, x176, x220, x223, t;
+    fsqr(x2, a);
+    fmul(x2, x2, a);
+    fsqr(x3, x2);
+    fmul(x3, x3, a);
+    fsqr_n(x6, x3, 3);
+    fmul(x6, x6, x3);
+    fsqr_n(x9, x6, 3);
+    fmul(x9, x9, x3);
+    fsqr_n(x11, x9, 2);
+    fmul(x11, x11, x2);
+    fsqr_n(x22, x11, 11);
+    fmul(x22, x22, x11);
+    fsqr_n(x44, x22, 22);
+    fmul(x44, x44, x22);
+    fsqr_n(x88, x44, 44);
+    fmul(x88, x88, x44);
+    fsqr_n(x176, x88, 88);
+    fmul(x176, x176, x88);
+    fsqr_n(x220, x176, 44);
+    fmul(x220, x220, x44);
+    fsqr_n(x223, x220, 3);
+    fmul(x223, x223, x3);
+    fsqr_n(t, x223, 23);
+    fmul(t, t, x22);
+    fsqr_n(t, t, 6);
+    fmul(t, t, x2);
+    fsqr(t, t);
+    fsqr(r, t);
+    F c, an = a;
+    fsqr(c, r);
+    fnorm(c);
+    fnorm(an);
+    return memcmp(c.n, an.n, sizeof c.n) == 0;
+}
+
+// ------------------------------------------------------------ scalars mod n
+struct Sc {
+    uint64_t d[4];
+};
+const uint64_t CN[3] = {0x402DA1732FC9BEBFULL, 0x4551231950B75FC4ULL, 1};   // 2^256 - n
+
+inline bool sc_ge_n(const uint64_t a[4]) {
+    for (int i = 3; i >= 0; i--) {
+        if (a[i] > NW[i]) return true;
+        if (a[i] < NW[i]) return false;
+    }
+    return true;
+}
+inline void sc_sub_n(uint64_t a[4]) {   // a -= n, i.e. a += 2^256 - n (mod 2^256)
+    u128 c = 0;
+    for (int i = 0; i < 4; i++) {
+        c += (u128)a[i] + (i < 3 ? CN[i] : 0);
+        a[i] = (uint64_t)c;
+        c >>= 64;
+    }
+}
+inline void sc_from_be(Sc& r, const uint8_t* b, bool* overflow) {
+    for (int k = 0; k < 4; k++) {
+        uint64_t x = 0;
+        for (int j = 0; j < 8; j++) x = (x << 8) | b[8 * (3 - k) + j];
+        r.d[k] = x;
+    }
+    const bool ov = sc_ge_n(r.d);
+    if (overflow) *overflow = ov;
+    if (ov) sc_sub_n(r.d);
+}
+inline bool sc_is_zero(const Sc& a) { return (a.d[0] | a.d[1] | a.d[2] | a.d[3]) == 0; }
+inline void sc_neg(Sc& r, const Sc& a) {
+    if (sc_is_zero(a)) {
+        r = a;
+        return;
+    }
+    u128 b = 0;
+    for (int i = 0; i < 4; i++) {
+        const u128 t = (u128)NW[i] - a.d[i] - b;
+        r.d[i] = (uint64_t)t;
+        b = (t >> 127) & 1;
+    }
+}
+inline void sc_add(Sc& r, const Sc& a, const Sc& b) {
+    u128 c = 0;
+    uint64_t o[4];
+    for (int i = 0; i < 4; i++) {
+        c += (u128)a.d[i] + b.d[i];
+        o[i] = (uint64_t)c;
+        c >>= 64;
+    }
+    if (c || sc_ge_n(o)) sc_sub_n(o);
+    memcpy(r.d, o, sizeof o);
+}
+// out (nl + 3 words) = lo (nl words) + hi (nh words) * (2^256 - n)
+inline void mul_add_cn(uint64_t* out, int nout, const uint64_t* lo, int nl, const uint64_t* hi, int nh) {
+    for (int i = 0; i < nout; i++) out[i] = i < nl ? lo[i] : 0;
+    for (int i = 0; i < nh; i++) {
+        u128 c = 0;
+        for (int j = 0; j < 3; j++) {
+            c += (u128)hi[i] * CN[j] + out[i + j];
+            out[i + j] = (uint64_t)c;
+            c >>= 64;
+        }
+        for (int k = i + 3; c && k < nout; k++) {
+            c += out[k];
+            out[k] = (uint64_t)c;
+            c >>= 64;
+        }
+    }
+}
+inline void sc_reduce512(Sc& r, const uint64_t t[8]) {
+    uint64_t a[7], b[5], c[4];
+    mul_add_cn(a, 7, t, 4, t + 4, 4);    // t_lo + t_hi (2^256 - n) < 2^386
+    mul_add_cn(b, 5, a, 4, a + 4, 3);    // < 2^260: b[4] < 16
+    u128 acc = (u128)b[0] + (u128)b[4] * CN[0];
+    c[0] = (uint64_t)acc;
+    acc = (acc >> 64) + b[1] + (u128)b[4] * CN[1];
+    c[1] = (uint64_t)acc;
+    acc = (acc >> 64) + b[2] + (u128)b[4] * CN[2];
+    c[2] = (uint64_t)acc;
+    acc = (acc >> 64) + b[3];
+    c[3] = (uint64_t)acc;
+    if ((uint64_t)(acc >> 64)) sc_sub_n(c);   // wrapped past 2^256 (c is then small): add 2^256 - n
+    if (sc_ge_n(c)) sc_sub_n(c);
+    memcpy(r.d, c, sizeof c);
+}
+inline void sc_mul(Sc& r, const Sc& a, const Sc& b) {
+    uint64_t t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 4; i++) {
+        u128 c = 0;
+        for (int j = 0; j < 4; j++) {
+            c += (u128)a.d[i] * b.d[j] + t[i + j];
+            t[i + j] = (uint64_t)c;
+            c >>= 64;
+        }
+        t[i + 4] = (uint64_t)c;
+    }
+    sc_reduce512(r, t);
+}
+inline void sc_inv(Sc& r, const Sc& a) {
+    S62 x;
+    s62_from_u64(x, a.d);
+    modinv62(x, mod_n());
+    s62_to_u64(r.d, x);
+}
+
+// ------------------------------------------------------------ GLV split
+// k = k1 + k2 lambda (mod n), |k1|, |k2| < 2^128: c1 = round(k g1 / 2^384),
+// c2 = round(k g2 / 2^384), k2 = -c1 b1 - c2 b2, k1 = k - k2 lambda (the
+// lattice constants of hd_group.h, as 64-bit words).
+const uint64_t G1W[4] = {0xE893209A45DBB031ULL, 0x3DAA8A1471E8CA7FULL, 0xE86C90E49284EB15ULL, 0x3086D221A7D46BCDULL};
+const uint64_t G2W[4] = {0x1571B4AE8AC47F71ULL, 0x221208AC9DF506C6ULL, 0x6F547FA90ABFE4C4ULL, 0xE4437ED6010E8828ULL};
+const Sc MB1{{0x6F547FA90ABFE4C3ULL, 0xE4437ED6010E8828ULL, 0, 0}};
+const Sc MB2{{0xD765CDA83DB1562CULL, 0x8A280AC50774346DULL, 0xFFFFFFFFFFFFFFFEULL, 0xFFFFFFFFFFFFFFFFULL}};
+const Sc MLAM{{0xE0CFC810B51283CFULL, 0xA880B9FC8EC739C2ULL, 0x5AD9E3FD77ED9BA4ULL, 0xAC9C52B33FA3CF1FULL}};
+
+inline void sc_mul_shift384(Sc& r, const Sc& k, const uint64_t g[4]) {
+    uint64_t t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 4; i++) {
+        u128 c = 0;
+        for (int j = 0; j < 4; j++) {
+            c += (u128)k.d[i] * g[j] + t[i + j];
+            t[i + j] = (uint64_t)c;
+            c >>= 64;
+        }
+        t[i + 4] = (uint64_t)c;
+    }
+    u128 c = (u128)(t[5] >> 63) + t[6];   // round on bit 383
+    r.d[0] = (uint64_t)c;
+    c = (c >> 64) + t[7];
+    r.d[1] = (uint64_t)c;
+    r.d[2] = (uint64_t)(c >> 64);
+    r.d[3] = 0;
+}
+inline void sc_split(Sc& k1, Sc& k2, const Sc& k) {
+    Sc c1, c2, t;
+    sc_mul_shift384(c1, k, G1W);
+    sc_mul_shift384(c2, k, G2W);
+    sc_mul(c1, c1, MB1);
+    sc_mul(c2, c2, MB2);
+    sc_add(k2, c1, c2);
+    sc_mul(t, k2, MLAM);
+    sc_add(k1, k, t);
+}
+// a 129-bit signed magnitude of k (k > n/2 means -(n - k))
+inline bool sc_abs(uint64_t a[3], const Sc& k) {
+    const uint64_t NH[4] = {0xDFE92F46681B20A0ULL, 0x5D576E7357A4501DULL, 0xFFFFFFFFFFFFFFFFULL, 0x7FFFFFFFFFFFFFFFULL};
+    bool gt = false;
+    for (int i = 3; i >= 0; i--) {
+        if (k.d[i] != NH[i]) {
+            gt = k.d[i] > NH[i];
+            break;
+        }
+    }
+    Sc m = k;
+    if (gt) sc_neg(m, k);
+    a[0] = m.d[0];
+    a[1] = m.d[1];
+    a[2] = m.d[2];
+    return gt;
+}
+// width-w NAF of a 3-word magnitude (digits odd, |d| < 2^(w-1)), sign applied;
+// returns the number of digit positions used
+inline int wnaf(int* out, int len, const uint64_t a[3], bool neg, int w) {
+    auto bits = [&](int pos, int cnt) -> uint32_t {
+        uint32_t v = 0;
+        for (int t = 0; t < cnt; t++) {
+            const int b = pos + t;
+            if (b < 192) v |= (uint32_t)((a[b >> 6] >> (b & 63)) & 1) << t;
+        }
+        return v;
+    };
+    for (int i = 0; i < len; i++) out[i] = 0;
+    int bit = 0, carry = 0, last = 0;
+    while (bit < len) {
+        if ((int)bits(bit, 1) == carry) {
+            bit++;
+            continue;
+        }
+        int now = w;
+        if (now > len - bit) now = len - bit;
+        int word = (int)bits(bit, now) + carry;
+        carry = (word >> (w - 1)) & 1;
+        word -= carry << w;
+        out[bit] = neg ? -word : word;
+        last = bit;
+        bit += now;
+    }
+    return last + 1;
+}
+
+// ------------------------------------------------------------ group
+struct GA {   // affine
+    F x, y;
+};
+struct GJ {   // Jacobian, magnitudes 1
+    F x, y, z;
+    bool inf;
+};
+inline void gj_set_ga(GJ& r, const GA& a) {
+    r.x = a.x;
+    r.y = a.y;
+    fset(r.z, 1);
+    r.inf = false;
+}
+// dbl-2009-l (a = 0): 2M + 5S
+inline void gj_double(GJ& r, const GJ& a) {
+    if (a.inf) {
+        r.inf = true;
+        return;
+    }
+    F A, B, C, D, E, Fq, t, u;
+    fsqr(A, a.x);
+    fsqr(B, a.y);
+    fsqr(C, B);
+    fadd(t, a.x, B);
+    fsqr(t, t);
+    fneg(u, A, 1);
+    fadd(t, t, u);
+    fneg(u, C, 1);
+    fadd(t, t, u);
+    fmul_int(t, 2);
+    fnorm_weak(t);
+    D = t;                    // 1
+    E = A;
+    fmul_int(E, 3);           // 3
+    fsqr(Fq, E);
+    F z3;
+    fmul(z3, a.y, a.z);
+    fmul_int(z3, 2);
+    fnorm_weak(z3);
+    u = D;
+    fmul_int(u, 2);
+    fneg(u, u, 2);
+    fadd(r.x, Fq, u);
+    fnorm_weak(r.x);          // X3 = F - 2D
+    fneg(u, r.x, 1);
+    fadd(t, D, u);            // D - X3: 5
+    fmul(t, E, t);
+    u = C;
+    fmul_int(u, 8);
+    fneg(u, u, 8);
+    fadd(r.y, t, u);
+    fnorm_weak(r.y);          // Y3 = E (D - X3) - 8C
+    r.z = z3;
+    r.inf = false;
+}
+// a + b, b affine (madd: 8M + 3S), exceptional cases by branches
+inline void gj_add_ga(GJ& r, const GJ& a, const GA& b) {
+    if (a.inf) {
+        gj_set_ga(r, b);
+        return;
+    }
+    F z1z1, u2, s2, h, rr, t, hh, hhh, v;
+    fsqr(z1z1, a.z);
+    fmul(u2, b.x, z1z1);
+    fmul(s2, b.y, a.z);
+    fmul(s2, s2, z1z1);
+    fneg(t, a.x, 1);
+    fadd(h, u2, t);
+    fnorm_weak(h);
+    fneg(t, a.y, 1);
+    fadd(rr, s2, t);
+    fnorm_weak(rr);
+    if (fis_zero(h)) {
+        if (fis_zero(rr)) {
+            gj_double(r, a);
+        } else {
+            r.inf = true;
+        }
+        return;
+    }
+    fsqr(hh, h);
+    fmul(hhh, h, hh);
+    fmul(v, a.x, hh);
+    F x3, y3, z3;
+    fsqr(x3, rr);
+    fneg(t, hhh, 1);
+    fadd(x3, x3, t);
+    t = v;
+    fmul_int(t, 2);
+    fneg(t, t, 2);
+    fadd(x3, x3, t);
+    fnorm_weak(x3);
+    fneg(t, x3, 1);
+    fadd(t, v, t);
+    fmul(y3, rr, t);
+    fmul(t, a.y, hhh);
+    fneg(t, t, 1);
+    fadd(y3, y3, t);
+    fnorm_weak(y3);
+    fmul(z3, a.z, h);
+    r.x = x3;
+    r.y = y3;
+    r.z = z3;
+    r.inf = false;
+}
+// a + b, both Jacobian (12M + 4S)
+inline void gj_add(GJ& r, const GJ& a, const GJ& b) {
+    if (a.inf) {
+        r = b;
+        return;
+    }
+    if (b.inf) {
+        r = a;
+        return;
+    }
+    F z1z1, z2z2, u1, u2, s1, s2, h, rr, t, hh, hhh, v;
+    fsqr(z1z1, a.z);
+    fsqr(z2z2, b.z);
+    fmul(u1, a.x, z2z2);
+    fmul(u2, b.x, z1z1);
+    fmul(s1, a.y, b.z);
+    fmul(s1, s1, z2z2);
+    fmul(s2, b.y, a.z);
+    fmul(s2, s2, z1z1);
+    fneg(t, u1, 1);
+    fadd(h, u2, t);
+    fnorm_weak(h);
+    fneg(t, s1, 1);
+    fadd(rr, s2, t);
+    fnorm_weak(rr);
+    if (fis_zero(h)) {
+        if (fis_zero(rr)) {
+            gj_double(r, a);
+        } else {
+            r.inf = true;
+        }
+        return;
+    }
+    fsqr(hh, h);
+    fmul(hhh, h, hh);
+    fmul(v, u1, hh);
+    F x3, y3, z3;
+    fsqr(x3, rr);
+    fneg(t, hhh, 1);
+    fadd(x3, x3, t);
+    t = v;
+    fmul_int(t, 2);
+    fneg(t, t, 2);
+    fadd(x3, x3, t);
+    fnorm_weak(x3);
+    fneg(t, x3, 1);
+    fadd(t, v, t);
+    fmul(y3, rr, t);
+    fmul(t, s1, hhh);
+    fneg(t, t, 1);
+    fadd(y3, y3, t);
+    fnorm_weak(y3);
+    fmul(z3, a.z, b.z);
+    fmul(z3, z3, h);
+    r.x = x3;
+    r.y = y3;
+    r.z = z3;
+    r.inf = false;
+}
+
+const uint8_t GX[32] = {0x79, 0xBE, 0x66, 0x7E, 0xF9, 0xDC, 0xBB, 0xAC, 0x55, 0xA0, 0x62, 0x95, 0xCE, 0x87, 0x0B, 0x07,
+                        0x02, 0x9B, 0xFC, 0xDB, 0x2D, 0xCE, 0x28, 0xD9, 0x59, 0xF2, 0x81, 0x5B, 0x16, 0xF8, 0x17, 0x98};
+const uint8_t GY[32] = {0x48, 0x3A, 0xDA, 0x77, 0x26, 0xA3, 0xC4, 0x65, 0x5D, 0xA4, 0xFB, 0xFC, 0x0E, 0x11, 0x08, 0xA8,
+                        0xFD, 0x17, 0xB4, 0x48, 0xA6, 0x85, 0x54, 0x19, 0x9C, 0x47, 0xD0, 0x8F, 0xFB, 0x10, 0xD4, 0xB8};
+const uint8_t BETA[32] = {0x7A, 0xE9, 0x6A, 0x2B, 0x65, 0x7C, 0x07, 0x10, 0x6E, 0x64, 0x47, 0x9E, 0xAC, 0x34, 0x34, 0xE9,
+                          0x9C, 0xF0, 0x49, 0x75, 0x12, 0xF5, 0x89, 0x95, 0xC1, 0x39, 0x6C, 0x28, 0x71, 0x95, 0x01, 0xEE};
+
+constexpr int WG = 15;                        // wNAF width of G and lambda G
+constexpr int NG = 1 << (WG - 2);             // odd multiples 1G .. (2^(WG-1) - 1) G: 8,192
+constexpr int WR = 5;                         // wNAF width of R and lambda R
+constexpr int NR = 1 << (WR - 2);             // 8
+
+struct GTables {
+    std::vector<GA> g, lg;   // odd multiples of G and of lambda G (affine)
+    F beta;
+};
+const GTables& gtables() {
+    static GTables t;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        f_from_be(t.beta, BETA);
+        GA g;
+        f_from_be(g.x, GX);
+        f_from_be(g.y, GY);
+        std::vector<GJ> j(NG);
+        GJ g2, gj;
+        gj_set_ga(gj, g);
+        gj_double(g2, gj);
+        j[0] = gj;
+        for (int k = 1; k < NG; k++) gj_add(j[k], j[k - 1], g2);
+        // to affine: one inversion (Montgomery's trick over the Z)
+        std::vector<F> pre(NG);
+        pre[0] = j[0].z;
+        for (int k = 1; k < NG; k++) fmul(pre[k], pre[k - 1], j[k].z);
+        F inv;
+        finv(inv, pre[NG - 1]);
+        t.g.resize(NG);
+        t.lg.resize(NG);
+        for (int k = NG - 1; k >= 0; k--) {
+            F zi, zi2, zi3;
+            if (k > 0) {
+                fmul(zi, inv, pre[k - 1]);
+                fmul(inv, inv, j[k].z);
+            } else {
+                zi = inv;
+            }
+            fsqr(zi2, zi);
+            fmul(zi3, zi2, zi);
+            fmul(t.g[k].x, j[k].x, zi2);
+            fmul(t.g[k].y, j[k].y, zi3);
+            fnorm(t.g[k].x);
+            fnorm(t.g[k].y);
+            fmul(t.lg[k].x, t.g[k].x, t.beta);
+            fnorm(t.lg[k].x);
+            t.lg[k].y = t.g[k].y;
+        }
+    });
+    return t;
+}
+
+// Q = u1 G + u2 R (Strauss over the GLV halves); false: Q is infinity
+inline bool ecmult(GA& q, const Sc& u1, const Sc& u2, const GA& R) {
+    const GTables& T = gtables();
+    Sc a1, a2, b1, b2;
+    sc_split(a1, a2, u1);
+    sc_split(b1, b2, u2);
+    uint64_t m[3];
+    int wa1[130], wa2[130], wb1[130], wb2[130];
+    bool s;
+    int len = 0;
+    s = sc_abs(m, a1);
+    len = std::max(len, wnaf(wa1, 130, m, s, WG));
+    s = sc_abs(m, a2);
+    len = std::max(len, wnaf(wa2, 130, m, s, WG));
+    s = sc_abs(m, b1);
+    len = std::max(len, wnaf(wb1, 130, m, s, WR));
+    s = sc_abs(m, b2);
+    len = std::max(len, wnaf(wb2, 130, m, s, WR));
+    // odd multiples of R (Jacobian) and of lambda R (beta X)
+    GJ tr[NR], tl[NR];
+    GJ r1, r2;
+    gj_set_ga(r1, R);
+    gj_double(r2, r1);
+    tr[0] = r1;
+    for (int k = 1; k < NR; k++) gj_add(tr[k], tr[k - 1], r2);
+    for (int k = 0; k < NR; k++) {
+        tl[k] = tr[k];
+        fmul(tl[k].x, tr[k].x, T.beta);
+    }
+    GJ acc;
+    acc.inf = true;
+    for (int i = len - 1; i >= 0; i--) {
+        gj_double(acc, acc);
+        auto addj = [&](const GJ* tab, int d) {
+            if (!d) return;
+            GJ p = tab[(d < 0 ? -d : d) >> 1];
+            if (d < 0) {
+                F t;
+                fneg(t, p.y, 1);
+                fnorm_weak(t);
+                p.y = t;
+            }
+            gj_add(acc, acc, p);
+        };
+        auto adda = [&](const std::vector<GA>& tab, int d) {
+            if (!d) return;
+            GA p = tab[(d < 0 ? -d : d) >> 1];
+            if (d < 0) {
+                F t;
+                fneg(t, p.y, 1);
+                fnorm_weak(t);
+                p.y = t;
+            }
+            gj_add_ga(acc, acc, p);
+        };
+        addj(tr, wb1[i]);
+        addj(tl, wb2[i]);
+        adda(T.g, wa1[i]);
+        adda(T.lg, wa2[i]);
+    }
+    if (acc.inf || fis_zero(acc.z)) return false;
+    F zi, zi2, zi3;
+    finv(zi, acc.z);
+    fsqr(zi2, zi);
+    fmul(zi3, zi2, zi);
+    fmul(q.x, acc.x, zi2);
+    fmul(q.y, acc.y, zi3);
+    fnorm(q.x);
+    fnorm(q.y);
+    return true;
+}
+
+enum { VALID = 0, BAD_RECID = 1, BAD_RS = 2, NO_POINT = 3, INFINITY_ = 4, MISMATCH = 5, NOT_ADMITTED = 6, BAD_TYPE = 7 };
+
+// the checks in go-ethereum / libsecp256k1 order
+inline int recover(GA& q, const uint8_t dig[32], const uint8_t sig[65]) {
+    const uint8_t v = sig[64];
+    if (v >= 4) return BAD_RECID;
+    Sc r, s, m;
+    bool ovr, ovs;
+    sc_from_be(r, sig, &ovr);
+    sc_from_be(s, sig + 32, &ovs);
+    if (ovr || ovs || sc_is_zero(r) || sc_is_zero(s)) return BAD_RS;
+    // x = r (+ n), < p
+    uint64_t xw[4];
+    memcpy(xw, r.d, sizeof xw);
+    if (v & 2) {
+        // r + n >= p  <=>  r >= p - n
+        const uint64_t PMN[4] = {0x402DA1722FC9BAEEULL, 0x4551231950B75FC4ULL, 1, 0};
+        bool ge = false;
+        for (int i = 3; i >= 0; i--) {
+            if (xw[i] != PMN[i]) {
+                ge = xw[i] > PMN[i];
+                break;
+            }
+            if (i == 0) ge = true;
+        }
+        if (ge) return NO_POINT;
+        u128 c = 0;
+        for (int i = 0; i < 4; i++) {
+            c += (u128)xw[i] + NW[i];
+            xw[i] = (uint64_t)c;
+            c >>= 64;
+        }
+    }
+    GA R;
+    R.x.n[0] = xw[0] & M52;
+    R.x.n[1] = ((xw[0] >> 52) | (xw[1] << 12)) & M52;
+    R.x.n[2] = ((xw[1] >> 40) | (xw[2] << 24)) & M52;
+    R.x.n[3] = ((xw[2] >> 28) | (xw[3] << 36)) & M52;
+    R.x.n[4] = xw[3] >> 16;
+    F y2, x3;
+    fsqr(x3, R.x);
+    fmul(x3, x3, R.x);
+    F seven;
+    fset(seven, 7);
+    fadd(y2, x3, seven);
+    if (!fsqrt(R.y, y2)) return NO_POINT;
+    fnorm(R.y);
+    if ((R.y.n[0] & 1) != (uint64_t)(v & 1)) {
+        F t;
+        fneg(t, R.y, 1);
+        fnorm(t);
+        R.y = t;
+    }
+    sc_from_be(m, dig, nullptr);
+    Sc rinv, u1, u2;
+    sc_inv(rinv, r);
+    sc_mul(u1, m, rinv);
+    sc_neg(u1, u1);
+    sc_mul(u2, s, rinv);
+    if (!ecmult(q, u1, u2, R)) return INFINITY_;
+    return VALID;
+}
+
+inline void be_words(uint32_t w[8], const uint8_t* b) {
+    for (int i = 0; i < 8; i++) w[i] = ((uint32_t)b[4 * i] << 24) | ((uint32_t)b[4 * i + 1] << 16) |
+                                       ((uint32_t)b[4 * i + 2] << 8) | b[4 * i + 3];
+}
+inline void words_be(uint8_t* b, const uint32_t w[8]) {
+    for (int i = 0; i < 8; i++) {
+        b[4 * i] = (uint8_t)(w[i] >> 24);
+        b[4 * i + 1] = (uint8_t)(w[i] >> 16);
+        b[4 * i + 2] = (uint8_t)(w[i] >> 8);
+        b[4 * i + 3] = (uint8_t)w[i];
+    }
+}
+
+}  // namespace sp
+
+extern "C" {
+
+// verdict / rec32 / signer per message, as hd_verify_batch (compressed: the
+// 33-byte SEC1 key is hashed, else the 65-byte one); adm32 any order (sorted
+// here, duplicates map to the first caller index).  Returns 0, or -1 for an
+// unsupported pubkey format.
+int secp_verify(uint32_t n, const uint8_t* type, const int64_t* h, const int64_t* r, const int64_t* vr,
+                const uint8_t* value32, const uint8_t* from32, const uint8_t* sig65, const uint8_t* adm32,
+                uint32_t n_adm, int compressed, uint8_t* verdict, uint8_t* rec32, int32_t* signer, int threads) {
+    using namespace sp;
+    if (compressed != 0 && compressed != 1) return -1;
+    (void)gtables();
+    std::vector<std::pair<std::string, int32_t>> adm;
+    for (uint32_t k = 0; k < n_adm; k++) adm.emplace_back(std::string((const char*)adm32 + 32 * (size_t)k, 32), (int32_t)k);
+    std::stable_sort(adm.begin(), adm.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    auto work = [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t i = lo; i < hi; i++) {
+            uint8_t out[32] = {0};
+            int32_t sg = -1;
+            int vd;
+            const uint8_t t = type[i];
+            if (t < 1 || t > 3) {
+                vd = BAD_TYPE;
+            } else {
+                uint32_t val[8], dw[8];
+                be_words(val, value32 + 32 * (size_t)i);
+                if (t == 1) hd::sha256_propose(dw, h[i], r[i], vr ? vr[i] : -1, val);
+                else hd::sha256_vote(dw, h[i], r[i], val);
+                uint8_t dig[32];
+                words_be(dig, dw);
+                GA q;
+                vd = recover(q, dig, sig65 + 65 * (size_t)i);
+                if (vd == VALID) {
+                    uint8_t xb[32], yb[32];
+                    f_to_be(xb, q.x);
+                    f_to_be(yb, q.y);
+                    uint32_t xw[8], yw[8], sw[8];
+                    be_words(xw, xb);
+                    be_words(yw, yb);
+                    if (compressed) hd::sha256_pub33(sw, 2u + (uint32_t)(q.y.n[0] & 1), xw);
+                    else hd::sha256_pub65(sw, xw, yw);
+                    words_be(out, sw);
+                    if (memcmp(out, from32 + 32 * (size_t)i, 32) != 0) {
+                        vd = MISMATCH;
+                    } else {
+                        const std::string key((const char*)out, 32);
+                        auto it = std::lower_bound(adm.begin(), adm.end(), key,
+                                                   [](const auto& a, const std::string& k) { return a.first < k; });
+                        if (it == adm.end() || it->first != key) vd = NOT_ADMITTED;
+                        else sg = it->second;
+                    }
+                }
+            }
+            verdict[i] = (uint8_t)vd;
+            if (rec32) memcpy(rec32 + 32 * (size_t)i, out, 32);
+            if (signer) signer[i] = vd == VALID ? sg : -1;
+        }
+    };
+    threads = std::max(1, threads);
+    std::vector<std::thread> th;
+    const uint32_t per = (n + (uint32_t)threads - 1) / (uint32_t)threads;
+    for (int k = 0; k < threads; k++) {
+        const uint32_t lo = std::min<uint32_t>(n, (uint32_t)k * per), hi = std::min<uint32_t>(n, lo + per);
+        if (lo < hi) th.emplace_back(work, lo, hi);
+    }
+    for (auto& x : th) x.join();
+    return 0;
+}
+
+}  // extern "C"

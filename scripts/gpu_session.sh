@@ -108,5 +108,9 @@ for step in "$@"; do
     absums) run ab_sums 900 bash scripts/gpu_ab_prof.sh "base:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5base.so" "new:HD_SUM_WAVES=0" "base2:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5base.so" "new2:HD_SUM_WAVES=0" "base5:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5base.so AB_ADV=30" "new5:AB_ADV=30" ;;
     absums2) run ab_sums2 900 bash scripts/gpu_ab_prof.sh "base:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5base.so" "p1:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5p1.so" "new:HD_SUM_WAVES=0" "base2:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5base.so" "p1b:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5p1.so" "new2:HD_SUM_WAVES=0" ;;
     absums3) run ab_sums3 900 bash scripts/gpu_ab_prof.sh "p1:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5p1.so" "pp:HD_SUM_WAVES=0" "p1b:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5p1.so" "ppb:HD_SUM_WAVES=0" "pp_pf2:HD_SUM_PF=2" "p1_pf2:HD_LIB=hyperdrive_amd/_lib/var/libhd_r5p1.so HD_SUM_PF=2" ;;
+    multinew) HD_TALLY_CHECK=1 run pytest_multinew 400 python -u -m pytest tests/test_multi_gpu.py -m gpu -x -v -p no:cacheprovider --timeout 200 --timeout-method thread ;;
+    c3async) HD_BENCH_ASYNC_TALLY=1 run c3host_async 300 python -u scripts/c3_host_probe.py 40 ;;
+    c3matrix) run c3_sync 300 python -u scripts/c3_host_probe.py 40 && HD_BENCH_NBUF=8 run c3_sync_nb8 300 python -u scripts/c3_host_probe.py 40 && C3_TS_PRIO=-1 run c3_sync_hi 300 python -u scripts/c3_host_probe.py 40 && HD_BENCH_ASYNC_TALLY=1 run c3_async 300 python -u scripts/c3_host_probe.py 40 && HD_BENCH_ASYNC_TALLY=1 C3_TS_PRIO=-1 run c3_async_hi 300 python -u scripts/c3_host_probe.py 40 ;;
+    c3trace) run c3trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c3trace -o run -- python3 scripts/c3_host_probe.py 20 ;;
   esac
 done

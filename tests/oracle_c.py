@@ -102,3 +102,28 @@ class GlvPort:
                                  _p(verdict), _p(rec), None, threads)
         assert rc == 0
         return verdict, rec
+
+
+class SecpPort:
+    """The CPU baseline "port-secp-class" (oracle/secp_port.cpp): a C++
+    restatement of the reference path in libsecp256k1's algorithm class
+    (5 x 52-bit field, GLV + wNAF Strauss ladder, precomputed G table,
+    divsteps inversions), threaded.  Not the oracle; bench.py's cpu_baseline
+    leg and its test only."""
+
+    def __init__(self, path: str):
+        self.lib = ctypes.CDLL(path)
+        self.lib.secp_verify.restype = ctypes.c_int
+        self.lib.secp_verify.argtypes = [ctypes.c_uint32] + [ctypes.c_void_p] * 8 + [ctypes.c_uint32, ctypes.c_int] + \
+            [ctypes.c_void_p] * 3 + [ctypes.c_int]
+
+    def verify(self, batch, admitted: np.ndarray, compressed: bool = True, threads: int = 1):
+        n = len(batch)
+        verdict = np.zeros(n, np.uint8)
+        rec = np.zeros((n, 32), np.uint8)
+        adm = np.ascontiguousarray(admitted, dtype=np.uint8).reshape(-1, 32)
+        rc = self.lib.secp_verify(n, _p(batch.type), _p(batch.height), _p(batch.round), _p(batch.valid_round),
+                                  _p(batch.value), _p(batch.frm), _p(batch.sig), _p(adm), len(adm), int(compressed),
+                                  _p(verdict), _p(rec), None, threads)
+        assert rc == 0
+        return verdict, rec

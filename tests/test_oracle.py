@@ -153,3 +153,26 @@ def test_glv_port_baseline_equals_c_oracle(coracle, hostmath):
         v, rec = gp.verify(b, sigs, True, threads=th)
         assert v.tolist() == cv.tolist()
         assert rec.tobytes() == crec.tobytes()
+
+
+def test_secp_class_port_equals_c_oracle(coracle, hostmath):
+    """The 'port-secp-class' CPU baseline (oracle/secp_port.cpp: 5 x 52-bit
+    field, GLV + wNAF Strauss ladder, divsteps inversions) gives the C
+    oracle's verdicts and recovered signatories on the 30 % adversarial mix
+    (every class: bad recid, r / s range, r + n >= p, no point, infinity,
+    mismatch, not admitted, bad type), on one and on several threads, for the
+    compressed and the uncompressed pubkey encodings."""
+    import subprocess
+    from oracle_c import SecpPort
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "oracle")], check=True)
+    sp = SecpPort(os.path.join(root, "oracle", "_build", "libsecpport.so"))
+    for compressed in (True, False):
+        sigs, foreign = hostmath.keys(50, compressed)
+        b, _ = hostmath.gen(0, 3, 3000, 50, 30, (sigs, foreign))
+        cv, crec = coracle.verify(b, sigs, compressed, threads=4)
+        assert len(set(cv.tolist())) >= 7
+        for th in (1, 5):
+            v, rec = sp.verify(b, sigs, compressed, threads=th)
+            assert v.tolist() == cv.tolist(), (compressed, th)
+            assert rec.tobytes() == crec.tobytes(), (compressed, th)

@@ -225,12 +225,9 @@ HD uint32_t fb_ref(int d, int w) {
 // admitted lookup, key state, digest, the early checks; m and r to the rows
 __global__ __launch_bounds__(256) void k_fast_prep(DevBatch b, const uint8_t* __restrict__ digest_in,
                                                    const uint32_t* __restrict__ state,
-                                                   const int32_t* __restrict__ adm_slot,
-                                                   const uint32_t* __restrict__ adm, uint32_t n_adm, int adm_steps,
-                                                   SplitRows rows, int adm_in_lds, const uint32_t* __restrict__ fdict) {
-    extern __shared__ uint32_t sh_adm[];
+                                                   const int32_t* __restrict__ adm_slot, AdmIndex ix,
+                                                   uint32_t n_adm, SplitRows rows, const uint32_t* __restrict__ fdict) {
     wave_prio(rows.prio);
-    if (adm_in_lds) adm_stage(sh_adm, adm, n_adm);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = b.n;
     if (i >= n) return;
@@ -243,7 +240,7 @@ __global__ __launch_bounds__(256) void k_fast_prep(DevBatch b, const uint8_t* __
     } else {
         uint32_t from_be[8];
         src.from_words(from_be);
-        idx = adm_in_lds ? admitted_find(sh_adm, n_adm, adm_steps, from_be) : admitted_find(adm, n_adm, adm_steps, from_be);
+        idx = n_adm ? adm_index_find(ix, from_be) : -1;
         int32_t sl = idx >= 0 ? adm_slot[idx] : -1;
         if (idx < 0 && fdict) {
             // an authenticated From outside the admitted set with a known key:
@@ -1251,9 +1248,8 @@ static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest
     // lanes of the K-per-lane kernels, a multiple of 64 (k_fast_final's bitmap words)
     const uint32_t T = ((n + (uint32_t)K - 1) / (uint32_t)K + 63u) & ~63u;
     const uint32_t tb = (T + 255) / 256, nb = (n + 255) / 256;
-    const size_t adm_lds = adm_lds_bytes(ctx->n_adm);
-    k_fast_prep<<<nb, 256, adm_lds, s>>>(b, d_digest, f->state, f->adm_slot, ctx->d_adm, ctx->n_adm, ctx->adm_steps,
-                                         rows, adm_lds > 0, f->fcap ? f->fdict : nullptr);
+    k_fast_prep<<<nb, 256, 0, s>>>(b, d_digest, f->state, f->adm_slot, hd_adm_index(ctx), ctx->n_adm, rows,
+                                   f->fcap ? f->fdict : nullptr);
     k_fast_sinv<K><<<tb, 256, 0, s>>>(n, T, rows);
     hipEvent_t* pe = fb_prof_pair(f->ev_sums, f->n_sums, f->prof);
     if (pe) (void)hipEventRecord(pe[0], s);

@@ -8,6 +8,7 @@
 
 #include "../../include/hd_verify.h"
 #include "hd_fixedbase.h"
+#include "hd_verify_msg.h"
 
 struct DevBatch {
     uint32_t n;
@@ -52,6 +53,10 @@ struct hd_ctx {
     size_t cap_sig_caller = 0;
     uint32_t n_sig_caller = 0;
     int adm_steps = 0;
+    // hashed index of d_adm (hd_verify_msg.h AdmIndex): adm_ix_mask + 1 slots
+    uint32_t* d_adm_ix = nullptr;
+    size_t cap_adm_ix = 0;
+    uint32_t adm_ix_mask = 0;
     DevBuf bufs[BUF__COUNT];
     TallyWork* tally = nullptr;
     FbWork* fb = nullptr;
@@ -78,6 +83,8 @@ int hd_fb_quiesce(hd_ctx* ctx);   // the known-key path's calls (hd_fastverify.h
 
 int hd_ctx_fail(hd_ctx* ctx, hipError_t e, const char* what);
 int hd_dev_grow(hd_ctx* ctx, void** p, size_t* cap, size_t need);
+// the admitted table's hashed index (valid lookups need ctx->n_adm > 0)
+inline hd::AdmIndex hd_adm_index(const hd_ctx* ctx) { return hd::AdmIndex{ctx->d_adm, ctx->d_adm_ix, ctx->adm_ix_mask}; }
 int hd_upload_batch(hd_ctx* ctx, const hd_batch* hb, hd_batch* db);
 int hd_verify_uploaded(hd_ctx* ctx, const hd_batch* db, uint8_t* verdict, uint8_t* recovered32, uint32_t* valid_bitmap);
 void hd_tally_release(hd_ctx* ctx);

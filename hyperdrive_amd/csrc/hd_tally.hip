@@ -80,10 +80,9 @@ struct CTab {   // (G slot, type, value)
     uint32_t* claim;
     uint32_t* n;
 };
-struct TallyCtr {   // 64 B, zero between calls (the last block of k_tally_firsts resets it)
+struct TallyCtr {   // 64 B, zero between calls (k_tally_emit resets it)
     uint32_t n_rounds;   // rounds numbered so far (k_tally_rounds)
-    uint32_t done;       // k_tally_firsts' finished blocks
-    uint32_t pad[14];
+    uint32_t pad[15];
 };
 
 
@@ -282,11 +281,8 @@ __global__ void k_tally_rounds(DevBatch b, const uint32_t* __restrict__ cand, ui
 #define HD_REF_HASHED 0x80000000u
 __global__ void k_tally_logs(DevBatch b, const uint32_t* __restrict__ cand, uint32_t m,
                              const uint32_t* __restrict__ gslot, const uint32_t* __restrict__ gid,
-                             const uint32_t* __restrict__ adm, uint32_t S, int adm_steps, uint32_t* __restrict__ Dd,
-                             uint32_t nd, uint32_t* __restrict__ D, uint32_t mask, uint32_t* __restrict__ ref,
-                             int adm_in_lds) {
-    extern __shared__ uint32_t sh_adm[];
-    if (adm_in_lds) adm_stage(sh_adm, adm, S);
+                             AdmIndex ix, uint32_t S, uint32_t* __restrict__ Dd, uint32_t nd,
+                             uint32_t* __restrict__ D, uint32_t mask, uint32_t* __restrict__ ref) {
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < m; q += stride) {
         const uint32_t g = gslot[q];
@@ -299,7 +295,7 @@ __global__ void k_tally_logs(DevBatch b, const uint32_t* __restrict__ cand, uint
         if (rid < nd) {
             uint32_t from_be[8];
             load_row32_be(from_be, b.from32, i);
-            signer = adm_in_lds ? admitted_find(sh_adm, S, adm_steps, from_be) : admitted_find(adm, S, adm_steps, from_be);
+            signer = adm_index_find(ix, from_be);
         }
         if (signer >= 0) {
             const uint32_t cell = (rid * 2u + (t == T_PRECOMMIT ? 1u : 0u)) * S + (uint32_t)signer;
@@ -427,33 +423,39 @@ __global__ void k_tally_values(DevBatch b, const uint32_t* __restrict__ cand, ui
 // first item is the one its slot's claim word holds; the per-item flags
 // "first of its round" / "first of its (round, type, value)" are bitmaps
 // Bg / Bc, one bit per item, and an item's output position is the number of
-// flags before it.  Both passes below give each block HD_TALLY_IPB
-// consecutive items (HD_TALLY_IPB / 32 bitmap words it alone writes):
+// flags before it.  Both passes below give each block IPB consecutive items
+// (IPB / 32 bitmap words it alone writes; IPB = 256 .. 2048, the largest
+// that still gives about four blocks per CU, tally_ipb()):
 //   k_tally_firsts  the block's flags as whole words (two ballots per
 //                   wavefront: no atomics, nothing to clear), their popcount
-//                   prefix within the block, and the block's totals; the
-//                   last block to finish (a ticket counter) scans the totals
-//                   into block offsets and writes the group counts into the
-//                   stage header;
-//   k_tally_emit    every first item writes its group's row at its position
-//                   (rows past the staged capacity go to the overflow
-//                   columns), then resets its table slots, so the tables are
-//                   clean for the next call without a clearing pass.
-#define HD_TALLY_IPB 2048u   // items per block (8 per thread)
+//                   prefix within the block, and the block's totals;
+//   k_tally_emit    each block first sums the totals of the blocks before it
+//                   (its offsets; the last block also writes the group counts
+//                   into the stage header), then every first item writes its
+//                   group's row at its position (rows past the staged
+//                   capacity go to the overflow columns) and resets its table
+//                   slots, so the tables are clean for the next call without
+//                   a clearing pass.
+// The offsets are summed by every emit block rather than scanned once by the
+// last block of k_tally_firsts: that scan needed a ticket counter, and the
+// device-scope release each block made before taking its ticket writes back
+// the block's XCD L2 -- dirty with the verify kernels' rows when the tally
+// runs beside them (39 us for 501 blocks of a 128k batch, against ~5 us
+// for the sums, nb^2 / 2 L2-resident words).
+#define HD_TALLY_IPB_MAX 2048u   // items per block (8 per thread)
 
+template <uint32_t IPB>
 __global__ __launch_bounds__(256) void k_tally_firsts(uint32_t m, const uint32_t* __restrict__ gslot,
                                                       const uint32_t* __restrict__ cslot, const uint32_t* G_claim,
                                                       const uint32_t* C_claim, uint32_t* __restrict__ Bg,
                                                       uint32_t* __restrict__ Bc, uint32_t* __restrict__ pre_g,
-                                                      uint32_t* __restrict__ pre_c, uint32_t* blk, TallyCtr* ctr,
-                                                      uint32_t* stage_hdr) {
-    constexpr uint32_t W = HD_TALLY_IPB / 32;   // words per block
+                                                      uint32_t* __restrict__ pre_c, uint32_t* __restrict__ blk) {
+    constexpr uint32_t W = IPB / 32;   // words per block (<= 64: one wavefront scans them)
     __shared__ uint32_t wg[W], wc[W];
-    __shared__ bool last;
     const uint32_t nb = gridDim.x;
-    const uint32_t lo = blockIdx.x * HD_TALLY_IPB;
+    const uint32_t lo = blockIdx.x * IPB;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (uint32_t k = 0; k < HD_TALLY_IPB / 256; k++) {
+    for (uint32_t k = 0; k < IPB / 256; k++) {
         const uint32_t q = lo + k * 256 + threadIdx.x;
         bool fg = false, fc = false;
         if (q < m) {
@@ -474,7 +476,7 @@ __global__ __launch_bounds__(256) void k_tally_firsts(uint32_t m, const uint32_t
         }
     }
     __syncthreads();
-    if (threadIdx.x < W) {   // one lane per word (W == 64: wavefront 0)
+    if (threadIdx.x < W) {   // one lane per word (wavefront 0)
         const uint32_t t = threadIdx.x, gw = wg[t], cw = wc[t];
         uint32_t ig = (uint32_t)__popc(gw), ic = (uint32_t)__popc(cw);
         for (int d = 1; d < 64; d <<= 1) {   // inclusive scan across the wavefront
@@ -493,39 +495,6 @@ __global__ __launch_bounds__(256) void k_tally_firsts(uint32_t m, const uint32_t
             blk[blockIdx.x] = ig;
             blk[nb + blockIdx.x] = ic;
         }
-    }
-    // the last block to finish scans the block totals
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(&ctr->done, 1u) == nb - 1;
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    typedef hipcub::BlockScan<uint32_t, 256> Scan;
-    __shared__ typename Scan::TempStorage ts;
-    __shared__ uint32_t carry[2];
-    for (int j = 0; j < 2; j++) {
-        if (threadIdx.x == 0) carry[j] = 0;
-        __syncthreads();
-        const uint32_t* tot = blk + (size_t)j * nb;
-        uint32_t* off = blk + (size_t)(2 + j) * nb;
-        for (uint32_t base = 0; base < nb; base += 256) {
-            const uint32_t k = base + threadIdx.x;
-            // written by other blocks of this launch: read through L2
-            const uint32_t v = k < nb ? __hip_atomic_load(tot + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-            uint32_t ex, agg;
-            Scan(ts).ExclusiveSum(v, ex, agg);
-            if (k < nb) off[k] = carry[j] + ex;
-            __syncthreads();
-            if (threadIdx.x == 0) carry[j] += agg;
-            __syncthreads();
-        }
-    }
-    if (threadIdx.x == 0) {
-        stage_hdr[0] = carry[0];   // rounds (hr rows)
-        stage_hdr[1] = carry[1];   // (round, type, value) groups
-        ctr->n_rounds = 0;
-        ctr->done = 0;
     }
 }
 
@@ -552,6 +521,7 @@ HD_HOSTONLY TallyCols tally_cols(char* base, uint32_t h, uint32_t c) {
     return x;
 }
 
+template <uint32_t IPB>
 __global__ __launch_bounds__(256) void k_tally_emit(DevBatch b, const uint32_t* __restrict__ cand, uint32_t m,
                                                     const uint32_t* __restrict__ gidx, const uint32_t* __restrict__ gslot,
                                                     const uint32_t* __restrict__ cslot, const uint32_t* __restrict__ ref,
@@ -559,11 +529,35 @@ __global__ __launch_bounds__(256) void k_tally_emit(DevBatch b, const uint32_t* 
                                                     const uint32_t* __restrict__ Bg, const uint32_t* __restrict__ Bc,
                                                     const uint32_t* __restrict__ pre_g, const uint32_t* __restrict__ pre_c,
                                                     const uint32_t* __restrict__ blk, TallyCols st, uint32_t H,
-                                                    uint32_t Cg, TallyCols ov) {
+                                                    uint32_t Cg, TallyCols ov, TallyCtr* ctr, uint32_t* stage_hdr) {
     const uint32_t nb = gridDim.x;
-    const uint32_t og = blk[2 * nb + blockIdx.x], oc = blk[3 * nb + blockIdx.x];
-    const uint32_t lo = blockIdx.x * HD_TALLY_IPB;
-    for (uint32_t k = 0; k < HD_TALLY_IPB / 256; k++) {
+    // this block's offsets: the totals of the blocks before it
+    __shared__ uint32_t part[2][4];
+    uint32_t sg = 0, sc = 0;
+    for (uint32_t k = threadIdx.x; k < blockIdx.x; k += 256) {
+        sg += blk[k];
+        sc += blk[nb + k];
+    }
+    for (int d = 32; d > 0; d >>= 1) {
+        sg += (uint32_t)__shfl_xor((int)sg, d, 64);
+        sc += (uint32_t)__shfl_xor((int)sc, d, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        part[0][threadIdx.x >> 6] = sg;
+        part[1][threadIdx.x >> 6] = sc;
+    }
+    __syncthreads();
+    const uint32_t og = part[0][0] + part[0][1] + part[0][2] + part[0][3];
+    const uint32_t oc = part[1][0] + part[1][1] + part[1][2] + part[1][3];
+    if (threadIdx.x == 0) {
+        if (blockIdx.x == nb - 1) {
+            stage_hdr[0] = og + blk[nb - 1];        // rounds (hr rows)
+            stage_hdr[1] = oc + blk[2 * nb - 1];    // (round, type, value) groups
+        }
+        if (blockIdx.x == 0) ctr->n_rounds = 0;     // k_tally_rounds' numbering, for the next call
+    }
+    const uint32_t lo = blockIdx.x * IPB;
+    for (uint32_t k = 0; k < IPB / 256; k++) {
         const uint32_t q = lo + k * 256 + threadIdx.x;
         if (q >= m) break;
         const uint32_t g = gslot[q];
@@ -610,7 +604,7 @@ __global__ void k_tally_check_clean(uint32_t cap, const uint32_t* __restrict__ t
         for (int k = 3; k < 7; k++) ok &= tabs[(size_t)k * cap + s] == 0u;
         if (!ok && atomicAdd(bad, 1u) == 0) printf("hd tally check: slot %u not clean after the emit\n", s);
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0 && (ctr->n_rounds | ctr->done)) atomicAdd(bad, 1u);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && ctr->n_rounds) atomicAdd(bad, 1u);
 }
 
 // ------------------------------------------------- consistency check (debug)
@@ -807,12 +801,9 @@ __device__ __forceinline__ bool round_listed(const RoundList& l, int64_t h, int6
 // (possible when the set changed since verification): a row carries the
 // admitted index, not the From, so such a candidate cannot be routed
 __global__ __launch_bounds__(256) void k_route_count(DevBatch b, const uint32_t* __restrict__ bitmap, uint32_t nparts,
-                                                     const uint32_t* __restrict__ adm, uint32_t n_adm, int adm_steps,
-                                                     int adm_in_lds, uint32_t* __restrict__ cnt,
+                                                     AdmIndex ix, uint32_t n_adm, uint32_t* __restrict__ cnt,
                                                      uint32_t* __restrict__ outside, RoundList rl) {
-    extern __shared__ uint32_t sh_adm[];
     __shared__ uint32_t c[HD_ROUTE_MAX_PARTS];
-    if (adm_in_lds) adm_stage(sh_adm, adm, n_adm);
     if (threadIdx.x < nparts) c[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -820,8 +811,7 @@ __global__ __launch_bounds__(256) void k_route_count(DevBatch b, const uint32_t*
         atomicAdd(&c[part_of(hash_hr(b.height[i], b.round[i]), nparts)], 1u);
         uint32_t from_be[8];
         load_row32_be(from_be, b.from32, i);
-        const int32_t sg = adm_in_lds ? admitted_find(sh_adm, n_adm, adm_steps, from_be)
-                                      : admitted_find(adm, n_adm, adm_steps, from_be);
+        const int32_t sg = n_adm ? adm_index_find(ix, from_be) : -1;
         if (sg < 0) atomicAdd(outside, 1u);
     }
     __syncthreads();
@@ -833,11 +823,9 @@ __global__ __launch_bounds__(256) void k_route_count(DevBatch b, const uint32_t*
 // wavefront ballots, so each owner's rows keep the batch order
 __global__ __launch_bounds__(256) void k_route_write(DevBatch b, const uint32_t* __restrict__ bitmap, uint32_t nparts,
                                                      uint32_t base, const uint32_t* __restrict__ off,
-                                                     const uint32_t* __restrict__ adm, uint32_t n_adm, int adm_steps,
-                                                     int adm_in_lds, RouteRow* __restrict__ rows, RoundList rl) {
-    extern __shared__ uint32_t sh_adm[];
+                                                     AdmIndex ix, uint32_t n_adm, RouteRow* __restrict__ rows,
+                                                     RoundList rl) {
     __shared__ uint32_t wcnt[4][HD_ROUTE_MAX_PARTS];
-    if (adm_in_lds) adm_stage(sh_adm, adm, n_adm);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const bool c = i < b.n && candidate(b, nullptr, bitmap, i, Part{0, 1}) && round_listed(rl, b.height[i], b.round[i]);
@@ -854,8 +842,7 @@ __global__ __launch_bounds__(256) void k_route_write(DevBatch b, const uint32_t*
     for (uint32_t v = 0; v < w; v++) pos += wcnt[v][o];
     uint32_t from_be[8];
     load_row32_be(from_be, b.from32, i);
-    const int32_t sg = adm_in_lds ? admitted_find(sh_adm, n_adm, adm_steps, from_be)
-                                  : admitted_find(adm, n_adm, adm_steps, from_be);
+    const int32_t sg = n_adm ? adm_index_find(ix, from_be) : -1;
     RouteRow row;
     row.h = b.height[i];
     row.r = b.round[i];
@@ -930,6 +917,14 @@ void hd_tally_release(hd_ctx* ctx) {
 }
 
 static inline uint32_t nblk(uint32_t n) { return (n + 255) / 256; }
+// items per block of the order passes: the largest power of two in 256 ..
+// HD_TALLY_IPB_MAX that leaves about four blocks per CU (a 128k-message batch
+// at 2048 ran 63 blocks, latency-bound on a quarter of the chip)
+static inline uint32_t tally_ipb(uint32_t m, uint32_t n_cu) {
+    uint32_t ipb = HD_TALLY_IPB_MAX;
+    while (ipb > 256u && (m + ipb - 1) / ipb < 4u * n_cu) ipb >>= 1;
+    return ipb;
+}
 
 // dense log cells allowed (words): rounds numbered past nd = this / 2S take
 // the hashed table (e.g. a batch of a million single-message rounds)
@@ -1100,8 +1095,9 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     uint32_t cap = 1024;
     while (cap < 2 * m) cap <<= 1;
     const uint32_t mask = cap - 1;
-    const uint32_t nbo = (m + HD_TALLY_IPB - 1) / HD_TALLY_IPB;   // blocks of the order passes
-    const size_t nw = (size_t)nbo * (HD_TALLY_IPB / 32);
+    const uint32_t ipb = tally_ipb(m, (uint32_t)ctx->n_cu);
+    const uint32_t nbo = (m + ipb - 1) / ipb;   // blocks of the order passes
+    const size_t nw = (size_t)nbo * (ipb / 32);
     // one allocation for the tables: the claim words (G, C, D: empty), the
     // counters (G x 3, C: zero), the round numbers (gid); then the call
     // counters (TallyCtr)
@@ -1110,8 +1106,8 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     uint32_t* gslot = (uint32_t*)tbuf(ctx, T_GSLOT, 4 * (size_t)m, &rc);
     uint32_t* ref = (uint32_t*)tbuf(ctx, T_DSLOT, 4 * (size_t)m, &rc);
     uint32_t* cslot = (uint32_t*)tbuf(ctx, T_CSLOT, 4 * (size_t)m, &rc);
-    // Bg | Bc | pre_g | pre_c (nw words each) | block totals and offsets (4 nbo)
-    uint32_t* bits = (uint32_t*)tbuf(ctx, T_BITS, 4 * (4 * nw + 4 * (size_t)nbo), &rc);
+    // Bg | Bc | pre_g | pre_c (nw words each) | block totals (2 nbo)
+    uint32_t* bits = (uint32_t*)tbuf(ctx, T_BITS, 4 * (4 * nw + 2 * (size_t)nbo), &rc);
     // dense log cells (nd rounds x 2 x S) for admitted signatories, the hashed
     // D table for the rest: room for every item's round up to HD_TALLY_DENSE_MAX words
     const uint32_t S = ctx->n_adm;
@@ -1134,9 +1130,7 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     tw->dirty = true;   // until every launch below is queued
     k_tally_rounds<<<grid, 256, 0, s>>>(b, cand, m, d_verdict, d_bitmap, part, G, mask, gslot, d_dup, ctr, Dd, 2 * S,
                                         nd);
-    const size_t adm_lds = nd ? adm_lds_bytes(S) : 0;
-    k_tally_logs<<<grid, 256, adm_lds, s>>>(b, cand, m, gslot, G.gid, ctx->d_adm, S, ctx->adm_steps, Dd, nd, d, mask,
-                                            ref, adm_lds > 0);
+    k_tally_logs<<<grid, 256, 0, s>>>(b, cand, m, gslot, G.gid, hd_adm_index(ctx), S, Dd, nd, d, mask, ref);
     k_tally_values<<<grid, 256, 0, s>>>(b, cand, m, Dd, S, d, G, C, mask, gslot, ref, cslot, d_dup);
     if (dup_global && gidx) k_dup_scatter<<<nblk(n), 256, 0, s>>>(n, d_dup, gidx, dup_global);
     TCHK(hipGetLastError(), "tally kernels");
@@ -1150,10 +1144,19 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
     char* ovf = (char*)tbuf(ctx, T_NSEL, 57 * (size_t)m + 64, &rc);
     if (rc) return rc;
     const TallyCols sc = tally_cols(st + rows_off, H, Cg), oc = tally_cols(ovf, m, m);
-    k_tally_firsts<<<nbo, 256, 0, s>>>(m, gslot, cslot, G.claim, C.claim, Bg, Bc, pre_g, pre_c, blk, ctr,
-                                       (uint32_t*)st);
-    k_tally_emit<<<nbo, 256, 0, s>>>(b, cand, m, gidx, gslot, cslot, ref, G, C, d, Bg, Bc, pre_g, pre_c, blk, sc, H,
-                                     Cg, oc);
+    switch (ipb) {
+#define HD_TALLY_ORDER(IPB)                                                                                         \
+    case IPB:                                                                                                       \
+        k_tally_firsts<IPB><<<nbo, 256, 0, s>>>(m, gslot, cslot, G.claim, C.claim, Bg, Bc, pre_g, pre_c, blk);       \
+        k_tally_emit<IPB><<<nbo, 256, 0, s>>>(b, cand, m, gidx, gslot, cslot, ref, G, C, d, Bg, Bc, pre_g, pre_c, blk, \
+                                              sc, H, Cg, oc, ctr, (uint32_t*)st);                                   \
+        break;
+        HD_TALLY_ORDER(256u)
+        HD_TALLY_ORDER(512u)
+        HD_TALLY_ORDER(1024u)
+        HD_TALLY_ORDER(2048u)
+#undef HD_TALLY_ORDER
+    }
     TCHK(hipGetLastError(), "tally order kernels");
     tw->dirty = false;
     if (check) {
@@ -1391,10 +1394,9 @@ static int route_candidates(hd_ctx* ctx, const hd_batch* dshard, const uint32_t*
     off = cnt + cells;
     starts = off + cells;
     tmp = (void*)(((uintptr_t)(starts + nparts + 2) + 63) & ~(uintptr_t)63);
-    const size_t adm_lds = adm_lds_bytes(ctx->n_adm);
     TCHK(hipMemsetAsync(starts + nparts + 1, 0, 4, s), "route outside count");
-    k_route_count<<<nb, 256, adm_lds, s>>>(b, d_valid_bitmap, nparts, ctx->d_adm, ctx->n_adm, ctx->adm_steps,
-                                           adm_lds > 0, cnt, starts + nparts + 1, rl);
+    k_route_count<<<nb, 256, 0, s>>>(b, d_valid_bitmap, nparts, hd_adm_index(ctx), ctx->n_adm, cnt,
+                                     starts + nparts + 1, rl);
     TCHK(hipGetLastError(), "k_route_count");
     TCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, (int)cells, s), "route scan");
     k_route_starts<<<1, 64, 0, s>>>(off, cnt, nparts, nb, starts);
@@ -1410,8 +1412,8 @@ static int route_candidates(hd_ctx* ctx, const hd_batch* dshard, const uint32_t*
     }
     for (uint32_t o = 0; o < nparts; o++) counts[o] = st[o + 1] - st[o];
     if (st[nparts] > cap_rows) return HD_ECAP;
-    k_route_write<<<nb, 256, adm_lds, s>>>(b, d_valid_bitmap, nparts, base_index, off, ctx->d_adm, ctx->n_adm,
-                                           ctx->adm_steps, adm_lds > 0, reinterpret_cast<RouteRow*>(d_rows), rl);
+    k_route_write<<<nb, 256, 0, s>>>(b, d_valid_bitmap, nparts, base_index, off, hd_adm_index(ctx), ctx->n_adm,
+                                     reinterpret_cast<RouteRow*>(d_rows), rl);
     TCHK(hipGetLastError(), "k_route_write");
     return hd_ctx_note_stream(ctx, s);
 }

@@ -262,7 +262,7 @@ int hd_ctx_destroy(hd_ctx* ctx) {
     }
     ctx->caller_ev.clear();
     if (ctx->ev_slow) (void)hipEventDestroy(ctx->ev_slow);
-    void* ptrs[] = {ctx->d_gtab, ctx->d_adm, ctx->d_adm_perm, ctx->d_sig_caller};
+    void* ptrs[] = {ctx->d_gtab, ctx->d_adm, ctx->d_adm_perm, ctx->d_sig_caller, ctx->d_adm_ix};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& b : ctx->bufs)
@@ -333,6 +333,9 @@ int hd_set_signatories(hd_ctx* ctx, const uint8_t* sigs32, uint32_t n) {
         perm.push_back((int32_t)order[k]);
     }
     uint32_t m = (uint32_t)perm.size();
+    const uint32_t ix_slots = adm_index_slots(m);
+    std::vector<uint32_t> ix(ix_slots);
+    adm_index_build(words.data(), m, ix.data(), ix_slots);
     size_t cap_a = ctx->cap_adm, cap_p = ctx->cap_adm_perm;
     int rc = hd_dev_grow(ctx, (void**)&ctx->d_adm, &cap_a, 32 * (size_t)std::max(m, 1u));
     if (rc) return rc;
@@ -340,6 +343,8 @@ int hd_set_signatories(hd_ctx* ctx, const uint8_t* sigs32, uint32_t n) {
     rc = hd_dev_grow(ctx, (void**)&ctx->d_adm_perm, &cap_p, 4 * (size_t)std::max(m, 1u));
     if (rc) return rc;
     ctx->cap_adm_perm = cap_p;
+    rc = hd_dev_grow(ctx, (void**)&ctx->d_adm_ix, &ctx->cap_adm_ix, 4 * (size_t)ix_slots);
+    if (rc) return rc;
     rc = hd_dev_grow(ctx, (void**)&ctx->d_sig_caller, &ctx->cap_sig_caller, 32 * (size_t)std::max(n, 1u));
     if (rc) return rc;
     hipError_t e = hipSuccess;
@@ -349,10 +354,13 @@ int hd_set_signatories(hd_ctx* ctx, const uint8_t* sigs32, uint32_t n) {
             e = hipMemcpyAsync(ctx->d_adm_perm, perm.data(), 4 * (size_t)m, hipMemcpyHostToDevice, ctx->stream);
         if (e == hipSuccess)
             e = hipMemcpyAsync(ctx->d_sig_caller, sigs32, 32 * (size_t)n, hipMemcpyHostToDevice, ctx->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(ctx->d_adm_ix, ix.data(), 4 * (size_t)ix_slots, hipMemcpyHostToDevice, ctx->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     }
     if (e != hipSuccess) return hd_ctx_fail(ctx, e, "set_signatories upload");
     ctx->n_adm = m;
+    ctx->adm_ix_mask = ix_slots - 1;
     ctx->n_sig_caller = n;
     int steps = 0;
     while ((1u << steps) < m) steps++;

@@ -57,18 +57,56 @@ HD int32_t admitted_find(AdmTab adm, uint32_t n, int steps, const uint32_t key[8
     return cmp_be256(e, key) == 0 ? (int32_t)lo : -1;
 }
 
-// The admitted table is searched by every message of a batch.  Kernels stage
-// it in LDS (dynamic shared memory, one copy per block) when it holds at most
-// HD_ADM_LDS_MAX entries, so the binary search's dependent loads are LDS reads
-// instead of L2 round trips.
-#define HD_ADM_LDS_MAX 1024u
-#if defined(__HIPCC__)
-__device__ __forceinline__ void adm_stage(uint32_t* sh, const uint32_t* __restrict__ adm, uint32_t n) {
-    for (uint32_t k = threadIdx.x; k < 8 * n; k += blockDim.x) sh[k] = adm[k];
-    __syncthreads();
+// Hashed index of the admitted table (hd_set_signatories builds it), searched
+// by every message of the batch-wide kernels (k_fast_prep, the tally and
+// route passes): an open-addressing array of sorted indices at load factor
+// <= 1/4, keyed by the first four words of the From.  A lookup is one or two
+// dependent loads of the slot array (L2-resident, 4 B per slot) and one
+// 32-byte compare, where the binary search takes log2(n) dependent 32-byte
+// steps and wanted the table staged in LDS by every block.  Same answer as
+// admitted_find: the sorted index of the entry equal to key, or -1.
+struct AdmIndex {
+    const uint32_t* adm;    // the sorted table (8 BE words per entry)
+    const uint32_t* slot;   // sorted index per slot, 0xFFFFFFFF empty
+    uint32_t mask;          // slots - 1
+};
+HD uint32_t adm_hash(const uint32_t key[8]) {
+    uint64_t x = ((uint64_t)key[0] << 32 | key[1]) ^ (((uint64_t)key[2] << 32 | key[3]) * 0x9E3779B97F4A7C15ull);
+    x ^= x >> 31;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 29;
+    return (uint32_t)x;
 }
-#endif
-HD_HOSTONLY size_t adm_lds_bytes(uint32_t n) { return n <= HD_ADM_LDS_MAX ? 32 * (size_t)n : 0; }
+template <typename AdmTab>
+HD int32_t adm_index_find(const AdmTab adm, const uint32_t* slot, uint32_t mask, const uint32_t key[8]) {
+    uint32_t s = adm_hash(key) & mask;
+    while (true) {
+        const uint32_t idx = slot[s];
+        if (idx == 0xFFFFFFFFu) return -1;
+        bool eq = true;
+        HD_UNROLL for (int w = 0; w < 8; w++) eq &= adm[idx * 8 + w] == key[w];
+        if (eq) return (int32_t)idx;
+        s = (s + 1) & mask;
+    }
+}
+HD int32_t adm_index_find(const AdmIndex& ix, const uint32_t key[8]) {
+    return adm_index_find(ix.adm, ix.slot, ix.mask, key);
+}
+// host: the slot array for n sorted entries (words: 8 BE words each); slots =
+// the smallest power of two >= max(16, 4n)
+HD_HOSTONLY uint32_t adm_index_slots(uint32_t n) {
+    uint32_t c = 16;
+    while (c < 4 * n) c <<= 1;
+    return c;
+}
+HD_HOSTONLY void adm_index_build(const uint32_t* words, uint32_t n, uint32_t* slot, uint32_t slots) {
+    for (uint32_t s = 0; s < slots; s++) slot[s] = 0xFFFFFFFFu;
+    for (uint32_t k = 0; k < n; k++) {
+        uint32_t s = adm_hash(words + 8 * (size_t)k) & (slots - 1);
+        while (slot[s] != 0xFFFFFFFFu) s = (s + 1) & (slots - 1);
+        slot[s] = k;
+    }
+}
 
 // Full verdict for one message.  Src supplies the message fields on demand
 // (type(), h(), r(), vr(), value(w), from(w), sig_r(w), sig_s(w), sig_v(),

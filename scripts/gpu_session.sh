@@ -112,5 +112,7 @@ for step in "$@"; do
     c3async) HD_BENCH_ASYNC_TALLY=1 run c3host_async 300 python -u scripts/c3_host_probe.py 40 ;;
     c3matrix) run c3_sync 300 python -u scripts/c3_host_probe.py 40 && HD_BENCH_NBUF=8 run c3_sync_nb8 300 python -u scripts/c3_host_probe.py 40 && C3_TS_PRIO=-1 run c3_sync_hi 300 python -u scripts/c3_host_probe.py 40 && HD_BENCH_ASYNC_TALLY=1 run c3_async 300 python -u scripts/c3_host_probe.py 40 && HD_BENCH_ASYNC_TALLY=1 C3_TS_PRIO=-1 run c3_async_hi 300 python -u scripts/c3_host_probe.py 40 ;;
     c3trace) run c3trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c3trace -o run -- python3 scripts/c3_host_probe.py 20 ;;
+    tally_trace3) run tally_trace3 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/tally_trace3 -o run -- python3 scripts/tally_probe.py C3 40 ;;
+    c3sync) run c3_sync 300 python -u scripts/c3_host_probe.py 40 ;;
   esac
 done

@@ -620,3 +620,22 @@ extern "C" int hdh_fb_is_infinity(const uint8_t* rx, const uint8_t* ry, const ui
     le_in(s.v, s32);
     return fb_is_infinity<HD_FB_WG>(m, s, R, fb_gt.data()) ? 1 : 0;
 }
+
+// the admitted table's hashed index (hd_verify_msg.h AdmIndex) against the
+// binary search, for n sorted 32-byte entries and q query keys: out[k] = the
+// index lookup, out[q + k] = the binary search
+extern "C" void hdh_adm_lookup(const uint8_t* sorted32, uint32_t n, const uint8_t* keys32, uint32_t q, int32_t* out) {
+    std::vector<uint32_t> words(8 * (size_t)n);
+    for (size_t k = 0; k < words.size(); k++) words[k] = hd::load_be32(sorted32 + 4 * k);
+    const uint32_t slots = hd::adm_index_slots(n);
+    std::vector<uint32_t> ix(slots);
+    hd::adm_index_build(words.data(), n, ix.data(), slots);
+    int steps = 0;
+    while ((1u << steps) < n) steps++;
+    for (uint32_t k = 0; k < q; k++) {
+        uint32_t key[8];
+        for (int w = 0; w < 8; w++) key[w] = hd::load_be32(keys32 + 32 * (size_t)k + 4 * w);
+        out[k] = n ? hd::adm_index_find(words.data(), ix.data(), slots - 1, key) : -1;
+        out[q + k] = hd::admitted_find(words.data(), n, steps, key);
+    }
+}

@@ -430,3 +430,29 @@ def test_infinity_from_the_g_table(fb, oracle):
         if m and R[0] < O.N:        # the reference's recovery of (m, r = x_R, s, v = parity): infinity
             v, _ = O.recover(b32(m), b32(R[0]) + b32(s) + bytes([R[1] & 1]))
             assert v == O.INFINITY
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 7, 100, 1000, 4096])
+def test_admitted_index_equals_binary_search(fb, n):
+    """The hashed admitted index (hd_verify_msg.h adm_index_find, used by
+    k_fast_prep and the tally / route passes) returns what the binary search
+    over the sorted table returns, for every member, for non-members, and for
+    non-members sharing a member's first four words (the hashed prefix)."""
+    fb.hdh_adm_lookup.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                  ctypes.c_void_p]
+    rng = np.random.default_rng(n + 5)
+    # rows sorted lexicographically (uint8: byte order), duplicates dropped
+    table = np.unique(rng.integers(0, 256, (n, 32), dtype=np.uint8), axis=0)
+    queries = [table.copy()] if n else []
+    queries.append(rng.integers(0, 256, (257, 32), dtype=np.uint8))
+    if n:
+        near = table.copy()
+        near[:, 31] ^= 1                  # same hashed prefix, different tail
+        queries.append(near)
+    q = np.ascontiguousarray(np.concatenate(queries))
+    out = np.zeros(2 * len(q), np.int32)
+    t = np.ascontiguousarray(table)
+    fb.hdh_adm_lookup(t.ctypes.data, len(t), q.ctypes.data, len(q), out.ctypes.data)
+    assert out[:len(q)].tolist() == out[len(q):].tolist()
+    if n:
+        assert out[:len(t)].tolist() == list(range(len(t)))

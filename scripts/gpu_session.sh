@@ -114,5 +114,6 @@ for step in "$@"; do
     c3trace) run c3trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c3trace -o run -- python3 scripts/c3_host_probe.py 20 ;;
     tally_trace3) run tally_trace3 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/tally_trace3 -o run -- python3 scripts/tally_probe.py C3 40 ;;
     c3sync) run c3_sync 300 python -u scripts/c3_host_probe.py 40 ;;
+    abhead) HD_LIB=hyperdrive_amd/_lib/var/libhd_r5c.so run bench_old_a 300 python bench.py --no-cpu --no-aux && run bench_new_a 300 python bench.py --no-cpu --no-aux && HD_LIB=hyperdrive_amd/_lib/var/libhd_r5c.so run bench_old_b 300 python bench.py --no-cpu --no-aux && run bench_new_b 300 python bench.py --no-cpu --no-aux ;;
   esac
 done

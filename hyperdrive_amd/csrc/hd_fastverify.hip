@@ -127,9 +127,19 @@ struct FbWork {
     uint32_t* fdict = nullptr;
     uint32_t* fnext = nullptr;
     uint32_t fbase = 0, fcap = 0, fres = 0;
-    uint32_t* fpend_host = nullptr;
+    uint32_t* fpend_host = nullptr;   // [0] claim count, [1] the fmiss flag (SlowCtl)
     uint32_t* fpend_dev = nullptr;
     uint32_t fseen = 0;
+    // Slot eviction (fb_evict): fhit[0, 64) counts each foreign slot's
+    // known-key checks, fhit[64, 64 + HD_FD_BUCKETS) the recoveries of each
+    // slotless dictionary entry (fbhit), fkey the slotless entries' keys.
+    // fwait / fcalls: calls between checks while misses are flagged
+    // (doubling, up to HD_FD_EVICT_WAIT_MAX, while checks swap nothing).
+    uint32_t* fhit = nullptr;
+    ge* fkey = nullptr;
+    uint32_t fwait = 1, fcalls = 0;
+    bool fforce = false;   // build the LEARNED slots at this call's end (an eviction re-keyed one)
+    uint32_t evictions = 0;
 };
 
 namespace {
@@ -226,7 +236,8 @@ HD uint32_t fb_ref(int d, int w) {
 __global__ __launch_bounds__(256) void k_fast_prep(DevBatch b, const uint8_t* __restrict__ digest_in,
                                                    const uint32_t* __restrict__ state,
                                                    const int32_t* __restrict__ adm_slot, AdmIndex ix,
-                                                   uint32_t n_adm, SplitRows rows, const uint32_t* __restrict__ fdict) {
+                                                   uint32_t n_adm, SplitRows rows, const uint32_t* __restrict__ fdict,
+                                                   uint32_t* __restrict__ fhit, uint32_t fbase) {
     wave_prio(rows.prio);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = b.n;
@@ -250,6 +261,7 @@ __global__ __launch_bounds__(256) void k_fast_prep(DevBatch b, const uint8_t* __
         }
         if (sl >= 0 && state[sl] == HD_FB_READY) {
             slot = (uint32_t)sl;
+            if (idx == -2) atomicAdd(&fhit[sl - (int32_t)fbase], 1u);   // a foreign slot's use (fb_evict)
             FastIn in;
             if (digest_in) {
                 load_row32_be(in.digest_be, digest_in, i);
@@ -938,8 +950,9 @@ static bool fb_foreign_pending(const FbWork* f) {
 int fb_learn(hd_ctx* ctx, hipStream_t s) {
     FbWork* f = ctx->fb;
     const bool fnew = fb_foreign_pending(f);
-    if (f->nr_host && *(volatile uint32_t*)f->nr_host == 0 && !fnew) return HD_OK;
+    if (f->nr_host && *(volatile uint32_t*)f->nr_host == 0 && !fnew && !f->fforce) return HD_OK;
     if (fnew) f->fseen = *(volatile uint32_t*)f->fpend_host;
+    f->fforce = false;
     const uint32_t g = (uint32_t)std::max(ctx->n_cu, 1) * 4u;
     k_fb_list<<<1, 256, 0, s>>>(f->nslots, f->state, f->list, f->counts);
     if (f->wp == HD_FB_WW) {
@@ -951,6 +964,137 @@ int fb_learn(hd_ctx* ctx, hipStream_t s) {
     }
     k_fb_ready<<<1, 256, 0, s>>>(f->list, f->counts, f->state, f->nr_dev, f->fbase, f->fbase + f->fres);
     FBCHK(hipGetLastError(), "fb table kernels");
+    return HD_OK;
+}
+
+// the foreign block's host-side state after its dictionary was emptied
+void fb_foreign_forget(FbWork* f) {
+    ((volatile uint32_t*)f->fpend_host)[0] = 0;
+    ((volatile uint32_t*)f->fpend_host)[1] = 0;
+    f->fseen = 0;
+    f->fwait = 1;
+    f->fcalls = 0;
+    f->fforce = false;
+}
+
+// Foreign-slot eviction.  The fcap foreign slots go to the first Froms whose
+// NOT_ADMITTED recovery claims them; later Froms stay in the dictionary
+// without a slot (key kept, recoveries counted).  While such recoveries are
+// flagged, every fwait-th call (fwait doubling up to HD_FD_EVICT_WAIT_MAX
+// while checks change nothing) waits for the context's calls to finish --
+// nothing may read a table about to be re-keyed -- and reads the counters:
+// the slotless Froms by recoveries since the last check, hottest first, take
+// the slots of the READY foreign keys with the fewest known-key checks while
+// hot >= 2 cold + 4 (hysteresis: two senders of similar rates do not trade
+// places every check).  A demoted From keeps its key and may come back;
+// slotless entries without a recovery since the last check leave the
+// dictionary (throwaway Froms cannot fill its 128 buckets either).  The
+// dictionary is rebuilt on the host and uploaded, the counters restart, and
+// the promoted slots (state LEARNED) are built at this call's end
+// (fforce).  Verdicts never depend on it: a slot that is not READY sends its
+// messages to the full recovery.
+#define HD_FD_EVICT_WAIT_MAX 1024u
+int fb_evict(hd_ctx* ctx, bool* changed) {
+    FbWork* f = ctx->fb;
+    *changed = false;
+    if (!f->fcap || !f->fhit || !f->fkey || !f->fdict) return HD_OK;
+    volatile uint32_t* miss = (volatile uint32_t*)f->fpend_host + 1;
+    if (*miss == 0) return HD_OK;
+    if (++f->fcalls < f->fwait) return HD_OK;
+    f->fcalls = 0;
+    int rq = hd_fb_quiesce(ctx);
+    if (rq) return rq;
+    *miss = 0;
+    hipStream_t s = ctx->stream;
+    const uint32_t B = HD_FD_BUCKETS, R = f->fres;
+    std::vector<uint32_t> fd(HD_FD_WORDS), hit(64 + B), st(R);
+    std::vector<ge> key(B), pub(R);
+    FBCHK(hipMemcpyAsync(fd.data(), f->fdict, 4 * (size_t)HD_FD_WORDS, hipMemcpyDeviceToHost, s), "evict read");
+    FBCHK(hipMemcpyAsync(hit.data(), f->fhit, 4 * hit.size(), hipMemcpyDeviceToHost, s), "evict read");
+    FBCHK(hipMemcpyAsync(key.data(), f->fkey, sizeof(ge) * B, hipMemcpyDeviceToHost, s), "evict read");
+    FBCHK(hipMemcpyAsync(pub.data(), f->pub + f->fbase, sizeof(ge) * R, hipMemcpyDeviceToHost, s), "evict read");
+    FBCHK(hipMemcpyAsync(st.data(), f->state + f->fbase, 4 * (size_t)R, hipMemcpyDeviceToHost, s), "evict read");
+    FBCHK(hipStreamSynchronize(s), "evict read");
+    struct Ent {
+        uint32_t from[8];
+        uint32_t slot, hits;
+        ge key;
+        bool moved;
+    };
+    std::vector<Ent> held, loose;
+    for (uint32_t b = 0; b < B; b++) {
+        if (fd[b] != 2u) continue;
+        Ent e;
+        memcpy(e.from, &fd[2 * B + 8 * b], 32);
+        e.slot = fd[B + b];
+        e.moved = false;
+        if (e.slot != 0xFFFFFFFFu && e.slot >= f->fbase && e.slot < f->fbase + R) {
+            e.hits = hit[e.slot - f->fbase];
+            e.key = pub[e.slot - f->fbase];
+            held.push_back(e);
+        } else {
+            e.slot = 0xFFFFFFFFu;
+            e.hits = hit[64 + b];
+            e.key = key[b];
+            loose.push_back(e);
+        }
+    }
+    std::stable_sort(loose.begin(), loose.end(), [](const Ent& a, const Ent& b) { return a.hits > b.hits; });
+    std::vector<Ent*> cold;
+    for (Ent& e : held)
+        if (st[e.slot - f->fbase] == HD_FB_READY) cold.push_back(&e);   // built slots only: a new one had no chance
+    std::stable_sort(cold.begin(), cold.end(), [](const Ent* a, const Ent* b) { return a->hits < b->hits; });
+    std::vector<Ent> promoted;
+    size_t swaps = 0;
+    while (swaps < loose.size() && swaps < cold.size() && loose[swaps].hits >= 2 * cold[swaps]->hits + 4) {
+        Ent& hot = loose[swaps];
+        Ent* old = cold[swaps];
+        hot.slot = old->slot;
+        hot.moved = true;
+        old->slot = 0xFFFFFFFFu;
+        old->moved = true;
+        promoted.push_back(hot);
+        swaps++;
+    }
+    // the new dictionary: slot holders first (they always fit: at most 64 of
+    // 128 buckets), then the slotless Froms worth keeping
+    std::vector<Ent> keep;
+    for (const Ent& e : held) keep.push_back(e);
+    for (const Ent& e : loose)
+        if (e.moved || e.hits > 0) keep.push_back(e);
+    std::stable_partition(keep.begin(), keep.end(), [](const Ent& e) { return e.slot != 0xFFFFFFFFu; });
+    const bool dropped = keep.size() < held.size() + loose.size();
+    if (swaps == 0 && !dropped) {
+        f->fwait = std::min(2 * f->fwait, HD_FD_EVICT_WAIT_MAX);
+        FBCHK(hipMemsetAsync(f->fhit, 0, 4 * hit.size(), s), "evict counters");
+        FBCHK(hipStreamSynchronize(s), "evict counters");
+        return HD_OK;
+    }
+    std::vector<uint32_t> nd(HD_FD_WORDS, 0u);
+    std::vector<ge> nkey(B);
+    for (const Ent& e : keep) {
+        uint32_t b = fdict_bucket(e.from);
+        int p = 0;
+        for (; p < 8 && nd[b] != 0u; p++) b = (b + 1u) & (B - 1u);
+        if (p == 8) continue;   // no room (slotless: simply forgotten)
+        nd[b] = 2u;
+        nd[B + b] = e.slot;
+        memcpy(&nd[2 * B + 8 * b], e.from, 32);
+        nkey[b] = e.key;
+    }
+    FBCHK(hipMemcpyAsync(f->fdict, nd.data(), 4 * (size_t)HD_FD_WORDS, hipMemcpyHostToDevice, s), "evict write");
+    FBCHK(hipMemcpyAsync(f->fkey, nkey.data(), sizeof(ge) * B, hipMemcpyHostToDevice, s), "evict write");
+    FBCHK(hipMemsetAsync(f->fhit, 0, 4 * hit.size(), s), "evict counters");
+    const uint32_t learned = HD_FB_LEARNED;
+    for (const Ent& e : promoted) {
+        FBCHK(hipMemcpyAsync(f->pub + e.slot, &e.key, sizeof(ge), hipMemcpyHostToDevice, s), "evict key");
+        FBCHK(hipMemcpyAsync(f->state + e.slot, &learned, 4, hipMemcpyHostToDevice, s), "evict state");
+    }
+    FBCHK(hipStreamSynchronize(s), "evict write");
+    f->fwait = swaps ? 1u : std::min(2 * f->fwait, HD_FD_EVICT_WAIT_MAX);
+    f->fforce = swaps > 0;
+    f->evictions += (uint32_t)swaps;
+    *changed = true;
     return HD_OK;
 }
 
@@ -1018,8 +1162,8 @@ int hd_fb_init(hd_ctx* ctx) {
     FBCHK(hipHostMalloc((void**)&f->est_host, 8, hipHostMallocMapped | hipHostMallocCoherent), "fb list estimate");
     f->est_host[0] = f->est_host[1] = 0xFFFFFFFFu;
     FBCHK(hipHostGetDevicePointer((void**)&f->est_dev, f->est_host, 0), "fb list estimate map");
-    FBCHK(hipHostMalloc((void**)&f->fpend_host, 4, hipHostMallocMapped | hipHostMallocCoherent), "fb foreign claims");
-    *f->fpend_host = 0;
+    FBCHK(hipHostMalloc((void**)&f->fpend_host, 8, hipHostMallocMapped | hipHostMallocCoherent), "fb foreign claims");
+    f->fpend_host[0] = f->fpend_host[1] = 0;
     FBCHK(hipHostGetDevicePointer((void**)&f->fpend_dev, f->fpend_host, 0), "fb foreign claims map");
     int rc = fb_alloc_slots(ctx);
     if (rc) return rc;
@@ -1041,7 +1185,7 @@ void hd_fb_release(hd_ctx* ctx) {
         for (void* p : sp)
             if (p) (void)hipFree(p);
     }
-    void* ptrs[] = {f->counts, f->adm_slot, f->zr, f->fdict, f->fnext};
+    void* ptrs[] = {f->counts, f->adm_slot, f->zr, f->fdict, f->fnext, f->fhit, f->fkey};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (f->nr_host) (void)hipHostFree(f->nr_host);
@@ -1162,11 +1306,13 @@ int hd_fb_map_signatories(hd_ctx* ctx, const uint8_t* sorted, uint32_t m) {
     if (f->fres) {
         if (!f->fdict) FBCHK(hipMalloc(&f->fdict, 4 * (size_t)HD_FD_WORDS), "fb foreign dictionary");
         if (!f->fnext) FBCHK(hipMalloc(&f->fnext, 4), "fb foreign count");
+        if (!f->fhit) FBCHK(hipMalloc(&f->fhit, 4 * (64 + (size_t)HD_FD_BUCKETS)), "fb foreign hits");
+        if (!f->fkey) FBCHK(hipMalloc(&f->fkey, sizeof(ge) * HD_FD_BUCKETS), "fb foreign keys");
         FBCHK(hipMemsetAsync(f->fdict, 0, 4 * (size_t)HD_FD_WORDS, s), "fb foreign reset");
         FBCHK(hipMemsetAsync(f->fnext, 0, 4, s), "fb foreign reset");
+        FBCHK(hipMemsetAsync(f->fhit, 0, 4 * (64 + (size_t)HD_FD_BUCKETS), s), "fb foreign reset");
         FBCHK(hipMemsetAsync(f->state + f->fbase, 0, 4 * (size_t)f->fres, s), "fb foreign reset");
-        *(volatile uint32_t*)f->fpend_host = 0;
-        f->fseen = 0;
+        fb_foreign_forget(f);
     }
     rc = hd_dev_grow(ctx, (void**)&f->adm_slot, &f->cap_adm_slot, 4 * adm_slot.size());
     if (rc) return rc;
@@ -1183,12 +1329,10 @@ int hd_fb_clear_keys(hd_ctx* ctx) {
     if (f->fres && f->fdict) {   // the foreign keys are learned again too
         FBCHK(hipMemsetAsync(f->fdict, 0, 4 * (size_t)HD_FD_WORDS, ctx->stream), "fb clear");
         FBCHK(hipMemsetAsync(f->fnext, 0, 4, ctx->stream), "fb clear");
+        FBCHK(hipMemsetAsync(f->fhit, 0, 4 * (64 + (size_t)HD_FD_BUCKETS), ctx->stream), "fb clear");
     }
     FBCHK(hipStreamSynchronize(ctx->stream), "fb clear");
-    if (f->fres) {
-        *(volatile uint32_t*)f->fpend_host = 0;
-        f->fseen = 0;
-    }
+    if (f->fres) fb_foreign_forget(f);
     return fb_count_not_ready(ctx);
 }
 
@@ -1249,7 +1393,7 @@ static void launch_split(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest
     const uint32_t T = ((n + (uint32_t)K - 1) / (uint32_t)K + 63u) & ~63u;
     const uint32_t tb = (T + 255) / 256, nb = (n + 255) / 256;
     k_fast_prep<<<nb, 256, 0, s>>>(b, d_digest, f->state, f->adm_slot, hd_adm_index(ctx), ctx->n_adm, rows,
-                                   f->fcap ? f->fdict : nullptr);
+                                   f->fcap ? f->fdict : nullptr, f->fhit, f->fbase);
     k_fast_sinv<K><<<tb, 256, 0, s>>>(n, T, rows);
     hipEvent_t* pe = fb_prof_pair(f->ev_sums, f->n_sums, f->prof);
     if (pe) (void)hipEventRecord(pe[0], s);
@@ -1274,9 +1418,13 @@ int hd_fb_verify(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_
     FbWork::Scratch& sc = f->sc[j];
     if (!sc.done) FBCHK(hipEventCreateWithFlags(&sc.done, hipEventDisableTiming), "fb scratch event");
     if (!sc.count) FBCHK(hipMalloc(&sc.count, 8), "fb scratch count");
+    // foreign slots re-keyed (fb_evict; it waited for every earlier call)
+    bool evicted = false;
+    int re = fb_evict(ctx, &evicted);
+    if (re) return re;
     // see FbWork: in the steady state only this set's previous user orders
     // this call; otherwise the previous call does, on whatever stream
-    const bool steady = f->nr_host && *(volatile uint32_t*)f->nr_host == 0 && !fb_foreign_pending(f);
+    const bool steady = !evicted && f->nr_host && *(volatile uint32_t*)f->nr_host == 0 && !fb_foreign_pending(f);
     if (sc.used && sc.stream != s) FBCHK(hipStreamWaitEvent(s, sc.done, 0), "fb scratch order");
     if (f->any && f->last != s && !(steady && f->steady)) FBCHK(hipStreamWaitEvent(s, f->done, 0), "fb stream order");
     hipEvent_t* pe = fb_prof_pair(f->ev_call, f->n_call, f->prof);
@@ -1359,7 +1507,8 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         }
         const SlowCtl ctl{lift ? sc.slow2 : sc.slow, lift ? sc.count + 1 : sc.count, f->adm_slot, f->state, f->pub,
                           d_bitmap, lift ? f->est_dev + 1 : f->est_dev, ctx->var[HD_VAR_WAVE_PRIO],
-                          f->fcap ? f->fdict : nullptr, f->fnext, f->fbase, f->fcap, f->fpend_dev};
+                          f->fcap ? f->fdict : nullptr, f->fnext, f->fbase, f->fcap, f->fpend_dev,
+                          f->fcap ? f->fhit + 64 : nullptr, f->fkey, f->fpend_dev + 1};
         rc = hd_launch_slow(ctx, b, d_digest, d_verdict, d_rec32, d_signer, nullptr, ctl,
                             fallback_blocks(f->est_host[lift ? 1 : 0], full), s);
         if (rc) return rc;
@@ -1436,6 +1585,24 @@ int hd_ctx_profile_read(hd_ctx* ctx, uint32_t* calls, double* verify_ms, uint32_
     if (verify_ms) *verify_ms = tc;
     if (sums_launches) *sums_launches = ns;
     if (sums_ms) *sums_ms = ts;
+    return HD_OK;
+}
+
+int hd_ctx_foreign_stats(hd_ctx* ctx, uint32_t* ready_slots, uint32_t* evictions) {
+    if (!ctx) return HD_EINVAL;
+    if (ready_slots) *ready_slots = 0;
+    if (evictions) *evictions = 0;
+    if (!ctx->fb) return HD_OK;
+    (void)hipSetDevice(ctx->device);
+    FbWork* f = ctx->fb;
+    int rq = hd_ctx_quiesce(ctx);
+    if (rq) return rq;
+    if (ready_slots && f->fres) {
+        std::vector<uint32_t> st(f->fres);
+        FBCHK(hipMemcpy(st.data(), f->state + f->fbase, 4 * (size_t)f->fres, hipMemcpyDeviceToHost), "state read");
+        for (uint32_t v : st) *ready_slots += v == HD_FB_READY;
+    }
+    if (evictions) *evictions = f->evictions;
     return HD_OK;
 }
 

@@ -47,6 +47,7 @@ struct hd_ctx {
     int32_t* d_adm_perm = nullptr;  // sorted index -> caller's index
     size_t cap_adm = 0, cap_adm_perm = 0;
     uint32_t n_adm = 0;
+    uint32_t adm_ver = 0;           // bumped by every hd_set_signatories (hd_mq's prefetch checks it)
     // the hd_set_signatories array as given (caller order, duplicates kept):
     // the From rows of the compact host batch (hd_verify_submit_compact)
     uint8_t* d_sig_caller = nullptr;
@@ -121,6 +122,12 @@ struct SlowCtl {
     uint32_t* fnext;
     uint32_t fbase, fcap;
     uint32_t* fpend;          // host-mapped: the claim count, so the host builds the new tables
+    // slot eviction (hd_fastverify.hip fb_evict): a From the dictionary holds
+    // without a slot keeps its key in fkey[bucket] and counts its recoveries
+    // in fbhit[bucket]; fmiss (host-mapped) is set on every such recovery
+    uint32_t* fbhit;
+    hd::ge* fkey;
+    uint32_t* fmiss;
 };
 int hd_launch_slow(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_digest, uint8_t* d_verdict, uint8_t* d_rec32,
                    int32_t* d_signer, uint32_t* d_bitmap, const SlowCtl& ctl, uint32_t blocks, hipStream_t s);

@@ -537,9 +537,10 @@ __global__ void k_mq_commit(uint32_t nsend, const uint32_t* __restrict__ newhead
 // with a 64-byte header: {delivered, removed}.
 #define HD_MQ_ROW 160
 #define HD_MQ_HDR 64
-__device__ __forceinline__ void mq_row_put(uint8_t* __restrict__ row, const Pool& p, uint32_t e) {
+__device__ __forceinline__ void mq_row_put(uint8_t* __restrict__ row, const Pool& p, uint32_t e, uint32_t allowed) {
     // whole dwords only (the stage may be mapped host memory: one PCIe write
-    // per dword instead of per byte); bytes 152..155 = sig[64], type, 0, 0
+    // per dword instead of per byte); bytes 152..155 = sig[64], type, allowed
+    // (a prefetched row: its sender was in procsAllowed), 0
     uint32_t* o = reinterpret_cast<uint32_t*>(row);
     const uint64_t hv = (uint64_t)p.h[e], rv = (uint64_t)p.r[e], vv = (uint64_t)p.vr[e];
     o[0] = (uint32_t)hv;
@@ -556,21 +557,27 @@ __device__ __forceinline__ void mq_row_put(uint8_t* __restrict__ row, const Pool
     for (int j = 0; j < 16; j++)
         o[22 + j] = (uint32_t)sg[4 * j] | ((uint32_t)sg[4 * j + 1] << 8) | ((uint32_t)sg[4 * j + 2] << 16) |
                     ((uint32_t)sg[4 * j + 3] << 24);
-    o[38] = (uint32_t)sg[64] | ((uint32_t)p.type[e] << 8);
+    o[38] = (uint32_t)sg[64] | ((uint32_t)p.type[e] << 8) | (allowed << 16);
     o[39] = (uint32_t)p.sender[e];
 }
+// Prefetch (hpf > h): the same launch also stages every message of the
+// heights (h, hpf] -- allowed or not, flagged in byte 154 -- after the
+// delivered rows, in queue order, when they fit `pf_rows`; the host then
+// serves the consumes of those heights without the device (hd_mq pf_*).  The
+// heads are committed through h only.  Header words: {delivered, removed,
+// seq, staged window rows, window: 1 staged / 2 over pf_rows / 0 none}.
 __global__ __launch_bounds__(1024) void k_mq_consume1(uint32_t nsend, Pool p, uint32_t* __restrict__ head,
                                                       const uint32_t* __restrict__ send, int64_t h, uint32_t na,
                                                       const uint32_t* __restrict__ list, int be_words, Dict d,
                                                       uint32_t rows, uint32_t cap, uint8_t* __restrict__ stage,
-                                                      uint32_t seq) {
+                                                      uint32_t seq, int64_t hpf, uint32_t pf_rows) {
     typedef hipcub::BlockScan<uint32_t, 1024> Scan;
     typedef hipcub::BlockReduce<uint32_t, 1024> Red;
     __shared__ typename Scan::TempStorage ts;
     __shared__ typename Red::TempStorage rs;
     __shared__ uint8_t allow[1024];
-    __shared__ uint32_t off[1024], lo_of[1024];
-    __shared__ uint32_t tot_d;
+    __shared__ uint32_t off[1024], lo_of[1024], off2[1024], cut_of[1024];
+    __shared__ uint32_t tot_d, tot_p;
     const uint32_t t = threadIdx.x;
     allow[t] = 0;
     __syncthreads();
@@ -584,9 +591,10 @@ __global__ __launch_bounds__(1024) void k_mq_consume1(uint32_t nsend, Pool p, ui
         if (id != kEmpty) allow[id] = 1;
     }
     __syncthreads();
-    uint32_t rem = 0, del = 0, cut = 0, h0 = 0;
+    uint32_t rem = 0, del = 0, cut = 0, h0 = 0, pre = 0;
     if (t < nsend) {
         uint32_t lo = head[t], hi = send[t];
+        const uint32_t end = hi;
         h0 = lo;
         // a flush per height cuts a few messages off each run's front: look at
         // the first four at once (independent loads), search only past them
@@ -611,19 +619,37 @@ __global__ __launch_bounds__(1024) void k_mq_consume1(uint32_t nsend, Pool p, ui
         cut = lo;
         rem = lo - h0;
         del = allow[t] ? rem : 0u;
+        if (hpf > h) {   // the window's end, searched past the consume's cut
+            hi = end;
+            while (lo < hi) {
+                const uint32_t mid = lo + (hi - lo) / 2;
+                if (p.h[mid] <= hpf) lo = mid + 1;
+                else hi = mid;
+            }
+            pre = lo - cut;
+        }
     }
     uint32_t o = 0, agg = 0;
     Scan(ts).ExclusiveSum(del, o, agg);
     const uint32_t rsum = Red(rs).Sum(rem);
     off[t] = t < nsend ? o : agg;       // entries past nsend sort after every row
     lo_of[t] = h0;
+    cut_of[t] = cut;
+    __syncthreads();                    // the scan storage is reused
+    uint32_t o2 = 0, agg2 = 0;
+    Scan(ts).ExclusiveSum(pre, o2, agg2);
+    off2[t] = t < nsend ? o2 : agg2;
     if (t == 0) {
+        const bool staged = hpf > h && agg <= rows && agg <= cap && agg2 <= pf_rows;
         tot_d = agg;
+        tot_p = staged ? agg2 : 0u;
         reinterpret_cast<uint32_t*>(stage)[0] = agg;
         reinterpret_cast<uint32_t*>(stage)[1] = rsum;
+        reinterpret_cast<uint32_t*>(stage)[3] = tot_p;
+        reinterpret_cast<uint32_t*>(stage)[4] = staged ? 1u : (hpf > h && agg2 > pf_rows ? 2u : 0u);
     }
     __syncthreads();
-    const uint32_t total = tot_d, nw = total < rows ? total : rows;
+    const uint32_t total = tot_d, nw = total < rows ? total : rows, np = tot_p;
     uint8_t* out = stage + HD_MQ_HDR;
     for (uint32_t k = t; k < nw; k += 1024) {
         // the sender of delivered row k: the last s with off[s] <= k whose run is non-empty
@@ -633,7 +659,17 @@ __global__ __launch_bounds__(1024) void k_mq_consume1(uint32_t nsend, Pool p, ui
             if (off[m] <= k) a = m;
             else b = m;
         }
-        mq_row_put(out + (size_t)HD_MQ_ROW * k, p, lo_of[a] + (k - off[a]));
+        mq_row_put(out + (size_t)HD_MQ_ROW * k, p, lo_of[a] + (k - off[a]), 1u);
+    }
+    uint8_t* win = out + (size_t)HD_MQ_ROW * nw;   // the window's rows follow the delivered ones
+    for (uint32_t k = t; k < np; k += 1024) {
+        uint32_t a = 0, b = nsend;
+        while (b - a > 1) {
+            const uint32_t m = (a + b) / 2;
+            if (off2[m] <= k) a = m;
+            else b = m;
+        }
+        mq_row_put(win + (size_t)HD_MQ_ROW * k, p, cut_of[a] + (k - off2[a]), allow[a]);
     }
     if (total <= cap && t < nsend) head[t] = cut;
     if (seq) {
@@ -728,6 +764,20 @@ struct hd_mq {
     size_t mstage_cap = 0;
     uint32_t seq = 0;
     bool mapped = true;
+    // Consume prefetch (mapped path): a consume of height h also stages the
+    // rows of the heights (h, h + pf_win] (k_mq_consume1); while nothing is
+    // inserted, the admitted set stays and the consumes stay inside that
+    // window, they are served from the stage by the host alone.  The device
+    // heads stay at pf_dev until pf_sync commits them through pf_done.
+    bool pf = false;
+    int64_t pf_dev = 0;        // heads committed on the device through this height
+    int64_t pf_done = 0;       // consumed (or dropped) through this height
+    int64_t pf_max = 0;        // the staged window ends here
+    uint32_t pf_adm_ver = 0;   // the admitted set the allow flags were read against
+    int pf_win = 64;           // window heights (halved when a window overflows the stage)
+    const uint8_t* pf_base = nullptr;     // first window row in the stage
+    std::vector<uint32_t> pf_start;       // rows of height pf_dev + 1 + j: pf_idx[pf_start[j] .. pf_start[j + 1])
+    std::vector<uint32_t> pf_idx;
 };
 
 #define QCHK(expr, what)                                           \
@@ -950,6 +1000,8 @@ static int mq_runs(hd_mq* q, hipStream_t s) {
     return HD_OK;
 }
 
+static int pf_sync(hd_mq* q);   // the consume prefetch (below)
+
 static int mq_insert_flagged(hd_mq* q, const hd_batch* d_batch, const uint8_t* flag, hipStream_t s) {
     const uint32_t nb = d_batch->n;
     int rc = mq_compact(q, s);
@@ -1087,6 +1139,10 @@ int hd_mq_insert_device(hd_mq* q, const hd_batch* d_batch, const uint8_t* d_inse
     if (!d_batch->type || !d_batch->height || !d_batch->round || !d_batch->value32 || !d_batch->from32)
         return HD_EINVAL;
     (void)hipSetDevice(q->ctx->device);
+    {
+        const int rs = pf_sync(q);   // the queue on the device as consumed so far
+        if (rs) return rs;
+    }
     hipStream_t s = stream ? (hipStream_t)stream : q->ctx->stream;
     int rc = 0;
     uint8_t* flag = (uint8_t*)qbuf(q, MQ_FLAG, nb, &rc);
@@ -1105,6 +1161,10 @@ int hd_mq_insert_verified_device(hd_mq* q, const hd_batch* d_batch, const uint8_
     if (!d_batch->type || !d_batch->height || !d_batch->round || !d_batch->value32 || !d_batch->from32)
         return HD_EINVAL;
     (void)hipSetDevice(q->ctx->device);
+    {
+        const int rs = pf_sync(q);   // the queue on the device as consumed so far
+        if (rs) return rs;
+    }
     hipStream_t s = stream ? (hipStream_t)stream : q->ctx->stream;
     int rc = 0;
     uint8_t* flag = (uint8_t*)qbuf(q, MQ_FLAG, nb, &rc);
@@ -1145,6 +1205,97 @@ static int mq_commit(hd_mq* q, uint32_t removed, hipStream_t s) {
     return HD_OK;
 }
 
+#define HD_MQ_PF_ROWS 16384u     // window rows a prefetch may stage (160 B each)
+#define HD_MQ_PF_WIN_MAX 64
+
+// unpack `rows` staged rows (pointers) into the caller's SoA outputs
+static void mq_unpack(const uint8_t* const* rows, uint32_t c, const hd_batch_out* out, int32_t* out_sender) {
+    for (uint32_t k = 0; k < c; k++) {
+        const uint8_t* row = rows[k];
+        out->type[k] = row[153];
+        memcpy(out->height + k, row, 8);
+        memcpy(out->round + k, row + 8, 8);
+        if (out->valid_round) memcpy(out->valid_round + k, row + 16, 8);
+        memcpy(out->value32 + 32 * (size_t)k, row + 24, 32);
+        memcpy(out->from32 + 32 * (size_t)k, row + 56, 32);
+        if (out->sig65) memcpy(out->sig65 + 65 * (size_t)k, row + 88, 65);
+        if (out_sender) memcpy(out_sender + k, row + 156, 4);
+    }
+    if (out->adv_class && c) memset(out->adv_class, 0, c);
+}
+
+// Commit the heads through pf_done on the device (the consumes served from
+// the stage removed those messages on the host's count only) and forget the
+// window.  Every operation that reads or changes the device queue calls it
+// first.
+static int pf_sync(hd_mq* q) {
+    if (!q->pf) return HD_OK;
+    q->pf = false;
+    if (q->pf_done <= q->pf_dev) return HD_OK;
+    hipStream_t s = q->ctx->stream;
+    uint32_t tot[2];
+    int rc = mq_plan(q, q->pf_done, 0, nullptr, tot, s);
+    if (rc) return rc;
+    if (tot[1]) {
+        QCHK(hipMemcpyAsync(q->buf[MQ_HEADS].p, q->buf[MQ_NEWHEAD].p, 4 * (size_t)q->nsend, hipMemcpyDeviceToDevice,
+                            s), "prefetch commit");
+        q->dead = true;
+    }
+    QCHK(hipStreamSynchronize(s), "prefetch commit");
+    return HD_OK;
+}
+
+// Index the window rows the last consume staged (np rows after the c
+// delivered ones) by height, for the consumes of (h, h + win].
+static void pf_index(hd_mq* q, int64_t h, int64_t hmax, const uint8_t* win, uint32_t np) {
+    const uint32_t nh = (uint32_t)(hmax - h);
+    q->pf_start.assign(nh + 1, 0u);
+    q->pf_idx.resize(np);
+    std::vector<uint32_t> hk(np);
+    for (uint32_t k = 0; k < np; k++) {
+        int64_t hv;
+        memcpy(&hv, win + (size_t)HD_MQ_ROW * k, 8);
+        hk[k] = (uint32_t)(hv - h - 1);   // in [0, nh): the kernel staged heights (h, hmax] only
+        q->pf_start[hk[k] + 1]++;
+    }
+    for (uint32_t j = 0; j < nh; j++) q->pf_start[j + 1] += q->pf_start[j];
+    std::vector<uint32_t> fill(q->pf_start.begin(), q->pf_start.end() - 1);
+    for (uint32_t k = 0; k < np; k++) q->pf_idx[fill[hk[k]]++] = k;   // row order kept within a height
+    q->pf_base = win;
+    q->pf_dev = q->pf_done = h;
+    q->pf_max = hmax;
+    q->pf_adm_ver = q->ctx->adm_ver;
+    q->pf = true;
+}
+
+// A consume of height h from the window (the caller checked pf, the admitted
+// set and h <= pf_max): the rows of the heights (pf_done, h] in queue order.
+static int pf_consume(hd_mq* q, int64_t h, const hd_batch_out* out, int32_t* out_sender, uint32_t cap,
+                      uint32_t* n_out, uint32_t* n_removed) {
+    *n_out = 0;
+    if (n_removed) *n_removed = 0;
+    if (h <= q->pf_done) return HD_OK;
+    const uint32_t j0 = (uint32_t)(q->pf_done - q->pf_dev) - 0u, j1 = (uint32_t)(h - q->pf_dev);
+    // heights (pf_done, h] are buckets j0 .. j1 - 1 (bucket j = height pf_dev + 1 + j)
+    std::vector<uint32_t> ids(q->pf_idx.begin() + q->pf_start[j0], q->pf_idx.begin() + q->pf_start[j1]);
+    if (j1 - j0 > 1) std::sort(ids.begin(), ids.end());   // several heights: back to queue order
+    std::vector<const uint8_t*> rows;
+    rows.reserve(ids.size());
+    for (uint32_t k : ids) {
+        const uint8_t* row = q->pf_base + (size_t)HD_MQ_ROW * k;
+        if (row[154]) rows.push_back(row);   // the sender is in procsAllowed
+    }
+    const uint32_t c = (uint32_t)rows.size(), nr = (uint32_t)ids.size();
+    *n_out = c;
+    if (c > cap) return HD_ECAP;   // nothing consumed
+    if (n_removed) *n_removed = nr;
+    mq_unpack(rows.data(), c, out, out_sender);
+    q->live -= nr;
+    q->pf_done = h;
+    q->last_deliv = c;
+    return HD_OK;
+}
+
 // Consume of a queue with at most 1024 senders and a capacity of at most
 // HD_MQ_FUSED_ROWS: one kernel (k_mq_consume1), then a download of the
 // header and of as many 160-byte rows as the previous consume delivered
@@ -1162,12 +1313,16 @@ static int mq_consume1(hd_mq* q, int64_t h, const uint32_t* list, uint32_t na, i
     if (q->mapped) {
         // the kernel writes the header and rows straight into mapped host
         // memory and, last, the call's sequence number: no copy, no stream
-        // synchronisation on the common path
-        if (q->mstage_cap < bytes) {
+        // synchronisation on the common path.  In the admitted-set mode the
+        // launch also stages the next heights' window (prefetch).
+        const bool pf = be != 0;
+        const int64_t hpf = pf ? h + q->pf_win : h;
+        const size_t bytes_pf = bytes + (pf ? (size_t)HD_MQ_ROW * HD_MQ_PF_ROWS : 0);
+        if (q->mstage_cap < bytes_pf) {
             if (q->mstage) (void)hipHostFree(q->mstage);
             q->mstage = nullptr;
             q->mstage_cap = 0;
-            const size_t want = std::max(bytes, (size_t)1 << 16);
+            const size_t want = std::max(bytes_pf, (size_t)1 << 16);
             QCHK(hipHostMalloc(&q->mstage, want, hipHostMallocMapped | hipHostMallocCoherent), "mq mapped stage");
             void* dp = nullptr;
             QCHK(hipHostGetDevicePointer(&dp, q->mstage, 0), "mq mapped stage pointer");
@@ -1177,7 +1332,7 @@ static int mq_consume1(hd_mq* q, int64_t h, const uint32_t* list, uint32_t na, i
         const uint32_t seq = ++q->seq ? q->seq : ++q->seq;   // never 0 (0 = no signal)
         k_mq_consume1<<<1, 1024, 0, s>>>(q->nsend, q->pool, (uint32_t*)q->buf[MQ_HEADS].p,
                                          (const uint32_t*)q->buf[MQ_SEND].p, h, na, list, be, dict_of(q), rows, cap,
-                                         q->mstage_dev, seq);
+                                         q->mstage_dev, seq, hpf, pf ? HD_MQ_PF_ROWS : 0u);
         QCHK(hipGetLastError(), "k_mq_consume1");
         hs = (uint8_t*)q->mstage;
         volatile uint32_t* word = (volatile uint32_t*)hs + 2;
@@ -1196,6 +1351,13 @@ static int mq_consume1(hd_mq* q, int64_t h, const uint32_t* list, uint32_t na, i
         nr = ((const uint32_t*)hs)[1];
         *n_out = c;
         if (c > cap) return HD_ECAP;   // nothing committed
+        const uint32_t np = ((const uint32_t*)hs)[3], win = ((const uint32_t*)hs)[4];
+        if (win == 1) {
+            pf_index(q, h, hpf, hs + HD_MQ_HDR + (size_t)HD_MQ_ROW * c, np);
+            q->pf_win = std::min(2 * q->pf_win, HD_MQ_PF_WIN_MAX);
+        } else if (win == 2) {
+            q->pf_win = std::max(1, q->pf_win / 2);   // the window overflowed the stage: a narrower one next time
+        }
     } else {
         uint8_t* dst = (uint8_t*)qbuf(q, MQ_STAGE, bytes, &rc);
         if (rc) return rc;
@@ -1209,7 +1371,7 @@ static int mq_consume1(hd_mq* q, int64_t h, const uint32_t* list, uint32_t na, i
         }
         k_mq_consume1<<<1, 1024, 0, s>>>(q->nsend, q->pool, (uint32_t*)q->buf[MQ_HEADS].p,
                                          (const uint32_t*)q->buf[MQ_SEND].p, h, na, list, be, dict_of(q), rows, cap,
-                                         dst, 0u);
+                                         dst, 0u, h, 0u);
         QCHK(hipGetLastError(), "k_mq_consume1");
         const uint32_t guess = std::min(rows, std::max(64u, 2 * q->last_deliv));
         hs = (uint8_t*)q->hstage;
@@ -1233,18 +1395,9 @@ static int mq_consume1(hd_mq* q, int64_t h, const uint32_t* list, uint32_t na, i
         q->live -= nr;
         q->dead = true;
     }
-    const uint8_t* row = hs + HD_MQ_HDR;
-    for (uint32_t k = 0; k < c; k++, row += HD_MQ_ROW) {
-        out->type[k] = row[153];
-        memcpy(out->height + k, row, 8);
-        memcpy(out->round + k, row + 8, 8);
-        if (out->valid_round) memcpy(out->valid_round + k, row + 16, 8);
-        memcpy(out->value32 + 32 * (size_t)k, row + 24, 32);
-        memcpy(out->from32 + 32 * (size_t)k, row + 56, 32);
-        if (out->sig65) memcpy(out->sig65 + 65 * (size_t)k, row + 88, 65);
-        if (out_sender) memcpy(out_sender + k, row + 156, 4);
-    }
-    if (out->adv_class && c) memset(out->adv_class, 0, c);
+    std::vector<const uint8_t*> rp(c);
+    for (uint32_t k = 0; k < c; k++) rp[k] = hs + HD_MQ_HDR + (size_t)HD_MQ_ROW * k;
+    mq_unpack(rp.data(), c, out, out_sender);
     return HD_OK;
 }
 
@@ -1262,6 +1415,13 @@ int hd_mq_consume(hd_mq* q, int64_t h, const uint8_t* allowed32, uint32_t n_allo
     if (allowed32 == nullptr && n_allowed != 0) return HD_EINVAL;
     *n_out = 0;
     if (n_removed) *n_removed = 0;
+    if (q->pf) {   // a staged window: served by the host while it still holds
+        if (!allowed32 && q->pf_adm_ver == q->ctx->adm_ver && h <= q->pf_max)
+            return pf_consume(q, h, out, out_sender, cap, n_out, n_removed);
+        (void)hipSetDevice(q->ctx->device);
+        const int rs = pf_sync(q);
+        if (rs) return rs;
+    }
     if (q->live == 0) return HD_OK;
     (void)hipSetDevice(q->ctx->device);
     hipStream_t s = q->ctx->stream;
@@ -1366,6 +1526,18 @@ int hd_mq_consume_votes(hd_mq* q, struct hd_votes* v, int64_t h, const uint8_t* 
 
 int hd_mq_drop_below(hd_mq* q, int64_t h) {
     if (!q) return HD_EINVAL;
+    if (q->pf) {
+        if (h - 1 <= q->pf_done) return HD_OK;   // nothing below h is left
+        if (h - 1 <= q->pf_max) {                // the window's heights (pf_done, h - 1] leave undelivered
+            const uint32_t j0 = (uint32_t)(q->pf_done - q->pf_dev), j1 = (uint32_t)(h - 1 - q->pf_dev);
+            q->live -= q->pf_start[j1] - q->pf_start[j0];
+            q->pf_done = h - 1;
+            return HD_OK;
+        }
+        (void)hipSetDevice(q->ctx->device);
+        const int rs = pf_sync(q);
+        if (rs) return rs;
+    }
     if (q->live == 0) return HD_OK;
     (void)hipSetDevice(q->ctx->device);
     hipStream_t s = q->ctx->stream;

@@ -51,7 +51,10 @@ struct DevSrc {
 
 // A NOT_ADMITTED recovery's key into the foreign-key dictionary (once per
 // From; a bucket another lane is writing is left alone -- learning is only an
-// optimisation) and, while reserved slots last, into its own table slot.
+// optimisation) and, while reserved slots last, into its own table slot.  A
+// From without a slot keeps its key in its bucket (fkey) and counts each
+// further recovery (fbhit, and the host-mapped fmiss flag), so that the host
+// can later hand it the slot of a colder key (fb_evict).
 __device__ void fdict_learn(const SlowCtl& ctl, const uint32_t from_be[8], const ge& q) {
     uint32_t* fd = ctl.fdict;
     uint32_t b = fdict_bucket(from_be);
@@ -65,6 +68,8 @@ __device__ void fdict_learn(const SlowCtl& ctl, const uint32_t from_be[8], const
                 ctl.fb_pub[slot] = q;
                 __threadfence();
                 atomicExch(&ctl.fb_state[slot], HD_FB_LEARNED);
+            } else if (ctl.fkey) {
+                ctl.fkey[b] = q;
             }
             HD_UNROLL for (int w = 0; w < 8; w++) fd[2u * HD_FD_BUCKETS + 8u * b + w] = from_be[w];
             fd[HD_FD_BUCKETS + b] = slot;
@@ -75,9 +80,22 @@ __device__ void fdict_learn(const SlowCtl& ctl, const uint32_t from_be[8], const
             return;
         }
         if (c != 2u) return;
+        // the bucket was written by a lane of this launch, possibly on another
+        // XCD: read it at device scope (a plain load may hit this XCD's L2
+        // line from before the write -- the From would not match and claim a
+        // second bucket, and a second slot)
         uint32_t diff = 0;
-        HD_UNROLL for (int w = 0; w < 8; w++) diff |= fd[2u * HD_FD_BUCKETS + 8u * b + w] ^ from_be[w];
-        if (!diff) return;
+        HD_UNROLL for (int w = 0; w < 8; w++)
+            diff |= __hip_atomic_load(&fd[2u * HD_FD_BUCKETS + 8u * b + w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ^
+                    from_be[w];
+        if (!diff) {
+            const uint32_t sl = __hip_atomic_load(&fd[HD_FD_BUCKETS + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (ctl.fbhit && sl == 0xFFFFFFFFu) {   // known, without a slot
+                atomicAdd(&ctl.fbhit[b], 1u);
+                __hip_atomic_store(ctl.fmiss, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            return;
+        }
     }
 }
 
@@ -360,6 +378,7 @@ int hd_set_signatories(hd_ctx* ctx, const uint8_t* sigs32, uint32_t n) {
     }
     if (e != hipSuccess) return hd_ctx_fail(ctx, e, "set_signatories upload");
     ctx->n_adm = m;
+    ctx->adm_ver++;
     ctx->adm_ix_mask = ix_slots - 1;
     ctx->n_sig_caller = n;
     int steps = 0;

@@ -111,11 +111,15 @@ class Ingress:
 
     def push_wires(self, parts, with_sig: bool = True):
         """Several wire buffers [(mtype, device byte buffer, n), ...] in
-        arrival order.  Each is unmarshalled and verified on one of two
-        streams, alternating, so the buffers' verify calls run concurrently on
-        the device (one call's fallback recoveries and inversion kernels leave
-        most SIMD slots to the other's); the mq inserts then follow in arrival
-        order.  Returns the verdicts of each buffer's complete records."""
+        arrival order.  Each is unmarshalled into its rows of one combined
+        device batch and verified on one of two streams, alternating, so the
+        buffers' verify calls run concurrently on the device (one call's
+        fallback recoveries and inversion kernels leave most SIMD slots to the
+        other's); the combined batch then goes into the mq with ONE insert
+        (arrival order is batch order: inserting the buffers one after another
+        keeps the same messages, hd_mq.h -- each insert re-sorts the whole
+        queue, so one insert instead of two saves a full sort and its host
+        round trips).  Returns the verdicts of each buffer's complete records."""
         torch = _torch()
         if not parts:
             return []
@@ -127,26 +131,39 @@ class Ingress:
         # buffers), not for each other: with the caller's stream being one of
         # the two, waiting on "the current stream" inside the loop would chain
         # each buffer's verification behind the previous one's
-        ready = torch.cuda.Event()
+        sizes = []
+        for mtype, buf, n in parts:
+            size = record_size(mtype, with_sig)
+            sizes.append(min(n, buf.numel() // size) if size else 0)
+        # each buffer's rows start at a multiple of 16 (unmarshal_device's
+        # 16-byte aligned sig rows); the rows between buffers keep verdict 0xFF,
+        # which the insert skips
+        total = sum((c + 15) // 16 * 16 for c in sizes)
+        every = DeviceBatch.empty(max(total, 1), str(dev))
+        verdicts = torch.full((max(total, 1),), 0xFF, dtype=torch.uint8, device=dev)
+        ready = torch.cuda.Event()   # after the fill above, on the same (current) stream
         ready.record(torch.cuda.current_stream(dev))
-        staged = []
-        for k, (mtype, buf, n) in enumerate(parts):
+        out, used, lo = [], [], 0
+        for k, ((mtype, buf, _), complete) in enumerate(zip(parts, sizes)):
+            if complete == 0:
+                out.append(torch.empty(0, dtype=torch.uint8, device=dev))
+                continue
             s = self._streams[k % 2]
             s.wait_event(ready)
-            size = record_size(mtype, with_sig)
-            complete = min(n, buf.numel() // size) if size else 0
-            if complete == 0:
-                staged.append((None, torch.empty(0, dtype=torch.uint8, device=dev), s))
-                continue
-            db, _ = unmarshal_device(self.v, mtype, buf, complete, with_sig, stream=s, sync=False, wait=False)
-            verdict = torch.empty(complete, dtype=torch.uint8, device=dev)
+            rows = every.rows(lo, complete)
+            db, _ = unmarshal_device(self.v, mtype, buf, complete, with_sig, stream=s, sync=False, out=rows,
+                                     wait=False)
+            verdict = verdicts[lo: lo + complete]
             self.v.authenticate_batch_device(db.c_struct(), verdict.data_ptr(), s.cuda_stream)
-            staged.append((db, verdict, s))
-        out = []
-        for db, verdict, s in staged:
-            if db is not None:
-                self.mq.insert_verified_device(db, verdict, self.height, stream=s)
             out.append(verdict)
+            used.append(s)
+            lo += (complete + 15) // 16 * 16
+        if used:
+            s0 = used[0]
+            for s in used[1:]:
+                if s is not s0:
+                    s0.wait_stream(s)
+            self.mq.insert_verified_device(every.rows(0, lo), verdicts[:lo], self.height, stream=s0)
         return out
 
     def flush(self) -> FlushResult:

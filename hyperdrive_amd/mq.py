@@ -172,8 +172,8 @@ class MessageQueue:
         self._check(rc, "hd_mq_consume_votes")
         k = int(got.value)
         self.last_removed = int(removed.value)
-        b = Batch(a["type"][:k].copy(), a["height"][:k].copy(), a["round"][:k].copy(), a["valid_round"][:k].copy(),
-                  a["value"][:k].copy(), a["frm"][:k].copy(), a["sig"][:k].copy())
+        b = Batch._wrap(a["type"][:k].copy(), a["height"][:k].copy(), a["round"][:k].copy(),
+                        a["valid_round"][:k].copy(), a["value"][:k].copy(), a["frm"][:k].copy(), a["sig"][:k].copy())
         return b, snd[:k].copy(), st[:k].copy(), dbl[:k].copy(), ev[:k].copy()
 
     def _vote_arrays(self):

@@ -81,6 +81,15 @@ class Batch:
         return len(self.type)
 
     @classmethod
+    def _wrap(cls, mtype, height, round_, valid_round, value, frm, sig) -> "Batch":
+        """Fields the library just wrote (contiguous, right dtypes and shapes):
+        no conversion pass (the per-flush result of the mq consume)."""
+        b = object.__new__(cls)
+        b.type, b.height, b.round, b.valid_round, b.value, b.frm, b.sig = (mtype, height, round_, valid_round, value,
+                                                                           frm, sig)
+        return b
+
+    @classmethod
     def from_lists(cls, mtype, height, round_, valid_round, value, frm, sig) -> "Batch":
         n = len(mtype)
         return cls(np.array(mtype, np.uint8), np.array(height, np.int64), np.array(round_, np.int64),
@@ -252,6 +261,14 @@ class Verifier:
         self._check(self._lib.hd_ctx_fastpath_stats(self._ctx, ctypes.byref(k), ctypes.byref(f)),
                     "hd_ctx_fastpath_stats")
         return int(k.value), int(f.value)
+
+    def foreign_stats(self) -> Tuple[int, int]:
+        """(foreign-key slots with built tables, slotless Froms promoted so far
+        into a colder foreign key's slot)."""
+        r, e = ctypes.c_uint32(), ctypes.c_uint32()
+        self._check(self._lib.hd_ctx_foreign_stats(self._ctx, ctypes.byref(r), ctypes.byref(e)),
+                    "hd_ctx_foreign_stats")
+        return int(r.value), int(e.value)
 
     def fastpath_geometry(self) -> Tuple[int, int, int]:
         """(G table windows, per-key table windows, messages sharing one

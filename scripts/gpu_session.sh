@@ -115,5 +115,10 @@ for step in "$@"; do
     tally_trace3) run tally_trace3 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/tally_trace3 -o run -- python3 scripts/tally_probe.py C3 40 ;;
     c3sync) run c3_sync 300 python -u scripts/c3_host_probe.py 40 ;;
     abhead) HD_LIB=hyperdrive_amd/_lib/var/libhd_r5c.so run bench_old_a 300 python bench.py --no-cpu --no-aux && run bench_new_a 300 python bench.py --no-cpu --no-aux && HD_LIB=hyperdrive_amd/_lib/var/libhd_r5c.so run bench_old_b 300 python bench.py --no-cpu --no-aux && run bench_new_b 300 python bench.py --no-cpu --no-aux ;;
+    ing5trace) run ing5trace 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ing5trace -o run -- python3 scripts/ingress_c5_run.py && run ing5 300 python scripts/ingress_c5_run.py ;;
+    c3trace_async) HD_BENCH_ASYNC_TALLY=1 run c3trace_async 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/c3trace_async -o run -- python3 scripts/c3_host_probe.py 20 ;;
+    evict) run pytest_evict 600 python -u -m pytest tests/test_gpu_verify.py tests/test_golden.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "foreign or evict or authenticate or matches_golden" ;;
+    mqpf) run pytest_mqpf 600 python -u -m pytest tests/test_mq.py tests/test_ingress.py tests/test_c1_network.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    mapprobe) run mapped_read_probe 120 scripts/mapped_read_probe ;;
   esac
 done

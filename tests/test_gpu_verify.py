@@ -275,6 +275,63 @@ def test_foreign_keys_vs_c_oracle(gpu, coracle):
         v.close()
 
 
+def _subset(hb, idx):
+    from hyperdrive_amd.verify import Batch
+    return Batch(hb.type[idx], hb.height[idx], hb.round[idx],
+                 None if hb.valid_round is None else hb.valid_round[idx], hb.value[idx], hb.frm[idx], hb.sig[idx])
+
+
+def test_foreign_slot_eviction(gpu, coracle):
+    """Foreign-key slots are not first come, first served for good: with 4
+    slots, 4 throwaway Froms (one NOT_ADMITTED message each) claim them first;
+    a fifth foreign sender with many messages then counts recoveries while it
+    has no slot, and a later call hands it the slot of the coldest throwaway
+    key (hd_fastverify.hip fb_evict), after which its messages take the
+    known-key check.  Every call's verdicts and recovered signatories equal
+    the C oracle; the throwaway keys' messages stay exact after losing their
+    slots."""
+    from hyperdrive_amd.device import generate
+    N, S = 65536, 100
+    v = gpu.Verifier(0)
+    try:
+        v.set_variant("foreign_keys", 4)
+        ks = v.gen_keys(S)
+        v.set_signatories(ks[0])
+        db, _, _ = generate(v, 0, N, S, 30, keys=ks)
+        hb = db.to_host()
+        cv, _ = coracle.verify(hb, ks[0], True, threads=16)
+        na = np.flatnonzero(cv == 6)                       # NOT_ADMITTED: authenticated foreign senders
+        froms = {}
+        for i in na.tolist():
+            froms.setdefault(hb.frm[i].tobytes(), []).append(i)
+        senders = sorted(froms.values(), key=len, reverse=True)
+        assert len(senders) >= 5 and len(senders[0]) >= 50, [len(x) for x in senders]
+        hot = senders[0]
+        junk = [x[0] for x in senders[1:5]]
+        valid = np.flatnonzero(cv == 0)[:4096].tolist()
+        first = _subset(hb, np.array(junk + valid))
+        fv, frec = coracle.verify(first, ks[0], True, threads=16)
+        for _ in range(3):                                 # the junk keys claim and build the 4 slots
+            r = v.verify_batch(first)
+            assert r.verdict.tolist() == fv.tolist() and r.recovered.tobytes() == frec.tobytes()
+        assert v.foreign_stats() == (4, 0)
+        second = _subset(hb, np.array(hot + valid))
+        sv, srec = coracle.verify(second, ks[0], True, threads=16)
+        falls = []
+        for _ in range(6):
+            r = v.verify_batch(second)
+            assert r.verdict.tolist() == sv.tolist() and r.recovered.tobytes() == srec.tobytes()
+            falls.append(v.fastpath_stats()[1])
+        ready, evicted = v.foreign_stats()
+        assert evicted == 1 and ready == 4, (ready, evicted, falls)
+        assert falls[0] >= len(hot) and falls[-1] == 0, falls   # the hot sender reached the known-key check
+        for _ in range(2):                                 # the evicted key's message: exact, via the recovery
+            r = v.verify_batch(first)
+            assert r.verdict.tolist() == fv.tolist() and r.recovered.tobytes() == frec.tobytes()
+    finally:
+        v.close()
+
+
 def test_fallback_burst_after_clean_batches(gpu, coracle):
     """The fallback kernels (k_slow_lift, k_verify over the leftover list) size
     their grids by the latest list length seen (hd_fastverify.hip

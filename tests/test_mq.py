@@ -275,6 +275,56 @@ def test_consume_uses_admitted_set_at_call(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_prefetched_consumes_match_oracle(gpu, seed):
+    """Consumes against the admitted set stage the next heights' window
+    (hd_mq.hip k_mq_consume1 prefetch) and serve the following consumes on
+    the host: every delivery, removed count and queue size still equals the
+    oracle through height-by-height flushes, skipped heights, consumes below
+    the last one, drops inside and past the window, inserts and admitted-set
+    changes between consumes (each of which ends the window)."""
+    from hyperdrive_amd.mq import MessageQueue
+    rng = np.random.default_rng(100 + seed)
+    keys = _senders(rng, 9)
+    v = gpu.Verifier(0)
+    adm = keys[:6]
+    v.set_signatories(adm)
+    q = MessageQueue(v, 40)
+    o = OracleMQ(40)
+    ids = {}
+    cur = 0
+    for step in range(60):
+        op = rng.random()
+        if step % 20 == 0 or op < 0.08:
+            db, d_ins, host, ins = _batch(rng, int(rng.integers(200, 2000)), keys, cur + 80, 3)
+            q.insert_device(db, d_ins)
+            for i, m in enumerate(host):
+                if ins[i]:
+                    o.insert(m[5], m)
+        elif op < 0.12:
+            adm = keys[rng.random(len(keys)) < 0.6]
+            v.set_signatories(adm)
+        elif op < 0.2:
+            hh = cur + int(rng.integers(-3, 90))
+            q.drop_below(hh)
+            o.drop_below(hh)
+        else:
+            r = rng.random()
+            cur = cur + (1 if r < 0.7 else int(rng.integers(-5, 20)))
+            b, sn = q.consume(cur)
+            n, want = o.consume(cur, allowed={k.tobytes() for k in adm})
+            _check_consumed(b, sn, want, ids)
+            assert q.last_removed == n, step
+        assert len(q) == len(o), step
+    b, sn = q.consume(10 ** 9)
+    n, want = o.consume(10 ** 9, allowed={k.tobytes() for k in adm})
+    _check_consumed(b, sn, want, ids)
+    assert len(q) == 0
+    q.close()
+    v.close()
+
+
+@pytest.mark.gpu
 def test_million_message_insert(verifier):
     """1M messages from 100 senders, cap 1000: every sender keeps its 1000
     smallest (height, round, arrival) messages, in that order."""

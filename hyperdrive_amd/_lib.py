@@ -108,7 +108,7 @@ SIGNATURES = {
     "hd_ctx_fastpath_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
                                              ctypes.POINTER(ctypes.c_uint32)]),
     "hd_ctx_foreign_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
-                                            ctypes.POINTER(ctypes.c_uint32)]),
+                                            ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
     "hd_ctx_fastpath_geometry": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
                                                 ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "hd_ctx_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),

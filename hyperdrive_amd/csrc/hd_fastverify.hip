@@ -140,6 +140,7 @@ struct FbWork {
     uint32_t fwait = 1, fcalls = 0;
     bool fforce = false;   // build the LEARNED slots at this call's end (an eviction re-keyed one)
     uint32_t evictions = 0;
+    uint32_t evict_checks = 0;   // fb_evict passes that waited for the context's calls
 };
 
 namespace {
@@ -1005,6 +1006,7 @@ int fb_evict(hd_ctx* ctx, bool* changed) {
     int rq = hd_fb_quiesce(ctx);
     if (rq) return rq;
     *miss = 0;
+    f->evict_checks++;
     hipStream_t s = ctx->stream;
     const uint32_t B = HD_FD_BUCKETS, R = f->fres;
     std::vector<uint32_t> fd(HD_FD_WORDS), hit(64 + B), st(R);
@@ -1588,10 +1590,11 @@ int hd_ctx_profile_read(hd_ctx* ctx, uint32_t* calls, double* verify_ms, uint32_
     return HD_OK;
 }
 
-int hd_ctx_foreign_stats(hd_ctx* ctx, uint32_t* ready_slots, uint32_t* evictions) {
+int hd_ctx_foreign_stats(hd_ctx* ctx, uint32_t* ready_slots, uint32_t* evictions, uint32_t* checks) {
     if (!ctx) return HD_EINVAL;
     if (ready_slots) *ready_slots = 0;
     if (evictions) *evictions = 0;
+    if (checks) *checks = 0;
     if (!ctx->fb) return HD_OK;
     (void)hipSetDevice(ctx->device);
     FbWork* f = ctx->fb;
@@ -1603,6 +1606,7 @@ int hd_ctx_foreign_stats(hd_ctx* ctx, uint32_t* ready_slots, uint32_t* evictions
         for (uint32_t v : st) *ready_slots += v == HD_FB_READY;
     }
     if (evictions) *evictions = f->evictions;
+    if (checks) *checks = f->evict_checks;
     return HD_OK;
 }
 

@@ -31,6 +31,7 @@
 // (process.go:838-843, 875-880).
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -553,6 +554,7 @@ __global__ __launch_bounds__(256) void k_tally_emit(DevBatch b, const uint32_t* 
         if (blockIdx.x == nb - 1) {
             stage_hdr[0] = og + blk[nb - 1];        // rounds (hr rows)
             stage_hdr[1] = oc + blk[2 * nb - 1];    // (round, type, value) groups
+            stage_hdr[2] = 0;                       // an async ticket's completion word (k_tally_signal)
         }
         if (blockIdx.x == 0) ctr->n_rounds = 0;     // k_tally_rounds' numbering, for the next call
     }
@@ -594,6 +596,15 @@ __global__ __launch_bounds__(256) void k_tally_emit(DevBatch b, const uint32_t* 
         const uint32_t rf = ref[q];
         if ((rf & HD_REF_HASHED) && D[rf & ~HD_REF_HASHED] == q) D[rf & ~HD_REF_HASHED] = kEmpty;   // the log's winner
     }
+}
+
+// An async tally's completion, after its download on the same stream: word 2
+// of the caller's pinned stage (mapped) becomes 1.  hd_tally_collect polls it
+// instead of synchronising an event: a thread blocked in hipEventSynchronize
+// slowed the verify launches of the submitting thread 4x (c3_host_probe,
+// HD_BENCH_ASYNC_TALLY=1: 0.18 ms per verify enqueue against 0.04).
+__global__ void k_tally_signal(uint32_t* word) {
+    if (threadIdx.x == 0) __hip_atomic_store(word, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // HD_TALLY_CHECK after k_tally_emit: the tables are clean again
@@ -1024,6 +1035,17 @@ static int tally_check_clean(hd_ctx* ctx, uint32_t cap, const uint32_t* tabs, Ta
 // dense cells are cleared by the round that takes them (k_tally_rounds), and
 // the bitmaps are written whole: nothing is cleared per call unless the
 // table capacity changed or an earlier call did not finish its launches.
+// the device address of an async stage's completion word (word 2), or NULL
+// when the stage is not mapped pinned memory (collect then waits on the event)
+static uint32_t* ticket_signal(void* stage) {
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, stage, 0) != hipSuccess || !dp) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return reinterpret_cast<uint32_t*>(dp) + 2;
+}
+
 static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdict, const uint32_t* d_bitmap,
                         Part part, hd_tally_out* out, hipStream_t s, const uint32_t* gidx = nullptr,
                         uint8_t* dup_global = nullptr, hd_tally_ticket* tk = nullptr) {
@@ -1164,8 +1186,11 @@ static int tally_device(hd_ctx* ctx, const hd_batch* hb, const uint8_t* d_verdic
         if (rc) return rc;
     }
     const size_t total = stage_bytes(H, Cg);
-    if (tk) {   // queued; hd_tally_collect waits for tk->done, then reads the stage
+    if (tk) {   // queued; hd_tally_collect waits for the signal (or tk->done), then reads the stage
+        // the completion word restarts at 0 (the stage's previous ticket was collected)
+        reinterpret_cast<volatile uint32_t*>(tk->stage)[2] = 0u;
         TCHK(hipMemcpyAsync(tk->stage, st, total, hipMemcpyDeviceToHost, s), "tally download");
+        if (uint32_t* sig = ticket_signal(tk->stage)) k_tally_signal<<<1, 64, 0, s>>>(sig);
         if (!tk->done) TCHK(hipEventCreateWithFlags((hipEvent_t*)&tk->done, hipEventDisableTiming), "tally event");
         TCHK(hipEventRecord((hipEvent_t)tk->done, s), "tally event record");
         return hd_ctx_note_stream(ctx, s);
@@ -1301,7 +1326,22 @@ int hd_tally_collect(hd_ctx* ctx, const hd_tally_ticket* ticket, hd_tally_out* o
     if (ticket->n == 0) return HD_OK;
     if (!ticket->stage || ticket->need == 0 || !ticket->done) return HD_EINVAL;
     (void)hipSetDevice(ctx->device);
-    TCHK(hipEventSynchronize((hipEvent_t)ticket->done), "tally collect wait");
+    if (ticket_signal(ticket->stage)) {
+        // poll the completion word without a HIP call per iteration; past
+        // ~0.2 s, wait for the event (a fault surfaces there) and read it once more
+        volatile const uint32_t* w = reinterpret_cast<volatile const uint32_t*>(ticket->stage) + 2;
+        const auto t0 = std::chrono::steady_clock::now();
+        while (*w != 1u) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+                TCHK(hipEventSynchronize((hipEvent_t)ticket->done), "tally collect wait");
+                if (*w != 1u) return hd_ctx_fail(ctx, hipErrorUnknown, "tally collect signal");
+                break;
+            }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+    } else {
+        TCHK(hipEventSynchronize((hipEvent_t)ticket->done), "tally collect wait");
+    }
     const char* st = (const char*)ticket->stage;
     const uint32_t n_hr = reinterpret_cast<const uint32_t*>(st)[0];
     const uint32_t n_cnt = reinterpret_cast<const uint32_t*>(st)[1];

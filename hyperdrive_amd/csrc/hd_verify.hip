@@ -80,16 +80,15 @@ __device__ void fdict_learn(const SlowCtl& ctl, const uint32_t from_be[8], const
             return;
         }
         if (c != 2u) return;
-        // the bucket was written by a lane of this launch, possibly on another
-        // XCD: read it at device scope (a plain load may hit this XCD's L2
-        // line from before the write -- the From would not match and claim a
-        // second bucket, and a second slot)
+        // the bucket may have been written by a lane of this launch on another
+        // XCD: read it with read-modify-write atomics, performed where the
+        // writer's release made it visible (a plain load may hit this XCD's
+        // L2 line from before the write -- the From would not match, claim a
+        // second bucket and a second slot).  Rare: the full recovery's leftovers.
         uint32_t diff = 0;
-        HD_UNROLL for (int w = 0; w < 8; w++)
-            diff |= __hip_atomic_load(&fd[2u * HD_FD_BUCKETS + 8u * b + w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ^
-                    from_be[w];
+        HD_UNROLL for (int w = 0; w < 8; w++) diff |= atomicAdd(&fd[2u * HD_FD_BUCKETS + 8u * b + w], 0u) ^ from_be[w];
         if (!diff) {
-            const uint32_t sl = __hip_atomic_load(&fd[HD_FD_BUCKETS + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t sl = atomicAdd(&fd[HD_FD_BUCKETS + b], 0u);
             if (ctl.fbhit && sl == 0xFFFFFFFFu) {   // known, without a slot
                 atomicAdd(&ctl.fbhit[b], 1u);
                 __hip_atomic_store(ctl.fmiss, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -195,7 +194,12 @@ int hd_dev_grow(hd_ctx* ctx, void** p, size_t* cap, size_t need) {
     if (*p) (void)hipFree(*p);
     *p = nullptr;
     *cap = 0;
-    size_t want = std::max(need, (size_t)4096);
+    // 1/8 slack: batches of nearly the same size (the two halves of a wire
+    // push, a partition's candidates) then share a buffer.  A regrow frees the
+    // old buffer, and hipFree waits for the whole device: in the ingress push
+    // it serialised the two concurrent verify calls until every scratch set
+    // had seen the larger half (profiles/round5: 0.23 ms host gap per push).
+    size_t want = std::max(need + need / 8, (size_t)4096);
     hipError_t e = hipMalloc(p, want);
     if (e != hipSuccess) return hd_ctx_fail(ctx, e, "hipMalloc");
     *cap = want;

@@ -262,13 +262,13 @@ class Verifier:
                     "hd_ctx_fastpath_stats")
         return int(k.value), int(f.value)
 
-    def foreign_stats(self) -> Tuple[int, int]:
+    def foreign_stats(self, checks: bool = False):
         """(foreign-key slots with built tables, slotless Froms promoted so far
-        into a colder foreign key's slot)."""
-        r, e = ctypes.c_uint32(), ctypes.c_uint32()
-        self._check(self._lib.hd_ctx_foreign_stats(self._ctx, ctypes.byref(r), ctypes.byref(e)),
+        into a colder foreign key's slot[, eviction checks so far])."""
+        r, e, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        self._check(self._lib.hd_ctx_foreign_stats(self._ctx, ctypes.byref(r), ctypes.byref(e), ctypes.byref(c)),
                     "hd_ctx_foreign_stats")
-        return int(r.value), int(e.value)
+        return (int(r.value), int(e.value), int(c.value)) if checks else (int(r.value), int(e.value))
 
     def fastpath_geometry(self) -> Tuple[int, int, int]:
         """(G table windows, per-key table windows, messages sharing one

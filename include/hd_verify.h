@@ -137,8 +137,9 @@ int hd_ctx_fastpath_stats(hd_ctx* ctx, uint32_t* known_keys, uint32_t* last_fall
  * tables are built; evictions = slotless Froms promoted so far into the slot
  * of a colder foreign key (a From with more recoveries since the last check
  * than twice the slot holder's known-key checks + 4; hd_fastverify.hip
- * fb_evict).  Either may be NULL; synchronises the context's calls. */
-int hd_ctx_foreign_stats(hd_ctx* ctx, uint32_t* ready_slots, uint32_t* evictions);
+ * fb_evict); checks = eviction checks so far (each waited for the context's
+ * earlier verify calls).  Any may be NULL; synchronises the context's calls. */
+int hd_ctx_foreign_stats(hd_ctx* ctx, uint32_t* ready_slots, uint32_t* evictions, uint32_t* checks);
 /* Shape of the known-key check as the context runs it now (for cost models):
  * g_windows / key_windows: fixed-base windows of the G table and of the
  * per-key tables (one table point each; the first is loaded, the rest are

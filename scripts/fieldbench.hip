@@ -10,6 +10,7 @@
 
 #include "../hyperdrive_amd/csrc/hd_group.h"
 #include "fe8_proto.h"
+#include "kara_proto.h"
 
 using namespace hd;
 
@@ -166,6 +167,7 @@ __global__ __launch_bounds__(256, 3) void k_bench(uint32_t iters, uint32_t* out)
         if (OP == 4) gej_add(p, p, pj);
         if (OP == 5) fe_normalize(a);
         if (OP == 6) { fe x = a; fe_inv_divsteps(a, x); }
+        if (OP == 10) fe_mul_kara(a, a, b);
     }
     if (OP == 8 || OP == 9) {   // 8 x 32-bit words with carry-out mads (hd_fe8.h)
         fe8 x, y;
@@ -192,8 +194,8 @@ __global__ __launch_bounds__(256, 3) void k_bench(uint32_t iters, uint32_t* out)
 }
 
 static const char* NAMES[] = {"fe_mul", "fe_sqr", "gej_dbl", "gej_add_ge", "gej_add", "fe_normalize", "fe_inv_divsteps",
-                              "f5_mul (FP64 FMA)", "fe8_mul", "fe8_sqr"};
-#define NOPS 10
+                              "f5_mul (FP64 FMA)", "fe8_mul", "fe8_sqr", "fe_mul_kara"};
+#define NOPS 11
 
 // f5_mul against fe_mul: a chain of `iters` products from the same seeds,
 // canonical results compared per lane (count of mismatching lanes)
@@ -265,6 +267,30 @@ __global__ __launch_bounds__(256) void k_fe8_check(uint32_t iters, uint32_t* bad
     if (d) atomicAdd(bad, 1u);
 }
 
+// fe_mul_kara against fe_mul: chains of `iters` products from the same seeds
+// (extremes on lane 0: p - 1), canonical results compared per lane
+__global__ __launch_bounds__(256) void k_kara_check(uint32_t iters, uint32_t* bad) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    fe a, b;
+    seed_fe(a, t * 7 + 1);
+    seed_fe(b, t * 13 + 5);
+    if (t == 0) {
+        for (int i = 0; i < 9; i++) a.n[i] = b.n[i] = fe_p_limb(i);
+        a.n[0] -= 1;
+        b.n[0] -= 1;
+    }
+    fe c = a;
+    for (uint32_t it = 0; it < iters; it++) {
+        fe_mul(a, a, b);
+        fe_mul_kara(c, c, b);
+    }
+    fe_normalize(a);
+    fe_normalize(c);
+    uint32_t d = 0;
+    for (int i = 0; i < 9; i++) d |= a.n[i] ^ c.n[i];
+    if (d) atomicAdd(bad, 1u);
+}
+
 template <int OP>
 static void run(int blocks, uint32_t iters, uint32_t* d, int ncu) {
     hipEvent_t e0, e1;
@@ -312,6 +338,10 @@ int main(int argc, char** argv) {
     (void)hipMemcpy(hb8, bad, 8, hipMemcpyDeviceToHost);
     printf("fe8 vs fe: %u of %d lanes differ after 64 chained products and squares; add/sub identity failures %u\n",
            hb8[0], ncu * 4 * 256, hb8[1]);
+    (void)hipMemset(bad, 0, 4);
+    k_kara_check<<<ncu * 4, 256>>>(64, bad);
+    (void)hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost);
+    printf("fe_mul_kara vs fe_mul: %u of %d lanes differ after 64 chained products\n", hb, ncu * 4 * 256);
     run_all<0>(ncu * wps, d, ncu);
     return 0;
 }

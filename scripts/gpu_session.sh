@@ -120,5 +120,6 @@ for step in "$@"; do
     evict) run pytest_evict 600 python -u -m pytest tests/test_gpu_verify.py tests/test_golden.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "foreign or evict or authenticate or matches_golden" ;;
     mqpf) run pytest_mqpf 600 python -u -m pytest tests/test_mq.py tests/test_ingress.py tests/test_c1_network.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     mapprobe) run mapped_read_probe 120 scripts/mapped_read_probe ;;
+    c3both) run c3_sync 300 python -u scripts/c3_host_probe.py 40 && HD_BENCH_ASYNC_TALLY=1 run c3_async 300 python -u scripts/c3_host_probe.py 40 ;;
   esac
 done

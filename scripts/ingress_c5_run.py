@@ -20,5 +20,6 @@ sigs, foreign = v.gen_keys(100)
 v.set_signatories(sigs)
 r = bench.ingress_c5(v, (sigs, foreign), 100, 1 << 20, ws, str(dev))
 r.pop("note", None)
+r["foreign_stats"] = v.foreign_stats(checks=True)
 print(json.dumps(r), flush=True)
 v.close()

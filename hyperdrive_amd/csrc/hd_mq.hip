@@ -570,7 +570,8 @@ __global__ __launch_bounds__(1024) void k_mq_consume1(uint32_t nsend, Pool p, ui
                                                       const uint32_t* __restrict__ send, int64_t h, uint32_t na,
                                                       const uint32_t* __restrict__ list, int be_words, Dict d,
                                                       uint32_t rows, uint32_t cap, uint8_t* __restrict__ stage,
-                                                      uint32_t seq, int64_t hpf, uint32_t pf_rows) {
+                                                      uint32_t seq, int64_t hpf, uint32_t pf_rows,
+                                                      uint32_t* __restrict__ win_meta) {
     typedef hipcub::BlockScan<uint32_t, 1024> Scan;
     typedef hipcub::BlockReduce<uint32_t, 1024> Red;
     __shared__ typename Scan::TempStorage ts;
@@ -661,24 +662,62 @@ __global__ __launch_bounds__(1024) void k_mq_consume1(uint32_t nsend, Pool p, ui
         }
         mq_row_put(out + (size_t)HD_MQ_ROW * k, p, lo_of[a] + (k - off[a]), 1u);
     }
-    uint8_t* win = out + (size_t)HD_MQ_ROW * nw;   // the window's rows follow the delivered ones
-    for (uint32_t k = t; k < np; k += 1024) {
+    if (win_meta) {   // the window's rows are written by k_mq_window_rows (many blocks)
+        if (t == 0) {
+            win_meta[0] = np;
+            win_meta[1] = nw;
+        }
+        if (t < nsend) {
+            win_meta[2 + t] = off2[t];
+            win_meta[2 + 1024 + t] = cut_of[t];
+            win_meta[2 + 2048 + t] = allow[t];
+        }
+    }
+    if (total <= cap && t < nsend) head[t] = cut;
+    if (seq || win_meta) {
+        // mapped host stage: every row and the header reach host memory
+        // before the sequence word the host spins on (written here, or by
+        // k_mq_signal after the window's rows)
+        __threadfence_system();
+        __syncthreads();
+        if (seq && t == 0)
+            __hip_atomic_store(reinterpret_cast<uint32_t*>(stage) + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// The prefetch window's rows (k_mq_consume1's plan in win_meta: count,
+// delivered rows before them, and per sender the window's offset, start and
+// allow flag), after the delivered rows of the stage; a grid of blocks, so
+// the 160-byte rows cross PCIe from many CUs instead of one.
+__global__ __launch_bounds__(256) void k_mq_window_rows(uint32_t nsend, Pool p, const uint32_t* __restrict__ win_meta,
+                                                        uint8_t* __restrict__ stage) {
+    __shared__ uint32_t o2[1024], co[1024], al[1024];
+    const uint32_t np = win_meta[0], nw = win_meta[1];
+    if (np == 0) return;
+    for (uint32_t t = threadIdx.x; t < nsend; t += blockDim.x) {
+        o2[t] = win_meta[2 + t];
+        co[t] = win_meta[2 + 1024 + t];
+        al[t] = win_meta[2 + 2048 + t];
+    }
+    __syncthreads();
+    uint8_t* win = stage + HD_MQ_HDR + (size_t)HD_MQ_ROW * nw;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < np; k += gridDim.x * blockDim.x) {
         uint32_t a = 0, b = nsend;
         while (b - a > 1) {
             const uint32_t m = (a + b) / 2;
-            if (off2[m] <= k) a = m;
+            if (o2[m] <= k) a = m;
             else b = m;
         }
-        mq_row_put(win + (size_t)HD_MQ_ROW * k, p, cut_of[a] + (k - off2[a]), allow[a]);
+        mq_row_put(win + (size_t)HD_MQ_ROW * k, p, co[a] + (k - o2[a]), al[a]);
     }
-    if (total <= cap && t < nsend) head[t] = cut;
-    if (seq) {
-        // mapped host stage: every row and the header reach host memory
-        // before the sequence word the host spins on
+    __threadfence_system();
+}
+
+// the mapped stage's sequence word, after every row of the consume (stream order)
+__global__ void k_mq_signal(uint8_t* __restrict__ stage, uint32_t seq) {
+    if (threadIdx.x == 0) {
         __threadfence_system();
-        __syncthreads();
-        if (t == 0) __hip_atomic_store(reinterpret_cast<uint32_t*>(stage) + 2, seq, __ATOMIC_RELEASE,
-                                       __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(stage) + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -735,7 +774,7 @@ int bits_of(uint64_t range) {
 
 enum MqSlot { MQ_FLAG, MQ_NEWIDX, MQ_NSEL, MQ_HK, MQ_RK, MQ_SK, MQ_PERM0, MQ_PERM1, MQ_K64A, MQ_K64B, MQ_K32A, MQ_K32B,
               MQ_HEAD, MQ_KEEP, MQ_SEL, MQ_RED, MQ_TMP, MQ_SID, MQ_LSLOT, MQ_LCLAIM, MQ_LID, MQ_REPS, MQ_ALLOW,
-              MQ_LIST, MQ_DELIV, MQ_SEL2, MQ_HEADS, MQ_SEND, MQ_NEWHEAD, MQ_OFF, MQ_TOT, MQ_STAGE, MQ__N };
+              MQ_LIST, MQ_DELIV, MQ_SEL2, MQ_HEADS, MQ_SEND, MQ_NEWHEAD, MQ_OFF, MQ_TOT, MQ_STAGE, MQ_WIN, MQ__N };
 
 struct hd_mq {
     hd_ctx* ctx = nullptr;
@@ -1330,9 +1369,15 @@ static int mq_consume1(hd_mq* q, int64_t h, const uint32_t* list, uint32_t na, i
             q->mstage_cap = want;
         }
         const uint32_t seq = ++q->seq ? q->seq : ++q->seq;   // never 0 (0 = no signal)
+        uint32_t* meta = pf ? (uint32_t*)qbuf(q, MQ_WIN, 4 * (2 + 3 * 1024), &rc) : nullptr;
+        if (rc) return rc;
         k_mq_consume1<<<1, 1024, 0, s>>>(q->nsend, q->pool, (uint32_t*)q->buf[MQ_HEADS].p,
                                          (const uint32_t*)q->buf[MQ_SEND].p, h, na, list, be, dict_of(q), rows, cap,
-                                         q->mstage_dev, seq, hpf, pf ? HD_MQ_PF_ROWS : 0u);
+                                         q->mstage_dev, pf ? 0u : seq, hpf, pf ? HD_MQ_PF_ROWS : 0u, meta);
+        if (pf) {
+            k_mq_window_rows<<<64, 256, 0, s>>>(q->nsend, q->pool, meta, q->mstage_dev);
+            k_mq_signal<<<1, 64, 0, s>>>(q->mstage_dev, seq);
+        }
         QCHK(hipGetLastError(), "k_mq_consume1");
         hs = (uint8_t*)q->mstage;
         volatile uint32_t* word = (volatile uint32_t*)hs + 2;
@@ -1371,7 +1416,7 @@ static int mq_consume1(hd_mq* q, int64_t h, const uint32_t* list, uint32_t na, i
         }
         k_mq_consume1<<<1, 1024, 0, s>>>(q->nsend, q->pool, (uint32_t*)q->buf[MQ_HEADS].p,
                                          (const uint32_t*)q->buf[MQ_SEND].p, h, na, list, be, dict_of(q), rows, cap,
-                                         dst, 0u, h, 0u);
+                                         dst, 0u, h, 0u, nullptr);
         QCHK(hipGetLastError(), "k_mq_consume1");
         const uint32_t guess = std::min(rows, std::max(64u, 2 * q->last_deliv));
         hs = (uint8_t*)q->hstage;

@@ -33,7 +33,6 @@ in one go; the reference may advance the height in the middle of a flush
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
 from typing import Optional
 
 import numpy as np
@@ -45,15 +44,34 @@ from .verify import PROPOSE, Batch, Verifier
 from .votes import VoteLog
 
 
-@dataclass
 class FlushResult:
-    consumed: Batch            # every message delivered (sender in procsAllowed), in consumption order
-    senders: np.ndarray        # int32 sender-queue id per delivered message (queue creation order)
-    vote_status: np.ndarray    # HD_VOTE_* per consumed message (NOT_VOTE for proposes)
-    double_of: np.ndarray      # batch index of the logged vote for DOUBLE, else votes.NO_INDEX
-    proposes: np.ndarray       # indices (into consumed) of the proposes, for the CPU
-    removed: int = 0           # messages consumed, delivered or dropped by procsAllowed (Consume's n)
-    events: Optional[np.ndarray] = None   # uint8 HD_VOTE_EV_* per consumed message (votes.EV_*), f known
+    """One flush's delivery.  consumed: every message delivered (sender in
+    procsAllowed), in consumption order; senders: int32 sender-queue id per
+    delivered message (queue creation order); vote_status: HD_VOTE_* per
+    consumed message (NOT_VOTE for proposes); double_of: batch index of the
+    logged vote for DOUBLE, else votes.NO_INDEX; proposes: indices (into
+    consumed) of the proposes, for the CPU (computed on first access);
+    removed: messages consumed, delivered or dropped by procsAllowed
+    (Consume's n); events: uint8 HD_VOTE_EV_* per consumed message
+    (votes.EV_*), f known.  (A plain slotted class: a flush per height builds
+    one, and a dataclass's init showed in the per-flush host time.)"""
+    __slots__ = ("consumed", "senders", "vote_status", "double_of", "removed", "events", "_proposes")
+
+    def __init__(self, consumed: Batch, senders: np.ndarray, vote_status: np.ndarray, double_of: np.ndarray,
+                 proposes: Optional[np.ndarray] = None, removed: int = 0, events: Optional[np.ndarray] = None):
+        self.consumed = consumed
+        self.senders = senders
+        self.vote_status = vote_status
+        self.double_of = double_of
+        self._proposes = proposes
+        self.removed = removed
+        self.events = events
+
+    @property
+    def proposes(self) -> np.ndarray:
+        if self._proposes is None:
+            self._proposes = np.flatnonzero(self.consumed.type == PROPOSE)
+        return self._proposes
 
 
 class Ingress:
@@ -169,11 +187,11 @@ class Ingress:
     def flush(self) -> FlushResult:
         """mq.Consume(CurrentHeight, ..., procsAllowed) with procsAllowed = the
         verifier's admitted set now, then the vote-log inserts."""
-        b, senders, status, double_of, events = self.mq.consume_votes(self.height, self.votes)
+        mq = self.mq
+        b, senders, status, double_of, events = mq.consume_votes(self.height, self.votes)
         self.votes.last_events = events
-        self._clean = (self.height, self.mq.inserts)
-        return FlushResult(b, senders, status, double_of, np.flatnonzero(b.type == PROPOSE), self.mq.last_removed,
-                           events)
+        self._clean = (self.height, mq.inserts)
+        return FlushResult(b, senders, status, double_of, None, mq.last_removed, events)
 
     def advance_height(self, height: int) -> None:
         """The Process's own height change after a commit (process.go:710-725:

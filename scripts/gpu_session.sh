@@ -121,5 +121,6 @@ for step in "$@"; do
     mqpf) run pytest_mqpf 600 python -u -m pytest tests/test_mq.py tests/test_ingress.py tests/test_c1_network.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     mapprobe) run mapped_read_probe 120 scripts/mapped_read_probe ;;
     c3both) run c3_sync 300 python -u scripts/c3_host_probe.py 40 && HD_BENCH_ASYNC_TALLY=1 run c3_async 300 python -u scripts/c3_host_probe.py 40 ;;
+    votesprobe) run votes_probe 120 python -u scripts/votes_probe.py ;;
   esac
 done

@@ -33,11 +33,27 @@ def work_stream(device=None, priority: int = 0):
     lower is higher, -1 = high) applies when the stream is first created: a
     high-priority verify stream keeps its workgroups ahead of side work (the
     tally of an earlier batch) queued on normal streams."""
+    return verify_streams(device, 1, priority)[0]
+
+
+def verify_streams(device=None, k: int = 2, priority: int = 0):
+    """work_stream(device) and the streams that verify beside it, k in all,
+    created together when the work stream is first made.  The runtime maps
+    streams onto the device's few hardware queues (GPU_MAX_HW_QUEUES, 4) round
+    robin in creation order, so streams created one after another get
+    different queues; a verify stream created later (after a tally stream, or
+    by another component) may share the work stream's queue and serialise
+    behind its kernels (the C5 ingress inside bench.py: push 2.84 ms against
+    2.30 ms standalone).  Every component that verifies beside the work
+    stream (bench.Pipeline, Ingress.push_wires) takes its streams from here."""
     torch = _torch()
     dev = torch.device("cuda", torch.cuda.current_device() if device is None else torch.device(device).index or 0)
-    if dev not in _STREAMS:
-        _STREAMS[dev] = torch.cuda.Stream(device=dev, priority=priority)
-    return _STREAMS[dev]
+    have = _STREAMS.setdefault(dev, [])
+    if not have:
+        have.extend(torch.cuda.Stream(device=dev, priority=priority) for _ in range(max(k, 3)))
+    while len(have) < k:
+        have.append(torch.cuda.Stream(device=dev, priority=have[0].priority))
+    return have[:k]
 
 
 @dataclass

@@ -38,7 +38,7 @@ from typing import Optional
 import numpy as np
 
 from .codec import record_size, unmarshal_device
-from .device import DeviceBatch, _torch, work_stream
+from .device import DeviceBatch, _torch, verify_streams, work_stream
 from .mq import MessageQueue
 from .verify import PROPOSE, Batch, Verifier
 from .votes import VoteLog
@@ -143,8 +143,7 @@ class Ingress:
             return []
         dev = parts[0][1].device
         if getattr(self, "_streams", None) is None or self._streams[0].device != dev:
-            s0 = work_stream(dev)
-            self._streams = [s0, torch.cuda.Stream(device=dev, priority=s0.priority)]
+            self._streams = verify_streams(dev, 2)
         # every stream waits for the caller's work queued so far (the wire
         # buffers), not for each other: with the caller's stream being one of
         # the two, waiting on "the current stream" inside the loop would chain

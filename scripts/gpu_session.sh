@@ -122,5 +122,7 @@ for step in "$@"; do
     mapprobe) run mapped_read_probe 120 scripts/mapped_read_probe ;;
     c3both) run c3_sync 300 python -u scripts/c3_host_probe.py 40 && HD_BENCH_ASYNC_TALLY=1 run c3_async 300 python -u scripts/c3_host_probe.py 40 ;;
     votesprobe) run votes_probe 120 python -u scripts/votes_probe.py ;;
+    flushtl) run flush_timeline 300 python -u scripts/flush_timeline.py ;;
+    bench_fast2) run bench_fast_a 300 python bench.py --no-cpu --no-aux && run bench_fast_b 300 python bench.py --no-cpu --no-aux ;;
   esac
 done

@@ -630,8 +630,9 @@ def main():
                                     "C2: batch-verify 1M Prevote/Precommit from 100 signatories + 2f+1 tally"),
                        "messages_per_gpu": B, "global_batch": total, "signatories": S, "adversarial_pct": args.adv,
                        "outputs_per_step": "verdict, recovered signatory, valid bitmap, tally",
-                       "parallelism": (f"shard-by-index x{world} (each rank holds only its shard); candidates routed "
-                                       f"to their round's owner by an RCCL all-to-all; owners' tables all-gathered"
+                       "parallelism": (f"shard-by-index x{world} (each rank holds, verifies and tallies only its "
+                                       f"shard); round sets all-gathered, only rounds held by several ranks routed "
+                                       f"to their owner (RCCL all-to-all); count rows all-gathered"
                                        if world > 1 else "one GPU")},
             "roofline": {
                 "bound": "valu",

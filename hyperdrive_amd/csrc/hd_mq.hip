@@ -210,12 +210,13 @@ __global__ void k_mq_newflag(uint32_t m, const uint32_t* __restrict__ lslot, con
     if (e < m) flag[e] = lslot[e] != kEmpty && lclaim[lslot[e]] == e;
 }
 // new sender k (batch order) gets id base + k
-__global__ void k_mq_assign(uint32_t r, const uint32_t* __restrict__ reps, const uint32_t* __restrict__ newidx,
+__global__ void k_mq_assign(const uint32_t* __restrict__ r_dev, const uint32_t* __restrict__ reps,
+                            const uint32_t* __restrict__ newidx,
                             const uint8_t* __restrict__ from32, uint32_t base, uint32_t* __restrict__ keys,
                             uint32_t* __restrict__ slots, uint32_t mask, uint64_t seed,
                             const uint32_t* __restrict__ lslot, uint32_t* __restrict__ lid) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= r) return;
+    if (k >= *r_dev) return;
     const uint32_t e = reps[k], id = base + k;
     uint4 a, b;
     load_key(from32 + 32 * (size_t)newidx[e], a, b);
@@ -338,7 +339,9 @@ __device__ __forceinline__ uint32_t ld_bytes(const uint8_t* p, uint32_t lo, uint
     for (uint32_t t = lo; t < hi; t++) v |= (uint32_t)p[t] << (8 * t);
     return v;
 }
-__global__ __launch_bounds__(256) void k_mq_gather(MqSrc s, uint32_t n, const uint32_t* __restrict__ sel, Pool d) {
+__global__ __launch_bounds__(256) void k_mq_gather(MqSrc s, uint32_t n, const uint32_t* __restrict__ sel, Pool d,
+                                                   const uint32_t* __restrict__ n_dev = nullptr) {
+    if (n_dev) n = *n_dev;   // the count on the device (the grid covers an upper bound)
     __shared__ uint32_t rows_lds[256 * 17];
     __shared__ uint8_t off_lds[256];
     const uint32_t tid = threadIdx.x;
@@ -417,7 +420,8 @@ __global__ __launch_bounds__(256) void k_mq_gather(MqSrc s, uint32_t n, const ui
 }
 
 __global__ void k_mq_compose(uint32_t n, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ sel,
-                             uint32_t* __restrict__ ids) {
+                             uint32_t* __restrict__ ids, const uint32_t* __restrict__ n_dev = nullptr) {
+    if (n_dev) n = *n_dev;
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k < n) ids[k] = perm[sel[k]];
 }
@@ -439,7 +443,8 @@ __global__ void k_mq_pred(uint32_t n, const int64_t* __restrict__ ph, const int3
 // per sender run of a freshly sorted pool: head = its first index, send = one
 // past its last (senders without messages keep 0, 0)
 __global__ void k_mq_runs(uint32_t M, const int32_t* __restrict__ snd, uint32_t* __restrict__ head,
-                          uint32_t* __restrict__ send) {
+                          uint32_t* __restrict__ send, const uint32_t* __restrict__ M_dev = nullptr) {
+    if (M_dev) M = *M_dev;
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= M) return;
     const int32_t s = snd[k];
@@ -843,11 +848,12 @@ static Dict dict_of(const hd_mq* q) { return Dict{q->keys, q->slots, q->tcap - 1
 // syncs before reading it), and with count == nullptr it is not downloaded
 // (a caller that knows it).  Counts queued together use different slots.
 static int select_idx(hd_mq* q, const uint8_t* flag, uint32_t n, uint32_t* out, uint32_t* count, hipStream_t s,
-                      int slot = 0, bool wait = true) {
+                      int slot = 0, bool wait = true, uint32_t** count_dev = nullptr) {
     int rc = 0;
     uint32_t* nsel = (uint32_t*)qbuf(q, MQ_NSEL, 64, &rc);
     if (rc) return rc;
     nsel += slot;
+    if (count_dev) *count_dev = nsel;
     hipcub::CountingInputIterator<uint32_t> iota(0);
     size_t need = 0;
     QCHK(hipcub::DeviceSelect::Flagged(nullptr, need, iota, flag, out, nsel, n, s), "select size");
@@ -860,7 +866,8 @@ static int select_idx(hd_mq* q, const uint8_t* flag, uint32_t n, uint32_t* out, 
 }
 
 static int key_ranges(hd_mq* q, uint32_t T, const int64_t* rk, const int64_t* hk, const uint32_t* sk, int64_t* rmn,
-                      int64_t* rmx, int64_t* hmn, int64_t* hmx, uint32_t* smx, hipStream_t s) {
+                      int64_t* rmx, int64_t* hmn, int64_t* hmx, uint32_t* smx, hipStream_t s,
+                      const uint32_t* extra_dev = nullptr, uint32_t* extra = nullptr) {
     int rc = 0;
     unsigned long long* red = (unsigned long long*)qbuf(q, MQ_RED, 5 * sizeof(uint64_t), &rc);
     if (rc) return rc;
@@ -870,6 +877,8 @@ static int key_ranges(hd_mq* q, uint32_t T, const int64_t* rk, const int64_t* hk
     QCHK(hipGetLastError(), "k_mq_minmax3");
     uint64_t host[5];
     QCHK(hipMemcpyAsync(host, red, sizeof(host), hipMemcpyDeviceToHost, s), "key ranges");
+    // a count queued earlier rides the same round trip (the new senders)
+    if (extra_dev) QCHK(hipMemcpyAsync(extra, extra_dev, 4, hipMemcpyDeviceToHost, s), "key ranges extra");
     QCHK(hipStreamSynchronize(s), "key ranges sync");
     const uint64_t sign = 0x8000000000000000ull;
     *rmn = (int64_t)(host[0] ^ sign);
@@ -974,8 +983,12 @@ static int keys_reserve(hd_mq* q, uint32_t n, hipStream_t s) {
 
 // sender ids of the m insertable messages (newidx), interning new Froms in
 // batch order
+// Sender ids of the m insertable messages (newidx), interning new Froms in
+// batch order.  The number of new senders stays on the device (*r_dev): the
+// caller reads it with its next download and then adds it to q->nsend (the
+// ids and keys are written for it here, with room for m new senders).
 static int intern_senders(hd_mq* q, const hd_batch* b, const uint32_t* newidx, uint32_t m, uint32_t** sid_out,
-                          hipStream_t s) {
+                          uint32_t** r_dev, hipStream_t s) {
     int rc = dict_reserve(q, m, s);
     if (rc) return rc;
     uint32_t lcap = 1024;
@@ -991,18 +1004,14 @@ static int intern_senders(hd_mq* q, const hd_batch* b, const uint32_t* newidx, u
     k_mq_lookup<<<nblk(m), 256, 0, s>>>(m, newidx, b->from32, dict_of(q), lclaim, lcap - 1, sid, lslot);
     k_mq_newflag<<<nblk(m), 256, 0, s>>>(m, lslot, lclaim, nflag);
     QCHK(hipGetLastError(), "mq lookup");
-    uint32_t r = 0;
-    rc = select_idx(q, nflag, m, reps, &r, s);
+    rc = select_idx(q, nflag, m, reps, nullptr, s, 1, false, r_dev);
     if (rc) return rc;
-    if (r) {
-        rc = keys_reserve(q, q->nsend + r, s);
-        if (rc) return rc;
-        k_mq_assign<<<nblk(r), 256, 0, s>>>(r, reps, newidx, b->from32, q->nsend, q->keys, q->slots, q->tcap - 1,
-                                            q->seed, lslot, lid);
-        k_mq_sid<<<nblk(m), 256, 0, s>>>(m, lslot, lid, sid);
-        QCHK(hipGetLastError(), "mq assign");
-        q->nsend += r;
-    }
+    rc = keys_reserve(q, q->nsend + m, s);
+    if (rc) return rc;
+    k_mq_assign<<<nblk(m), 256, 0, s>>>(*r_dev, reps, newidx, b->from32, q->nsend, q->keys, q->slots, q->tcap - 1,
+                                        q->seed, lslot, lid);
+    k_mq_sid<<<nblk(m), 256, 0, s>>>(m, lslot, lid, sid);
+    QCHK(hipGetLastError(), "mq assign");
     *sid_out = sid;
     return HD_OK;
 }
@@ -1023,7 +1032,8 @@ static int mq_compact(hd_mq* q, hipStream_t s) {
 }
 
 // per-sender runs of the (freshly sorted, compact) pool
-static int mq_runs(hd_mq* q, hipStream_t s) {
+// (n_dev: the pool's size is still on the device, at most q->pool.n)
+static int mq_runs(hd_mq* q, hipStream_t s, const uint32_t* n_dev = nullptr) {
     int rc = 0;
     const uint32_t ns = std::max(q->nsend, 1u);
     uint32_t* head = (uint32_t*)qbuf(q, MQ_HEADS, 4 * (size_t)ns, &rc);
@@ -1031,7 +1041,7 @@ static int mq_runs(hd_mq* q, hipStream_t s) {
     if (rc) return rc;
     QCHK(hipMemsetAsync(head, 0, 4 * (size_t)ns, s), "clear runs");
     QCHK(hipMemsetAsync(send, 0, 4 * (size_t)ns, s), "clear runs");
-    if (q->pool.n) k_mq_runs<<<nblk(q->pool.n), 256, 0, s>>>(q->pool.n, q->pool.sender, head, send);
+    if (q->pool.n) k_mq_runs<<<nblk(q->pool.n), 256, 0, s>>>(q->pool.n, q->pool.sender, head, send, n_dev);
     QCHK(hipGetLastError(), "k_mq_runs");
     q->runs_for = q->nsend;
     q->live = q->pool.n;
@@ -1053,7 +1063,8 @@ static int mq_insert_flagged(hd_mq* q, const hd_batch* d_batch, const uint8_t* f
     if (rc || m == 0) return rc;
     // 2. their sender queues (the From of each message)
     uint32_t* nsid = nullptr;
-    rc = intern_senders(q, d_batch, newidx, m, &nsid, s);
+    uint32_t* r_dev = nullptr;   // new senders: read with the key ranges below
+    rc = intern_senders(q, d_batch, newidx, m, &nsid, &r_dev, s);
     if (rc) return rc;
     // 3. merged sequence: pool (sorted) then the new messages (arrival order)
     const uint32_t M = q->pool.n, T = M + m;
@@ -1071,8 +1082,9 @@ static int mq_insert_flagged(hd_mq* q, const hd_batch* d_batch, const uint8_t* f
     //    stability keeps arrival order among equal keys)
     //    (the three keys' ranges in one reduction and one host round trip)
     int64_t rmn, rmx, hmn, hmx;
-    uint32_t smx;
-    if ((rc = key_ranges(q, T, rk, hk, sk, &rmn, &rmx, &hmn, &hmx, &smx, s))) return rc;
+    uint32_t smx, r = 0;
+    if ((rc = key_ranges(q, T, rk, hk, sk, &rmn, &rmx, &hmn, &hmx, &smx, s, r_dev, &r))) return rc;
+    q->nsend += r;
     hipcub::DoubleBuffer<uint32_t> perm(p0, p1);
     const int rb = bits_of((uint64_t)rmx - (uint64_t)rmn), hb = bits_of((uint64_t)hmx - (uint64_t)hmn),
               sb = bits_of(smx);
@@ -1110,21 +1122,32 @@ static int mq_insert_flagged(hd_mq* q, const hd_batch* d_batch, const uint8_t* f
         QCHK(hipcub::DeviceScan::InclusiveScan(tmp, need, head, head, hipcub::Max(), T, s), "scan heads");
     }
     k_mq_keep<<<nblk(T), 256, 0, s>>>(T, head, q->max_cap, keep);
-    uint32_t kept = 0;
-    rc = select_idx(q, keep, T, sel, &kept, s);
+    // the kept count stays on the device: compose, gather and the runs cover
+    // T entries and stop at it; it comes back with the final synchronisation
+    uint32_t* kept_dev = nullptr;
+    rc = select_idx(q, keep, T, sel, nullptr, s, 3, false, &kept_dev);
     if (rc) return rc;
     // sel holds kept positions in sorted order -> element ids -> new pool
     uint32_t* ids = head;  // head is consumed by k_mq_keep; reuse its space
-    k_mq_compose<<<nblk(kept), 256, 0, s>>>(kept, perm.Current(), sel, ids);
-    rc = pool_reserve(q->ctx, q->spare, std::max(kept, 1u));
+    k_mq_compose<<<nblk(T), 256, 0, s>>>(T, perm.Current(), sel, ids, kept_dev);
+    rc = pool_reserve(q->ctx, q->spare, std::max(T, 1u));
     if (rc) return rc;
-    k_mq_gather<<<nblk(kept), 256, 0, s>>>(src, kept, ids, q->spare);
+    k_mq_gather<<<nblk(T), 256, 0, s>>>(src, T, ids, q->spare, kept_dev);
     QCHK(hipGetLastError(), "mq insert kernels");
     std::swap(q->pool, q->spare);
-    q->pool.n = kept;
-    rc = mq_runs(q, s);
+    q->pool.n = T;   // an upper bound until the count arrives
+    rc = mq_runs(q, s, kept_dev);
     if (rc) return rc;
+    uint32_t* kh = (uint32_t*)q->hstage;
+    if (q->hstage_cap < 64) {
+        QCHK(hipHostMalloc(&q->hstage, 1u << 16, hipHostMallocDefault), "mq host stage");
+        q->hstage_cap = 1u << 16;
+        kh = (uint32_t*)q->hstage;
+    }
+    QCHK(hipMemcpyAsync(kh, kept_dev, 4, hipMemcpyDeviceToHost, s), "kept count");
     QCHK(hipStreamSynchronize(s), "mq insert sync");
+    q->pool.n = kh[0];
+    q->live = q->pool.n;
     return HD_OK;
 }
 

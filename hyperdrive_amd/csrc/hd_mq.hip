@@ -1337,7 +1337,7 @@ static int pf_consume(hd_mq* q, int64_t h, const hd_batch_out* out, int32_t* out
     *n_out = 0;
     if (n_removed) *n_removed = 0;
     if (h <= q->pf_done) return HD_OK;
-    const uint32_t j0 = (uint32_t)(q->pf_done - q->pf_dev) - 0u, j1 = (uint32_t)(h - q->pf_dev);
+    const uint32_t j0 = (uint32_t)(q->pf_done - q->pf_dev), j1 = (uint32_t)(h - q->pf_dev);
     // heights (pf_done, h] are buckets j0 .. j1 - 1 (bucket j = height pf_dev + 1 + j)
     std::vector<uint32_t> ids(q->pf_idx.begin() + q->pf_start[j0], q->pf_idx.begin() + q->pf_start[j1]);
     if (j1 - j0 > 1) std::sort(ids.begin(), ids.end());   // several heights: back to queue order

@@ -126,6 +126,7 @@ for step in "$@"; do
     bench_fast2) run bench_fast_a 300 python bench.py --no-cpu --no-aux && run bench_fast_b 300 python bench.py --no-cpu --no-aux ;;
     abchunk) run ing_c0a 300 python scripts/ingress_c5_run.py && HD_INGRESS_CHUNK=262144 run ing_c256a 300 python scripts/ingress_c5_run.py && HD_INGRESS_CHUNK=131072 run ing_c128a 300 python scripts/ingress_c5_run.py && run ing_c0b 300 python scripts/ingress_c5_run.py && HD_INGRESS_CHUNK=262144 run ing_c256b 300 python scripts/ingress_c5_run.py && HD_INGRESS_CHUNK=131072 run ing_c128b 300 python scripts/ingress_c5_run.py ;;
     abcur) run ab_cur 600 bash scripts/gpu_ab_prof.sh "cur:X=1" "cur5:AB_ADV=30" ;;
+    abonecall) run ing_two_a 300 python scripts/ingress_c5_run.py && HD_ING_ONECALL=1 run ing_one_a 300 python scripts/ingress_c5_run.py && run bench_two 300 python bench.py --no-cpu --no-aux && HD_ING_ONECALL=1 run bench_one 300 python bench.py --no-cpu --no-aux && run ing_two_b 300 python scripts/ingress_c5_run.py && HD_ING_ONECALL=1 run ing_one_b 300 python scripts/ingress_c5_run.py ;;
     abingorder) run bench_ing_first_a 300 python bench.py --no-cpu --no-aux && HD_BENCH_INGRESS_LAST=1 run bench_ing_last_a 300 python bench.py --no-cpu --no-aux && run bench_ing_first_b 300 python bench.py --no-cpu --no-aux && HD_BENCH_INGRESS_LAST=1 run bench_ing_last_b 300 python bench.py --no-cpu --no-aux ;;
   esac
 done

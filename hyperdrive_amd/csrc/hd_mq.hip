@@ -808,6 +808,11 @@ struct hd_mq {
     size_t mstage_cap = 0;
     uint32_t seq = 0;
     bool mapped = true;
+    // mapped reply block of the insert's host round trips (mq_reply): word 0
+    // is the sequence word, the values follow
+    uint32_t* rep = nullptr;
+    uint32_t* rep_dev = nullptr;
+    uint32_t rep_seq = 0;
     // Consume prefetch (mapped path): a consume of height h also stages the
     // rows of the heights (h, h + pf_win] (k_mq_consume1); while nothing is
     // inserted, the admitted set stays and the consumes stay inside that
@@ -847,6 +852,64 @@ static Dict dict_of(const hd_mq* q) { return Dict{q->keys, q->slots, q->tcap - 1
 // stream sync when wait is set; with wait unset it is only queued (the caller
 // syncs before reading it), and with count == nullptr it is not downloaded
 // (a caller that knows it).  Counts queued together use different slots.
+// The insert's host round trips (the insertable count; the key ranges with
+// the new senders; the kept count).  One thread per word copies device words
+// into the mapped reply block, then the sequence word follows (system fence,
+// release store), and the host spins on it.  In the C5 insert trace each
+// round trip through a download into host memory and hipStreamSynchronize
+// left the stream idle ~40 us (the copy, the host's wake-up, the next launch).
+#define HD_MQ_REPLY_WORDS 16
+struct ReplySrc {
+    const uint32_t* p[HD_MQ_REPLY_WORDS];
+    uint32_t n;
+};
+__global__ void k_mq_reply(ReplySrc src, uint32_t* __restrict__ rep, uint32_t seq) {
+    const uint32_t t = threadIdx.x;
+    const uint32_t* w = nullptr;
+#pragma unroll
+    for (uint32_t k = 0; k < HD_MQ_REPLY_WORDS; k++)
+        if (t == k) w = src.p[k];
+    // the words were written by earlier kernels, some by atomics (the key
+    // ranges): a read-modify-write reads them where the atomics landed
+    if (t < src.n) rep[1 + t] = atomicAdd(const_cast<uint32_t*>(w), 0u);
+    __threadfence_system();
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(rep, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Queue the reply of n device words (stream order) and wait for it; out[k] =
+// *words[k].  Past ~0.2 s the stream is synchronised (a fault surfaces there).
+static int mq_reply(hd_mq* q, hipStream_t s, const uint32_t* const* words, uint32_t n, uint32_t* out) {
+    if (!q->rep) {
+        void* h = nullptr;
+        QCHK(hipHostMalloc(&h, 4 * (1 + HD_MQ_REPLY_WORDS) + 64, hipHostMallocMapped | hipHostMallocCoherent),
+             "mq reply block");
+        q->rep = (uint32_t*)h;
+        void* d = nullptr;
+        QCHK(hipHostGetDevicePointer(&d, h, 0), "mq reply pointer");
+        q->rep_dev = (uint32_t*)d;
+        q->rep[0] = 0;
+    }
+    ReplySrc src{};
+    for (uint32_t k = 0; k < n; k++) src.p[k] = words[k];
+    src.n = n;
+    const uint32_t seq = ++q->rep_seq ? q->rep_seq : ++q->rep_seq;   // never 0
+    k_mq_reply<<<1, 64, 0, s>>>(src, q->rep_dev, seq);
+    QCHK(hipGetLastError(), "k_mq_reply");
+    volatile uint32_t* word = q->rep;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (*word != seq) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+            QCHK(hipStreamSynchronize(s), "mq reply sync");
+            if (*word != seq) return hd_ctx_fail(q->ctx, hipErrorUnknown, "mq reply signal");
+            break;
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    for (uint32_t k = 0; k < n; k++) out[k] = ((volatile uint32_t*)q->rep)[1 + k];
+    return HD_OK;
+}
+
 static int select_idx(hd_mq* q, const uint8_t* flag, uint32_t n, uint32_t* out, uint32_t* count, hipStream_t s,
                       int slot = 0, bool wait = true, uint32_t** count_dev = nullptr) {
     int rc = 0;
@@ -860,14 +923,18 @@ static int select_idx(hd_mq* q, const uint8_t* flag, uint32_t n, uint32_t* out, 
     void* tmp = qbuf(q, MQ_TMP, need, &rc);
     if (rc) return rc;
     QCHK(hipcub::DeviceSelect::Flagged(tmp, need, iota, flag, out, nsel, n, s), "select");
+    if (count && wait) {
+        const uint32_t* w[1] = {nsel};
+        return mq_reply(q, s, w, 1, count);
+    }
     if (count) QCHK(hipMemcpyAsync(count, nsel, 4, hipMemcpyDeviceToHost, s), "select count");
-    if (count && wait) QCHK(hipStreamSynchronize(s), "select sync");
     return HD_OK;
 }
 
-static int key_ranges(hd_mq* q, uint32_t T, const int64_t* rk, const int64_t* hk, const uint32_t* sk, int64_t* rmn,
-                      int64_t* rmx, int64_t* hmn, int64_t* hmx, uint32_t* smx, hipStream_t s,
-                      const uint32_t* extra_dev = nullptr, uint32_t* extra = nullptr) {
+// min / max of the three sort keys (k_mq_minmax3) into the device words
+// *red; key_ranges_read brings them back with counts queued meanwhile
+static int key_ranges_launch(hd_mq* q, uint32_t T, const int64_t* rk, const int64_t* hk, const uint32_t* sk,
+                             hipStream_t s, unsigned long long** red_out) {
     int rc = 0;
     unsigned long long* red = (unsigned long long*)qbuf(q, MQ_RED, 5 * sizeof(uint64_t), &rc);
     if (rc) return rc;
@@ -875,11 +942,25 @@ static int key_ranges(hd_mq* q, uint32_t T, const int64_t* rk, const int64_t* hk
     const uint32_t blocks = std::min(nblk(T), 256u);
     k_mq_minmax3<<<blocks, 256, 0, s>>>(T, rk, hk, sk, red);
     QCHK(hipGetLastError(), "k_mq_minmax3");
+    *red_out = red;
+    return HD_OK;
+}
+
+// the key ranges and n_extra device counts queued earlier (the new senders,
+// the prefilter's survivors) in one round trip
+static int key_ranges_read(hd_mq* q, const unsigned long long* red, hipStream_t s, int64_t* rmn, int64_t* rmx,
+                           int64_t* hmn, int64_t* hmx, uint32_t* smx, const uint32_t* const* extra_dev,
+                           uint32_t n_extra, uint32_t* extra) {
+    // the five 64-bit reductions as ten words, then the counts
+    const uint32_t* w[HD_MQ_REPLY_WORDS];
+    for (int k = 0; k < 10; k++) w[k] = (const uint32_t*)red + k;
+    for (uint32_t k = 0; k < n_extra; k++) w[10 + k] = extra_dev[k];
+    uint32_t got[HD_MQ_REPLY_WORDS];
+    const int rc = mq_reply(q, s, w, 10 + n_extra, got);
+    if (rc) return rc;
     uint64_t host[5];
-    QCHK(hipMemcpyAsync(host, red, sizeof(host), hipMemcpyDeviceToHost, s), "key ranges");
-    // a count queued earlier rides the same round trip (the new senders)
-    if (extra_dev) QCHK(hipMemcpyAsync(extra, extra_dev, 4, hipMemcpyDeviceToHost, s), "key ranges extra");
-    QCHK(hipStreamSynchronize(s), "key ranges sync");
+    memcpy(host, got, sizeof(host));
+    for (uint32_t k = 0; k < n_extra; k++) extra[k] = got[10 + k];
     const uint64_t sign = 0x8000000000000000ull;
     *rmn = (int64_t)(host[0] ^ sign);
     *rmx = (int64_t)(~host[1] ^ sign);
@@ -887,6 +968,27 @@ static int key_ranges(hd_mq* q, uint32_t T, const int64_t* rk, const int64_t* hk
     *hmx = (int64_t)(~host[3] ^ sign);
     *smx = (uint32_t)~host[4];
     return HD_OK;
+}
+
+// Stable radix sort of (key, perm) pairs on bits [0, bits) of the key.
+// rocprim's default dispatch takes its merge-sort path up to 2^20 items, and
+// that path ignores the bit range: ~10 block-merge rounds of two kernels each
+// (~210 us for a C5 insert of 855k pairs).  A merge-sort limit of 0 sends
+// every size above one block to the onesweep path, which sorts only the
+// digits the range covers (a 20-bit (sender, height, round) key: 3 passes).
+typedef rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config, 0>
+    OnesweepSort;
+template <class K>
+static hipError_t sort_pairs_bits(void* tmp, size_t& need, hipcub::DoubleBuffer<K>& keys,
+                                  hipcub::DoubleBuffer<uint32_t>& perm, uint32_t n, int bits, hipStream_t s) {
+    rocprim::double_buffer<K> k(keys.Current(), keys.Alternate());
+    rocprim::double_buffer<uint32_t> v(perm.Current(), perm.Alternate());
+    const hipError_t e = rocprim::radix_sort_pairs<OnesweepSort>(tmp, need, k, v, n, 0u, (unsigned)bits, s);
+    if (tmp && e == hipSuccess) {
+        if (k.current() != keys.Current()) keys.selector ^= 1;
+        if (v.current() != perm.Current()) perm.selector ^= 1;
+    }
+    return e;
 }
 
 // stable sort of perm (DoubleBuffer) by a 64-bit field rebased to its min
@@ -901,10 +1003,10 @@ static int sort_pass64(hd_mq* q, hipcub::DoubleBuffer<uint32_t>& perm, const int
     k_mq_rekey64<<<nblk(T), 256, 0, s>>>(T, perm.Current(), field, mn, ka);
     hipcub::DoubleBuffer<uint64_t> keys(ka, kb);
     size_t need = 0;
-    QCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, need, keys, perm, T, 0, bits, s), "sort size");
+    QCHK(sort_pairs_bits(nullptr, need, keys, perm, T, bits, s), "sort size");
     void* tmp = qbuf(q, MQ_TMP, need, &rc);
     if (rc) return rc;
-    QCHK(hipcub::DeviceRadixSort::SortPairs(tmp, need, keys, perm, T, 0, bits, s), "sort 64");
+    QCHK(sort_pairs_bits(tmp, need, keys, perm, T, bits, s), "sort 64");
     return HD_OK;
 }
 
@@ -919,10 +1021,10 @@ static int sort_pass32(hd_mq* q, hipcub::DoubleBuffer<uint32_t>& perm, const uin
     k_mq_rekey32<<<nblk(T), 256, 0, s>>>(T, perm.Current(), field, ka);
     hipcub::DoubleBuffer<uint32_t> keys(ka, kb);
     size_t need = 0;
-    QCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, need, keys, perm, T, 0, bits, s), "sort size");
+    QCHK(sort_pairs_bits(nullptr, need, keys, perm, T, bits, s), "sort size");
     void* tmp = qbuf(q, MQ_TMP, need, &rc);
     if (rc) return rc;
-    QCHK(hipcub::DeviceRadixSort::SortPairs(tmp, need, keys, perm, T, 0, bits, s), "sort 32");
+    QCHK(sort_pairs_bits(tmp, need, keys, perm, T, bits, s), "sort 32");
     return HD_OK;
 }
 
@@ -1080,10 +1182,12 @@ static int mq_insert_flagged(hd_mq* q, const hd_batch* d_batch, const uint8_t* f
     k_mq_keys<<<nblk(T), 256, 0, s>>>(src, T, hk, rk, sk, p0);
     // 4. stable LSD passes: round, height, sender (mq.go:120-128 order; the
     //    stability keeps arrival order among equal keys)
-    //    (the three keys' ranges in one reduction and one host round trip)
+    //    (the three keys' ranges and the new senders in one host round trip)
+    unsigned long long* red = nullptr;
+    if ((rc = key_ranges_launch(q, T, rk, hk, sk, s, &red))) return rc;
     int64_t rmn, rmx, hmn, hmx;
     uint32_t smx, r = 0;
-    if ((rc = key_ranges(q, T, rk, hk, sk, &rmn, &rmx, &hmn, &hmx, &smx, s, r_dev, &r))) return rc;
+    if ((rc = key_ranges_read(q, red, s, &rmn, &rmx, &hmn, &hmx, &smx, &r_dev, 1, &r))) return rc;
     q->nsend += r;
     hipcub::DoubleBuffer<uint32_t> perm(p0, p1);
     const int rb = bits_of((uint64_t)rmx - (uint64_t)rmn), hb = bits_of((uint64_t)hmx - (uint64_t)hmn),
@@ -1098,10 +1202,10 @@ static int mq_insert_flagged(hd_mq* q, const hd_batch* d_batch, const uint8_t* f
             k_mq_combine<<<nblk(T), 256, 0, s>>>(T, rk, hk, sk, rmn, hmn, rb, hb, ka);
             hipcub::DoubleBuffer<uint64_t> keys(ka, kb);
             size_t need = 0;
-            QCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, need, keys, perm, T, 0, rb + hb + sb, s), "sort size");
+            QCHK(sort_pairs_bits(nullptr, need, keys, perm, T, rb + hb + sb, s), "sort size");
             void* tmp = qbuf(q, MQ_TMP, need, &rc);
             if (rc) return rc;
-            QCHK(hipcub::DeviceRadixSort::SortPairs(tmp, need, keys, perm, T, 0, rb + hb + sb, s), "sort keys");
+            QCHK(sort_pairs_bits(tmp, need, keys, perm, T, rb + hb + sb, s), "sort keys");
         }
     } else {
         if ((rc = sort_pass64(q, perm, rk, T, s, rmn, rmx))) return rc;
@@ -1138,15 +1242,10 @@ static int mq_insert_flagged(hd_mq* q, const hd_batch* d_batch, const uint8_t* f
     q->pool.n = T;   // an upper bound until the count arrives
     rc = mq_runs(q, s, kept_dev);
     if (rc) return rc;
-    uint32_t* kh = (uint32_t*)q->hstage;
-    if (q->hstage_cap < 64) {
-        QCHK(hipHostMalloc(&q->hstage, 1u << 16, hipHostMallocDefault), "mq host stage");
-        q->hstage_cap = 1u << 16;
-        kh = (uint32_t*)q->hstage;
-    }
-    QCHK(hipMemcpyAsync(kh, kept_dev, 4, hipMemcpyDeviceToHost, s), "kept count");
-    QCHK(hipStreamSynchronize(s), "mq insert sync");
-    q->pool.n = kh[0];
+    uint32_t kept = 0;
+    const uint32_t* w[1] = {kept_dev};
+    if ((rc = mq_reply(q, s, w, 1, &kept))) return rc;
+    q->pool.n = kept;
     q->live = q->pool.n;
     return HD_OK;
 }
@@ -1178,6 +1277,7 @@ int hd_mq_destroy(hd_mq* q) {
         if (b.p) (void)hipFree(b.p);
     if (q->hstage) (void)hipHostFree(q->hstage);
     if (q->mstage) (void)hipHostFree(q->mstage);
+    if (q->rep) (void)hipHostFree(q->rep);
     delete q;
     return HD_OK;
 }

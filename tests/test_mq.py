@@ -355,6 +355,47 @@ def test_million_message_insert(verifier):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cap,S,span", [(1, 50, 1 << 40), (7, 300, 3), (300, 120, 1 << 62), (5, 5000, 100)])
+def test_large_inserts_match_restatement(verifier, cap, S, span):
+    """Two 70,000-message inserts into one queue (the second merges with the
+    sorted pool), heights over a span of 3 (all ties: arrival order decides),
+    100, 2^40 and 2^62 (a packed key wider than 64 bits: the three-pass
+    sort), 50 to 5,000 senders.  The queue keeps, per sender, the first `cap`
+    messages by (height, round, arrival) over both batches together."""
+    import torch
+    from hyperdrive_amd.device import DeviceBatch
+    from hyperdrive_amd.mq import MessageQueue
+    rng = np.random.default_rng(cap * 7919 + S)
+    keys = _senders(rng, S)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    q = MessageQueue(verifier, cap)
+    n = 70000
+    hs, rs, ss = [], [], []
+    for step in range(2):
+        lo = -(span // 2)
+        h = (lo + rng.integers(0, span, n)).astype(np.int64)
+        r = rng.integers(-1, 3, n).astype(np.int64)
+        snd = (np.arange(n) % S) if step == 0 else rng.integers(0, S, n)
+        tag = np.zeros((n, 32), np.uint8)
+        tag[:, :4] = (np.arange(n, dtype=np.uint32) + step * n).view(np.uint8).reshape(n, 4)
+        db = DeviceBatch(n, t(np.full(n, 2, np.uint8)), t(h), t(r), t(np.full(n, -1, np.int64)), t(tag),
+                         t(keys[snd]), t(np.zeros((n, 65), np.uint8)))
+        q.insert_device(db)
+        hs.append(h)
+        rs.append(r)
+        ss.append(snd)
+    h, r, snd = np.concatenate(hs), np.concatenate(rs), np.concatenate(ss)
+    order = np.lexsort((np.arange(2 * n), r, h, snd))
+    keep = np.concatenate([order[snd[order] == k][:cap] for k in range(S)])
+    assert len(q) == len(keep) and q.senders == S
+    b, s = q.consume((1 << 63) - 1, keys)
+    idx = b.value[:, :4].copy().view(np.uint32).ravel()
+    assert idx.tolist() == keep.tolist()
+    assert s.tolist() == snd[keep].tolist()
+    q.close()
+
+
+@pytest.mark.gpu
 def test_extreme_keys_and_empty_inputs(verifier):
     """int64-extreme heights / rounds (InvalidRound = -1, negative and maximal
     values) order exactly like the restatement; empty batches, batches with no

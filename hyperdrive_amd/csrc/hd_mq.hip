@@ -693,10 +693,15 @@ __global__ __launch_bounds__(1024) void k_mq_consume1(uint32_t nsend, Pool p, ui
 // The prefetch window's rows (k_mq_consume1's plan in win_meta: count,
 // delivered rows before them, and per sender the window's offset, start and
 // allow flag), after the delivered rows of the stage; a grid of blocks, so
-// the 160-byte rows cross PCIe from many CUs instead of one.
+// the 160-byte rows cross PCIe from many CUs instead of one.  A block builds
+// its 256 consecutive rows in LDS and then writes them as one contiguous
+// 40 KB range of 16-byte stores (consecutive lanes, consecutive addresses):
+// the stage is mapped host memory, and a lane writing its own row dword by
+// dword sent every dword as its own PCIe write.
 __global__ __launch_bounds__(256) void k_mq_window_rows(uint32_t nsend, Pool p, const uint32_t* __restrict__ win_meta,
                                                         uint8_t* __restrict__ stage) {
     __shared__ uint32_t o2[1024], co[1024], al[1024];
+    __shared__ uint4 rows_lds[256 * HD_MQ_ROW / 16];
     const uint32_t np = win_meta[0], nw = win_meta[1];
     if (np == 0) return;
     for (uint32_t t = threadIdx.x; t < nsend; t += blockDim.x) {
@@ -705,15 +710,25 @@ __global__ __launch_bounds__(256) void k_mq_window_rows(uint32_t nsend, Pool p, 
         al[t] = win_meta[2 + 2048 + t];
     }
     __syncthreads();
-    uint8_t* win = stage + HD_MQ_HDR + (size_t)HD_MQ_ROW * nw;
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < np; k += gridDim.x * blockDim.x) {
-        uint32_t a = 0, b = nsend;
-        while (b - a > 1) {
-            const uint32_t m = (a + b) / 2;
-            if (o2[m] <= k) a = m;
-            else b = m;
+    // 64 + 160 nw: 16-byte aligned in the (page-aligned) stage
+    uint4* win = reinterpret_cast<uint4*>(stage + HD_MQ_HDR + (size_t)HD_MQ_ROW * nw);
+    constexpr uint32_t Q = HD_MQ_ROW / 16;   // 16-byte words per row
+    for (uint32_t base = blockIdx.x * 256u; base < np; base += gridDim.x * 256u) {
+        const uint32_t k = base + threadIdx.x;
+        if (k < np) {
+            uint32_t a = 0, b = nsend;
+            while (b - a > 1) {
+                const uint32_t m = (a + b) / 2;
+                if (o2[m] <= k) a = m;
+                else b = m;
+            }
+            mq_row_put(reinterpret_cast<uint8_t*>(rows_lds + Q * threadIdx.x), p, co[a] + (k - o2[a]), al[a]);
         }
-        mq_row_put(win + (size_t)HD_MQ_ROW * k, p, co[a] + (k - o2[a]), al[a]);
+        __syncthreads();
+        const uint32_t nq = Q * min(256u, np - base);
+        uint4* dst = win + (size_t)Q * base;
+        for (uint32_t i = threadIdx.x; i < nq; i += 256u) dst[i] = rows_lds[i];
+        __syncthreads();
     }
     __threadfence_system();
 }

@@ -782,6 +782,64 @@ __global__ __launch_bounds__(256) void k_mq_minmax3(uint32_t T, const int64_t* _
     }
 }
 
+// Stable select of the set flags' indices in two dependent launches: block
+// b counts the flags of its 4,096-element tile; then block b sums the counts
+// of the tiles before it, scans its own tile and writes the indices in
+// order, and the last block writes the total.  rocprim's select takes four
+// launches (a fill, a look-back init, the partition and a transform), each
+// at the ~5 us floor of a dependent launch in the insert's trace.
+#define HD_SEL_TILE 4096u        // 256 threads x 16 flags (one 16-byte load)
+#define HD_SEL_MAX_TILES 1024u   // larger inputs take rocprim's select
+__device__ __forceinline__ uint32_t sel_load16(const uint8_t* __restrict__ flag, uint32_t n, uint32_t i0) {
+    // bit j = flag[i0 + j] != 0, for the indices below n
+    uint32_t m = 0;
+    if (i0 + 16 <= n) {
+        const uint4 v = *reinterpret_cast<const uint4*>(flag + i0);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        for (int q = 0; q < 4; q++)
+            for (int b = 0; b < 4; b++) m |= (uint32_t)(((w[q] >> (8 * b)) & 0xFFu) != 0) << (4 * q + b);
+    } else {
+        for (uint32_t j = 0; j < 16; j++) m |= (uint32_t)(i0 + j < n && flag[i0 + j] != 0) << j;
+    }
+    return m;
+}
+__global__ __launch_bounds__(256) void k_sel_count(uint32_t n, const uint8_t* __restrict__ flag,
+                                                   uint32_t* __restrict__ tile_count) {
+    typedef hipcub::BlockReduce<uint32_t, 256> Red;
+    __shared__ typename Red::TempStorage tmp;
+    const uint32_t c = __popc(sel_load16(flag, n, blockIdx.x * HD_SEL_TILE + 16 * threadIdx.x));
+    const uint32_t sum = Red(tmp).Sum(c);
+    if (threadIdx.x == 0) tile_count[blockIdx.x] = sum;
+}
+__global__ __launch_bounds__(256) void k_sel_scatter(uint32_t n, const uint8_t* __restrict__ flag,
+                                                     const uint32_t* __restrict__ tile_count,
+                                                     uint32_t* __restrict__ out, uint32_t* __restrict__ count) {
+    typedef hipcub::BlockReduce<uint32_t, 256> Red;
+    typedef hipcub::BlockScan<uint32_t, 256> Scan;
+    __shared__ union {
+        typename Red::TempStorage red;
+        typename Scan::TempStorage scan;
+    } tmp;
+    __shared__ uint32_t base_s;
+    uint32_t pre = 0;
+    for (uint32_t j = threadIdx.x; j < blockIdx.x; j += 256u) pre += tile_count[j];
+    pre = Red(tmp.red).Sum(pre);
+    if (threadIdx.x == 0) base_s = pre;
+    __syncthreads();
+    const uint32_t base = base_s;
+    const uint32_t i0 = blockIdx.x * HD_SEL_TILE + 16 * threadIdx.x;
+    uint32_t m = sel_load16(flag, n, i0);
+    uint32_t off, tot;
+    Scan(tmp.scan).ExclusiveSum((uint32_t)__popc(m), off, tot);
+    uint32_t o = base + off;
+    while (m) {
+        const uint32_t j = __ffs(m) - 1;
+        out[o++] = i0 + j;
+        m &= m - 1;
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *count = base + tot;
+}
+
 inline uint32_t nblk(uint32_t n) { return (n + 255) / 256; }
 
 int bits_of(uint64_t range) {
@@ -794,7 +852,7 @@ int bits_of(uint64_t range) {
 
 enum MqSlot { MQ_FLAG, MQ_NEWIDX, MQ_NSEL, MQ_HK, MQ_RK, MQ_SK, MQ_PERM0, MQ_PERM1, MQ_K64A, MQ_K64B, MQ_K32A, MQ_K32B,
               MQ_HEAD, MQ_KEEP, MQ_SEL, MQ_RED, MQ_TMP, MQ_SID, MQ_LSLOT, MQ_LCLAIM, MQ_LID, MQ_REPS, MQ_ALLOW,
-              MQ_LIST, MQ_DELIV, MQ_SEL2, MQ_HEADS, MQ_SEND, MQ_NEWHEAD, MQ_OFF, MQ_TOT, MQ_STAGE, MQ_WIN, MQ__N };
+              MQ_LIST, MQ_DELIV, MQ_SEL2, MQ_HEADS, MQ_SEND, MQ_NEWHEAD, MQ_OFF, MQ_TOT, MQ_STAGE, MQ_WIN, MQ_SELCNT, MQ__N };
 
 struct hd_mq {
     hd_ctx* ctx = nullptr;
@@ -932,12 +990,21 @@ static int select_idx(hd_mq* q, const uint8_t* flag, uint32_t n, uint32_t* out, 
     if (rc) return rc;
     nsel += slot;
     if (count_dev) *count_dev = nsel;
-    hipcub::CountingInputIterator<uint32_t> iota(0);
-    size_t need = 0;
-    QCHK(hipcub::DeviceSelect::Flagged(nullptr, need, iota, flag, out, nsel, n, s), "select size");
-    void* tmp = qbuf(q, MQ_TMP, need, &rc);
-    if (rc) return rc;
-    QCHK(hipcub::DeviceSelect::Flagged(tmp, need, iota, flag, out, nsel, n, s), "select");
+    const uint32_t tiles = std::max((n + HD_SEL_TILE - 1) / HD_SEL_TILE, 1u);
+    if (tiles <= HD_SEL_MAX_TILES && ((uintptr_t)flag & 15) == 0) {
+        uint32_t* tc = (uint32_t*)qbuf(q, MQ_SELCNT, 4 * (size_t)HD_SEL_MAX_TILES, &rc);
+        if (rc) return rc;
+        k_sel_count<<<tiles, 256, 0, s>>>(n, flag, tc);
+        k_sel_scatter<<<tiles, 256, 0, s>>>(n, flag, tc, out, nsel);
+        QCHK(hipGetLastError(), "select");
+    } else {
+        hipcub::CountingInputIterator<uint32_t> iota(0);
+        size_t need = 0;
+        QCHK(hipcub::DeviceSelect::Flagged(nullptr, need, iota, flag, out, nsel, n, s), "select size");
+        void* tmp = qbuf(q, MQ_TMP, need, &rc);
+        if (rc) return rc;
+        QCHK(hipcub::DeviceSelect::Flagged(tmp, need, iota, flag, out, nsel, n, s), "select");
+    }
     if (count && wait) {
         const uint32_t* w[1] = {nsel};
         return mq_reply(q, s, w, 1, count);

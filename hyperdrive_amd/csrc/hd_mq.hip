@@ -280,8 +280,10 @@ __device__ __forceinline__ void src_keys(const MqSrc& s, uint32_t e, uint32_t& s
 }
 
 __global__ void k_mq_keys(MqSrc s, uint32_t T, int64_t* __restrict__ hk, int64_t* __restrict__ rk,
-                          uint32_t* __restrict__ sk, uint32_t* __restrict__ iota) {
+                          uint32_t* __restrict__ sk, uint32_t* __restrict__ iota,
+                          unsigned long long* __restrict__ red) {
     const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < 5) red[e] = ~0ull;   // k_mq_minmax3's identities (the next launch)
     if (e >= T) return;
     uint32_t snd;
     int64_t h, r;
@@ -419,10 +421,14 @@ __global__ __launch_bounds__(256) void k_mq_gather(MqSrc s, uint32_t n, const ui
     }
 }
 
+// (also clears the ns-entry head / send arrays k_mq_runs fills two launches
+// later, in place of two memsets)
 __global__ void k_mq_compose(uint32_t n, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ sel,
-                             uint32_t* __restrict__ ids, const uint32_t* __restrict__ n_dev = nullptr) {
+                             uint32_t* __restrict__ ids, const uint32_t* __restrict__ n_dev, uint32_t ns,
+                             uint32_t* __restrict__ head, uint32_t* __restrict__ send) {
     if (n_dev) n = *n_dev;
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint32_t i = k; i < ns; i += gridDim.x * blockDim.x) head[i] = send[i] = 0;
     if (k < n) ids[k] = perm[sel[k]];
 }
 
@@ -1014,17 +1020,13 @@ static int select_idx(hd_mq* q, const uint8_t* flag, uint32_t n, uint32_t* out, 
 }
 
 // min / max of the three sort keys (k_mq_minmax3) into the device words
-// *red; key_ranges_read brings them back with counts queued meanwhile
+// red[0..4] (set to ~0 by k_mq_keys, the launch before); key_ranges_read
+// brings them back with counts queued meanwhile
 static int key_ranges_launch(hd_mq* q, uint32_t T, const int64_t* rk, const int64_t* hk, const uint32_t* sk,
-                             hipStream_t s, unsigned long long** red_out) {
-    int rc = 0;
-    unsigned long long* red = (unsigned long long*)qbuf(q, MQ_RED, 5 * sizeof(uint64_t), &rc);
-    if (rc) return rc;
-    QCHK(hipMemsetAsync(red, 0xFF, 5 * sizeof(uint64_t), s), "key ranges init");
+                             hipStream_t s, unsigned long long* red) {
     const uint32_t blocks = std::min(nblk(T), 256u);
     k_mq_minmax3<<<blocks, 256, 0, s>>>(T, rk, hk, sk, red);
     QCHK(hipGetLastError(), "k_mq_minmax3");
-    *red_out = red;
     return HD_OK;
 }
 
@@ -1217,14 +1219,11 @@ static int mq_compact(hd_mq* q, hipStream_t s) {
 
 // per-sender runs of the (freshly sorted, compact) pool
 // (n_dev: the pool's size is still on the device, at most q->pool.n)
-static int mq_runs(hd_mq* q, hipStream_t s, const uint32_t* n_dev = nullptr) {
-    int rc = 0;
-    const uint32_t ns = std::max(q->nsend, 1u);
-    uint32_t* head = (uint32_t*)qbuf(q, MQ_HEADS, 4 * (size_t)ns, &rc);
-    uint32_t* send = (uint32_t*)qbuf(q, MQ_SEND, 4 * (size_t)ns, &rc);
-    if (rc) return rc;
-    QCHK(hipMemsetAsync(head, 0, 4 * (size_t)ns, s), "clear runs");
-    QCHK(hipMemsetAsync(send, 0, 4 * (size_t)ns, s), "clear runs");
+// (head / send: the MQ_HEADS / MQ_SEND buffers of ns entries, already
+// cleared in stream order by k_mq_compose)
+static int mq_runs(hd_mq* q, hipStream_t s, const uint32_t* n_dev) {
+    uint32_t* head = (uint32_t*)q->buf[MQ_HEADS].p;
+    uint32_t* send = (uint32_t*)q->buf[MQ_SEND].p;
     if (q->pool.n) k_mq_runs<<<nblk(q->pool.n), 256, 0, s>>>(q->pool.n, q->pool.sender, head, send, n_dev);
     QCHK(hipGetLastError(), "k_mq_runs");
     q->runs_for = q->nsend;
@@ -1261,12 +1260,13 @@ static int mq_insert_flagged(hd_mq* q, const hd_batch* d_batch, const uint8_t* f
     uint32_t* p0 = (uint32_t*)qbuf(q, MQ_PERM0, 4 * (size_t)T, &rc);
     uint32_t* p1 = (uint32_t*)qbuf(q, MQ_PERM1, 4 * (size_t)T, &rc);
     if (rc) return rc;
-    k_mq_keys<<<nblk(T), 256, 0, s>>>(src, T, hk, rk, sk, p0);
+    unsigned long long* red = (unsigned long long*)qbuf(q, MQ_RED, 5 * sizeof(uint64_t), &rc);
+    if (rc) return rc;
+    k_mq_keys<<<nblk(T), 256, 0, s>>>(src, T, hk, rk, sk, p0, red);
     // 4. stable LSD passes: round, height, sender (mq.go:120-128 order; the
     //    stability keeps arrival order among equal keys)
     //    (the three keys' ranges and the new senders in one host round trip)
-    unsigned long long* red = nullptr;
-    if ((rc = key_ranges_launch(q, T, rk, hk, sk, s, &red))) return rc;
+    if ((rc = key_ranges_launch(q, T, rk, hk, sk, s, red))) return rc;
     int64_t rmn, rmx, hmn, hmx;
     uint32_t smx, r = 0;
     if ((rc = key_ranges_read(q, red, s, &rmn, &rmx, &hmn, &hmx, &smx, &r_dev, 1, &r))) return rc;
@@ -1315,7 +1315,11 @@ static int mq_insert_flagged(hd_mq* q, const hd_batch* d_batch, const uint8_t* f
     if (rc) return rc;
     // sel holds kept positions in sorted order -> element ids -> new pool
     uint32_t* ids = head;  // head is consumed by k_mq_keep; reuse its space
-    k_mq_compose<<<nblk(T), 256, 0, s>>>(T, perm.Current(), sel, ids, kept_dev);
+    const uint32_t ns = std::max(q->nsend, 1u);
+    uint32_t* heads = (uint32_t*)qbuf(q, MQ_HEADS, 4 * (size_t)ns, &rc);
+    uint32_t* sends = (uint32_t*)qbuf(q, MQ_SEND, 4 * (size_t)ns, &rc);
+    if (rc) return rc;
+    k_mq_compose<<<nblk(T), 256, 0, s>>>(T, perm.Current(), sel, ids, kept_dev, ns, heads, sends);
     rc = pool_reserve(q->ctx, q->spare, std::max(T, 1u));
     if (rc) return rc;
     k_mq_gather<<<nblk(T), 256, 0, s>>>(src, T, ids, q->spare, kept_dev);

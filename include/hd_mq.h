@@ -39,7 +39,11 @@ int hd_mq_destroy(hd_mq* q);
  * message), in batch order, into the queue of its from32.  The reference
  * assumes the caller authenticated the sender (mq.go:85-106).
  * valid_round may be NULL (then -1); sig65 may be NULL (then zeros).
- * Synchronises `stream` (a hipStream_t, NULL = the ctx's stream). */
+ * Returns once every kernel the insert queued on `stream` (a hipStream_t,
+ * NULL = the ctx's stream), and all work queued there before it, has
+ * completed: the host spins on a word the insert's last kernel writes to
+ * mapped memory instead of synchronising the stream, so d_batch may be
+ * reused at once. */
 int hd_mq_insert_device(hd_mq* q, const hd_batch* d_batch, const uint8_t* d_insert, void* stream);
 
 /* Replica.Run ingress of a verified batch (replica/replica.go:117-131):
@@ -48,7 +52,7 @@ int hd_mq_insert_device(hd_mq* q, const hd_batch* d_batch, const uint8_t* d_inse
  * equals From -- and its height >= min_height (filterHeight,
  * replica.go:247-249; min_height = the Process's CurrentHeight).  Membership
  * is NOT checked here: hd_mq_consume applies procsAllowed (mq.go:49-51).
- * Synchronises `stream`. */
+ * Returns as hd_mq_insert_device does. */
 int hd_mq_insert_verified_device(hd_mq* q, const hd_batch* d_batch, const uint8_t* d_verdict, int64_t min_height,
                                  void* stream);
 

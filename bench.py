@@ -8,17 +8,21 @@ value, 5 % nil, 5 % random), seeded, signed with RFC6979 on the GPU before the
 timed region.  One step = the hot path over one batch: verification (digest
 -> recover / known-key check -> signatory -> Equal(From) -> admitted; verdict,
 recovered signatory and valid bitmap written for every message) of this
-rank's shard, the valid-bitmap all-gather over RCCL (N > 1), and the
-first-wins 2f+1 tally.  Inputs are resident in HBM when timing starts.
+rank's shard and the first-wins 2f+1 tally of it (N > 1: with the exchange
+below).  Inputs are resident in HBM when timing starts.
 
-Multi-GPU: one process per GPU (torch.distributed.run), weak scaling: rank k
-generates and verifies only messages [k*B, (k+1)*B) of the N*B-message stream
-(C4 generator; --global-batch: one C4 batch split over the ranks).  Each rank
-tallies its own shard; the ranks all-gather their (height, round) sets, and
-only the candidates of rounds present in more than one shard (the rounds a
-shard boundary cuts) are routed to the round's owner over RCCL; the small
-count tables are then all-gathered and merged (hyperdrive_amd/shard.py).  The
-line reports routed_out per rank.
+Multi-GPU: one process per GPU, weak scaling: rank k generates and verifies
+only messages [k*B, (k+1)*B) of the N*B-message stream (C4 generator;
+--global-batch: one C4 batch split over the ranks).  `bench.py --gpus N`
+under torch.distributed.run uses the launcher's ranks; without a launcher
+(no WORLD_SIZE) it starts the N ranks itself as child processes
+(launch_ranks) and relays rank 0's line.  Each rank tallies its own shard;
+the ranks all-gather their (height, round) sets, and only the candidates of
+rounds present in more than one shard (the rounds a shard boundary cuts) are
+routed to the round's owner over RCCL; the small count tables are then
+all-gathered and merged (hyperdrive_amd/shard.py).  The line reports
+ranks_seen (the process group's size) and, per rank, its device, shard,
+timed span and routed_out / routed_in.
 
 Prints ONE JSON line on rank 0, with:
   roofline      the dominant kernel (k_fast_sums) timed live with HIP events
@@ -74,7 +78,7 @@ BYTES_PER_MSG = 146 + 33        # HBM in + out per message
 VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -96,10 +100,109 @@ def parse():
     ap.add_argument("--no-aux", action="store_true", help="skip the SURVEY §8(f) side measurements")
     ap.add_argument("--no-sub", action="store_true", help="skip the C3 / C5 sub-benchmarks")
     ap.add_argument("--sub-steps", type=int, default=20)
+    ap.add_argument("--no-c4-check", action="store_true",
+                    help="skip the untimed full-size bit-exact check of a 16M 30 %% adversarial C4 batch")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank) or gloo: a rehearsal of the N > 1 path with ranks "
                          "sharing the visible GPUs and host-side collectives")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_env(base, rank: int, world: int, port: int) -> dict:
+    """The environment torch.distributed.run gives rank `rank` of a one-node
+    job of `world` ranks (env:// rendezvous on 127.0.0.1)."""
+    env = dict(base)
+    env.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                "LOCAL_WORLD_SIZE": str(world), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                "MASTER_PORT": str(port)})
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")     # RCCL's dmabuf IPC on this pool
+    return env
+
+
+def launch_ranks(args, argv, child=None, device_count=None, timeout=None) -> int:
+    """`bench.py --gpus N` without an external launcher: start N child
+    processes, one per rank (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set as
+    torch.distributed.run sets them), relay rank 0's JSON line and return the
+    exit status.  This process never touches the GPU (torch.cuda.device_count()
+    does not initialise it on this image) and never execs: the ranks are
+    children.  With nccl (RCCL, one GPU per rank) more ranks than visible GPUs
+    is refused before any rank starts.  The line is dropped (status 1) unless
+    rank 0 reports ranks_seen == n_gpus == N."""
+    import subprocess
+    n = args.gpus
+    if args.dist_backend == "nccl":
+        if device_count is None:
+            import torch
+            device_count = torch.cuda.device_count()
+        if n > device_count:
+            print(json.dumps({"error": f"--gpus {n} with the nccl backend needs {n} GPUs, "
+                                       f"torch.cuda.device_count() = {device_count}"}), flush=True)
+            print(f"bench.py: --gpus {n} > {device_count} visible GPU(s); nccl (RCCL) needs one GPU per rank "
+                  f"(use --dist-backend gloo to rehearse several ranks on fewer GPUs)", file=sys.stderr)
+            return 2
+    port = free_port()
+    cmd = child or [sys.executable, "-u", os.path.abspath(__file__)]
+    procs = []
+    for r in range(n):
+        procs.append(subprocess.Popen(cmd + list(argv), env=rank_env(os.environ, r, n, port),
+                                      stdout=subprocess.PIPE if r == 0 else None, text=True))
+    import threading
+    lines = []
+
+    def relay():
+        for line in procs[0].stdout:                    # rank 0's stdout; progress stays visible
+            line = line.rstrip("\n")
+            if line.startswith("{"):
+                lines.append(line)
+            else:
+                print(line, flush=True)
+
+    reader = threading.Thread(target=relay, daemon=True)
+    reader.start()
+    t0 = time.monotonic()
+    try:
+        # poll every rank: one that fails ends the job (the others would wait
+        # in a collective for it forever)
+        while any(p.poll() is None for p in procs):
+            if any(p.poll() not in (None, 0) for p in procs):
+                break
+            if timeout is not None and time.monotonic() - t0 > timeout:
+                print(f"bench.py: ranks still running after {timeout} s", file=sys.stderr)
+                break
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        rcs = [p.wait() for p in procs]
+        reader.join(timeout=10)
+    bad = [(r, rc) for r, rc in enumerate(rcs) if rc != 0]
+    if bad:
+        for line in lines:
+            print(line, flush=True)
+        print(f"bench.py: rank(s) failed: {bad}", file=sys.stderr)
+        return 1
+    if not lines:
+        print("bench.py: rank 0 printed no result line", file=sys.stderr)
+        return 1
+    try:
+        out = json.loads(lines[-1])
+    except ValueError:
+        print(f"bench.py: rank 0's result line is not JSON: {lines[-1][:200]}", file=sys.stderr)
+        return 1
+    if out.get("ranks_seen") != n or out.get("n_gpus") != n:
+        print(json.dumps({"error": f"launched {n} ranks but rank 0 saw ranks_seen={out.get('ranks_seen')}, "
+                                   f"n_gpus={out.get('n_gpus')}"}), flush=True)
+        return 1
+    print(lines[-1], flush=True)
+    return 0
 
 
 def cpu_baseline(args, S):
@@ -495,11 +598,20 @@ def timed(pipe, steps, dist, dev):
 
 
 def main():
-    args = parse()
+    argv = sys.argv[1:]
+    args = parse(argv)
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no external launcher: this process starts the ranks itself
+        sys.exit(launch_ranks(args, argv))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(json.dumps({"error": f"WORLD_SIZE={world} but --gpus {args.gpus}"}), flush=True)
+        sys.exit(1)
     import numpy as np
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -582,12 +694,22 @@ def main():
     calls, verify_ms, sums_launches, sums_ms = v.profile_read()
     v.profile(False)
     pipe.wss = all_streams
+    own_elapsed = elapsed
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     verdict, recovered, bitmap = pipe.last(args.steps)
     known, fallback = v.fastpath_stats()
+    ranks_seen, per_rank = 1, None
+    if dist is not None:
+        # what every rank saw: its device, shard, own timed span and tally exchange
+        ranks_seen = dist.get_world_size()
+        mine = {"rank": rank, "device": dev.index, "pid": os.getpid(), "shard": [lo, hi],
+                "ms_per_step": own_elapsed / args.steps * 1e3,
+                "valid": int((verdict == 0).sum()), **pipe.tally_info}
+        per_rank = [None] * ranks_seen
+        dist.all_gather_object(per_rank, mine)
 
     # correctness gate: without --adv every message of the workload is an honest
     # vote by construction, so every verdict must be VALID, every recovered
@@ -617,6 +739,7 @@ def main():
             "value": value,
             "unit": "msgs/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_step,
@@ -632,7 +755,8 @@ def main():
                        "outputs_per_step": "verdict, recovered signatory, valid bitmap, tally",
                        "parallelism": (f"shard-by-index x{world} (each rank holds, verifies and tallies only its "
                                        f"shard); round sets all-gathered, only rounds held by several ranks routed "
-                                       f"to their owner (RCCL all-to-all); count rows all-gathered"
+                                       f"to their owner (all-to-all); count rows all-gathered; backend "
+                                       f"{'RCCL' if args.dist_backend == 'nccl' else args.dist_backend}"
                                        if world > 1 else "one GPU")},
             "roofline": {
                 "bound": "valu",
@@ -674,6 +798,10 @@ def main():
             "verify_streams": len(all_streams),
             "tally_mode": "async" if pipe.async_tally else "thread", "tally_retries": pipe.tally_retries,
         }
+        if per_rank is not None:
+            out["dist_backend"] = args.dist_backend
+            out["per_rank"] = per_rank
+            out["distinct_devices"] = len({p["device"] for p in per_rank})
         if world == 1:
             out["oracle_sample_check"] = oracle_sample_check(db, verdict, recovered, sigs)
             if not args.no_aux:
@@ -691,10 +819,45 @@ def main():
                     out["sub"] = sub_benchmarks(args, v, sigs, foreign, dev, ws, ts)
                 except Exception as e:
                     out["sub"] = {"error": repr(e)}
+            if not args.no_c4_check:
+                try:
+                    out["c4_16m_bit_exact"] = c4_bit_exact(v, sigs, foreign, dev, ws)
+                except Exception as e:  # reported, never fatal for the GPU number
+                    out["c4_16m_bit_exact"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def c4_bit_exact(v, sigs, foreign, dev, ws, n=1 << 24, adv=30):
+    """Untimed: BASELINE configs[3] at full size with the C5 mix -- 16,777,216
+    messages of the C4 generator (the headline's 100 signatories), 30 %
+    adversarial across the 13 classes, verified by the headline's context
+    (the product path, one call) and tallied by the library; then every
+    verdict, recovered signatory, tally row and round decision is recomputed
+    on the host (tests/bitexact.py: oracle/secp_port.cpp for the verdicts,
+    oracle_tally for the rows and predicate bits; the checker, not the thing
+    measured)."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import bitexact
+    from hyperdrive_amd.device import generate
+    db, _, _ = generate(v, 0, n, len(sigs), adv, keys=(sigs, foreign), start=1 << 30, device=str(dev))
+    verdict = torch.empty(n, dtype=torch.uint8, device=dev)
+    rec = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    v.verify_batch_device(db.c_struct(), verdict.data_ptr(), rec.data_ptr(), None, None, ws.cuda_stream)
+    ws.synchronize()
+    gpu_s = time.perf_counter() - t0
+    hb = db.to_host()
+    del db
+    res = bitexact.full_check(v, hb, verdict.cpu().numpy(), rec.cpu().numpy(), sigs)
+    res.update({"adversarial_pct": adv, "gpu_verify_s": gpu_s, "stream_start": 1 << 30,
+                "all_bit_exact": bool(res["verdicts"] and res["signatories"] and res["tally_rows"]
+                                      and res["decisions"])})
+    return res
 
 
 def oracle_sample_check(db, verdict, recovered, sigs, n=512):
@@ -1196,11 +1359,7 @@ def run_cpu_baseline(args, v, db, sigs, gpu_verdict, gpu_recovered):
                  {k: quorum.decide(gt, int(h), int(r), f, pv(int(h), int(r)), True)[k] for k in bits}
                  for (h, r), d in zip(tal["hr"][:, :2].tolist(), tal["decide"].tolist()))
     exact_tally = c_counts == gt.count and c_any == gt.distinct_any
-    figures.setdefault("all_threads", figures["per_gpu_share"])
     best = max(figures.values(), key=lambda fig: fig["msgs_per_s"])
-    # the GLV port (oracle/glv_port.cpp: the repository's own recovery with
-    # GLV and 12-bit G tables, built for the host) on the same sample and
-    # threads, then the same tally; bit-exact against the GPU as well
     glv = {}
     try:
         gp = glv_port()
@@ -1235,13 +1394,16 @@ def run_cpu_baseline(args, v, db, sigs, gpu_verdict, gpu_recovered):
         kind, value, cores = "port-glv", glv["msgs_per_s"], glv["threads"]
     if secp.get("msgs_per_s", 0) > value and secp.get("bit_exact_vs_gpu"):
         kind, value, cores = "port-secp-class", secp["msgs_per_s"], secp["threads"]
+    chosen = {"port": best, "port-glv": glv, "port-secp-class": secp}[kind]
     return {"value": value, "unit": "msgs/s", "cores": cores, "kind": kind,
+            "verify_s": chosen["verify_s"], "tally_decide_s": chosen["tally_decide_s"],
             "port_secp_class": secp, "port_glv": glv,
-            "port_naive": {"msgs_per_s": best["msgs_per_s"], "threads": best["threads"]},
+            "port_naive": {"msgs_per_s": best["msgs_per_s"], "threads": best["threads"], "by_threads": figures},
             "cpu_model": model, "host_cpus_allowed": allowed, "host_cpus_online": online,
             "cgroup_cpu_quota": cgroup_cpu_quota(),
-            "per_gpu_share": figures["per_gpu_share"], "all_threads": figures["all_threads"],
-            "value_from": "the faster of the all-threads and per-GPU-share runs",
+            "value_from": (f"'{kind}' on {cores} threads: the fastest of the three host ports that is bit-exact "
+                           f"with the GPU; all three run on the thread count at which the naive port was faster "
+                           f"(" + ", ".join(f"{k} {fig['threads']}" for k, fig in figures.items()) + ")"),
             "bit_exact_vs_gpu": bool(exact_verify and exact_tally and dec_ok),
             "bit_exact_detail": {"verdicts_and_signatories": bool(exact_verify), "tally_rows": bool(exact_tally),
                                  "decisions": bool(dec_ok), "rounds_decided": int(len(tal["hr"])),

@@ -141,6 +141,7 @@ struct FbWork {
     bool fforce = false;   // build the LEARNED slots at this call's end (an eviction re-keyed one)
     uint32_t evictions = 0;
     uint32_t evict_checks = 0;   // fb_evict passes that waited for the context's calls
+    uint32_t evict_aborts = 0;   // passes whose new dictionary had no bucket for a slot holder
 };
 
 namespace {
@@ -1078,6 +1079,17 @@ int fb_evict(hd_ctx* ctx, bool* changed) {
         uint32_t b = fdict_bucket(e.from);
         int p = 0;
         for (; p < 8 && nd[b] != 0u; p++) b = (b + 1u) & (B - 1u);
+        if (p == 8 && e.slot != 0xFFFFFFFFu) {
+            // a slot holder finds no bucket within the probe limit: the new
+            // dictionary would strand its slot (READY / LEARNED, no From
+            // mapping to it, never seen by a later pass).  Keep the old
+            // dictionary and slots for this pass.
+            f->evict_aborts++;
+            f->fwait = std::min(2 * f->fwait, HD_FD_EVICT_WAIT_MAX);
+            FBCHK(hipMemsetAsync(f->fhit, 0, 4 * hit.size(), s), "evict counters");
+            FBCHK(hipStreamSynchronize(s), "evict counters");
+            return HD_OK;
+        }
         if (p == 8) continue;   // no room (slotless: simply forgotten)
         nd[b] = 2u;
         nd[B + b] = e.slot;

@@ -862,6 +862,10 @@ enum MqSlot { MQ_FLAG, MQ_NEWIDX, MQ_NSEL, MQ_HK, MQ_RK, MQ_SK, MQ_PERM0, MQ_PER
 
 struct hd_mq {
     hd_ctx* ctx = nullptr;
+    // an insert failed after it had started changing the queue's device state
+    // (new senders interned, the pool swapped): the host's view (pool.n,
+    // nsend) may no longer match it, so every later call is refused
+    bool failed = false;
     uint32_t max_cap = 1000;
     Pool pool, spare;
     DevBuf buf[MQ__N];
@@ -1234,7 +1238,25 @@ static int mq_runs(hd_mq* q, hipStream_t s, const uint32_t* n_dev) {
 
 static int pf_sync(hd_mq* q);   // the consume prefetch (below)
 
+static int mq_insert_flagged_impl(hd_mq* q, const hd_batch* d_batch, const uint8_t* flag, hipStream_t s,
+                                  bool* dirty);
+
+// An insert that fails once it has begun to change the device state (new
+// senders interned into the dictionary, the pool swapped) leaves the host's
+// view of the queue (pool.n, nsend) out of step with it: the queue is then
+// marked failed and refuses every later call.
 static int mq_insert_flagged(hd_mq* q, const hd_batch* d_batch, const uint8_t* flag, hipStream_t s) {
+    bool dirty = false;
+    const int rc = mq_insert_flagged_impl(q, d_batch, flag, s, &dirty);
+    if (rc && dirty) {
+        q->failed = true;
+        q->ctx->last_error += " (message queue state lost: the queue refuses further calls)";
+    }
+    return rc;
+}
+
+static int mq_insert_flagged_impl(hd_mq* q, const hd_batch* d_batch, const uint8_t* flag, hipStream_t s,
+                                  bool* dirty) {
     const uint32_t nb = d_batch->n;
     int rc = mq_compact(q, s);
     if (rc) return rc;
@@ -1247,6 +1269,7 @@ static int mq_insert_flagged(hd_mq* q, const hd_batch* d_batch, const uint8_t* f
     // 2. their sender queues (the From of each message)
     uint32_t* nsid = nullptr;
     uint32_t* r_dev = nullptr;   // new senders: read with the key ranges below
+    *dirty = true;
     rc = intern_senders(q, d_batch, newidx, m, &nsid, &r_dev, s);
     if (rc) return rc;
     // 3. merged sequence: pool (sorted) then the new messages (arrival order)
@@ -1336,6 +1359,11 @@ static int mq_insert_flagged(hd_mq* q, const hd_batch* d_batch, const uint8_t* f
     return HD_OK;
 }
 
+static int mq_refuse(hd_mq* q) {
+    q->ctx->last_error = "message queue: an earlier insert failed part-way; the queue's state is lost";
+    return HD_EDEVICE;
+}
+
 extern "C" {
 
 int hd_mq_create(hd_ctx* ctx, uint32_t max_capacity, hd_mq** out) {
@@ -1382,6 +1410,7 @@ int hd_mq_senders(hd_mq* q, uint32_t* n) {
 
 int hd_mq_insert_device(hd_mq* q, const hd_batch* d_batch, const uint8_t* d_insert, void* stream) {
     if (!q || !d_batch) return HD_EINVAL;
+    if (q->failed) return mq_refuse(q);
     const uint32_t nb = d_batch->n;
     if (nb == 0) return HD_OK;  // empty device tensors may have NULL data pointers
     if (!d_batch->type || !d_batch->height || !d_batch->round || !d_batch->value32 || !d_batch->from32)
@@ -1403,6 +1432,7 @@ int hd_mq_insert_device(hd_mq* q, const hd_batch* d_batch, const uint8_t* d_inse
 int hd_mq_insert_verified_device(hd_mq* q, const hd_batch* d_batch, const uint8_t* d_verdict, int64_t min_height,
                                  void* stream) {
     if (!q || !d_batch) return HD_EINVAL;
+    if (q->failed) return mq_refuse(q);
     const uint32_t nb = d_batch->n;
     if (nb == 0) return HD_OK;
     if (!d_verdict) return HD_EINVAL;
@@ -1564,7 +1594,9 @@ static int mq_consume1(hd_mq* q, int64_t h, const uint32_t* list, uint32_t na, i
         // synchronisation on the common path.  In the admitted-set mode the
         // launch also stages the next heights' window (prefetch).
         const bool pf = be != 0;
-        const int64_t hpf = pf ? h + q->pf_win : h;
+        // the window's end, clamped: a consume within pf_win of INT64_MAX
+        // stages what is left up to INT64_MAX (no signed overflow)
+        const int64_t hpf = !pf ? h : (h > INT64_MAX - q->pf_win ? INT64_MAX : h + q->pf_win);
         const size_t bytes_pf = bytes + (pf ? (size_t)HD_MQ_ROW * HD_MQ_PF_ROWS : 0);
         if (q->mstage_cap < bytes_pf) {
             if (q->mstage) (void)hipHostFree(q->mstage);
@@ -1665,6 +1697,7 @@ static int mq_consume1(hd_mq* q, int64_t h, const uint32_t* list, uint32_t na, i
 int hd_mq_consume(hd_mq* q, int64_t h, const uint8_t* allowed32, uint32_t n_allowed, const hd_batch_out* out,
                   int32_t* out_sender, uint32_t cap, uint32_t* n_out, uint32_t* n_removed) {
     if (!q || !out || !n_out) return HD_EINVAL;
+    if (q->failed) return mq_refuse(q);
     if (!out->type || !out->height || !out->round || !out->value32 || !out->from32) return HD_EINVAL;
     if (allowed32 == nullptr && n_allowed != 0) return HD_EINVAL;
     *n_out = 0;
@@ -1780,6 +1813,7 @@ int hd_mq_consume_votes(hd_mq* q, struct hd_votes* v, int64_t h, const uint8_t* 
 
 int hd_mq_drop_below(hd_mq* q, int64_t h) {
     if (!q) return HD_EINVAL;
+    if (q->failed) return mq_refuse(q);
     if (q->pf) {
         if (h - 1 <= q->pf_done) return HD_OK;   // nothing below h is left
         if (h - 1 <= q->pf_max) {                // the window's heights (pf_done, h - 1] leave undelivered

@@ -181,6 +181,21 @@ int hd_ctx_note_stream(hd_ctx* ctx, hipStream_t s) {
     for (auto& se : ctx->caller_ev)
         if (se.first == s) ev = se.second;
     if (!ev) {
+        // a new caller stream: first forget the streams whose last recorded
+        // work has completed (destroy has nothing to wait for there), so a
+        // caller making a stream per call does not grow the list.  The event
+        // is re-recorded on the handle's current stream at every call, so a
+        // reused handle is ordered correctly either way.
+        auto& L = ctx->caller_ev;
+        for (size_t k = 0; k < L.size();) {
+            if (hipEventQuery(L[k].second) == hipSuccess) {
+                (void)hipEventDestroy(L[k].second);
+                L[k] = L.back();
+                L.pop_back();
+            } else {
+                k++;
+            }
+        }
         hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
         if (e != hipSuccess) return hd_ctx_fail(ctx, e, "caller stream event");
         ctx->caller_ev.emplace_back(s, ev);

@@ -22,7 +22,8 @@
 // (process/message.go:53-78, 165-186, 263-284; mq/mq.go:49-51).  Digests and
 // the pubkey hash use the repository's host-compilable SHA-256 lanes.
 // It is checked verdict for verdict and byte for byte against the C oracle
-// (tests/test_secp_port.py) and against the GPU in bench.py.
+// (tests/test_oracle.py test_secp_class_port_equals_c_oracle) and against
+// the GPU in bench.py.
 #include <algorithm>
 #include <cstdint>
 #include <cstring>

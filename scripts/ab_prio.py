@@ -3,7 +3,7 @@ through bench.py's Pipeline (verify + tally): C2 (1M, 100 signatories), C5
 (30 % adversarial) and C3 (1000 signatories, 128,064 messages).  Prints one
 JSON line per workload: ms/step per setting and round.
 
-AB_VARS="wave_prio=0,3;sum_cap=0,2" (Verifier.VARIANTS names; every
+AB_VARS="wave_prio=0,3;split_k=-1,8" (Verifier.VARIANTS names; every
 combination), AB_STREAMS="1,2"."""
 import json
 import os

@@ -320,6 +320,22 @@ def test_prefetched_consumes_match_oracle(gpu, seed):
     n, want = o.consume(10 ** 9, allowed={k.tobytes() for k in adm})
     _check_consumed(b, sn, want, ids)
     assert len(q) == 0
+    # admitted-set consumes within the window width of INT64_MAX: the
+    # window's end clamps at INT64_MAX instead of overflowing
+    top = (1 << 63) - 1
+    db, d_ins, host, ins = _batch(rng, 300, keys, 40, 3)
+    db.height += top - 40
+    q.insert_device(db, d_ins)
+    for i, m in enumerate(host):
+        if ins[i]:
+            o.insert(m[5], (m[0] + top - 40,) + m[1:])
+    for hh in (top - 30, top - 29, top - 5, top):
+        b, sn = q.consume(hh)
+        n, want = o.consume(hh, allowed={k.tobytes() for k in adm})
+        _check_consumed(b, sn, want, ids)
+        assert q.last_removed == n, hh
+        assert len(q) == len(o), hh
+    assert len(q) == 0
     q.close()
     v.close()
 

@@ -970,7 +970,59 @@ def sub_benchmarks(args, v, sigs, foreign, dev, ws, ts):
         "cold_first_batch_s": cold3, "tally": p3.tally_info}
     del p3, db3
     v3.close()
+    out["many_signatories"] = many_signatories(args, dev, ws, ts)
     return out
+
+
+def many_signatories(args, dev, ws, ts, sizes=(2000, 4000), steps=10):
+    """The per-key table budget with thousands of signatories (replica.go:54,
+    136-144: the admitted set and f): the C2 stream (1M messages, signer =
+    i % S) from S = 2,000 and 4,000 signatories, each on a context of its
+    own, with the default table width -- 13-bit windows (5 MB per key) once
+    the 16-bit tables (40 MB per key) of every key no longer fit the
+    context's 64 GiB budget -- and with the 16-bit width forced (the round-5
+    behaviour: the keys past ~1,600 slots get no table and take the full
+    recovery, ~10x per message).  Per line: msgs/s over `steps` steps of
+    verify + tally, keys with tables, the last step's full-recovery count."""
+    import torch
+    import hyperdrive_amd as hd
+    from hyperdrive_amd.device import generate
+    B = args.batch
+    res = {}
+    for S in sizes:
+        for width in (0, 16):
+            vS = hd.Verifier(dev.index)
+            try:
+                if width:
+                    vS.set_variant("key_width", width)
+                ks = vS.gen_keys(S)
+                vS.set_signatories(ks[0])
+                db, _, _ = generate(vS, 0, B, S, 0, keys=ks, device=str(dev))
+                p = Pipeline(vS, db, B, 0, 0, 1, None, ws, ts)
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                p.run(1)
+                torch.cuda.synchronize(dev)
+                cold = time.perf_counter() - t0
+                for _ in range(2):              # tables of keys learned late are built by the next calls
+                    p.run(1)
+                    torch.cuda.synchronize(dev)
+                el = timed(p, steps, None, dev)
+                vd, rec, _ = p.last(steps)
+                known, fallback = vS.fastpath_stats()
+                res[f"S{S}_" + ("default" if not width else f"forced_{width}bit")] = {
+                    "signatories": S, "messages": B, "msgs_per_s": B * steps / el, "ms_per_step": el / steps * 1e3,
+                    "key_windows": vS.fastpath_geometry()[1], "keys_with_tables": known,
+                    "full_recovery_msgs_last_step": fallback, "cold_first_batch_s": cold,
+                    "all_valid_and_recovered": bool((vd == 0).all()) and bool((rec == db.frm).all())}
+                p.close()
+                del p, db
+            finally:
+                vS.close()
+    res["note"] = ("C2 stream with S signatories; default: the context picks 20-, 16- or 13-bit key tables by its "
+                   "64 GiB budget (13-bit here: every key gets a table); forced_16bit: the round-5 tiers, where keys "
+                   "past the budget's slots take the full recovery")
+    return res
 
 
 def host_buffers(v, args, sigs, foreign, dev, steps=12):
@@ -1043,13 +1095,15 @@ def host_buffers(v, args, sigs, foreign, dev, steps=12):
 def ingress_c5(v, keys, S, n, ws, dev, heights=64):
     """BASELINE config 5 through the replica ingress (hyperdrive_amd/ingress.py):
     the C2 stream with 30 % of the messages corrupted, shuffled so that heights
-    arrive out of order, marshalled per message type to wire bytes.  Timed:
-    the pushes (unmarshal -> verify -> filterHeight -> mq insert with a
+    arrive out of order, marshalled per message type to wire bytes.  A cycle:
+    the push (unmarshal -> verify -> filterHeight -> mq insert with a
     per-sender capacity of 1000, every authenticated message buffered), then
     `heights` flushes with ResetHeight between (mq.Consume of the current
-    height against procsAllowed -> vote logs).  Checked: the messages
-    delivered are exactly the VALID ones of heights 1..`heights` (the queues
-    keep each sender's lowest heights, mq.go:125-142)."""
+    height against procsAllowed -> vote logs).  Timed: 8 cycles back to back
+    with cycle c+1's unmarshal + authentication on the device beside cycle c's
+    flushes (replica.go:117-145, 251-264), and 3 serial cycles.  Checked:
+    every cycle delivers exactly the VALID messages of heights 1..`heights`
+    (the queues keep each sender's lowest heights, mq.go:125-142)."""
     import torch
     from hyperdrive_amd.codec import marshal_device
     from hyperdrive_amd.device import DeviceBatch, generate
@@ -1070,39 +1124,83 @@ def ingress_c5(v, keys, S, n, ws, dev, heights=64):
         ing.push_wires([(t, wire, sub.n) for t, sub, wire in parts])   # consume's mapped stage (first flush)
         ing.flush()
         ing.mq.drop_below(2 ** 62)
-    reps = []
-    for rep in range(3):        # three timed cycles; the median one is reported
+    wires = [(t, wire, sub.n) for t, sub, wire in parts]
+
+    def restart():                  # the next cycle starts from height 1 and an empty queue
         ing.height = 1
         ing.votes.reset(1)
         ing._clean = None
         ing.mq.drop_below(2 ** 62)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        verdicts = ing.push_wires([(t, wire, sub.n) for t, sub, wire in parts])
-        torch.cuda.synchronize()                      # push_ms includes the device work it queued
-        t1 = time.perf_counter()
-        delivered = 0
+
+    def flushes():
+        got = 0
         for h in range(1, heights + 1):
             if h > 1:
                 ing.reset_height(h)
-            delivered += len(ing.flush().consumed)
+            got += len(ing.flush().consumed)
+        return got
+
+    want = None
+    # serial cycles (push, then the flushes), as in rounds 2-5; the median one
+    reps = []
+    for rep in range(3):
+        restart()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        verdicts = ing.push_wires(wires)
+        torch.cuda.synchronize()                      # push_ms includes the device work it queued
+        t1 = time.perf_counter()
+        delivered = flushes()
         t2 = time.perf_counter()
         reps.append((t2 - t0, t1 - t0, t2 - t1))
+        if want is None:
+            want = sum(int(((vd == 0) & (sub.height >= 1) & (sub.height <= heights)).sum())
+                       for vd, (_, sub, _) in zip(verdicts, parts))
     tot, push, flush = sorted(reps)[1]
-    want = sum(int(((vd == 0) & (sub.height >= 1) & (sub.height <= heights)).sum())
-               for vd, (_, sub, _) in zip(verdicts, parts))
+    serial_ok = delivered == want
+    # overlapped cycles (the replica's steady state): cycle c+1's wire buffers
+    # are unmarshalled and authenticated on the device (push_wires_begin)
+    # while the host flushes cycle c's heights from the queue, and go into the
+    # queue (push_finish: filterHeight + mq insert) after those flushes --
+    # the reference's loop (replica.go:100-147) reaches a message only after
+    # the ones before it.  Every cycle delivers exactly its VALID messages of
+    # the flushed heights.
+    C = 8
+    restart()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    pend = ing.push_wires_begin(wires)
+    per_cycle, flush_s, ok_all = [], 0.0, True
+    for c in range(C):
+        ing.push_finish(pend)                          # cycle c into the queue
+        if c + 1 < C:
+            pend = ing.push_wires_begin(wires)         # cycle c + 1 authenticating beside the flushes
+        f0 = time.perf_counter()
+        got = flushes()
+        flush_s += time.perf_counter() - f0
+        ok_all &= got == want
+        per_cycle.append(got)
+        if c + 1 < C:
+            restart()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
     vh = torch.bincount(torch.cat(verdicts).long(), minlength=9).cpu().tolist()
     buffered = len(ing.mq)
     ing.close()
-    return {"messages": n, "push_ms": push * 1e3, "push_msgs_per_s": n / push,
-            "flushes": heights, "flush_ms": flush * 1e3, "total_msgs_per_s": n / tot,
-            "reps_total_ms": [round(r[0] * 1e3, 3) for r in reps],
-            "reps_push_ms": [round(r[1] * 1e3, 3) for r in reps], "reps_flush_ms": [round(r[2] * 1e3, 3) for r in reps],
-            "verdicts": vh, "delivered": delivered, "delivered_equals_valid_at_flushed_heights": delivered == want,
-            "buffered_after": buffered,
+    return {"messages": n, "total_msgs_per_s": n * C / el, "cycles": C, "ms_per_cycle": el / C * 1e3,
+            "flush_ms_per_cycle": flush_s / C * 1e3, "flushes": heights,
+            "delivered_per_cycle": per_cycle[0], "delivered_equals_valid_at_flushed_heights": bool(ok_all and serial_ok),
+            "serial": {"push_ms": push * 1e3, "push_msgs_per_s": n / push, "flush_ms": flush * 1e3,
+                       "total_msgs_per_s": n / tot, "reps_total_ms": [round(r[0] * 1e3, 3) for r in reps],
+                       "reps_push_ms": [round(r[1] * 1e3, 3) for r in reps],
+                       "reps_flush_ms": [round(r[2] * 1e3, 3) for r in reps],
+                       "delivered": delivered, "delivered_equals_valid_at_flushed_heights": bool(serial_ok)},
+            "verdicts": vh, "buffered_after": buffered,
             "note": "30 % adversarial C2 batch in random order (heights out of order), prevote and precommit wire "
-                    "buffers; wall time of the synchronous ingress calls (authenticate -> filterHeight -> mq "
-                    "insert, then the flushes), median of 3 cycles"}
+                    "buffers; per cycle: authenticate -> filterHeight -> mq insert, then 64 flushes with "
+                    "ResetHeight between (mq.Consume + vote logs).  total_msgs_per_s: 8 cycles back to back, each "
+                    "cycle's unmarshal + authentication queued on the device while the host flushes the previous "
+                    "cycle (Ingress.push_wires_begin / push_finish); serial: push then flushes, median of 3"}
 
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured float4 copy)

@@ -865,8 +865,12 @@ __global__ void k_fb_ready(const uint32_t* __restrict__ list, const uint32_t* __
 }
 
 // per-key table geometry of width wp
-size_t fb_tab_entries(int wp) { return wp == HD_FB_WW ? FbL<HD_FB_WW>::TAB : FbL<HD_FB_W>::TAB; }
-int fb_nwin(int wp) { return wp == HD_FB_WW ? FbL<HD_FB_WW>::NWIN : FbL<HD_FB_W>::NWIN; }
+size_t fb_tab_entries(int wp) {
+    return wp == HD_FB_WW ? FbL<HD_FB_WW>::TAB : wp == HD_FB_WN ? FbL<HD_FB_WN>::TAB : FbL<HD_FB_W>::TAB;
+}
+int fb_nwin(int wp) {
+    return wp == HD_FB_WW ? FbL<HD_FB_WW>::NWIN : wp == HD_FB_WN ? FbL<HD_FB_WN>::NWIN : FbL<HD_FB_W>::NWIN;
+}
 double fb_slot_bytes(int wp) {
     return (double)sizeof(gp) * (double)fb_tab_entries(wp) + (double)sizeof(ge) * (fb_nwin(wp) + 1) + 8;
 }
@@ -960,6 +964,9 @@ int fb_learn(hd_ctx* ctx, hipStream_t s) {
     if (f->wp == HD_FB_WW) {
         k_fb_bases<HD_FB_WW><<<g, 256, 0, s>>>(f->list, f->counts, f->pub, f->base);
         k_fb_runs<HD_FB_WW><<<fb_run_blocks(ctx), 256, 0, s>>>(f->list, f->counts, f->base, f->tabs, f->zr);
+    } else if (f->wp == HD_FB_WN) {
+        k_fb_bases<HD_FB_WN><<<g, 256, 0, s>>>(f->list, f->counts, f->pub, f->base);
+        k_fb_runs<HD_FB_WN><<<fb_run_blocks(ctx), 256, 0, s>>>(f->list, f->counts, f->base, f->tabs, f->zr);
     } else {
         k_fb_bases<HD_FB_W><<<g, 256, 0, s>>>(f->list, f->counts, f->pub, f->base);
         k_fb_runs<HD_FB_W><<<fb_run_blocks(ctx), 256, 0, s>>>(f->list, f->counts, f->base, f->tabs, f->zr);
@@ -1224,15 +1231,20 @@ static int split_k_for(const hd_ctx* ctx, uint32_t n) {
 }
 
 // Per-key window width for an admitted set of m: the wide tables
-// (HD_FB_WW, 13 additions for u2 instead of 16, 12x the bytes) when all m keys
-// fit the device's table budget next to what other contexts hold, else the
-// narrow ones.  HD_FB_PW=16|20 forces one.
+// (HD_FB_WW, 13 windows of u2, 490 MB per key) when all m keys fit the
+// device's table budget next to what other contexts hold; else the 16-bit
+// ones (16 windows, 40 MB) when all m keys fit the context's budget; else the
+// narrow ones (HD_FB_WN, 20 windows, 5 MB), so that thousands of signatories
+// still take the known-key check instead of the full recovery (a key
+// without a slot costs ~10x per message).  HD_VAR_KEY_WIDTH forces one.
 static int fb_pick_width(hd_ctx* ctx, uint32_t m) {
     if (ctx->var[HD_VAR_KEY_WIDTH]) return ctx->var[HD_VAR_KEY_WIDTH];
     FbWork* f = ctx->fb;
     const double others = (double)(fb_device_bytes(ctx->device) - std::min(fb_device_bytes(ctx->device), f->bytes));
-    const double need = fb_slot_bytes(HD_FB_WW) * ((double)m + 1);
-    return need <= f->budget - others ? HD_FB_WW : HD_FB_W;
+    if (fb_slot_bytes(HD_FB_WW) * ((double)m + 1) <= f->budget - others) return HD_FB_WW;
+    // (+ the foreign-key block's slots)
+    const double slots = (double)m + 1 + (ctx->var[HD_VAR_FOREIGN_KEYS] > 0 ? ctx->var[HD_VAR_FOREIGN_KEYS] : 0);
+    return fb_slot_bytes(HD_FB_W) * slots <= f->budget ? HD_FB_W : HD_FB_WN;
 }
 
 // mapped slots whose state is not READY (device idle: called after a sync)
@@ -1497,6 +1509,9 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         if (f->wp == HD_FB_WW) {
             if (k == 16) HD_SPLIT(16, HD_FB_WW);
             else HD_SPLIT(8, HD_FB_WW);
+        } else if (f->wp == HD_FB_WN) {
+            if (k == 16) HD_SPLIT(16, HD_FB_WN);
+            else HD_SPLIT(8, HD_FB_WN);
         } else {
             if (k == 16) HD_SPLIT(16, HD_FB_W);
             else HD_SPLIT(8, HD_FB_W);

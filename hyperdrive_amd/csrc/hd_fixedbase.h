@@ -33,6 +33,10 @@ namespace hd {
 #ifndef HD_FB_WW
 #define HD_FB_WW 20   // wide per-key tables: 13 windows, 12 x 2^19 + 2^16 points (490 MB), when the budget holds them
 #endif
+#ifndef HD_FB_WN
+#define HD_FB_WN 13   // narrow per-key tables: 20 windows, 19 x 4096 + 512 points (5.0 MB), when even the 16-bit
+                      // tables of every admitted key exceed the budget (thousands of signatories)
+#endif
 #ifndef HD_FB_WG
 #define HD_FB_WG 24   // the one shared G table: 11 windows, 10 x 2^23 + 2^16 points (6.0 GB)
 #endif

@@ -866,6 +866,9 @@ struct hd_mq {
     // (new senders interned, the pool swapped): the host's view (pool.n,
     // nsend) may no longer match it, so every later call is refused
     bool failed = false;
+    // an insert on a caller's stream waits for the context stream's queue
+    // work (a drop's or consume's head commits are queued there unsynchronised)
+    hipEvent_t order_ev = nullptr;
     uint32_t max_cap = 1000;
     Pool pool, spare;
     DevBuf buf[MQ__N];
@@ -1359,6 +1362,16 @@ static int mq_insert_flagged_impl(hd_mq* q, const hd_batch* d_batch, const uint8
     return HD_OK;
 }
 
+// stream s (an insert's) ordered after everything queued on the context's
+// stream so far
+static int mq_order_after_ctx(hd_mq* q, hipStream_t s) {
+    if (s == q->ctx->stream) return HD_OK;
+    if (!q->order_ev) QCHK(hipEventCreateWithFlags(&q->order_ev, hipEventDisableTiming), "mq order event");
+    QCHK(hipEventRecord(q->order_ev, q->ctx->stream), "mq order record");
+    QCHK(hipStreamWaitEvent(s, q->order_ev, 0), "mq order wait");
+    return HD_OK;
+}
+
 static int mq_refuse(hd_mq* q) {
     q->ctx->last_error = "message queue: an earlier insert failed part-way; the queue's state is lost";
     return HD_EDEVICE;
@@ -1392,6 +1405,7 @@ int hd_mq_destroy(hd_mq* q) {
     if (q->hstage) (void)hipHostFree(q->hstage);
     if (q->mstage) (void)hipHostFree(q->mstage);
     if (q->rep) (void)hipHostFree(q->rep);
+    if (q->order_ev) (void)hipEventDestroy(q->order_ev);
     delete q;
     return HD_OK;
 }
@@ -1424,6 +1438,7 @@ int hd_mq_insert_device(hd_mq* q, const hd_batch* d_batch, const uint8_t* d_inse
     int rc = 0;
     uint8_t* flag = (uint8_t*)qbuf(q, MQ_FLAG, nb, &rc);
     if (rc) return rc;
+    if ((rc = mq_order_after_ctx(q, s))) return rc;
     k_mq_flag_nz<<<nblk(nb), 256, 0, s>>>(nb, d_insert, flag);
     QCHK(hipGetLastError(), "k_mq_flag_nz");
     return mq_insert_flagged(q, d_batch, flag, s);
@@ -1447,6 +1462,7 @@ int hd_mq_insert_verified_device(hd_mq* q, const hd_batch* d_batch, const uint8_
     int rc = 0;
     uint8_t* flag = (uint8_t*)qbuf(q, MQ_FLAG, nb, &rc);
     if (rc) return rc;
+    if ((rc = mq_order_after_ctx(q, s))) return rc;
     k_mq_ingress<<<nblk(nb), 256, 0, s>>>(nb, d_verdict, d_batch->height, min_height, flag);
     QCHK(hipGetLastError(), "k_mq_ingress");
     return mq_insert_flagged(q, d_batch, flag, s);

@@ -74,6 +74,16 @@ class FlushResult:
         return self._proposes
 
 
+class PendingPush:
+    """push_wires_begin's handle: the combined device batch, its verdict
+    tensor (being written), the rows used, the verify streams and the
+    per-buffer verdict views."""
+    __slots__ = ("every", "verdicts", "lo", "used", "out")
+
+    def __init__(self, every, verdicts, lo, used, out):
+        self.every, self.verdicts, self.lo, self.used, self.out = every, verdicts, lo, used, out
+
+
 class Ingress:
     def __init__(self, v: Verifier, height: int = 1, max_capacity: int = 1000):
         self.v = v
@@ -137,10 +147,23 @@ class Ingress:
         (arrival order is batch order: inserting the buffers one after another
         keeps the same messages, hd_mq.h -- each insert re-sorts the whole
         queue, so one insert instead of two saves a full sort and its host
-        round trips).  Returns the verdicts of each buffer's complete records."""
+        round trips).  Returns the verdicts of each buffer's complete records.
+        = push_finish(push_wires_begin(parts))."""
+        return self.push_finish(self.push_wires_begin(parts, with_sig))
+
+    def push_wires_begin(self, parts, with_sig: bool = True) -> "PendingPush":
+        """The device half of push_wires: the unmarshal and authentication of
+        every buffer are queued on the verify streams and the call returns
+        without waiting.  The queue is untouched until push_finish, so the
+        caller may flush (serve the current heights from the queue, the
+        replica's flush, replica.go:251-264) while these messages are being
+        authenticated: the reference's loop handles a message only after the
+        ones before it (replica.go:100-147), and messages still in
+        authentication have not reached the replica yet.  filterHeight
+        (replica.go:247-249) applies at push_finish, with the height then."""
         torch = _torch()
         if not parts:
-            return []
+            return PendingPush(None, None, 0, [], [])
         dev = parts[0][1].device
         if getattr(self, "_streams", None) is None or self._streams[0].device != dev:
             self._streams = verify_streams(dev, 2)
@@ -175,13 +198,21 @@ class Ingress:
             out.append(verdict)
             used.append(s)
             lo += (complete + 15) // 16 * 16
-        if used:
-            s0 = used[0]
-            for s in used[1:]:
+        return PendingPush(every, verdicts, lo, used, out)
+
+    def push_finish(self, pend: "PendingPush"):
+        """The queue half of push_wires: filterHeight at the current height
+        and the one mq insert of the authenticated messages (after their
+        verification, in stream order).  Returns the verdicts of each
+        buffer's complete records."""
+        if pend.used:
+            s0 = pend.used[0]
+            for s in pend.used[1:]:
                 if s is not s0:
                     s0.wait_stream(s)
-            self.mq.insert_verified_device(every.rows(0, lo), verdicts[:lo], self.height, stream=s0)
-        return out
+            self.mq.insert_verified_device(pend.every.rows(0, pend.lo), pend.verdicts[:pend.lo], self.height,
+                                           stream=s0)
+        return pend.out
 
     def flush(self) -> FlushResult:
         """mq.Consume(CurrentHeight, ..., procsAllowed) with procsAllowed = the
@@ -221,4 +252,4 @@ class Ingress:
         return True
 
 
-__all__ = ["Ingress", "FlushResult"]
+__all__ = ["Ingress", "FlushResult", "PendingPush"]

@@ -25,9 +25,11 @@ for step in "$@"; do
     trace_c3) run trace_c3 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_c3 -o run -- python3 scripts/pipe_probe.py C3 6 ;;
     c4adv) run pytest_c4adv 600 python -u -m pytest tests/test_gpu_verify.py -m gpu -x -v -s -p no:cacheprovider --timeout 900 --timeout-method thread -k "c4_16m_adversarial" ;;
     selflaunch) run selflaunch_gloo2 300 python -u bench.py --gpus 2 --dist-backend gloo --steps 4 --warmup 1 --no-cpu --no-aux --no-sub --no-c4-check && (timeout -k 10 120 python bench.py --gpus 2 > gpurun_out/selflaunch_nccl2.log 2>&1; echo "rc=$?" >> gpurun_out/selflaunch_nccl2.log) ;;
+    r6tests) run pytest_r6 900 python -u -m pytest tests/test_fastpath.py tests/test_golden.py tests/test_ingress.py tests/test_mq.py tests/test_c1_network.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread && run pytest_r6_zero 300 python -u -m pytest tests/test_gpu_verify.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "zero_window" ;;
+    visprobe) run visibility_probe 120 scripts/visibility_probe 20 ;;
     mqpf) run pytest_mqpf 300 python -u -m pytest tests/test_mq.py -m gpu -x -v -p no:cacheprovider --timeout 200 --timeout-method thread -k "prefetched" ;;
     rehearse) run rehearse2 300 python bench.py --gpus 2 --dist-backend gloo --steps 4 --warmup 1 --no-cpu --no-aux --no-sub --no-c4-check && run rehearse3_c4 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 3 --master-addr 127.0.0.1 --master-port 29562 bench.py --gpus 3 --dist-backend gloo --global-batch 3145728 --steps 3 --warmup 1 --no-cpu --no-aux --no-sub --no-c4-check ;;
-    trace2) run trace2 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace2 -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub ;;
+    trace2) run trace2 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace2 -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub --no-c4-check ;;
     mqtest) run pytest_mq 600 python -u -m pytest tests/test_mq.py tests/test_ingress.py tests/test_c1_network.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     burst) run pytest_burst 300 python -u -m pytest tests/test_gpu_verify.py -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread -k "burst or adversarial" ;;
     golden) run pytest_golden 600 python -u -m pytest tests/test_golden.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
@@ -46,13 +48,13 @@ for step in "$@"; do
     gputest_all) run pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 600 python bench.py ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
-    prof1) HD_BENCH_VSTREAMS=1 run rocprof1 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof1 -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub ;;
-    prof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-aux --no-sub ;;
-    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 0 --no-cpu --no-aux --no-sub ;;
-    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 3 --warmup 0 --no-cpu --no-aux --no-sub ;;
+    prof1) HD_BENCH_VSTREAMS=1 run rocprof1 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof1 -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-aux --no-sub --no-c4-check ;;
+    prof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-aux --no-sub --no-c4-check ;;
+    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 0 --no-cpu --no-aux --no-sub --no-c4-check ;;
+    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 3 --warmup 0 --no-cpu --no-aux --no-sub --no-c4-check ;;
     listc) run list_counters 120 rocprofv3 -L ;;
-    pmc_stall) run pmc_stall 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_IFETCH SQ_INSTS_SMEM --output-format csv -d gpurun_out/pmc_stall -o run -- python3 bench.py --steps 3 --warmup 0 --no-cpu --no-aux --no-sub ;;
-    pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_sq -o run -- python3 bench.py --steps 3 --warmup 0 --no-cpu --no-aux --no-sub ;;
+    pmc_stall) run pmc_stall 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_IFETCH SQ_INSTS_SMEM --output-format csv -d gpurun_out/pmc_stall -o run -- python3 bench.py --steps 3 --warmup 0 --no-cpu --no-aux --no-sub --no-c4-check ;;
+    pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_sq -o run -- python3 bench.py --steps 3 --warmup 0 --no-cpu --no-aux --no-sub --no-c4-check ;;
     routedtest) HD_TALLY_CHECK=1 run pytest_routed 400 python -u -m pytest tests/test_multi_gpu.py tests/test_gpu_tally.py -m gpu -x -v -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     tallycheck) HD_TALLY_CHECK=1 run pytest_tallycheck 600 python -u -m pytest tests/test_gpu_tally.py tests/test_golden.py tests/test_multi_gpu.py tests/test_ingress.py tests/test_c1_network.py -m gpu -x -v -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     goldsums) run pytest_goldsums 600 python -u -m pytest tests/test_golden.py tests/test_gpu_verify.py tests/test_fastpath.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;

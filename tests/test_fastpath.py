@@ -325,11 +325,11 @@ def test_pairwise_check_equals_single(fb, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("width", [16, 20])
+@pytest.mark.parametrize("width", [13, 16, 20])
 def test_key_table_widths_equal_full_recovery(gpu, monkeypatch, width):
-    """Both per-key table widths (HD_FB_PW at context creation, then the
-    key_width variant: 16-bit windows, 16 additions for u2; 20-bit, 13
-    additions) give the full recovery's outputs on the adversarial mix, a
+    """Every per-key table width (HD_FB_PW at context creation, then the
+    key_width variant: 13-bit windows, 20 additions for u2; 16-bit, 16;
+    20-bit, 13) gives the full recovery's outputs on the adversarial mix, a
     ragged batch (n not a multiple of the 8 messages per lane of the split
     check), and after the admitted set is re-mapped at the other width (every
     key is learned again)."""
@@ -351,7 +351,7 @@ def test_key_table_widths_equal_full_recovery(gpu, monkeypatch, width):
         assert all(torch.equal(a, b) for a, b in zip(ref, got))
     assert fast.known_keys() > 0 and fast.fastpath_stats()[1] <= int((ref[0] != 0).sum())
     assert fast.variant("key_width") == width
-    fast.set_variant("key_width", 36 - width)      # (the environment is read at creation only)
+    fast.set_variant("key_width", {13: 20, 16: 13, 20: 16}[width])   # (the environment is read at creation only)
     fast.set_signatories(ks[0])
     assert fast.known_keys() == 0
     for _ in range(2):
@@ -456,3 +456,35 @@ def test_admitted_index_equals_binary_search(fb, n):
     assert out[:len(q)].tolist() == out[len(q):].tolist()
     if n:
         assert out[:len(t)].tolist() == list(range(len(t)))
+
+
+@pytest.mark.gpu
+def test_budget_picks_narrow_tables_for_many_keys(gpu, monkeypatch):
+    """The default width follows the table budget: with a budget that holds
+    every admitted key's 13-bit tables (5 MB) but not their 16-bit ones
+    (40 MB), the context takes 13-bit windows (20 key windows) and every key
+    still gets a slot -- no signatory is left to the full recovery -- with the
+    full recovery's outputs."""
+    import torch
+    from hyperdrive_amd.device import generate
+    from hyperdrive_amd.verify import Verifier
+    monkeypatch.setenv("HD_FB_MAX_BYTES", str(2e9))
+    S, n = 100, 40_000
+    fast = Verifier(0)
+    slow = Verifier(0)
+    slow.set_fastpath(False)
+    try:
+        ks = fast.gen_keys(S)
+        db, _, _ = generate(fast, 0, n, S, 10, keys=ks, start=31337)
+        for v in (fast, slow):
+            v.set_signatories(ks[0])
+        assert fast.fastpath_geometry()[1] == 20
+        ref = _run(slow, db, n)
+        for _ in range(3):
+            got = _run(fast, db, n)
+            assert all(torch.equal(a, b) for a, b in zip(ref, got))
+        assert fast.known_keys() == S
+        assert fast.fastpath_stats()[1] <= int((ref[0] != 0).sum()) + 5
+    finally:
+        fast.close()
+        slow.close()

@@ -128,3 +128,58 @@ def _run(ing, hb, order, first, later, H0, cap, coracle):
     # messages buffered while their sender was not admitted were delivered
     # after the ResetHeight that admitted it
     assert delivered_late > 0
+
+
+def test_overlapped_push_equals_serial(verifier):
+    """push_wires_begin queues a batch's unmarshal + authentication and
+    returns; flushes served meanwhile, then push_finish (filterHeight + mq
+    insert at the height reached), deliver exactly what the serial order
+    (flushes, then push_wires) delivers: every flush's messages, sender ids,
+    vote statuses and removed counts, and the queue afterwards."""
+    from hyperdrive_amd.codec import marshal_device
+    from hyperdrive_amd.device import DeviceBatch, generate
+    from hyperdrive_amd.ingress import Ingress
+    S, n = 7, 4000
+    db, sigs, _ = generate(verifier, 0, n, S, adv_pct=30, start=4242)
+    verifier.set_signatories(sigs)
+    H0 = int(db.height.min().item())
+
+    def wires(lo, hi):
+        out = []
+        for t in (2, 3):
+            idx = (db.type[lo:hi] == t).nonzero().flatten() + lo
+            sub = DeviceBatch(int(idx.numel()), *(getattr(db, f)[idx].contiguous()
+                                                   for f in ("type", "height", "round", "valid_round", "value",
+                                                             "frm", "sig")))
+            out.append((t, marshal_device(verifier, t, sub, with_sig=True), sub.n))
+        return out
+
+    w1, w2 = wires(0, n // 2), wires(n // 2, n)
+
+    def flushes(ing, h0, k):
+        res = []
+        for h in range(h0, h0 + k):
+            if h > ing.height:
+                ing.reset_height(h)
+            f = ing.flush()
+            res.append((f.consumed.height.tolist(), f.consumed.frm.tobytes(), f.consumed.sig.tobytes(),
+                        f.senders.tolist(), f.vote_status.tolist(), f.removed))
+        return res
+
+    serial, overlapped = Ingress(verifier, height=H0), Ingress(verifier, height=H0)
+    try:
+        serial.push_wires(w1)
+        a = flushes(serial, H0, 6)
+        serial.push_wires(w2)
+        a += flushes(serial, H0 + 6, 6)
+        overlapped.push_wires(w1)
+        pend = overlapped.push_wires_begin(w2)
+        b = flushes(overlapped, H0, 6)
+        overlapped.push_finish(pend)
+        b += flushes(overlapped, H0 + 6, 6)
+        assert a == b
+        assert sum(len(x[0]) for x in a) > 0
+        assert len(serial.mq) == len(overlapped.mq)
+    finally:
+        serial.close()
+        overlapped.close()

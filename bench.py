@@ -287,7 +287,7 @@ class Pipeline:
             self.t_out.dup = None
         self.t_part = None
         self.route_rows = None
-        if world > 1:
+        if dist is not None:
             from hyperdrive_amd.shard import tally_out
             # the shard's own tally, and the owner's tally of the shared rounds
             # it received (separate pinned outputs: the first one's uploads may
@@ -295,6 +295,8 @@ class Pipeline:
             self.t_part = tally_out(v, B, pinned=True)
             self.t_own = tally_out(v, total, pinned=True)
         self.tally_info = {}
+        self.tally_s = []            # host wall time of each synchronous tally (its thread)
+        self.phase_s = {}            # N > 1: host time per phase of the exchange, summed
         self.last_tally = None
         # HD_BENCH_ASYNC_TALLY=1 (single GPU): the tally is queued without a
         # host wait (hd_tally_device_bitmap_async) and a collector thread
@@ -397,10 +399,18 @@ class Pipeline:
         self.tickets[j] = None
 
     def tally(self, pending):
-        import torch
-        from hyperdrive_amd import _lib
         if pending is None or not self.do_tally:
             return
+        t0 = time.perf_counter()
+        try:
+            self._tally(pending)
+        finally:
+            self.tally_s.append(time.perf_counter() - t0)
+
+    def _tally(self, pending):
+        import numpy as np
+        import torch
+        from hyperdrive_amd import _lib
         bitmap, done = pending
         self.ts.wait_event(done)
         if self.dist is None:
@@ -412,33 +422,54 @@ class Pipeline:
             self.tally_info = {"n_hr": self.t_out.n_hr, "n_counts": self.t_out.n_counts}
             self.last_tally = (self.t_out, self.t_arr)
             return
-        from hyperdrive_amd.shard import (drop_rounds, exchange_routed, gather_tally_device, route_candidates,
-                                          shared_rounds, tally_part_device, tally_routed_device, unroute)
+        from hyperdrive_amd.shard import (drop_pairs_rows, exchange_ranges, exchange_routed, pack_tally,
+                                          ranges_overlap, round_range, route_candidates, routed_round_mask,
+                                          tally_routed_host, unroute)
+        lib = _lib.load()
         s = self.ts.cuda_stream
         g = self.tally_group
+        ph = self.phase_s
+        tp = time.perf_counter
         with torch.cuda.stream(self.ts):
-            local = tally_part_device(self.v, self.shard, bitmap.data_ptr(), 0, 1, s, self.t_part, self.dev)
-            local["counts"][:, 3] += self.lo           # reps -> global indices
+            t0 = tp()
+            t, a = self.t_part
+            rc = lib.hd_tally_device_bitmap_part(self.v.handle, ctypes.byref(self.shard), bitmap.data_ptr(), 0, 1,
+                                                 ctypes.byref(t), s)
+            if rc != 0:
+                raise _lib.HDError(rc, "hd_tally_device_bitmap_part", lib.hd_ctx_last_error(self.v.handle).decode())
+            nh = t.n_hr
+            hh, hr_ = a["hr_height"][:nh], a["hr_round"][:nh]
+            t1 = tp()
+            # the one per-step collective when no round straddles a shard edge
+            ranges = exchange_ranges(round_range(hh, hr_), self.world, group=g, device=self.dev)
+            t2 = tp()
+            local = pack_tally(a, t.n_counts, nh)          # host rows of the shard
+            local["counts"][:, 3] += self.lo                # reps -> global indices
             local["hr"][:, 5] += self.lo
-            shared = shared_rounds(local["hr"][:, :2], self.world, group=g)
-            routed_out = routed_in = 0
             mine = local
-            if shared.shape[0]:                        # (identical on every rank)
+            routed_out = routed_in = n_routed = 0
+            if ranges_overlap(ranges):                      # (identical on every rank)
+                m = routed_round_mask(hh, hr_, ranges, self.rank)
+                rh, rr = hh[m].astype(np.int64), hr_[m].astype(np.int64)
+                n_routed = int(m.sum())
+                order = np.lexsort((rr, rh))
+                rounds = torch.from_numpy(np.stack([rh[order], rr[order]], 1).reshape(-1, 2)).to(self.dev)
                 rows, counts = route_candidates(self.v, self.shard, bitmap.data_ptr(), self.lo, self.world, s,
-                                                rows=self.route_rows, rounds=shared)
+                                                rows=self.route_rows, rounds=rounds)
                 self.route_rows = rows
                 recv = exchange_routed(rows, counts, self.world, group=g)
                 routed_out, routed_in = int(sum(counts)), int(recv.shape[0])
-                mine = {k: drop_rounds(t, shared) for k, t in local.items()}
+                mine = {"counts": drop_pairs_rows(local["counts"], rh, rr), "hr": local["hr"][~m]}
                 if routed_in:
                     db, gidx = unroute(self.v, recv, s)
-                    own = tally_routed_device(self.v, db, gidx, s, self.t_own, self.dev)
-                    mine = {k: torch.cat([mine[k], own[k]]) for k in mine}
-            merged = gather_tally_device(mine, self.world, group=g)
-        self.tally_info = {"n_hr": len(merged["hr"]), "n_counts": len(merged["counts"]),
-                           "n_hr_this_rank": len(mine["hr"]), "shared_rounds": int(shared.shape[0]),
-                           "routed_in": routed_in, "routed_out": routed_out}
-        self.last_tally = merged
+                    own = tally_routed_host(self.v, db, gidx, s, self.t_own)
+                    mine = {k: np.concatenate([mine[k], own[k]]) for k in mine}
+            t3 = tp()
+        for k, dt in (("local", t1 - t0), ("ranges", t2 - t1), ("route", t3 - t2)):
+            ph.setdefault(k, []).append(dt)
+        self.tally_info = {"n_hr_this_rank": int(len(mine["hr"])), "n_counts_this_rank": int(len(mine["counts"])),
+                           "routed_rounds": n_routed, "routed_in": routed_in, "routed_out": routed_out}
+        self.last_tally = mine
 
     def run(self, steps):
         """steps verifications + tallies.  The tallies run on a host thread of
@@ -623,6 +654,13 @@ def main():
         else:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    elif os.environ.get("HD_BENCH_FORCE_DIST"):
+        # probe: one rank through the multi-rank tally path (RCCL group of 1):
+        # the host-side cost of the exchange's orchestration without xGMI
+        import torch.distributed as dist
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{free_port()}", world_size=1, rank=0,
+                                device_id=torch.device("cuda", 0))
     else:
         dist = None
         torch.cuda.set_device(0)
@@ -678,6 +716,7 @@ def main():
     if pipe.host_trace is not None:
         pipe.host_trace.clear()
     elapsed = timed(pipe, args.steps, dist, dev)
+    timed_tally_ms = [x * 1e3 for x in pipe.tally_s[-args.steps:]] or [0.0]
     if pipe.host_trace:
         t0h = pipe.host_trace[0][2]
         print("host trace:", [(a, k, round((t - t0h) * 1e3, 3)) for a, k, t in pipe.host_trace], file=sys.stderr)
@@ -705,11 +744,23 @@ def main():
     if dist is not None:
         # what every rank saw: its device, shard, own timed span and tally exchange
         ranks_seen = dist.get_world_size()
+        ts_ms = timed_tally_ms
         mine = {"rank": rank, "device": dev.index, "pid": os.getpid(), "shard": [lo, hi],
                 "ms_per_step": own_elapsed / args.steps * 1e3,
+                "tally_ms_mean": sum(ts_ms) / len(ts_ms), "tally_ms_max": max(ts_ms),
+                "tally_phase_ms_median": {k: float(np.median(v[-args.steps:])) * 1e3 for k, v in pipe.phase_s.items()},
                 "valid": int((verdict == 0).sum()), **pipe.tally_info}
         per_rank = [None] * ranks_seen
         dist.all_gather_object(per_rank, mine)
+        # untimed: the ranks' rows (disjoint rounds) merged once, for the totals
+        from hyperdrive_amd.shard import gather_tally_device
+        last = pipe.last_tally
+        merged = gather_tally_device({k: torch.from_numpy(np.ascontiguousarray(x)).to(dev) for k, x in last.items()},
+                                     world)
+        pipe.tally_info = {**pipe.tally_info, "n_hr": int(merged["hr"].shape[0]),
+                           "n_counts": int(merged["counts"].shape[0]),
+                           "note": "each rank keeps the rows of the rounds it tallied; n_hr / n_counts: all ranks' "
+                                   "rows merged once after the timed region"}
 
     # correctness gate: without --adv every message of the workload is an honest
     # vote by construction, so every verdict must be VALID, every recovered
@@ -789,6 +840,10 @@ def main():
             },
             "verdicts": hist,
             "tally": pipe.tally_info,
+            "tally_thread_ms": {"mean": sum(timed_tally_ms) / len(timed_tally_ms), "max": max(timed_tally_ms),
+                                "note": "host wall time of each step's tally on its thread, from its start (queued behind its "
+                                        "verification, whose end it waits for) to its results on the host (beside the next "
+                                        "verifications), timed region only"},
             "cold": {"first_batch_s": cold_s, "cold_msgs_per_s": total / cold_s,
                      "ctx_create_s": ctx_s, "cold_msgs_per_s_incl_ctx": total / (cold_s + ctx_s),
                      "note": "first batch on a fresh context: full recovery of every message, key learning and "

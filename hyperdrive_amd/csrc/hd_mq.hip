@@ -955,9 +955,12 @@ __global__ void k_mq_reply(ReplySrc src, uint32_t* __restrict__ rep, uint32_t se
 #pragma unroll
     for (uint32_t k = 0; k < HD_MQ_REPLY_WORDS; k++)
         if (t == k) w = src.p[k];
-    // the words were written by earlier kernels, some by atomics (the key
-    // ranges): a read-modify-write reads them where the atomics landed
-    if (t < src.n) rep[1 + t] = atomicAdd(const_cast<uint32_t*>(w), 0u);
+    // the words were written by earlier kernels of this stream, some by
+    // device-scope atomics (the key ranges): plain loads see them -- the
+    // kernel boundary orders them (scripts/visibility_probe.hip: 20 rounds x
+    // 2,048 reader blocks on all 8 XCDs after atomics from 8,192 blocks, 0
+    // stale words; profiles/round6/visibility_probe.log)
+    if (t < src.n) rep[1 + t] = *w;
     __threadfence_system();
     __syncthreads();
     if (t == 0) __hip_atomic_store(rep, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -178,6 +178,117 @@ def gather_tally_device(local, world: int, group=None):
     return merged
 
 
+# ---- the per-step exchange of the bench's N > 1 tally: round ranges --------
+# Each rank tallies its own shard (hd_tally_device_bitmap on the shard, rows
+# on the host).  A round whose candidates sit in one shard only is complete
+# there.  To find the rounds that may not be, the ranks exchange only the
+# lexicographic range [min, max] of their (height, round) pairs (one
+# all-gather of 4 int64): a round of this rank inside ANOTHER rank's range is
+# routed (every candidate of it in this shard goes to the round's owner,
+# partition_of); every other round stays local.  A round held by two ranks
+# lies inside both ranges, so both route it and its owner sees all of its
+# candidates (first-wins per (h, r, type, signer) needs them all,
+# process/process.go:823-892); a round routed by one rank only is tallied by
+# its owner from that rank's candidates alone -- the same rows.  In height
+# order (the C2 / C4 stream) only the rounds a shard boundary cuts fall inside
+# a neighbour's range; nothing else moves.  The ranks' final rows are disjoint
+# (each round tallied once) and their union is the single-GPU tally: each
+# rank holds the rounds it tallied, and merging them (gather_tally_device) is
+# the consumer's choice, not a per-step cost.
+EMPTY_RANGE = (np.iinfo(np.int64).max, np.iinfo(np.int64).max, np.iinfo(np.int64).min, np.iinfo(np.int64).min)
+
+
+def round_range(h: np.ndarray, r: np.ndarray) -> Tuple[int, int, int, int]:
+    """(hmin, rmin, hmax, rmax): the lexicographic extremes of the pairs
+    (h[k], r[k]); EMPTY_RANGE (min > max) for none."""
+    if len(h) == 0:
+        return EMPTY_RANGE
+    h = np.asarray(h, np.int64)
+    r = np.asarray(r, np.int64)
+    hmin, hmax = int(h.min()), int(h.max())
+    return hmin, int(r[h == hmin].min()), hmax, int(r[h == hmax].max())
+
+
+def _range_empty(g) -> bool:
+    return (g[0], g[1]) > (g[2], g[3])
+
+
+def exchange_ranges(rng, world: int, group=None, device=None) -> np.ndarray:
+    """All-gather every rank's round_range: an int64 [world, 4] array on the
+    host (one collective, one 32-byte-per-rank read back).  device: where the
+    collective runs (CUDA for RCCL; None or a gloo group: the CPU)."""
+    import torch
+    import torch.distributed as dist
+    if device is None or dist.get_backend(group) == "gloo":
+        device = "cpu"
+    t = torch.tensor(list(rng), dtype=torch.int64, device=device)
+    out = torch.empty(4 * world, dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(out, t, group=group)
+    return out.view(world, 4).cpu().numpy()
+
+
+def ranges_overlap(ranges: np.ndarray) -> bool:
+    """Whether any two non-empty ranges overlap -- exactly when some rank has a
+    round inside another's range (an overlap contains an endpoint of one
+    range, and endpoints are rounds), i.e. when any rank routes anything.
+    Every rank computes the same answer from the gathered ranges."""
+    live = [tuple(int(x) for x in g) for g in ranges if not _range_empty(g)]
+    for i in range(len(live)):
+        for j in range(i + 1, len(live)):
+            a, b = live[i], live[j]
+            lo = max((a[0], a[1]), (b[0], b[1]))
+            hi = min((a[2], a[3]), (b[2], b[3]))
+            if lo <= hi:
+                return True
+    return False
+
+
+def routed_round_mask(h: np.ndarray, r: np.ndarray, ranges: np.ndarray, rank: int) -> np.ndarray:
+    """Per pair (h[k], r[k]) of this rank: inside some other rank's range."""
+    h = np.asarray(h, np.int64)
+    r = np.asarray(r, np.int64)
+    m = np.zeros(len(h), bool)
+    for k, g in enumerate(ranges):
+        if k == rank or _range_empty(g):
+            continue
+        hmin, rmin, hmax, rmax = (int(x) for x in g)
+        ge = (h > hmin) | ((h == hmin) & (r >= rmin))
+        le = (h < hmax) | ((h == hmax) & (r <= rmax))
+        m |= ge & le
+    return m
+
+
+def pairs_isin(h: np.ndarray, r: np.ndarray, ph: np.ndarray, pr: np.ndarray) -> np.ndarray:
+    """Per pair (h[k], r[k]): one of the pairs (ph[j], pr[j])."""
+    h = np.asarray(h, np.int64)
+    r = np.asarray(r, np.int64)
+    ph = np.asarray(ph, np.int64)
+    pr = np.asarray(pr, np.int64)
+    if len(ph) == 0 or len(h) == 0:
+        return np.zeros(len(h), bool)
+    if len(ph) <= 8:
+        m = np.zeros(len(h), bool)
+        for a, b in zip(ph.tolist(), pr.tolist()):
+            m |= (h == a) & (r == b)
+        return m
+    # one int64 key per pair when both spans fit 32 bits, else a set lookup
+    h0, r0 = min(int(h.min()), int(ph.min())), min(int(r.min()), int(pr.min()))
+    h1, r1 = max(int(h.max()), int(ph.max())), max(int(r.max()), int(pr.max()))
+    if h1 - h0 < (1 << 31) and r1 - r0 < (1 << 32):
+        key = lambda x, y: ((x - h0) << 32) | (y - r0)
+        return np.isin(key(h, r), key(ph, pr))
+    want = set(zip(ph.tolist(), pr.tolist()))
+    return np.fromiter(((a, b) in want for a, b in zip(h.tolist(), r.tolist())), bool, len(h))
+
+
+def drop_pairs_rows(rows: np.ndarray, ph: np.ndarray, pr: np.ndarray) -> np.ndarray:
+    """rows (int64 [m, c], columns 0 and 1 height and round) without those of
+    the given pairs."""
+    if len(rows) == 0 or len(ph) == 0:
+        return rows
+    return rows[~pairs_isin(rows[:, 0], rows[:, 1], ph, pr)]
+
+
 # ---- routed tally (the C4 data path: no replicated batch) -----------------
 ROUTE_ROW_BYTES = 64       # include/hd_verify.h HD_ROUTE_ROW_BYTES
 
@@ -313,6 +424,20 @@ def tally_routed_device(v, db, gidx, stream, out, device):
         raise _lib.HDError(rc, "hd_tally_routed_device", lib.hd_ctx_last_error(v.handle).decode())
     packed = pack_tally(a, t.n_counts, t.n_hr)     # host copies of the pinned stage: the next call may reuse it
     return {"counts": torch.from_numpy(packed["counts"]).to(device), "hr": torch.from_numpy(packed["hr"]).to(device)}
+
+
+def tally_routed_host(v, db, gidx, stream, out) -> Dict[str, np.ndarray]:
+    """tally_routed_device with the packed rows left on the host (numpy
+    int64 {"counts": [k, 5], "hr": [m, 6]}, reps global indices)."""
+    from . import _lib
+    lib = _lib.load()
+    t, a = out
+    if db.n == 0:
+        return {"counts": np.zeros((0, 5), np.int64), "hr": np.zeros((0, 6), np.int64)}
+    rc = lib.hd_tally_routed_device(v.handle, ctypes.byref(db.c_struct()), gidx.data_ptr(), ctypes.byref(t), stream)
+    if rc != 0:
+        raise _lib.HDError(rc, "hd_tally_routed_device", lib.hd_ctx_last_error(v.handle).decode())
+    return pack_tally(a, t.n_counts, t.n_hr)
 
 
 def pack_tally(a, n_counts: int, n_hr: int) -> Dict[str, np.ndarray]:

@@ -389,3 +389,98 @@ def test_gloo_local_tally_plus_shared_rounds_equals_single_rank(world, name):
     if name == "height_order":
         # boundary rounds only: the one a boundary cuts, and one a copied vote reaches
         assert res[0][4] <= 2 * (world - 1) and routed <= 21 * res[0][4] < n_cand
+
+
+# ---- round ranges (the bench's per-step N > 1 exchange) --------------------
+def test_round_ranges_and_masks():
+    from hyperdrive_amd.shard import (EMPTY_RANGE, drop_pairs_rows, pairs_isin, ranges_overlap, round_range,
+                                      routed_round_mask)
+    assert round_range(np.array([], np.int64), np.array([], np.int64)) == EMPTY_RANGE
+    assert round_range(np.array([5, 3, 3, 7, 7]), np.array([1, 4, 2, 0, 9])) == (3, 2, 7, 9)
+    big = np.iinfo(np.int64).max
+    assert round_range(np.array([big, -big]), np.array([-1, 3])) == (-big, 3, big, -1)
+    r = np.array([[1, 0, 5, 3], [5, 3, 9, 0], list(EMPTY_RANGE), [20, 0, 30, 0]], np.int64)
+    assert ranges_overlap(r)                                       # (5, 3) is in both of the first two
+    assert not ranges_overlap(r[[0, 2, 3]])
+    assert not ranges_overlap(np.array([[1, 0, 5, 2], [5, 3, 9, 0]], np.int64))   # (5, 2) < (5, 3)
+    h, rr = np.array([1, 5, 5, 4]), np.array([0, 3, 2, 7])
+    assert routed_round_mask(h, rr, r, 0).tolist() == [False, True, False, False]
+    assert not routed_round_mask(h, rr, r[[0]], 0).any()
+    rows = np.array([[1, 0, 2], [5, 3, 2], [5, 3, 3], [4, 7, 2]], np.int64)
+    assert drop_pairs_rows(rows, np.array([5]), np.array([3])).tolist() == [[1, 0, 2], [4, 7, 2]]
+    # the vectorised (> 8 pairs) and the set (spans past 32 bits) forms agree with a set lookup
+    rng = np.random.default_rng(3)
+    for span in (1000, 1 << 40):
+        hh = rng.integers(-span, span, 5000)
+        r2 = rng.integers(0, 4, 5000)
+        ph, pr = hh[:40].copy(), r2[:40].copy()
+        want = {(a, b) for a, b in zip(ph.tolist(), pr.tolist())}
+        got = pairs_isin(hh, r2, ph, pr)
+        assert got.tolist() == [(a, b) in want for a, b in zip(hh.tolist(), r2.tolist())]
+
+
+def _range_worker(rank, world, port, name, empty, out_q):
+    from hyperdrive_amd.shard import (drop_pairs_rows, exchange_ranges, exchange_routed, gather_tally_device,
+                                      ranges_overlap, round_range, routed_round_mask)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b, verdicts = _case(name)
+    if empty is not None:                       # a shard with no candidate at all (an empty range)
+        lo_e, hi_e = shard_range(len(b), empty, world)
+        verdicts = [5 if lo_e <= i < hi_e else v for i, v in enumerate(verdicts)]
+    adm = sorted(set(b.frm))
+    lo, hi = shard_range(len(b), rank, world)
+    local = local_tally_rows(b, verdicts, lo, hi)
+    hh, hr = local["hr"][:, 0], local["hr"][:, 1]
+    ranges = exchange_ranges(round_range(hh, hr), world)
+    mine, routed, n_rounds = local, 0, 0
+    if ranges_overlap(ranges):
+        m = routed_round_mask(hh, hr, ranges, rank)
+        n_rounds = int(m.sum())
+        rows, counts = route_rows_np(b, verdicts, lo, hi, world, adm, rounds=set(zip(hh[m].tolist(), hr[m].tolist())))
+        recv = exchange_routed(torch.from_numpy(rows), counts, world)
+        own = routed_tally_rows(recv.numpy(), adm)
+        mine = {"counts": np.concatenate([drop_pairs_rows(local["counts"], hh[m], hr[m]), own["counts"]]),
+                "hr": np.concatenate([local["hr"][~m], own["hr"]])}
+        routed = sum(counts)
+    merged = gather_tally_device({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in mine.items()}, world)
+    out_q.put((rank, merged["counts"].tolist(), merged["hr"].tolist(), routed, n_rounds, len(mine["hr"])))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,world,empty", [("random_mix", 2, None), ("height_order", 2, None),
+                                              ("random_mix", 3, None), ("height_order", 3, None),
+                                              ("height_order", 3, 1), ("height_order", 4, 3)])
+def test_gloo_round_ranges_tally_equals_single_rank(name, world, empty):
+    """The bench's per-step N > 1 tally: each rank tallies its shard, the
+    ranks all-gather only their (height, round) ranges, a rank routes exactly
+    its rounds inside another rank's range (hd_route_candidates_listed_device,
+    restated) to their owners, keeps the rest, and adds the routed rounds it
+    owns.  The ranks' rows are disjoint and, merged, equal the single-rank
+    tally row for row -- with duplicates and a double vote straddling shard
+    boundaries, shards in random order (most rounds routed), and a shard with
+    no candidate (an empty range).  In height order only boundary rounds move."""
+    b, verdicts = _case(name)
+    if empty is not None:
+        lo_e, hi_e = shard_range(len(b), empty, world)
+        verdicts = [5 if lo_e <= i < hi_e else v for i, v in enumerate(verdicts)]
+    want = tally_rows(b, verdicts)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_range_worker, args=(r, world, port, name, empty, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, counts, hrs, routed, n_rounds, n_mine in res:
+        assert counts == want["counts"].tolist() and hrs == want["hr"].tolist()
+    assert sum(r[5] for r in res) == len(want["hr"])                # every round tallied by exactly one rank
+    if name == "height_order":
+        assert sum(r[4] for r in res) <= 3 * (world - 1)            # boundary rounds only
+        # (with 3 ranks an empty middle shard leaves no two neighbours to share a round)
+        assert (sum(r[4] for r in res) > 0) == ((world, empty) != (3, 1))

@@ -313,6 +313,7 @@ class Pipeline:
         import threading
         self.tally_lock = threading.Lock()   # submit (this thread) and collect (the collector) share tally state
         self.tally_group = None   # set by main() for RCCL ranks
+        self.range_group = None   # HD_BENCH_RANGE_GLOO: a gloo group for the per-step range exchange
         self.host_trace = [] if os.environ.get("HD_BENCH_HOSTTRACE") else None
 
     def verify(self, k):
@@ -441,7 +442,9 @@ class Pipeline:
             hh, hr_ = a["hr_height"][:nh], a["hr_round"][:nh]
             t1 = tp()
             # the one per-step collective when no round straddles a shard edge
-            ranges = exchange_ranges(round_range(hh, hr_), self.world, group=g, device=self.dev)
+            rg = self.range_group
+            ranges = exchange_ranges(round_range(hh, hr_), self.world, group=rg or g,
+                                     device=None if rg is not None else self.dev)
             t2 = tp()
             local = pack_tally(a, t.n_counts, nh)          # host rows of the shard
             local["counts"][:, 3] += self.lo                # reps -> global indices
@@ -700,6 +703,8 @@ def main():
     pipe = Pipeline(v, db, total, lo, rank, world, dist, ws, ts, tally=not args.no_tally)
     if dist is not None and args.dist_backend == "nccl":
         pipe.tally_group = dist.new_group(backend="nccl")
+        if os.environ.get("HD_BENCH_RANGE_GLOO"):    # A/B: the per-step range exchange over gloo (host)
+            pipe.range_group = dist.new_group(backend="gloo")
 
     # The first batch on a fresh context is the cold start: every message
     # takes the full recovery, the first VALID message of each signatory

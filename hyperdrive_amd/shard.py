@@ -380,7 +380,7 @@ def exchange_routed(rows, counts, world: int, group=None):
     import torch.distributed as dist
     if rows.is_cuda and dist.get_backend(group) == "gloo":
         # gloo moves host tensors only (CPU rehearsal of the multi-GPU path)
-        return exchange_routed(rows.cpu(), counts, world, group).to(rows.device)
+        return exchange_routed(rows[: sum(counts)].cpu(), counts, world, group).to(rows.device)
     send = torch.tensor(counts, dtype=torch.int64, device=rows.device)
     recv = torch.empty(world, dtype=torch.int64, device=rows.device)
     dist.all_to_all_single(recv, send, group=group)

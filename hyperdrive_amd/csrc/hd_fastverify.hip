@@ -1080,29 +1080,24 @@ int fb_evict(hd_ctx* ctx, bool* changed) {
         FBCHK(hipStreamSynchronize(s), "evict counters");
         return HD_OK;
     }
-    std::vector<uint32_t> nd(HD_FD_WORDS, 0u);
-    std::vector<ge> nkey(B);
-    for (const Ent& e : keep) {
-        uint32_t b = fdict_bucket(e.from);
-        int p = 0;
-        for (; p < 8 && nd[b] != 0u; p++) b = (b + 1u) & (B - 1u);
-        if (p == 8 && e.slot != 0xFFFFFFFFu) {
-            // a slot holder finds no bucket within the probe limit: the new
-            // dictionary would strand its slot (READY / LEARNED, no From
-            // mapping to it, never seen by a later pass).  Keep the old
-            // dictionary and slots for this pass.
-            f->evict_aborts++;
-            f->fwait = std::min(2 * f->fwait, HD_FD_EVICT_WAIT_MAX);
-            FBCHK(hipMemsetAsync(f->fhit, 0, 4 * hit.size(), s), "evict counters");
-            FBCHK(hipStreamSynchronize(s), "evict counters");
-            return HD_OK;
-        }
-        if (p == 8) continue;   // no room (slotless: simply forgotten)
-        nd[b] = 2u;
-        nd[B + b] = e.slot;
-        memcpy(&nd[2 * B + 8 * b], e.from, 32);
-        nkey[b] = e.key;
+    std::vector<uint32_t> nd(HD_FD_WORDS, 0u), efrom(8 * keep.size() + 8), eslot(keep.size() + 1);
+    std::vector<int32_t> where(keep.size() + 1);
+    for (size_t k = 0; k < keep.size(); k++) {
+        memcpy(&efrom[8 * k], keep[k].from, 32);
+        eslot[k] = keep[k].slot;
     }
+    if (!fdict_rebuild(nd.data(), where.data(), efrom.data(), eslot.data(), (uint32_t)keep.size())) {
+        // a slot holder would find no bucket: keep the old dictionary and
+        // slots for this pass (fdict_rebuild)
+        f->evict_aborts++;
+        f->fwait = std::min(2 * f->fwait, HD_FD_EVICT_WAIT_MAX);
+        FBCHK(hipMemsetAsync(f->fhit, 0, 4 * hit.size(), s), "evict counters");
+        FBCHK(hipStreamSynchronize(s), "evict counters");
+        return HD_OK;
+    }
+    std::vector<ge> nkey(B);
+    for (size_t k = 0; k < keep.size(); k++)
+        if (where[k] >= 0) nkey[where[k]] = keep[k].key;
     FBCHK(hipMemcpyAsync(f->fdict, nd.data(), 4 * (size_t)HD_FD_WORDS, hipMemcpyHostToDevice, s), "evict write");
     FBCHK(hipMemcpyAsync(f->fkey, nkey.data(), sizeof(ge) * B, hipMemcpyHostToDevice, s), "evict write");
     FBCHK(hipMemsetAsync(f->fhit, 0, 4 * hit.size(), s), "evict counters");

@@ -85,6 +85,35 @@ HD int32_t fdict_find(const uint32_t* fd, const uint32_t from_be[8]) {
     return -1;
 }
 
+// The dictionary rebuilt on the host (fb_evict) from n entries in priority
+// order -- slot holders first, then the slotless Froms worth keeping:
+// nd (HD_FD_WORDS words, zeroed here) gets each entry in the first free
+// bucket of its probe run, where[k] its bucket (-1: dropped).  A slotless
+// entry without a free bucket within the 8 probes is dropped; a slot holder
+// without one makes the rebuild fail (returns false): dropping it would
+// leave its slot READY / LEARNED with no From mapping to it, lost to every
+// later pass, so the caller keeps the old dictionary instead.
+inline bool fdict_rebuild(uint32_t* nd, int32_t* where, const uint32_t* ent_from_be, const uint32_t* ent_slot,
+                          uint32_t n) {
+    for (uint32_t w = 0; w < HD_FD_WORDS; w++) nd[w] = 0u;
+    for (uint32_t k = 0; k < n; k++) {
+        const uint32_t* from = ent_from_be + 8 * (size_t)k;
+        uint32_t b = fdict_bucket(from);
+        int p = 0;
+        for (; p < 8 && nd[b] != 0u; p++) b = (b + 1u) & (HD_FD_BUCKETS - 1u);
+        if (p == 8) {
+            if (ent_slot[k] != 0xFFFFFFFFu) return false;
+            where[k] = -1;
+            continue;
+        }
+        nd[b] = 2u;
+        nd[HD_FD_BUCKETS + b] = ent_slot[k];
+        for (int w = 0; w < 8; w++) nd[2u * HD_FD_BUCKETS + 8u * b + w] = from[w];
+        where[k] = (int32_t)b;
+    }
+    return true;
+}
+
 // slot states of the per-signatory tables (device memory, hd_fastverify.hip)
 #define HD_FB_EMPTY 0u     // no key known
 #define HD_FB_CLAIMED 1u   // a recovering lane is writing the key

@@ -639,3 +639,11 @@ extern "C" void hdh_adm_lookup(const uint8_t* sorted32, uint32_t n, const uint8_
         out[q + k] = hd::admitted_find(words.data(), n, steps, key);
     }
 }
+
+// the foreign-key dictionary's bucket and its host rebuild (fb_evict)
+extern "C" uint32_t hdh_fdict_bucket(const uint32_t* from_be) { return hd::fdict_bucket(from_be); }
+extern "C" int hdh_fdict_rebuild(const uint32_t* from_be, const uint32_t* slot, uint32_t n, uint32_t* nd,
+                                 int32_t* where) {
+    return hd::fdict_rebuild(nd, where, from_be, slot, n) ? 1 : 0;
+}
+extern "C" int32_t hdh_fdict_find(const uint32_t* nd, const uint32_t* from_be) { return hd::fdict_find(nd, from_be); }

@@ -488,3 +488,60 @@ def test_budget_picks_narrow_tables_for_many_keys(gpu, monkeypatch):
     finally:
         fast.close()
         slow.close()
+
+
+def test_foreign_dictionary_rebuild_keeps_slot_holders(hostmath):
+    """fb_evict's dictionary rebuild (hd_fixedbase.h fdict_rebuild, host
+    build): Froms whose buckets collide fill one probe run of 8.  Slotless
+    entries past it are dropped; a slot holder past it makes the rebuild fail,
+    so the caller keeps the old dictionary instead of stranding the slot
+    (ADVICE r5).  Every entry that got a bucket is found again by
+    fdict_find with its slot."""
+    import ctypes
+    L = hostmath.L
+    L.hdh_fdict_bucket.restype = ctypes.c_uint32
+    L.hdh_fdict_rebuild.restype = ctypes.c_int
+    L.hdh_fdict_find.restype = ctypes.c_int32
+    rng = np.random.default_rng(77)
+    NONE = 0xFFFFFFFF
+
+    def bucket(f):
+        return L.hdh_fdict_bucket(f.ctypes.data_as(ctypes.c_void_p))
+
+    same = []                                   # 10 Froms in bucket 5
+    while len(same) < 10:
+        f = rng.integers(0, 2 ** 32, 8, dtype=np.uint64).astype(np.uint32)
+        if bucket(f) == 5:
+            same.append(f)
+    other = [f for f in (rng.integers(0, 2 ** 32, (40, 8), dtype=np.uint64).astype(np.uint32)) if bucket(f) not in
+             range(5, 13)][:5]
+
+    def rebuild(froms, slots):
+        fr = np.ascontiguousarray(np.array(froms, np.uint32).reshape(-1, 8))
+        sl = np.array(slots, np.uint32)
+        nd = np.zeros(10 * 128, np.uint32)
+        where = np.zeros(len(slots), np.int32)
+        ok = L.hdh_fdict_rebuild(fr.ctypes.data_as(ctypes.c_void_p), sl.ctypes.data_as(ctypes.c_void_p),
+                                 len(slots), nd.ctypes.data_as(ctypes.c_void_p),
+                                 where.ctypes.data_as(ctypes.c_void_p))
+        return ok, nd, where
+
+    def find(nd, f):
+        return L.hdh_fdict_find(nd.ctypes.data_as(ctypes.c_void_p), np.ascontiguousarray(f).ctypes.data_as(
+            ctypes.c_void_p))
+
+    # 8 holders fill the run; 2 slotless colliding Froms and the others follow
+    froms = same[:8] + same[8:] + other
+    slots = list(range(100, 108)) + [NONE, NONE] + [NONE] * len(other)
+    ok, nd, where = rebuild(froms, slots)
+    assert ok == 1
+    assert sorted(where[:8].tolist()) == list(range(5, 13)) and where[8:10].tolist() == [-1, -1]
+    for f, s in zip(froms[:8], slots[:8]):
+        assert find(nd, f) == s
+    assert all(w >= 0 for w in where[10:])
+    # a ninth slot holder in the same run: the rebuild refuses
+    ok, _, _ = rebuild(same[:9], list(range(100, 109)))
+    assert ok == 0
+    # holders first: the same nine with the ninth slotless rebuild, the ninth dropped
+    ok, nd, where = rebuild(same[:9], list(range(100, 108)) + [NONE])
+    assert ok == 1 and where[8] == -1 and find(nd, same[8]) == -1

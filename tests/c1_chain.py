@@ -99,6 +99,25 @@ def make_stream(O):
     return out
 
 
+def replica_view(z, k: int, replicas: int = 4):
+    """Replica k's arrival of the same network stream (BASELINE configs[0]: 4
+    replicas, f = 1, 100 heights; replica/replica_test.go:378-423 runs n
+    replicas over one in-memory network): replica 0 sees the committed
+    order; replica k > 0 sees the same signed messages chunked with its own
+    random delays (-2 .. +6 chunks) and shuffled inside each chunk's
+    propose / prevote / precommit buffers."""
+    if k == 0:
+        return z
+    rng = np.random.default_rng(0xC1 + 17 * k)
+    n = len(z["type"])
+    h = z["height"].astype(np.int64)
+    chunk = np.clip((h - 1) // CHUNK + rng.integers(-2, 7, n), 0, HEIGHTS // CHUNK - 1)
+    order = np.lexsort((rng.random(n), z["type"], chunk))
+    out = {key: (val if key == "admitted" else val[order]) for key, val in z.items()}
+    out["chunk"] = chunk[order].astype(np.int32)
+    return out
+
+
 def _batch(z, idx):
     from hyperdrive_amd.verify import Batch
     return Batch(z["type"][idx], z["height"][idx], z["round"][idx], z["valid_round"][idx], z["value"][idx],

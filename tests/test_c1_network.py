@@ -17,7 +17,7 @@ import os
 import numpy as np
 import pytest
 
-from c1_chain import HEIGHTS, run_gpu, run_oracle
+from c1_chain import HEIGHTS, replica_view, run_gpu, run_oracle
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -67,3 +67,40 @@ def test_c1_gpu_ingress_matches_chain(gpu):
     for got, want in zip(rep.records, exp["records"]):
         assert got == want, (got, want)
     assert len(rep.records) == len(exp["records"])
+
+
+def _canonical_commits(oracle):
+    return [[h, oracle.canonical_value(h, 0).hex()] for h in range(1, HEIGHTS + 1)]
+
+
+def test_c1_four_replicas_commit_identically(coracle, oracle):
+    """C1 as the reference's network test states it (replica_test.go:414-423:
+    every live replica commits the same values): 4 replicas, each with its
+    own arrival order of the same broadcast stream, through the chain of CPU
+    restatements -- every replica commits the proposer's value at every
+    height 1..100."""
+    z, _ = _load()
+    want = _canonical_commits(oracle)
+    for k in range(4):
+        rep = run_oracle(replica_view(z, k), coracle)
+        assert [list(c) for c in rep.commits] == want, k
+
+
+@pytest.mark.gpu
+def test_c1_four_replicas_gpu(gpu, coracle, oracle):
+    """The same 4 replicas on the GPU, one context and one Ingress each (one
+    hd_ctx per replica): every replica's flush records equal its
+    own restatement chain's, and all four commit the same 100 values."""
+    z, _ = _load()
+    want = _canonical_commits(oracle)
+    ctxs = [gpu.Verifier(0) for _ in range(4)]
+    try:
+        for k, v in enumerate(ctxs):
+            view = replica_view(z, k)
+            rep = run_gpu(view, v)
+            ref = run_oracle(view, coracle)
+            assert rep.records == ref.records, k
+            assert [list(c) for c in rep.commits] == want, k
+    finally:
+        for v in ctxs:
+            v.close()

@@ -996,8 +996,10 @@ def sub_benchmarks(args, v, sigs, foreign, dev, ws, ts):
         "msgs_per_s": B * args.sub_steps / el, "ms_per_step": el / args.sub_steps * 1e3,
         "verdicts": torch.bincount(vd.long(), minlength=8).cpu().tolist(),
         "known_signatories": v.fastpath_stats()[0], "key_windows": v.fastpath_geometry()[1],
-        "note": "hd_set_signatories keeps the 100 known keys; the first batch learns the 50 new ones (full "
-                "recovery of their first messages, tables built in the same call)"}
+        "note": "hd_set_signatories keeps the known keys while the table width stays (the first batch learns the "
+                "new ones: full recovery of their first messages, tables built in the same call); when 150 keys' "
+                "tables no longer fit the width the 100 had (22-bit), the context re-maps at the next width and the "
+                "first batch learns every key again"}
     del p6, db6
     # C3: its own context (the 1000 keys' tables need the table budget the
     # C2 context holds: it is released first by the caller's order)
@@ -1034,15 +1036,16 @@ def sub_benchmarks(args, v, sigs, foreign, dev, ws, ts):
     return out
 
 
-def many_signatories(args, dev, ws, ts, sizes=(2000, 4000), steps=10):
+def many_signatories(args, dev, ws, ts, sizes=(2000, 4000, 8000), steps=10):
     """The per-key table budget with thousands of signatories (replica.go:54,
     136-144: the admitted set and f): the C2 stream (1M messages, signer =
-    i % S) from S = 2,000 and 4,000 signatories, each on a context of its
-    own, with the default table width -- 13-bit windows (5 MB per key) once
-    the 16-bit tables (40 MB per key) of every key no longer fit the
-    context's 64 GiB budget -- and with the 16-bit width forced (the round-5
-    behaviour: the keys past ~1,600 slots get no table and take the full
-    recovery, ~10x per message).  Per line: msgs/s over `steps` steps of
+    i % S) from S = 2,000, 4,000 and 8,000 signatories, each on a context of
+    its own (the headline's context keeps its tables beside it), with the
+    default table width -- the widest whose tables for every key fit what is
+    left of the device's budget: 16-bit windows (40 MB per key), then 13-bit
+    (5 MB per key) -- and, at 8,000, with the 16-bit width forced (the
+    round-5 tiers: the keys past the budget's slots get no table and take the
+    full recovery, ~10x per message).  Per line: msgs/s over `steps` steps of
     verify + tally, keys with tables, the last step's full-recovery count."""
     import torch
     import hyperdrive_amd as hd
@@ -1050,7 +1053,7 @@ def many_signatories(args, dev, ws, ts, sizes=(2000, 4000), steps=10):
     B = args.batch
     res = {}
     for S in sizes:
-        for width in (0, 16):
+        for width in ((0, 16) if S == sizes[-1] else (0,)):
             vS = hd.Verifier(dev.index)
             try:
                 if width:
@@ -1079,9 +1082,9 @@ def many_signatories(args, dev, ws, ts, sizes=(2000, 4000), steps=10):
                 del p, db
             finally:
                 vS.close()
-    res["note"] = ("C2 stream with S signatories; default: the context picks 20-, 16- or 13-bit key tables by its "
-                   "64 GiB budget (13-bit here: every key gets a table); forced_16bit: the round-5 tiers, where keys "
-                   "past the budget's slots take the full recovery")
+    res["note"] = ("C2 stream with S signatories; default: the context picks 22-, 20-, 16- or 13-bit key tables by "
+                   "what is left of the device's table budget (3/4 of its memory, the headline's context holding its "
+                   "own); forced_16bit: every key past the budget's 16-bit slots takes the full recovery")
     return res
 
 

@@ -866,10 +866,16 @@ __global__ void k_fb_ready(const uint32_t* __restrict__ list, const uint32_t* __
 
 // per-key table geometry of width wp
 size_t fb_tab_entries(int wp) {
-    return wp == HD_FB_WW ? FbL<HD_FB_WW>::TAB : wp == HD_FB_WN ? FbL<HD_FB_WN>::TAB : FbL<HD_FB_W>::TAB;
+    return wp == HD_FB_WX   ? FbL<HD_FB_WX>::TAB
+           : wp == HD_FB_WW ? FbL<HD_FB_WW>::TAB
+           : wp == HD_FB_WN ? FbL<HD_FB_WN>::TAB
+                            : FbL<HD_FB_W>::TAB;
 }
 int fb_nwin(int wp) {
-    return wp == HD_FB_WW ? FbL<HD_FB_WW>::NWIN : wp == HD_FB_WN ? FbL<HD_FB_WN>::NWIN : FbL<HD_FB_W>::NWIN;
+    return wp == HD_FB_WX   ? FbL<HD_FB_WX>::NWIN
+           : wp == HD_FB_WW ? FbL<HD_FB_WW>::NWIN
+           : wp == HD_FB_WN ? FbL<HD_FB_WN>::NWIN
+                            : FbL<HD_FB_W>::NWIN;
 }
 double fb_slot_bytes(int wp) {
     return (double)sizeof(gp) * (double)fb_tab_entries(wp) + (double)sizeof(ge) * (fb_nwin(wp) + 1) + 8;
@@ -961,7 +967,10 @@ int fb_learn(hd_ctx* ctx, hipStream_t s) {
     f->fforce = false;
     const uint32_t g = (uint32_t)std::max(ctx->n_cu, 1) * 4u;
     k_fb_list<<<1, 256, 0, s>>>(f->nslots, f->state, f->list, f->counts);
-    if (f->wp == HD_FB_WW) {
+    if (f->wp == HD_FB_WX) {
+        k_fb_bases<HD_FB_WX><<<g, 256, 0, s>>>(f->list, f->counts, f->pub, f->base);
+        k_fb_runs<HD_FB_WX><<<fb_run_blocks(ctx), 256, 0, s>>>(f->list, f->counts, f->base, f->tabs, f->zr);
+    } else if (f->wp == HD_FB_WW) {
         k_fb_bases<HD_FB_WW><<<g, 256, 0, s>>>(f->list, f->counts, f->pub, f->base);
         k_fb_runs<HD_FB_WW><<<fb_run_blocks(ctx), 256, 0, s>>>(f->list, f->counts, f->base, f->tabs, f->zr);
     } else if (f->wp == HD_FB_WN) {
@@ -1167,7 +1176,12 @@ int hd_fb_init(hd_ctx* ctx) {
     ctx->fb = new (std::nothrow) FbWork();
     if (!ctx->fb) return HD_ENOMEM;
     FbWork* f = ctx->fb;
-    f->budget = 64.0 * (1ull << 30);
+    // the device's table budget: HD_FB_MAX_BYTES, else 3/4 of its memory
+    // (216 GB of an MI355X's 288 GB); a replica that owns its GPU spends it
+    // on wider tables, i.e. fewer additions per message (fb_pick_width)
+    size_t total = 0;
+    f->budget = hipDeviceTotalMem(&total, ctx->device) == hipSuccess && total ? 0.75 * (double)total
+                                                                                  : 64.0 * (1ull << 30);
     if (const char* m = getenv("HD_FB_MAX_BYTES")) f->budget = atof(m);
     f->max_slots = (uint32_t)std::max(1.0, std::min(1e6, f->budget / fb_slot_bytes(f->wp)));
     FBCHK(hipMalloc(&f->counts, 8), "fb counts");
@@ -1225,21 +1239,39 @@ static int split_k_for(const hd_ctx* ctx, uint32_t n) {
     return n >= (1u << 20) - (1u << 16) ? 16 : 8;
 }
 
-// Per-key window width for an admitted set of m: the wide tables
-// (HD_FB_WW, 13 windows of u2, 490 MB per key) when all m keys fit the
-// device's table budget next to what other contexts hold; else the 16-bit
+// Per-key window width for an admitted set of m: the widest tables
+// (HD_FB_WX, 12 windows of u2, 1.48 GB per key) when all m keys and the
+// foreign-key block fit the device's table budget next to what other contexts
+// hold; else the wide ones (HD_FB_WW, 13 windows, 490 MB) when the m keys do;
+// else the 16-bit
 // ones (16 windows, 40 MB) when all m keys fit the context's budget; else the
 // narrow ones (HD_FB_WN, 20 windows, 5 MB), so that thousands of signatories
 // still take the known-key check instead of the full recovery (a key
 // without a slot costs ~10x per message).  HD_VAR_KEY_WIDTH forces one.
-static int fb_pick_width(hd_ctx* ctx, uint32_t m) {
+// The table bytes the device can still give this context: its free memory
+// (other processes' allocations included) plus what this context holds.
+static double fb_free_cap(hd_ctx* ctx) {
+    size_t fr = 0, tot = 0;
+    (void)hipSetDevice(ctx->device);
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 1e300;
+    return 0.9 * (double)fr + (double)ctx->fb->bytes;
+}
+
+// (cap: the widest width allowed, 0 = any; hd_fb_map_signatories narrows it
+// when an allocation fails)
+static int fb_pick_width(hd_ctx* ctx, uint32_t m, int cap) {
     if (ctx->var[HD_VAR_KEY_WIDTH]) return ctx->var[HD_VAR_KEY_WIDTH];
     FbWork* f = ctx->fb;
     const double others = (double)(fb_device_bytes(ctx->device) - std::min(fb_device_bytes(ctx->device), f->bytes));
-    if (fb_slot_bytes(HD_FB_WW) * ((double)m + 1) <= f->budget - others) return HD_FB_WW;
+    const double free_cap = fb_free_cap(ctx);
+    const double shared = std::min(f->budget - others, free_cap);
     // (+ the foreign-key block's slots)
     const double slots = (double)m + 1 + (ctx->var[HD_VAR_FOREIGN_KEYS] > 0 ? ctx->var[HD_VAR_FOREIGN_KEYS] : 0);
-    return fb_slot_bytes(HD_FB_W) * slots <= f->budget ? HD_FB_W : HD_FB_WN;
+    const auto allowed = [cap](int w) { return cap == 0 || w <= cap; };
+    if (allowed(HD_FB_WX) && fb_slot_bytes(HD_FB_WX) * slots <= shared) return HD_FB_WX;
+    if (allowed(HD_FB_WW) && fb_slot_bytes(HD_FB_WW) * ((double)m + 1) <= shared) return HD_FB_WW;
+    if (allowed(HD_FB_W) && fb_slot_bytes(HD_FB_W) * slots <= std::min(f->budget, free_cap)) return HD_FB_W;
+    return HD_FB_WN;
 }
 
 // mapped slots whose state is not READY (device idle: called after a sync)
@@ -1257,15 +1289,31 @@ static int fb_count_not_ready(hd_ctx* ctx) {
     return HD_OK;
 }
 
+static int fb_map(hd_ctx* ctx, const uint8_t* sorted, uint32_t m, int cap);
+
+// Map the admitted set to table slots.  A table allocation the device
+// cannot serve (another context or process took the memory since the width
+// was picked) retries at the next narrower width, down to 13 bits, instead
+// of failing the set change.
 int hd_fb_map_signatories(hd_ctx* ctx, const uint8_t* sorted, uint32_t m) {
+    int rc = HD_OK;
+    for (int cap : {0, HD_FB_WW, HD_FB_W, HD_FB_WN}) {
+        rc = fb_map(ctx, sorted, m, cap);
+        if (rc != HD_ENOMEM || ctx->var[HD_VAR_KEY_WIDTH]) break;
+        (void)hipGetLastError();   // the failed allocation must not surface in a later launch check
+    }
+    return rc;
+}
+
+static int fb_map(hd_ctx* ctx, const uint8_t* sorted, uint32_t m, int cap) {
     FbWork* f = ctx->fb;
     // no verify call of this context may still learn into a slot reassigned
     // here (hd_set_signatories quiesced the context already)
     int rq = hd_ctx_quiesce(ctx);
     if (rq) return rq;
     *(volatile uint32_t*)f->nr_host = 0xFFFFFFFFu;
-    const int wp = fb_pick_width(ctx, m);
-    if (wp != f->wp) {
+    const int wp = fb_pick_width(ctx, m, cap);
+    if (wp != f->wp || (cap && f->nslots < f->used)) {
         // another table width: every key is learned again (full recovery)
         fb_free_tables(ctx);
         f->slot_of.clear();
@@ -1273,7 +1321,8 @@ int hd_fb_map_signatories(hd_ctx* ctx, const uint8_t* sorted, uint32_t m) {
         f->used = 1;
         f->fcap = f->fres = 0;   // the foreign block goes with the tables
         f->wp = wp;
-        f->max_slots = (uint32_t)std::max(1.0, std::min(1e6, f->budget / fb_slot_bytes(wp)));
+        f->max_slots =
+            (uint32_t)std::max(1.0, std::min(1e6, std::min(f->budget, fb_free_cap(ctx)) / fb_slot_bytes(wp)));
         int ra = fb_alloc_slots(ctx);
         if (ra) return ra;
     }
@@ -1501,7 +1550,10 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
         const int k = split_k_for(ctx, n);
         f->last_k = k;
 #define HD_SPLIT(K, WP) launch_split<K, WP>(ctx, b, d_digest, d_verdict, d_rec32, d_signer, d_bitmap, rows, sc, s, auth)
-        if (f->wp == HD_FB_WW) {
+        if (f->wp == HD_FB_WX) {
+            if (k == 16) HD_SPLIT(16, HD_FB_WX);
+            else HD_SPLIT(8, HD_FB_WX);
+        } else if (f->wp == HD_FB_WW) {
             if (k == 16) HD_SPLIT(16, HD_FB_WW);
             else HD_SPLIT(8, HD_FB_WW);
         } else if (f->wp == HD_FB_WN) {

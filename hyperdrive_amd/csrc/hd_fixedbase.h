@@ -33,6 +33,10 @@ namespace hd {
 #ifndef HD_FB_WW
 #define HD_FB_WW 20   // wide per-key tables: 13 windows, 12 x 2^19 + 2^16 points (490 MB), when the budget holds them
 #endif
+#ifndef HD_FB_WX
+#define HD_FB_WX 22   // widest per-key tables: 12 windows, 11 x 2^21 + 2^14 points (1.48 GB), when every admitted
+                      // key's fits the device's budget (round 6: one addition fewer than 20-bit, -4 % k_fast_sums)
+#endif
 #ifndef HD_FB_WN
 #define HD_FB_WN 13   // narrow per-key tables: 20 windows, 19 x 4096 + 512 points (5.0 MB), when even the 16-bit
                       // tables of every admitted key exceed the budget (thousands of signatories)

@@ -321,7 +321,9 @@ int hd_ctx_set_variant(hd_ctx* ctx, int which, int value) {
         case HD_VAR_SUM_PREFETCH: ok = value == 1 || value == 2; break;
         case HD_VAR_RECOVER_G: case HD_VAR_SLOW_LIFT: ok = value == 0 || value == 1; break;
         case HD_VAR_SPLIT_K: ok = value == -1 || value == 8 || value == 16; break;
-        case HD_VAR_KEY_WIDTH: ok = value == 0 || value == HD_FB_W || value == HD_FB_WW || value == HD_FB_WN; break;
+        case HD_VAR_KEY_WIDTH:
+            ok = value == 0 || value == HD_FB_W || value == HD_FB_WW || value == HD_FB_WN || value == HD_FB_WX;
+            break;
         case HD_VAR_WAVE_PRIO: ok = value >= 0 && value <= 3; break;
         case HD_VAR_FOREIGN_KEYS: ok = value >= 0 && value <= 64; break;
         default: ok = false;   // a key of a variant removed in round 5 (measured without gain)

@@ -29,6 +29,7 @@ for step in "$@"; do
     proffull) run proffull 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/proffull -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-aux --no-sub --no-c4-check ;;
     abkw) run ab_kw 900 bash scripts/gpu_ab_prof.sh "kw20a:HD_FB_PW=20" "kw16a:HD_FB_PW=16" "kw13a:HD_FB_PW=13" "kw20b:HD_FB_PW=20" "kw16b:HD_FB_PW=16" "kw13b:HD_FB_PW=13" ;;
     abc3) for rep in a b; do run c3_def_$rep 200 python -u scripts/c3_ab.py def && HD_FAST_K=16 run c3_k16_$rep 200 python -u scripts/c3_ab.py k16 && HD_SUM_WAVES=3 run c3_w3_$rep 200 python -u scripts/c3_ab.py w3 && HD_FAST_K=16 HD_SUM_WAVES=3 run c3_k16w3_$rep 200 python -u scripts/c3_ab.py k16w3 && HD_SUM_WAVES=2 run c3_w2_$rep 200 python -u scripts/c3_ab.py w2; done ;;
+    abkw22) run ab_kw22 900 bash scripts/gpu_ab_prof.sh "kw20a:HD_FB_PW=20" "kw22a:HD_LIB=hyperdrive_amd/_lib/var/libhd_kw22.so HD_FB_MAX_BYTES=2.2e11" "kw20b:HD_FB_PW=20" "kw22b:HD_LIB=hyperdrive_amd/_lib/var/libhd_kw22.so HD_FB_MAX_BYTES=2.2e11" ;;
     abg) run ab_g 900 bash scripts/gpu_ab_prof.sh "g24a:HD_SUM_WAVES=0" "g22a:HD_LIB=hyperdrive_amd/_lib/var/libhd_g22.so" "g20a:HD_LIB=hyperdrive_amd/_lib/var/libhd_g20.so" "g24b:HD_SUM_WAVES=0" "g22b:HD_LIB=hyperdrive_amd/_lib/var/libhd_g22.so" "g20b:HD_LIB=hyperdrive_amd/_lib/var/libhd_g20.so" ;;
     distgloo) HD_BENCH_FORCE_DIST=1 HD_BENCH_RANGE_GLOO=1 run distgloo 300 python -u bench.py --no-cpu --no-aux --no-sub --no-c4-check && run nodist 300 python -u bench.py --no-cpu --no-aux --no-sub --no-c4-check && HD_BENCH_FORCE_DIST=1 run distprobe 300 python -u bench.py --no-cpu --no-aux --no-sub --no-c4-check && HD_BENCH_FORCE_DIST=1 HD_BENCH_RANGE_GLOO=1 run distgloo_b 300 python -u bench.py --no-cpu --no-aux --no-sub --no-c4-check ;;
     distprobe) HD_BENCH_FORCE_DIST=1 run distprobe 300 python -u bench.py --no-cpu --no-aux --no-sub --no-c4-check && run nodist 300 python -u bench.py --no-cpu --no-aux --no-sub --no-c4-check && HD_BENCH_FORCE_DIST=1 run distprobe_b 300 python -u bench.py --no-cpu --no-aux --no-sub --no-c4-check && run nodist_b 300 python -u bench.py --no-cpu --no-aux --no-sub --no-c4-check ;;

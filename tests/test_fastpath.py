@@ -325,11 +325,11 @@ def test_pairwise_check_equals_single(fb, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("width", [13, 16, 20])
+@pytest.mark.parametrize("width", [13, 16, 20, 22])
 def test_key_table_widths_equal_full_recovery(gpu, monkeypatch, width):
     """Every per-key table width (HD_FB_PW at context creation, then the
     key_width variant: 13-bit windows, 20 additions for u2; 16-bit, 16;
-    20-bit, 13) gives the full recovery's outputs on the adversarial mix, a
+    20-bit, 13; 22-bit, 12) gives the full recovery's outputs on the adversarial mix, a
     ragged batch (n not a multiple of the 8 messages per lane of the split
     check), and after the admitted set is re-mapped at the other width (every
     key is learned again)."""
@@ -351,7 +351,7 @@ def test_key_table_widths_equal_full_recovery(gpu, monkeypatch, width):
         assert all(torch.equal(a, b) for a, b in zip(ref, got))
     assert fast.known_keys() > 0 and fast.fastpath_stats()[1] <= int((ref[0] != 0).sum())
     assert fast.variant("key_width") == width
-    fast.set_variant("key_width", {13: 20, 16: 13, 20: 16}[width])   # (the environment is read at creation only)
+    fast.set_variant("key_width", {13: 20, 16: 13, 20: 22, 22: 16}[width])   # (the environment is read at creation only)
     fast.set_signatories(ks[0])
     assert fast.known_keys() == 0
     for _ in range(2):

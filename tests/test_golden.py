@@ -181,7 +181,7 @@ VARIANTS = [("default", None, None), ("verify_waves_2", "verify_waves", 2), ("ve
             ("sum_waves_2", "sum_waves", 2), ("sum_waves_3", "sum_waves", 3), ("sum_waves_4", "sum_waves", 4),
             ("sum_prefetch_2", "sum_prefetch", 2), ("split_k_8", "split_k", 8), ("split_k_16", "split_k", 16),
             ("recover_glv_g", "recover_g", 1), ("key_width_13", "key_width", 13), ("key_width_16", "key_width", 16),
-            ("key_width_20", "key_width", 20),
+            ("key_width_20", "key_width", 20), ("key_width_22", "key_width", 22),
             ("wave_prio_2", "wave_prio", 2), ("foreign_keys_0", "foreign_keys", 0), ("slow_lift_0", "slow_lift", 0)]
 
 

@@ -500,6 +500,8 @@ def _zero_digit_rows(oracle, S):
         (rng.randrange(1, O.N), rng.randrange(1, O.N) & ~ones(63, 79)),  # 16-bit key window 4 zero
         (rng.randrange(1, O.N), rng.randrange(1, O.N) & ~ones(51, 65)),  # 13-bit key window 4 zero
         (rng.randrange(1, O.N), rng.randrange(1, 2 ** 246)),     # key top window zero (13-bit tables)
+        (rng.randrange(1, O.N), rng.randrange(1, 2 ** 241)),     # key top window zero (22-bit tables)
+        (rng.randrange(1, O.N), rng.randrange(1, O.N) & ~ones(87, 109)),  # 22-bit key window 4 zero
         (rng.randrange(1, O.N), 2 ** 128 + 1),                   # sparse u2
         (rng.randrange(1, O.N), rng.randrange(1, O.N)),          # control
     ]
@@ -520,7 +522,7 @@ def _zero_digit_rows(oracle, S):
     return rows, digests, keys
 
 
-@pytest.mark.parametrize("key_width", [13, 16, 20])
+@pytest.mark.parametrize("key_width", [13, 16, 20, 22])
 def test_zero_window_digits_vs_oracle(gpu, oracle, key_width):
     """The known-key check's rare branch (k_fast_sums: a wavefront with a
     zero window digit adds the window's entry 0 and takes it off again; a sum

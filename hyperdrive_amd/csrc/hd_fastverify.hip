@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -1291,14 +1292,37 @@ static int fb_count_not_ready(hd_ctx* ctx) {
 
 static int fb_map(hd_ctx* ctx, const uint8_t* sorted, uint32_t m, int cap);
 
+// HD_FB_TRACE=1: one stderr line per table-mapping attempt (debug aid)
+static bool fb_trace() {
+    static const bool on = getenv("HD_FB_TRACE") != nullptr;
+    return on;
+}
+
+// One table mapping at a time per device: the width pick reads the bytes
+// the device's other contexts hold and its free memory, so contexts mapping
+// concurrently (hd_multi's per-device threads over one GPU) would each count
+// the memory the others are about to take and oversubscribe the device.
+static std::mutex g_fb_map_mutex[64];
+
 // Map the admitted set to table slots.  A table allocation the device
-// cannot serve (another context or process took the memory since the width
-// was picked) retries at the next narrower width, down to 13 bits, instead
-// of failing the set change.
+// cannot serve (another process took the memory since the width was picked)
+// retries at the next narrower width, down to 13 bits, instead of failing
+// the set change.
 int hd_fb_map_signatories(hd_ctx* ctx, const uint8_t* sorted, uint32_t m) {
+    std::lock_guard<std::mutex> lock(g_fb_map_mutex[(unsigned)ctx->device % 64u]);
     int rc = HD_OK;
     for (int cap : {0, HD_FB_WW, HD_FB_W, HD_FB_WN}) {
+        if (fb_trace()) {
+            size_t fr = 0, tot = 0;
+            (void)hipMemGetInfo(&fr, &tot);
+            fprintf(stderr, "[fb] ctx %p m %u cap %d: wp %d nslots %u used %u max %u bytes %.2fG dev %.2fG free %.2fG\n",
+                    (void*)ctx, m, cap, ctx->fb->wp, ctx->fb->nslots, ctx->fb->used, ctx->fb->max_slots,
+                    ctx->fb->bytes / 1e9, fb_device_bytes(ctx->device) / 1e9, fr / 1e9);
+        }
         rc = fb_map(ctx, sorted, m, cap);
+        if (fb_trace())
+            fprintf(stderr, "[fb] ctx %p -> rc %d wp %d nslots %u used %u %s\n", (void*)ctx, rc, ctx->fb->wp,
+                    ctx->fb->nslots, ctx->fb->used, rc ? ctx->last_error.c_str() : "");
         if (rc != HD_ENOMEM || ctx->var[HD_VAR_KEY_WIDTH]) break;
         (void)hipGetLastError();   // the failed allocation must not surface in a later launch check
     }

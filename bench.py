@@ -1042,7 +1042,7 @@ def many_signatories(args, dev, ws, ts, sizes=(2000, 4000, 8000), steps=10):
     i % S) from S = 2,000, 4,000 and 8,000 signatories, each on a context of
     its own (the headline's context keeps its tables beside it), with the
     default table width -- the widest whose tables for every key fit what is
-    left of the device's budget: 16-bit windows (40 MB per key), then 13-bit
+    left of the device's budget: 16-bit windows (36 MB per key), then 13-bit
     (5 MB per key) -- and, at 8,000, with the 16-bit width forced (the
     round-5 tiers: the keys past the budget's slots get no table and take the
     full recovery, ~10x per message).  Per line: msgs/s over `steps` steps of
@@ -1083,7 +1083,7 @@ def many_signatories(args, dev, ws, ts, sizes=(2000, 4000, 8000), steps=10):
             finally:
                 vS.close()
     res["note"] = ("C2 stream with S signatories; default: the context picks 22-, 20-, 16- or 13-bit key tables by "
-                   "what is left of the device's table budget (3/4 of its memory, the headline's context holding its "
+                   "what is left of the device's table budget (64 GiB, the headline's context holding its "
                    "own); forced_16bit: every key past the budget's 16-bit slots takes the full recovery")
     return res
 

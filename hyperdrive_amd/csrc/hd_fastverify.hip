@@ -1177,12 +1177,14 @@ int hd_fb_init(hd_ctx* ctx) {
     ctx->fb = new (std::nothrow) FbWork();
     if (!ctx->fb) return HD_ENOMEM;
     FbWork* f = ctx->fb;
-    // the device's table budget: HD_FB_MAX_BYTES, else 3/4 of its memory
-    // (216 GB of an MI355X's 288 GB); a replica that owns its GPU spends it
-    // on wider tables, i.e. fewer additions per message (fb_pick_width)
-    size_t total = 0;
-    f->budget = hipDeviceTotalMem(&total, ctx->device) == hipSuccess && total ? 0.75 * (double)total
-                                                                                  : 64.0 * (1ull << 30);
+    // the device's table budget: HD_FB_MAX_BYTES, else 64 GiB -- room for
+    // the headline's 100 signatories at 20 bits beside the G table and
+    // everything else the process keeps resident (its batches, torch's
+    // cache, more contexts).  A budget of 3/4 of the device (216 GB: 22-bit
+    // tables for 100 keys, one addition fewer) measured the same headline
+    // within noise and starved the process's other allocations; a replica
+    // that owns its GPU may still set it.
+    f->budget = 64.0 * (1ull << 30);
     if (const char* m = getenv("HD_FB_MAX_BYTES")) f->budget = atof(m);
     f->max_slots = (uint32_t)std::max(1.0, std::min(1e6, f->budget / fb_slot_bytes(f->wp)));
     FBCHK(hipMalloc(&f->counts, 8), "fb counts");
@@ -1243,9 +1245,9 @@ static int split_k_for(const hd_ctx* ctx, uint32_t n) {
 // Per-key window width for an admitted set of m: the widest tables
 // (HD_FB_WX, 12 windows of u2, 1.48 GB per key) when all m keys and the
 // foreign-key block fit the device's table budget next to what other contexts
-// hold; else the wide ones (HD_FB_WW, 13 windows, 490 MB) when the m keys do;
+// hold; else the wide ones (HD_FB_WW, 13 windows, 407 MB) when the m keys do;
 // else the 16-bit
-// ones (16 windows, 40 MB) when all m keys fit the context's budget; else the
+// ones (16 windows, 36 MB) when all m keys fit the context's budget; else the
 // narrow ones (HD_FB_WN, 20 windows, 5 MB), so that thousands of signatories
 // still take the known-key check instead of the full recovery (a key
 // without a slot costs ~10x per message).  HD_VAR_KEY_WIDTH forces one.

@@ -15,7 +15,7 @@
 // bases, so they run without doublings over per-base tables of W-bit Booth
 // windows: entry (j, d) = d 2^(W j) B for 1 <= d <= 2^(W-1), and each signed
 // digit costs one mixed addition (W = 16: 16 windows, 32 additions per
-// message for the two scalars, 40 MB of affine points per base).  No square
+// message for the two scalars, 36 MB of affine points per base).  No square
 // root is needed: the affine result is compared with x and the parity of y.
 //
 // verify_fast returns V_VALID only when that identity holds, an exact early
@@ -28,10 +28,10 @@
 namespace hd {
 
 #ifndef HD_FB_W
-#define HD_FB_W 16    // per-key tables: 16 windows, 15 x 32768 + 65536 points (40 MB)
+#define HD_FB_W 16    // per-key tables: 16 windows, 15 x 32768 + 65536 points (36 MB)
 #endif
 #ifndef HD_FB_WW
-#define HD_FB_WW 20   // wide per-key tables: 13 windows, 12 x 2^19 + 2^16 points (490 MB), when the budget holds them
+#define HD_FB_WW 20   // wide per-key tables: 13 windows, 12 x 2^19 + 2^16 points (407 MB), when the budget holds them
 #endif
 #ifndef HD_FB_WX
 #define HD_FB_WX 22   // widest per-key tables: 12 windows, 11 x 2^21 + 2^14 points (1.48 GB), when every admitted

@@ -170,8 +170,8 @@ int hd_ctx_profile(hd_ctx* ctx, int enable);
 #define HD_VAR_RECOVER_G 5      /* the full recovery's u1 G: 0 from the fixed-base G table (default), 1 from the
                                    GLV ladder's own 12-bit table [HD_RECOVER_GLV_G] */
 #define HD_VAR_KEY_WIDTH 7      /* per-key table windows: 0 by the table budget (default: 22 while every key's
-                                   1.48 GB table fits, else 20 (490 MB), else 16 (40 MB), else 13 (5 MB); the
-                                   budget is HD_FB_MAX_BYTES or 3/4 of the device's memory, shared by the
+                                   1.48 GB table fits, else 20 (407 MB), else 16 (36 MB), else 13 (5 MB); the
+                                   budget is HD_FB_MAX_BYTES or 64 GiB per device, shared by the
                                    process's contexts and bounded by the free memory), or 13, 16, 20, 22;
                                    applies from the next hd_set_signatories [HD_FB_PW] */
 #define HD_VAR_WAVE_PRIO 8      /* wave issue priority (s_setprio 0..3) of the known-key check's short kernels

@@ -51,7 +51,7 @@ for step in "$@"; do
     hostpipe) run pytest_host 300 python -u -m pytest tests/test_host_pipeline.py -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     host_trace) run host_trace 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/host_trace -o run -- python3 scripts/host_probe.py ;;
     multitest) run pytest_multi 300 python -u -m pytest tests/test_multi_gpu.py tests/test_gpu_tally.py -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread ;;
-    gtest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    gtest) run pytest_gpu 1120 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     gputest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     gputest_all) run pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 600 python bench.py ;;

@@ -462,7 +462,7 @@ def test_admitted_index_equals_binary_search(fb, n):
 def test_budget_picks_narrow_tables_for_many_keys(gpu, monkeypatch):
     """The default width follows the table budget: with a budget that holds
     every admitted key's 13-bit tables (5 MB) but not their 16-bit ones
-    (40 MB), the context takes 13-bit windows (20 key windows) and every key
+    (36 MB), the context takes 13-bit windows (20 key windows) and every key
     still gets a slot -- no signatory is left to the full recovery -- with the
     full recovery's outputs."""
     import torch

@@ -998,8 +998,8 @@ def sub_benchmarks(args, v, sigs, foreign, dev, ws, ts):
         "known_signatories": v.fastpath_stats()[0], "key_windows": v.fastpath_geometry()[1],
         "note": "hd_set_signatories keeps the known keys while the table width stays (the first batch learns the "
                 "new ones: full recovery of their first messages, tables built in the same call); when 150 keys' "
-                "tables no longer fit the width the 100 had (22-bit), the context re-maps at the next width and the "
-                "first batch learns every key again"}
+                "tables no longer fit the width the 100 had, the context re-maps at the next width and the first "
+                "batch learns every key again"}
     del p6, db6
     # C3: its own context (the 1000 keys' tables need the table budget the
     # C2 context holds: it is released first by the caller's order)

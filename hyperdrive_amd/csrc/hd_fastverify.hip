@@ -55,6 +55,7 @@ struct FbWork {
     ge* pub = nullptr;          // max_slots keys
     uint32_t* state = nullptr;  // max_slots HD_FB_* states
     int32_t* adm_slot = nullptr;  // admitted sorted index -> slot
+    bool map_ok = true;           // the last hd_fb_map_signatories succeeded (else: full recovery only)
     size_t cap_adm_slot = 0;
     uint32_t* list = nullptr;     // slot work list (max_slots)
     uint32_t* counts = nullptr;   // [0] slots to build (the table builder's)
@@ -933,6 +934,11 @@ int fb_grow_slots(hd_ctx* ctx, uint32_t want) {
     FbWork* f = ctx->fb;
     want = std::min(want, f->max_slots);
     const size_t TAB = fb_tab_entries(f->wp);
+    // test hook: HD_FB_FAIL_WIDTH=w fails every table allocation at width w
+    // as the device would when another process took the memory
+    // (tests/test_fastpath.py: the narrower-width retry of hd_fb_map_signatories)
+    if (const char* fw = getenv("HD_FB_FAIL_WIDTH"))
+        if (atoi(fw) == f->wp && f->nslots < want) return hd_ctx_fail(ctx, hipErrorOutOfMemory, "fb table chunk (HD_FB_FAIL_WIDTH)");
     while (f->nslots < want) {
         const uint32_t k = std::min<uint32_t>(HD_FB_CHUNK, f->max_slots - f->nslots);
         gp* c = nullptr;
@@ -1328,6 +1334,10 @@ int hd_fb_map_signatories(hd_ctx* ctx, const uint8_t* sorted, uint32_t m) {
         if (rc != HD_ENOMEM || ctx->var[HD_VAR_KEY_WIDTH]) break;
         (void)hipGetLastError();   // the failed allocation must not surface in a later launch check
     }
+    // a set change that failed here leaves slots mapped without tables (and
+    // the device's slot map of the previous set): until a mapping succeeds,
+    // every message takes the full recovery against the new admitted set
+    ctx->fb->map_ok = rc == HD_OK;
     return rc;
 }
 
@@ -1559,7 +1569,7 @@ static int fb_verify_impl(hd_ctx* ctx, const DevBatch& b, const uint8_t* d_diges
     rc = hd_dev_grow(ctx, (void**)&sc.slow2, &sc.cap_slow2, 4 * (size_t)b.n);
     if (rc) return rc;
     FBCHK(hipMemsetAsync(sc.count, 0, 8, s), "fb count reset");
-    if (ctx->n_adm > 0 && f->adm_slot) {
+    if (ctx->n_adm > 0 && f->adm_slot && f->map_ok) {
         const size_t row_words = 62;   // per message
         rc = hd_dev_grow(ctx, (void**)&sc.rows, &sc.cap_rows, 4 * row_words * (size_t)b.n);
         if (rc) return rc;

@@ -490,6 +490,53 @@ def test_budget_picks_narrow_tables_for_many_keys(gpu, monkeypatch):
         slow.close()
 
 
+@pytest.mark.gpu
+def test_failed_table_allocation_retries_narrower(gpu, monkeypatch):
+    """A per-key table allocation the device refuses (HD_FB_FAIL_WIDTH: the
+    library's test hook fails every table allocation at that width, as when
+    another process took the memory after the width was picked): the set
+    change retries at the next narrower width (20 -> 16 bits) and the
+    outputs equal the full recovery's.  With the width forced
+    (HD_VAR_KEY_WIDTH) there is no retry: hd_set_signatories fails with
+    HD_ENOMEM, and until a set change succeeds every message takes the full
+    recovery against the new set, with the same outputs; once the memory is
+    there the next set change maps the tables."""
+    import torch
+    from hyperdrive_amd import _lib
+    from hyperdrive_amd.device import generate
+    from hyperdrive_amd.verify import Verifier
+    monkeypatch.setenv("HD_FB_FAIL_WIDTH", "20")
+    S, n = 100, 40_000
+    fast, forced, slow = Verifier(0), Verifier(0), Verifier(0)
+    slow.set_fastpath(False)
+    forced.set_variant("key_width", 20)
+    try:
+        ks = fast.gen_keys(S)
+        db, _, _ = generate(fast, 0, n, S, 10, keys=ks, start=4242)
+        fast.set_signatories(ks[0])
+        slow.set_signatories(ks[0])
+        assert fast.fastpath_geometry()[1] == 16
+        with pytest.raises(_lib.HDError):
+            forced.set_signatories(ks[0])
+        ref = _run(slow, db, n)
+        for v in (fast, forced):
+            for _ in range(2):
+                got = _run(v, db, n)
+                assert all(torch.equal(a, b) for a, b in zip(ref, got))
+        assert fast.known_keys() == S
+        monkeypatch.delenv("HD_FB_FAIL_WIDTH")
+        forced.set_signatories(ks[0])
+        assert forced.fastpath_geometry()[1] == 13
+        for _ in range(3):
+            got = _run(forced, db, n)
+            assert all(torch.equal(a, b) for a, b in zip(ref, got))
+        assert forced.known_keys() == S
+    finally:
+        fast.close()
+        forced.close()
+        slow.close()
+
+
 def test_foreign_dictionary_rebuild_keeps_slot_holders(hostmath):
     """fb_evict's dictionary rebuild (hd_fixedbase.h fdict_rebuild, host
     build): Froms whose buckets collide fill one probe run of 8.  Slotless

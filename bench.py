@@ -17,12 +17,18 @@ only messages [k*B, (k+1)*B) of the N*B-message stream (C4 generator;
 under torch.distributed.run uses the launcher's ranks; without a launcher
 (no WORLD_SIZE) it starts the N ranks itself as child processes
 (launch_ranks) and relays rank 0's line.  Each rank tallies its own shard;
-the ranks all-gather their (height, round) sets, and only the candidates of
-rounds present in more than one shard (the rounds a shard boundary cuts) are
-routed to the round's owner over RCCL; the small count tables are then
-all-gathered and merged (hyperdrive_amd/shard.py).  The line reports
-ranks_seen (the process group's size) and, per rank, its device, shard,
-timed span and routed_out / routed_in.
+per step the ranks all-gather only their lexicographic (height, round)
+ranges, and only the candidates of rounds inside another rank's range (the
+rounds a shard boundary cuts) are routed to the round's owner over RCCL; each
+rank keeps the rows it tallied, and the rows of all ranks are merged once,
+after the timed region, for the line's totals (hyperdrive_amd/shard.py).  The
+line reports ranks_seen (the process group's size) and, per rank, its device,
+shard, timed span and routed_out / routed_in.
+
+Defaults: 400 timed steps after 10 warm-up steps (about 0.6 s timed).  The
+timed region includes the three-stream pipeline's fill and its drain (the
+last step's tally); over 20 steps that fixed ~2.4 ms is 7 % of the region
+(DESIGN.md §5, round 6).
 
 Prints ONE JSON line on rank 0, with:
   roofline      the dominant kernel (k_fast_sums) timed live with HIP events
@@ -81,8 +87,8 @@ VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=1 << 20, help="messages per GPU (weak scaling)")
     ap.add_argument("--global-batch", type=int, default=0,
                     help="messages over all GPUs (strong scaling; C4 = 16777216), split into contiguous shards")
@@ -99,7 +105,7 @@ def parse(argv=None):
                     help="priority of the tally stream")
     ap.add_argument("--no-aux", action="store_true", help="skip the SURVEY §8(f) side measurements")
     ap.add_argument("--no-sub", action="store_true", help="skip the C3 / C5 sub-benchmarks")
-    ap.add_argument("--sub-steps", type=int, default=20)
+    ap.add_argument("--sub-steps", type=int, default=100)
     ap.add_argument("--no-c4-check", action="store_true",
                     help="skip the untimed full-size bit-exact check of a 16M 30 %% adversarial C4 batch")
     ap.add_argument("--dist-backend", default="nccl",
@@ -1036,7 +1042,7 @@ def sub_benchmarks(args, v, sigs, foreign, dev, ws, ts):
     return out
 
 
-def many_signatories(args, dev, ws, ts, sizes=(2000, 4000, 8000), steps=10):
+def many_signatories(args, dev, ws, ts, sizes=(2000, 4000, 8000), steps=50):
     """The per-key table budget with thousands of signatories (replica.go:54,
     136-144: the admitted set and f): the C2 stream (1M messages, signer =
     i % S) from S = 2,000, 4,000 and 8,000 signatories, each on a context of

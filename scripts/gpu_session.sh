@@ -27,6 +27,7 @@ for step in "$@"; do
     selflaunch) run selflaunch_gloo2 300 python -u bench.py --gpus 2 --dist-backend gloo --steps 4 --warmup 1 --no-cpu --no-aux --no-sub --no-c4-check && (timeout -k 10 120 python bench.py --gpus 2 > gpurun_out/selflaunch_nccl2.log 2>&1; echo "rc=$?" >> gpurun_out/selflaunch_nccl2.log) ;;
     r6tests) run pytest_r6 900 python -u -m pytest tests/test_fastpath.py tests/test_golden.py tests/test_ingress.py tests/test_mq.py tests/test_c1_network.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread && run pytest_r6_zero 300 python -u -m pytest tests/test_gpu_verify.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "zero_window" ;;
     proffull) run proffull 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/proffull -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-aux --no-sub --no-c4-check ;;
+    proffinal) run proffinal 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/proffinal -o run -- python3 bench.py --no-cpu --no-aux --no-sub --no-c4-check ;;
     abkw) run ab_kw 900 bash scripts/gpu_ab_prof.sh "kw20a:HD_FB_PW=20" "kw16a:HD_FB_PW=16" "kw13a:HD_FB_PW=13" "kw20b:HD_FB_PW=20" "kw16b:HD_FB_PW=16" "kw13b:HD_FB_PW=13" ;;
     abc3) for rep in a b; do run c3_def_$rep 200 python -u scripts/c3_ab.py def && HD_FAST_K=16 run c3_k16_$rep 200 python -u scripts/c3_ab.py k16 && HD_SUM_WAVES=3 run c3_w3_$rep 200 python -u scripts/c3_ab.py w3 && HD_FAST_K=16 HD_SUM_WAVES=3 run c3_k16w3_$rep 200 python -u scripts/c3_ab.py k16w3 && HD_SUM_WAVES=2 run c3_w2_$rep 200 python -u scripts/c3_ab.py w2; done ;;
     abkw22) run ab_kw22 900 bash scripts/gpu_ab_prof.sh "kw20a:HD_FB_PW=20" "kw22a:HD_LIB=hyperdrive_amd/_lib/var/libhd_kw22.so HD_FB_MAX_BYTES=2.2e11" "kw20b:HD_FB_PW=20" "kw22b:HD_LIB=hyperdrive_amd/_lib/var/libhd_kw22.so HD_FB_MAX_BYTES=2.2e11" ;;
